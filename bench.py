@@ -1,0 +1,200 @@
+"""Benchmark of the hot path: homomorphic multiplications per second (BASELINE.json metric)
+on config 2 -- N=2^16, 45-prime chain (44 data limbs + 1 special prime), one HMult =
+multiply_inplace + relinearize_inplace + rescale_to_next_inplace.
+
+One step = BATCH independent HMults per GPU (same relin key, different ciphertexts), inputs
+resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun), each
+rank runs its own ciphertexts (images are independent in the reference), the relin key is
+generated on rank 0 and broadcast over RCCL/xGMI once at setup; no collective in the data
+path -> weak scaling.
+
+Prints one JSON line (rank 0).  The cpu_baseline leg times the repo's CPU restatement of the
+reference algorithm (oracle/, "port") on the host cores of the same box.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fhe-gpt-2_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import mhe  # noqa: E402
+
+LOG_N = 16
+C2_BITS = [51] + [46] * 30 + [51] * 13 + [51]
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+MIB = 1 << 20
+
+
+def hmult_bytes(L):
+    """Algorithmic HBM bytes of one HMult: 2 input cts (2L MiB) + relin key
+    slice (L(L+1) MiB) + output ct ((L-1) MiB) = L^2 + 4L - 1 MiB."""
+    return (L * L + 4 * L - 1) * MIB
+
+
+def rand_residues(shape, moduli_t, gen):
+    """Uniform residues on device: last two dims [limbs][n], limb l uniform in [0, q_l)."""
+    hi = torch.randint(0, 2**62, shape, generator=gen, device=moduli_t.device, dtype=torch.int64)
+    return torch.remainder(hi, moduli_t.view(*([1] * (len(shape) - 2)), -1, 1))
+
+
+def cpu_baseline(moduli, L, threads, seconds_hint):
+    """Time the oracle (CPU restatement, port of the reference algorithm) on `threads`
+    independent HMults run concurrently on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # test infrastructure: only the baseline leg uses it
+
+    n = 1 << LOG_N
+    oc = O.Context(LOG_N, moduli)
+    rng = np.random.default_rng(20261015)
+    qs = np.array(moduli, np.uint64)
+    key = rng.integers(0, 2**62, size=(L, 2, len(moduli), n), dtype=np.uint64) % qs[None, None, :, None]
+    a = rng.integers(0, 2**62, size=(threads, 2, L, n), dtype=np.uint64) % qs[None, None, :L, None]
+    b = rng.integers(0, 2**62, size=(threads, 2, L, n), dtype=np.uint64) % qs[None, None, :L, None]
+    t0 = time.perf_counter()
+    _, used = oc.hmult_batch(a, b, key, threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(threads / dt, 4),
+        "unit": "HMult/s",
+        "cores": int(used),
+        "kind": "port",
+        "sample": f"{threads} independent HMults (N=2^16, L={L}, 45-prime C2 chain), one per OpenMP thread, "
+                  f"oracle/mhe_oracle.c -O3; {dt:.1f} s wall",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8, help="independent HMults per GPU per step")
+    ap.add_argument("--limbs", type=int, default=44)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    L = args.limbs
+    moduli = mhe.coeff_modulus_create(1 << LOG_N, C2_BITS)
+    K = len(moduli)
+    assert 2 <= L <= K - 1
+    eng = mhe.Engine(LOG_N, moduli, device=local)
+    n = eng.n
+    q_t = torch.tensor(moduli, dtype=torch.int64, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(20261015 + rank)
+
+    # relin key: rank 0 draws it, RCCL broadcast to every GPU
+    key = torch.empty((K - 1, 2, K, n), dtype=torch.int64, device=dev)
+    if rank == 0:
+        g0 = torch.Generator(device=dev)
+        g0.manual_seed(7)
+        key.copy_(rand_residues((K - 1, 2, K, n), q_t, g0))
+    if world > 1:
+        dist.broadcast(key, src=0)
+    B = args.batch
+    a = rand_residues((B, 2, L, n), q_t[:L], gen)
+    b = rand_residues((B, 2, L, n), q_t[:L], gen)
+    out = torch.empty((B, 2, L - 1, n), dtype=torch.int64, device=dev)
+    eng.reserve(K - 1)
+    stream = torch.cuda.current_stream(dev)
+    sp = mhe.ctypes.c_void_p(stream.cuda_stream)
+    ptr = lambda t: mhe.ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    a_p = [ptr(a[i]) for i in range(B)]
+    b_p = [ptr(b[i]) for i in range(B)]
+    o_p = [ptr(out[i]) for i in range(B)]
+    k_p = ptr(key)
+
+    def step():
+        for i in range(B):
+            rc = eng.hmult_raw(a_p[i], b_p[i], k_p, K, o_p[i], L, sp)
+            if rc:
+                raise mhe.MheError(rc, mhe.lib().mhe_last_error().decode())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    gpu_s = ev0.elapsed_time(ev1) / 1e3
+    elapsed = max(wall, gpu_s)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    hmults_per_gpu = B * args.steps
+    value = world * hmults_per_gpu / elapsed
+    per_hmult_s = gpu_s / hmults_per_gpu  # HIP-event time of one HMult on this GPU's stream
+    achieved = hmult_bytes(L) / per_hmult_s / 1e9
+    result = {
+        "metric": "homomorphic ciphertext mults/sec (N=2^16, L limbs)",
+        "value": round(value, 3),
+        "unit": "HMult/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: uniform RNS residues (mt-style seeded) + random relin key, NTT form",
+        "config": {
+            "workload": "C2: N=2^16 45-prime chain (44 data limbs + special), HMult = multiply+relinearize+rescale",
+            "log_n": LOG_N,
+            "limbs": L,
+            "batch_per_gpu": B,
+            "parallelism": f"replicas{world} (independent ciphertexts per GPU, key broadcast over RCCL)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "hmult (tensor + key-switch + rescale kernel sequence, one launch group per HMult)",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "algorithmic_bytes_per_launch": hmult_bytes(L),
+            "avg_launch_us": round(per_hmult_s * 1e6, 2),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(moduli, L, args.cpu_threads, 20)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

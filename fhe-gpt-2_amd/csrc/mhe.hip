@@ -1,0 +1,1280 @@
+// libmhe: MI355X-native RNS-CKKS evaluator kernels behind the C ABI of include/mhe.h.
+//
+// Data layout in HBM: [poly][limb][n] u64, identical to SEAL's
+// Ciphertext::data() so host<->device moves are single memcpys.  Per-context tables:
+//   primes[K]        PrimeDev constants
+//   tw[K][n]         (psi^rev(j), Shoup quotient)       -- NTTTables::root_powers_
+//   itw[K][n]        (psi^-rev(j), Shoup quotient)      -- same transform as SEAL's scrambled
+//                                                          inv_root_powers_, bit-reversed index
+//   invq[K][K]       (q_j^-1 mod q_i, Shoup)            -- RNSTool::inv_q_last_mod_q for every j
+// Scratch workspaces are per stream (see Workspace).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mhe.h"
+#include "arith.h"
+#include "ntt.h"
+
+#define MHE_EXPORT extern "C" __attribute__((visibility("default")))
+
+typedef unsigned __int128 u128;
+
+// ============================================================================ errors
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do                                                                                         \
+    {                                                                                          \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return fail(MHE_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+#define HIP_LAUNCH_CHECK()                                                                     \
+    do                                                                                         \
+    {                                                                                          \
+        hipError_t e_ = hipGetLastError();                                                     \
+        if (e_ != hipSuccess) return fail(MHE_ERR_DEVICE, std::string("kernel launch: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ===================================================================== host number theory
+// (product code: the engine builds its own tables; it never calls the test oracle)
+namespace host
+{
+static u64 mulmod(u64 a, u64 b, u64 q)
+{
+    return (u64)((u128)a * b % q);
+}
+
+static u64 powmod(u64 b, u64 e, u64 q)
+{
+    u64 r = 1 % q;
+    b %= q;
+    while (e)
+    {
+        if (e & 1) r = mulmod(r, b, q);
+        b = mulmod(b, b, q);
+        e >>= 1;
+    }
+    return r;
+}
+
+// try_invert_uint_mod (util/numth.h:145)
+static bool invmod(u64 a, u64 q, u64 &out)
+{
+    __int128 r0 = q, r1 = a % q, s0 = 0, s1 = 1;
+    if (r1 == 0) return false;
+    while (r1)
+    {
+        __int128 qt = r0 / r1, r2 = r0 - qt * r1, s2 = s0 - qt * s1;
+        r0 = r1;
+        r1 = r2;
+        s0 = s1;
+        s1 = s2;
+    }
+    if (r0 != 1) return false;
+    __int128 v = s0 % (__int128)q;
+    if (v < 0) v += q;
+    out = (u64)v;
+    return true;
+}
+
+// is_prime (util/numth.cpp:179-277): deterministic Miller-Rabin bases for 64-bit inputs.
+static bool is_prime(u64 v)
+{
+    if (v < 2) return false;
+    static const u64 sm[] = { 2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37 };
+    for (u64 p : sm)
+    {
+        if (v == p) return true;
+        if (v % p == 0) return false;
+    }
+    u64 d = v - 1;
+    int r = 0;
+    while (!(d & 1))
+    {
+        d >>= 1;
+        r++;
+    }
+    for (u64 a : sm)
+    {
+        u64 x = powmod(a, d, v);
+        if (x == 1 || x == v - 1) continue;
+        bool ok = false;
+        for (int i = 0; i < r - 1; i++)
+        {
+            x = mulmod(x, x, v);
+            if (x == v - 1)
+            {
+                ok = true;
+                break;
+            }
+        }
+        if (!ok) return false;
+    }
+    return true;
+}
+
+// try_minimal_primitive_root (util/numth.cpp:398-424): smallest primitive degree-th root.
+static u64 minimal_primitive_root(u64 degree, u64 q)
+{
+    u64 quo = (q - 1) / degree;
+    if (quo * degree != q - 1) return 0;
+    u64 root = 0;
+    for (u64 c = 2; c < q && !root; c++)
+    {
+        u64 g = powmod(c, quo, q);
+        if (g && powmod(g, degree >> 1, q) == q - 1) root = g;
+    }
+    if (!root) return 0;
+    u64 gsq = mulmod(root, root, q), cur = root, best = root;
+    for (u64 i = 0; i < degree; i++)
+    {
+        if (cur < best) best = cur;
+        cur = mulmod(cur, gsq, q);
+    }
+    return best;
+}
+
+static u64 shoup(u64 w, u64 q)
+{
+    return (u64)(((u128)w << 64) / q);
+}
+
+static u32 rev_bits(u32 x, int bits)
+{
+    return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0;
+}
+} // namespace host
+
+// ============================================================================= context
+struct Workspace
+{
+    int max_limbs = 0;
+    u64 *base = nullptr;
+    u64 *coeff = nullptr; // [L][n]        INTT(target)
+    u64 *modup = nullptr; // [L+1][L][n]   lifted + NTT'd digits; reused by mod-down/rescale
+    u64 *acc = nullptr;   // [2][L+1][n]   key inner products
+    u64 *tmp = nullptr;   // [L][n]        permuted c1 for Galois
+    u64 *ct3 = nullptr;   // [3][L][n]     tensor output for hmult
+};
+
+struct mhe_ctx
+{
+    int device = 0;
+    int log_n = 0;
+    size_t n = 0;
+    int K = 0;
+    std::vector<u64> q;
+    std::vector<PrimeDev> primes_h;
+    PrimeDev *primes = nullptr;
+    Tw *tw = nullptr;
+    Tw *itw = nullptr;
+    Tw *invq = nullptr;
+    std::mutex mu;
+    std::map<hipStream_t, Workspace> ws;
+};
+
+static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    Workspace &w = c->ws[st];
+    if (w.max_limbs < limbs)
+    {
+        if (w.base) HIP_TRY(hipFree(w.base));
+        w.base = nullptr;
+        const size_t n = c->n, L = limbs;
+        const size_t Lc = L < 3 ? 3 : L;
+        size_t words = Lc * n + (L + 1) * L * n + 2 * (L + 1) * n + L * n + 3 * L * n;
+        HIP_TRY(hipSetDevice(c->device));
+        if (hipMalloc(&w.base, words * sizeof(u64)) != hipSuccess)
+        {
+            w.max_limbs = 0;
+            return fail(MHE_ERR_MEMORY, "workspace allocation failed");
+        }
+        w.coeff = w.base;
+        w.modup = w.coeff + Lc * n;
+        w.acc = w.modup + (L + 1) * L * n;
+        w.tmp = w.acc + 2 * (L + 1) * n;
+        w.ct3 = w.tmp + L * n;
+        w.max_limbs = limbs;
+    }
+    *out = &w;
+    return MHE_OK;
+}
+
+// ================================================================================ jobs
+// Plain transform over [poly][limb][n] with limb l on prime l (optionally src != dst).
+struct JobPlain
+{
+    const u64 *src;
+    u64 *dst;
+    const PrimeDev *primes;
+    const Tw *tw;
+    int limbs;
+    int log_n;
+    int mode; // forward row store: 0 = lazy [0,4q), 1 = full; inverse col store: 0 lazy [0,2q), 1 full
+    struct View
+    {
+        const u64 *src;
+        u64 *dst;
+        PrimeDev p;
+        const Tw *tw;
+        int mode;
+        bool skip;
+        __device__ u64 load(u32 x) const { return src[x]; }
+        __device__ void store_fwd(u32 x, u64 v) const
+        {
+            if (mode) v = csub(csub(v, p.two_q), p.q);
+            dst[x] = v;
+        }
+    };
+    __device__ View view(int y) const
+    {
+        const int l = y % limbs;
+        const size_t off = (size_t)y << log_n;
+        return View{ src + off, dst + off, primes[l], tw + ((size_t)l << log_n), mode, false };
+    }
+};
+
+// Views must expose store(); wrappers pick the forward / inverse reduction.
+struct JobFwdPlain : JobPlain
+{
+    struct V2 : View
+    {
+        __device__ void store(u32 x, u64 v) const { store_fwd(x, v); }
+    };
+    __device__ V2 view(int y) const { return V2{ JobPlain::view(y) }; }
+};
+
+struct JobInvPlain : JobPlain
+{
+    struct V2 : View
+    {
+        __device__ void store(u32 x, u64 v) const
+        {
+            if (mode) v = csub(v, p.q);
+            dst[x] = v;
+        }
+    };
+    __device__ V2 view(int y) const { return V2{ JobPlain::view(y) }; }
+};
+
+// Key-switching ModUp, column pass (evaluator.cpp:2386-2408): job y = I*L + J lifts digit J
+// (canonical mod q_J, from INTT(target)) to prime I and starts its NTT; I == L is the special
+// prime.  I == J is skipped: the MAC reads the input NTT form (evaluator.cpp:2380-2384).
+struct JobModUpCol
+{
+    const u64 *coeff; // [L][n]
+    u64 *modup;       // [L+1][L][n]
+    const PrimeDev *primes;
+    const Tw *tw;
+    int L, K, log_n;
+    struct View
+    {
+        const u64 *src;
+        u64 *dst;
+        PrimeDev p;
+        const Tw *tw;
+        bool reduce;
+        bool skip;
+        __device__ u64 load(u32 x) const
+        {
+            u64 v = src[x];
+            return reduce ? barrett64(v, p) : v;
+        }
+        __device__ void store(u32 x, u64 v) const { dst[x] = v; }
+    };
+    __device__ View view(int y) const
+    {
+        const int I = y / L, J = y % L;
+        const int pi = (I == L) ? K - 1 : I;
+        View v;
+        v.src = coeff + ((size_t)J << log_n);
+        v.dst = modup + ((size_t)y << log_n);
+        v.p = primes[pi];
+        v.tw = tw + ((size_t)pi << log_n);
+        v.reduce = primes[J].q > v.p.q; // key_modulus[J] <= key_modulus[key_index] -> copy
+        v.skip = (I == J);
+        return v;
+    }
+};
+
+struct JobModUpRow
+{
+    u64 *modup;
+    const PrimeDev *primes;
+    const Tw *tw;
+    int L, K, log_n;
+    struct View
+    {
+        u64 *buf;
+        PrimeDev p;
+        const Tw *tw;
+        bool skip;
+        __device__ u64 load(u32 x) const { return buf[x]; }
+        // canonical output keeps the 128-bit MAC safe for any digit count (< 2^8 terms)
+        __device__ void store(u32 x, u64 v) const { buf[x] = csub(csub(v, p.two_q), p.q); }
+    };
+    __device__ View view(int y) const
+    {
+        const int I = y / L, J = y % L;
+        const int pi = (I == L) ? K - 1 : I;
+        return View{ modup + ((size_t)y << log_n), primes[pi], tw + ((size_t)pi << log_n), I == J };
+    }
+};
+
+// Key-switching ModDown (evaluator.cpp:2466-2524).  t_last = INTT_lazy(acc[k][L]) in [0,2P);
+// column pass job y = k*L + i computes ((barrett(t_last + P/2) mod q_i) + fix_i) and starts
+// the NTT mod q_i; the row pass epilogue does ct[k][i] += (acc[k][i] + 4q_i - t) * P^-1.
+struct JobModDownCol
+{
+    const u64 *acc; // [2][L+1][n]
+    u64 *scratch;   // [2][L][n]
+    const PrimeDev *primes;
+    const Tw *tw;
+    int L, K, log_n;
+    struct View
+    {
+        const u64 *src;
+        u64 *dst;
+        PrimeDev p;
+        PrimeDev P;
+        const Tw *tw;
+        u64 half, fix;
+        bool reduce;
+        bool skip;
+        __device__ u64 load(u32 x) const
+        {
+            u64 t = barrett64(src[x] + half, P);
+            if (reduce) t = barrett64(t, p);
+            return t + fix;
+        }
+        __device__ void store(u32 x, u64 v) const { dst[x] = v; }
+    };
+    __device__ View view(int y) const
+    {
+        const int k = y / L, i = y % L;
+        View v;
+        v.src = acc + ((size_t)(k * (L + 1) + L) << log_n);
+        v.dst = scratch + ((size_t)y << log_n);
+        v.p = primes[i];
+        v.P = primes[K - 1];
+        v.tw = tw + ((size_t)i << log_n);
+        v.half = v.P.q >> 1;
+        v.fix = v.p.q - barrett64(v.half, v.p);
+        v.reduce = v.P.q > v.p.q;
+        v.skip = false;
+        return v;
+    }
+};
+
+struct JobModDownRow
+{
+    u64 *scratch;
+    const u64 *acc;
+    u64 *ct; // [2][L][n]
+    const PrimeDev *primes;
+    const Tw *tw;
+    const Tw *invq; // [K][K]
+    int L, K, log_n;
+    struct View
+    {
+        u64 *buf;
+        const u64 *accp;
+        u64 *ctp;
+        PrimeDev p;
+        const Tw *tw;
+        Tw inv;
+        bool skip;
+        __device__ u64 load(u32 x) const { return buf[x]; }
+        __device__ void store(u32 x, u64 t) const
+        {
+            u64 v = mul_shoup(accp[x] + p.four_q - t, inv.x, inv.y, p.q);
+            ctp[x] = addmod(v, ctp[x], p.q);
+        }
+    };
+    __device__ View view(int y) const
+    {
+        const int k = y / L, i = y % L;
+        View v;
+        v.buf = scratch + ((size_t)y << log_n);
+        v.accp = acc + ((size_t)(k * (L + 1) + i) << log_n);
+        v.ctp = ct + ((size_t)(k * L + i) << log_n);
+        v.p = primes[i];
+        v.tw = tw + ((size_t)i << log_n);
+        v.inv = invq[(size_t)(K - 1) * K + i];
+        v.skip = false;
+        return v;
+    }
+};
+
+// Rescale (util/rns.cpp:737-808): last[s] = INTT(in[s][L-1]) canonical; column pass job
+// y = s*(L-1) + i: ((last + half mod q_last) mod q_i) + (q_i - half mod q_i); row pass
+// epilogue out[s][i] = (in[s][i] + 4q_i - t) * q_last^-1 mod q_i.
+struct JobRescaleCol
+{
+    const u64 *last; // [size][n]
+    u64 *scratch;    // [size][L-1][n]
+    const PrimeDev *primes;
+    const Tw *tw;
+    int L, log_n;
+    struct View
+    {
+        const u64 *src;
+        u64 *dst;
+        PrimeDev p;
+        u64 ql, half, neg_half;
+        const Tw *tw;
+        bool reduce;
+        bool skip;
+        __device__ u64 load(u32 x) const
+        {
+            u64 v = csub(src[x] + half, ql);
+            if (reduce) v = barrett64(v, p);
+            return v + neg_half;
+        }
+        __device__ void store(u32 x, u64 v) const { dst[x] = v; }
+    };
+    __device__ View view(int y) const
+    {
+        const int s = y / (L - 1), i = y % (L - 1);
+        View v;
+        v.src = last + ((size_t)s << log_n);
+        v.dst = scratch + ((size_t)y << log_n);
+        v.p = primes[i];
+        v.ql = primes[L - 1].q;
+        v.half = v.ql >> 1;
+        v.neg_half = v.p.q - barrett64(v.half, v.p);
+        v.tw = tw + ((size_t)i << log_n);
+        v.reduce = v.p.q < v.ql;
+        v.skip = false;
+        return v;
+    }
+};
+
+struct JobRescaleRow
+{
+    u64 *scratch;
+    const u64 *in; // [size][L][n]
+    u64 *out;      // [size][L-1][n]
+    const PrimeDev *primes;
+    const Tw *tw;
+    const Tw *invq;
+    int L, K, log_n;
+    struct View
+    {
+        u64 *buf;
+        const u64 *inp;
+        u64 *outp;
+        PrimeDev p;
+        const Tw *tw;
+        Tw inv;
+        bool skip;
+        __device__ u64 load(u32 x) const { return buf[x]; }
+        __device__ void store(u32 x, u64 t) const { outp[x] = mul_shoup(inp[x] + p.four_q - t, inv.x, inv.y, p.q); }
+    };
+    __device__ View view(int y) const
+    {
+        const int s = y / (L - 1), i = y % (L - 1);
+        View v;
+        v.buf = scratch + ((size_t)y << log_n);
+        v.inp = in + ((size_t)(s * L + i) << log_n);
+        v.outp = out + ((size_t)(s * (L - 1) + i) << log_n);
+        v.p = primes[i];
+        v.tw = tw + ((size_t)i << log_n);
+        v.inv = invq[(size_t)(L - 1) * K + i];
+        v.skip = false;
+        return v;
+    }
+};
+
+// Rescale INTT of the last limb: src limb (L-1) of poly s -> last[s], canonical.
+struct JobLastInv
+{
+    const u64 *in;
+    u64 *last;
+    const PrimeDev *primes;
+    const Tw *itw;
+    int L, log_n;
+    int lazy;
+    struct View
+    {
+        const u64 *src;
+        u64 *dst;
+        PrimeDev p;
+        const Tw *tw;
+        int lazy;
+        bool skip;
+        __device__ u64 load(u32 x) const { return src[x]; }
+        __device__ void store(u32 x, u64 v) const { dst[x] = lazy ? v : csub(v, p.q); }
+    };
+    __device__ View view(int y) const
+    {
+        View v;
+        v.src = in + ((size_t)(y * L + (L - 1)) << log_n);
+        v.dst = last + ((size_t)y << log_n);
+        v.p = primes[L - 1];
+        v.tw = itw + ((size_t)(L - 1) << log_n);
+        v.lazy = lazy;
+        v.skip = false;
+        return v;
+    }
+};
+
+// Generic job on explicit (src, dst, prime) with a per-job stride: used for the key-switch
+// INTT of the target (limb J on prime J) and of the special accumulator limbs.
+struct JobStrided
+{
+    const u64 *src;
+    u64 *dst;
+    size_t src_stride, dst_stride; // in words, per job
+    int prime0;                    // prime index of job 0
+    int prime_step;                // 0: all jobs on prime0; 1: job y on prime0 + y
+    const PrimeDev *primes;
+    const Tw *tw;
+    int log_n;
+    int mode; // inverse store: 0 lazy, 1 full
+    struct View
+    {
+        const u64 *src;
+        u64 *dst;
+        PrimeDev p;
+        const Tw *tw;
+        int mode;
+        bool skip;
+        __device__ u64 load(u32 x) const { return src[x]; }
+        __device__ void store(u32 x, u64 v) const { dst[x] = mode ? csub(v, p.q) : v; }
+    };
+    __device__ View view(int y) const
+    {
+        const int pi = prime0 + prime_step * y;
+        return View{ src + y * src_stride, dst + y * dst_stride, primes[pi], tw + ((size_t)pi << log_n), mode, false };
+    }
+};
+
+// ============================================================================ kernels
+// Elementwise kernels process 2 residues per lane (16-B loads); n is a multiple of 512.
+#define ELEM_GRID(total2) dim3((unsigned)(((total2) + 255) / 256))
+
+__global__ void k_addsub(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                         size_t total2, int op)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 >= total2) return;
+    const size_t i = i2 * 2;
+    const int l = (int)((i >> log_n) % limbs);
+    const u64 q = primes[l].q;
+    ulonglong2 x = *(const ulonglong2 *)(a + i);
+    ulonglong2 r;
+    if (op == 0)
+    {
+        ulonglong2 y = *(const ulonglong2 *)(b + i);
+        r.x = addmod(x.x, y.x, q);
+        r.y = addmod(x.y, y.y, q);
+    }
+    else if (op == 1)
+    {
+        ulonglong2 y = *(const ulonglong2 *)(b + i);
+        r.x = submod(x.x, y.x, q);
+        r.y = submod(x.y, y.y, q);
+    }
+    else
+    {
+        r.x = x.x ? q - x.x : 0;
+        r.y = x.y ? q - x.y : 0;
+    }
+    *(ulonglong2 *)(out + i) = r;
+}
+
+// dyadic product with b broadcast over polys (multiply_plain_ntt)
+__global__ void k_mulplain(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                           size_t total2)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 >= total2) return;
+    const size_t i = i2 * 2;
+    const size_t limb_words = (size_t)limbs << log_n;
+    const int l = (int)((i >> log_n) % limbs);
+    const PrimeDev p = primes[l];
+    ulonglong2 x = *(const ulonglong2 *)(a + i);
+    ulonglong2 y = *(const ulonglong2 *)(b + i % limb_words);
+    ulonglong2 r;
+    r.x = mulmod(x.x, y.x, p);
+    r.y = mulmod(x.y, y.y, p);
+    *(ulonglong2 *)(out + i) = r;
+}
+
+struct ScalarTab
+{
+    u64 v[64];
+    u64 vq[64];
+};
+
+__global__ void k_scalar(const u64 *a, u64 *out, const PrimeDev *primes, ScalarTab s, int limbs, int log_n,
+                         size_t total2, int op)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 >= total2) return;
+    const size_t i = i2 * 2;
+    const int l = (int)((i >> log_n) % limbs);
+    const u64 q = primes[l].q;
+    ulonglong2 x = *(const ulonglong2 *)(a + i);
+    ulonglong2 r;
+    if (op == 0)
+    {
+        r.x = mul_shoup(x.x, s.v[l], s.vq[l], q);
+        r.y = mul_shoup(x.y, s.v[l], s.vq[l], q);
+    }
+    else
+    {
+        r.x = addmod(x.x, s.v[l], q);
+        r.y = addmod(x.y, s.v[l], q);
+    }
+    *(ulonglong2 *)(out + i) = r;
+}
+
+// ckks_multiply tile loop (evaluator.cpp:714-773) / ckks_square (:1000-1059), fused.
+__global__ void k_tensor(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                         size_t total2, int square)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 >= total2) return;
+    const size_t i = i2 * 2;
+    const size_t ps = (size_t)limbs << log_n;
+    const int l = (int)(i >> log_n);
+    const PrimeDev p = primes[l];
+    ulonglong2 x0 = *(const ulonglong2 *)(a + i), x1 = *(const ulonglong2 *)(a + ps + i);
+    ulonglong2 r0, r1, r2;
+    if (square)
+    {
+        r0.x = mulmod(x0.x, x0.x, p);
+        r0.y = mulmod(x0.y, x0.y, p);
+        u64 t = mulmod(x0.x, x1.x, p), u = mulmod(x0.y, x1.y, p);
+        r1.x = addmod(t, t, p.q);
+        r1.y = addmod(u, u, p.q);
+        r2.x = mulmod(x1.x, x1.x, p);
+        r2.y = mulmod(x1.y, x1.y, p);
+    }
+    else
+    {
+        ulonglong2 y0 = *(const ulonglong2 *)(b + i), y1 = *(const ulonglong2 *)(b + ps + i);
+        r0.x = mulmod(x0.x, y0.x, p);
+        r0.y = mulmod(x0.y, y0.y, p);
+        r1.x = addmod(mulmod(x0.x, y1.x, p), mulmod(x1.x, y0.x, p), p.q);
+        r1.y = addmod(mulmod(x0.y, y1.y, p), mulmod(x1.y, y0.y, p), p.q);
+        r2.x = mulmod(x1.x, y1.x, p);
+        r2.y = mulmod(x1.y, y1.y, p);
+    }
+    *(ulonglong2 *)(out + i) = r0;
+    *(ulonglong2 *)(out + ps + i) = r1;
+    *(ulonglong2 *)(out + 2 * ps + i) = r2;
+}
+
+// Key-switching inner product (evaluator.cpp:2410-2463): for output prime I (I == L -> P),
+// acc[k][I] = sum_J d_J[I] * key[J][k][I] mod q_I, where d_J[I] is the lifted NTT digit
+// (modup[I][J]) or, for I == J, the input target limb itself.  128-bit accumulation with a
+// single final Barrett reduction (digits are canonical so < 2^8 terms never overflow).
+__global__ __launch_bounds__(256) void k_ks_mac(const u64 *modup, const u64 *target, const u64 *key, u64 *acc,
+                                                const PrimeDev *primes, int L, int K, int key_limbs, int log_n)
+{
+    const u32 i = (blockIdx.x * 256 + threadIdx.x) * 2;
+    const int I = blockIdx.y;
+    const int pi = (I == L) ? K - 1 : I;
+    const int ki = (I == L) ? key_limbs - 1 : I;
+    const size_t n = (size_t)1 << log_n;
+    const PrimeDev p = primes[pi];
+    Acc128 a0x{ 0, 0 }, a0y{ 0, 0 }, a1x{ 0, 0 }, a1y{ 0, 0 };
+    const size_t kstride = (size_t)key_limbs * n;
+    for (int J = 0; J < L; J++)
+    {
+        const u64 *d = (I == J) ? target + (size_t)J * n : modup + ((size_t)I * L + J) * n;
+        ulonglong2 x = *(const ulonglong2 *)(d + i);
+        const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
+        ulonglong2 y0 = *(const ulonglong2 *)(k0 + i);
+        ulonglong2 y1 = *(const ulonglong2 *)(k0 + kstride + i);
+        mac128(a0x, x.x, y0.x);
+        mac128(a0y, x.y, y0.y);
+        mac128(a1x, x.x, y1.x);
+        mac128(a1y, x.y, y1.y);
+    }
+    ulonglong2 r0, r1;
+    r0.x = barrett128(a0x.lo, a0x.hi, p);
+    r0.y = barrett128(a0y.lo, a0y.hi, p);
+    r1.x = barrett128(a1x.lo, a1x.hi, p);
+    r1.y = barrett128(a1y.lo, a1y.hi, p);
+    *(ulonglong2 *)(acc + (size_t)I * n + i) = r0;
+    *(ulonglong2 *)(acc + (size_t)(L + 1 + I) * n + i) = r1;
+}
+
+// GaloisTool::apply_galois_ntt (util/galois.cpp:192-218) with the permutation of
+// generate_table_ntt (util/galois.cpp:18-51) computed on the fly: out[i] = in[tab(i)].
+__global__ void k_galois(const u64 *in, u64 *out, u32 elt, int log_n, size_t total)
+{
+    size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    const u32 n = 1u << log_n;
+    const u32 i = (u32)(g & (n - 1));
+    const size_t base = g - i;
+    const u32 reversed = __builtin_bitreverse32(n + i) >> (31 - log_n); // rev over log_n+1 bits
+    const u32 idx = (u32)(((u64)elt * reversed) >> 1) & (n - 1);
+    const u32 src = __builtin_bitreverse32(idx) >> (32 - log_n);
+    out[g] = in[base + src];
+}
+
+// ======================================================================= dispatch helpers
+static bool valid_ctx(mhe_ctx *c)
+{
+    return c && c->primes;
+}
+
+static hipStream_t S(void *s)
+{
+    return (hipStream_t)s;
+}
+
+static int check_limbs(mhe_ctx *c, int limbs, int lo)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (limbs < lo || limbs > c->K - 1) return fail(MHE_ERR_ARG, "encrypted is not valid for encryption parameters");
+    return MHE_OK;
+}
+
+// Forward NTT of [polys][limbs] (limb l on prime l).
+static int run_ntt_fwd(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limbs, int full, hipStream_t st)
+{
+    JobFwdPlain j;
+    j.src = src;
+    j.dst = dst;
+    j.primes = c->primes;
+    j.tw = c->tw;
+    j.limbs = limbs;
+    j.log_n = c->log_n;
+    j.mode = 0;
+    fwd_col(j, c->log_n, polys * limbs, st);
+    j.src = dst;
+    j.mode = full;
+    fwd_row(j, c->log_n, polys * limbs, st);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+static int run_ntt_inv(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limbs, int full, hipStream_t st)
+{
+    JobInvPlain j;
+    j.src = src;
+    j.dst = dst;
+    j.primes = c->primes;
+    j.tw = c->itw;
+    j.limbs = limbs;
+    j.log_n = c->log_n;
+    j.mode = 0;
+    inv_row(j, c->log_n, polys * limbs, st);
+    j.src = dst;
+    j.mode = full;
+    inv_col(j, c->log_n, polys * limbs, st);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+// switch_key_inplace: ct[2][L][n] += KS(target[L][n]) (evaluator.cpp:2281-2525).
+static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key, int key_limbs, int L,
+                          hipStream_t st)
+{
+    if (key_limbs < L + 1 || key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
+    Workspace *w;
+    int r = get_ws(c, st, c->K - 1, &w);
+    if (r) return r;
+    const int log_n = c->log_n;
+    const size_t n = c->n;
+    // 1. t_target = INTT(target), canonical (evaluator.cpp:2351-2354)
+    {
+        JobStrided j{ target, w->coeff, n, n, 0, 1, c->primes, c->itw, log_n, 0 };
+        inv_row(j, log_n, L, st);
+        j.src = w->coeff;
+        j.mode = 1;
+        inv_col(j, log_n, L, st);
+    }
+    // 2. ModUp: lift digit J to prime I, NTT (evaluator.cpp:2386-2408)
+    {
+        JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n };
+        fwd_col(j, log_n, (L + 1) * L, st);
+        JobModUpRow r2{ w->modup, c->primes, c->tw, L, c->K, log_n };
+        fwd_row(r2, log_n, (L + 1) * L, st);
+    }
+    // 3. inner products with the key (evaluator.cpp:2410-2463)
+    {
+        dim3 grid((unsigned)(n / 512), L + 1);
+        hipLaunchKernelGGL(k_ks_mac, grid, dim3(256), 0, st, w->modup, target, key, w->acc, c->primes, L, c->K,
+                           key_limbs, log_n);
+    }
+    // 4. ModDown (evaluator.cpp:2466-2524): INTT_lazy of the special limbs, then fused
+    //    lift + NTT + (c + 4q - t) * P^-1 + add.
+    {
+        JobStrided j{ w->acc + (size_t)L * n, w->acc + (size_t)L * n, (size_t)(L + 1) * n, (size_t)(L + 1) * n,
+                      c->K - 1, 0, c->primes, c->itw, log_n, 0 };
+        inv_row(j, log_n, 2, st);
+        inv_col(j, log_n, 2, st);
+        JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n };
+        fwd_col(dc, log_n, 2 * L, st);
+        JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
+        fwd_row(dr, log_n, 2 * L, st);
+    }
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+static int run_rescale(mhe_ctx *c, const u64 *in, u64 *out, int size, int L, hipStream_t st)
+{
+    Workspace *w;
+    int r = get_ws(c, st, c->K - 1, &w);
+    if (r) return r;
+    const int log_n = c->log_n;
+    // last[s] = INTT(in[s][L-1]) canonical -> w->coeff (size <= 3 polys)
+    JobLastInv li{ in, w->coeff, c->primes, c->itw, L, log_n, 1 };
+    inv_row(li, log_n, size, st);
+    {
+        JobStrided j2{ w->coeff, w->coeff, c->n, c->n, L - 1, 0, c->primes, c->itw, log_n, 1 };
+        inv_col(j2, log_n, size, st);
+    }
+    JobRescaleCol rc{ w->coeff, w->modup, c->primes, c->tw, L, log_n };
+    fwd_col(rc, log_n, size * (L - 1), st);
+    JobRescaleRow rr{ w->modup, in, out, c->primes, c->tw, c->invq, L, c->K, log_n };
+    fwd_row(rr, log_n, size * (L - 1), st);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+// ================================================================================ C ABI
+MHE_EXPORT const char *mhe_last_error(void)
+{
+    return g_err.c_str();
+}
+
+MHE_EXPORT int mhe_version(void)
+{
+    return 1;
+}
+
+MHE_EXPORT int mhe_coeff_modulus_create(uint64_t n, const int *bit_sizes, int count, uint64_t *out)
+{
+    if (!bit_sizes || !out || count <= 0 || count > 64 || (n & (n - 1)) || n < 2)
+        return fail(MHE_ERR_ARG, "bit_sizes is invalid");
+    std::map<int, std::vector<u64>> table;
+    std::map<int, int> cnt;
+    for (int i = 0; i < count; i++)
+    {
+        if (bit_sizes[i] < 2 || bit_sizes[i] > 60) return fail(MHE_ERR_ARG, "bit_sizes is invalid");
+        cnt[bit_sizes[i]]++;
+    }
+    for (auto &kv : cnt)
+    {
+        const int bits = kv.first;
+        const u64 factor = 2 * n;
+        u64 value = ((u64)1 << bits) - factor + 1, lower = (u64)1 << (bits - 1);
+        std::vector<u64> &v = table[bits];
+        while ((int)v.size() < kv.second && value > lower)
+        {
+            if (host::is_prime(value)) v.push_back(value);
+            value -= factor;
+        }
+        if ((int)v.size() < kv.second) return fail(MHE_ERR_ARG, "failed to find enough qualifying primes");
+    }
+    for (int i = 0; i < count; i++)
+    {
+        auto &v = table[bit_sizes[i]];
+        out[i] = v.back();
+        v.pop_back();
+    }
+    return MHE_OK;
+}
+
+MHE_EXPORT uint32_t mhe_galois_elt_from_step(int log_n, int step)
+{
+    const u64 n = (u64)1 << log_n, m = 2 * n;
+    if (step == 0) return (uint32_t)(m - 1);
+    u64 pos = (u64)(step < 0 ? -(long long)step : step);
+    if (pos >= (n >> 1)) return 0;
+    u64 s = step < 0 ? (n >> 1) - pos : pos;
+    u64 elt = 1;
+    while (s--) elt = (elt * 5) & (m - 1); // generator_ = 5 (util/galois.h:169)
+    return (uint32_t)elt;
+}
+
+MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, int count, int device)
+{
+    if (!out) return fail(MHE_ERR_ARG, "ctx is null");
+    *out = nullptr;
+    if (log_n < 12 || log_n > 16) return fail(MHE_ERR_ARG, "poly_modulus_degree is invalid");
+    if (!moduli || count < 2 || count > 64) return fail(MHE_ERR_ARG, "coeff_modulus is invalid");
+    const size_t n = (size_t)1 << log_n;
+    for (int i = 0; i < count; i++)
+    {
+        u64 q = moduli[i];
+        if (q < 2 || q >= ((u64)1 << 61) || (q - 1) % (2 * n) != 0 || !host::is_prime(q))
+            return fail(MHE_ERR_ARG, "coeff_modulus is not NTT-friendly prime");
+    }
+    mhe_ctx *c = new (std::nothrow) mhe_ctx;
+    if (!c) return fail(MHE_ERR_MEMORY, "out of memory");
+    c->device = device;
+    c->log_n = log_n;
+    c->n = n;
+    c->K = count;
+    c->q.assign(moduli, moduli + count);
+    std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
+    c->primes_h.resize(count);
+    for (int k = 0; k < count; k++)
+    {
+        const u64 q = moduli[k];
+        PrimeDev &p = c->primes_h[k];
+        p.q = q;
+        p.two_q = 2 * q;
+        p.four_q = 4 * q;
+        u128 ratio = (~(u128)0) / q;
+        p.r0 = (u64)ratio;
+        p.r1 = (u64)(ratio >> 64);
+        // NTTTables::initialize (util/ntt.cpp:30-89)
+        u64 psi = host::minimal_primitive_root(2 * n, q), ipsi = 0, ninv = 0;
+        if (!psi || !host::invmod(psi, q, ipsi) || !host::invmod(n % q, q, ninv))
+        {
+            delete c;
+            return fail(MHE_ERR_ARG, "invalid modulus");
+        }
+        Tw *t = &tw[(size_t)k * n], *it = &itw[(size_t)k * n];
+        u64 pw = 1, ipw = 1;
+        for (size_t i = 0; i < n; i++)
+        {
+            const u32 r = host::rev_bits((u32)i, log_n);
+            t[r].x = pw;
+            t[r].y = host::shoup(pw, q);
+            it[r].x = ipw;
+            it[r].y = host::shoup(ipw, q);
+            pw = host::mulmod(pw, psi, q);
+            ipw = host::mulmod(ipw, ipsi, q);
+        }
+        p.ninv = ninv;
+        p.ninv_q = host::shoup(ninv, q);
+        p.last_w = host::mulmod(it[1].x, ninv, q);
+        p.last_wq = host::shoup(p.last_w, q);
+    }
+    for (int j = 0; j < count; j++)
+        for (int i = 0; i < count; i++)
+        {
+            u64 inv = 0;
+            if (i != j) host::invmod(moduli[j] % moduli[i], moduli[i], inv);
+            invq[(size_t)j * count + i].x = inv;
+            invq[(size_t)j * count + i].y = host::shoup(inv, moduli[i]);
+        }
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipMalloc(&c->primes, sizeof(PrimeDev) * count);
+    if (e == hipSuccess) e = hipMalloc(&c->tw, sizeof(Tw) * tw.size());
+    if (e == hipSuccess) e = hipMalloc(&c->itw, sizeof(Tw) * itw.size());
+    if (e == hipSuccess) e = hipMalloc(&c->invq, sizeof(Tw) * invq.size());
+    if (e == hipSuccess) e = hipMemcpy(c->primes, c->primes_h.data(), sizeof(PrimeDev) * count, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->tw, tw.data(), sizeof(Tw) * tw.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->itw, itw.data(), sizeof(Tw) * itw.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(c->invq, invq.data(), sizeof(Tw) * invq.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess)
+    {
+        (void)hipFree(c->primes);
+        (void)hipFree(c->tw);
+        (void)hipFree(c->itw);
+        (void)hipFree(c->invq);
+        c->primes = nullptr;
+        delete c;
+        return fail(MHE_ERR_DEVICE, std::string("mhe_ctx_create: ") + hipGetErrorString(e));
+    }
+    *out = c;
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_ctx_destroy(mhe_ctx *c)
+{
+    if (!c) return MHE_OK;
+    (void)hipSetDevice(c->device);
+    for (auto &kv : c->ws)
+        if (kv.second.base) (void)hipFree(kv.second.base);
+    (void)hipFree(c->primes);
+    (void)hipFree(c->tw);
+    (void)hipFree(c->itw);
+    (void)hipFree(c->invq);
+    delete c;
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_ctx_reserve(mhe_ctx *c, int max_limbs, void *stream)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    Workspace *w;
+    return get_ws(c, S(stream), max_limbs < c->K - 1 ? c->K - 1 : max_limbs, &w);
+}
+
+MHE_EXPORT int mhe_malloc(mhe_ctx *c, void **dptr, size_t bytes)
+{
+    if (!valid_ctx(c) || !dptr) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipSetDevice(c->device));
+    if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) return fail(MHE_ERR_MEMORY, "device allocation failed");
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_free(mhe_ctx *c, void *dptr)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipFree(dptr));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_memcpy_h2d(mhe_ctx *c, void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_memcpy_d2h(mhe_ctx *c, void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_memcpy_d2d(mhe_ctx *c, void *dst, const void *src, size_t bytes, void *stream)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_stream_sync(mhe_ctx *c, void *stream)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipStreamSynchronize(S(stream)));
+    return MHE_OK;
+}
+
+static int check_poly_args(mhe_ctx *c, const void *a, int polys, int limbs)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (!a || polys < 1 || limbs < 1 || limbs > c->K) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_ntt_forward(mhe_ctx *c, uint64_t *data, int polys, int limbs, int lazy, void *stream)
+{
+    int r = check_poly_args(c, data, polys, limbs);
+    if (r) return r;
+    return run_ntt_fwd(c, data, data, polys, limbs, lazy ? 0 : 1, S(stream));
+}
+
+MHE_EXPORT int mhe_ntt_inverse(mhe_ctx *c, uint64_t *data, int polys, int limbs, int lazy, void *stream)
+{
+    int r = check_poly_args(c, data, polys, limbs);
+    if (r) return r;
+    return run_ntt_inv(c, data, data, polys, limbs, lazy ? 0 : 1, S(stream));
+}
+
+static int launch_addsub(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out, int polys, int limbs, int op, void *st)
+{
+    int r = check_poly_args(c, a, polys, limbs);
+    if (r) return r;
+    if (!out || (op < 2 && !b)) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
+    hipLaunchKernelGGL(k_addsub, ELEM_GRID(total2), dim3(256), 0, S(st), a, b, out, c->primes, limbs, c->log_n,
+                       total2, op);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_add(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs, void *s)
+{
+    return launch_addsub(c, a, b, out, polys, limbs, 0, s);
+}
+
+MHE_EXPORT int mhe_sub(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs, void *s)
+{
+    return launch_addsub(c, a, b, out, polys, limbs, 1, s);
+}
+
+MHE_EXPORT int mhe_negate(mhe_ctx *c, const uint64_t *a, uint64_t *out, int polys, int limbs, void *s)
+{
+    return launch_addsub(c, a, nullptr, out, polys, limbs, 2, s);
+}
+
+MHE_EXPORT int mhe_multiply_plain(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys,
+                                  int limbs, void *s)
+{
+    int r = check_poly_args(c, a, polys, limbs);
+    if (r) return r;
+    if (!b || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
+    hipLaunchKernelGGL(k_mulplain, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, out, c->primes, limbs, c->log_n,
+                       total2);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+static int launch_scalar(mhe_ctx *c, const u64 *a, const u64 *scalars, u64 *out, int polys, int limbs, int op,
+                         void *s)
+{
+    int r = check_poly_args(c, a, polys, limbs);
+    if (r) return r;
+    if (!scalars || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    ScalarTab t;
+    for (int l = 0; l < limbs; l++)
+    {
+        if (scalars[l] >= c->q[l]) return fail(MHE_ERR_ARG, "scalar must be less than modulus");
+        t.v[l] = scalars[l];
+        t.vq[l] = host::shoup(scalars[l], c->q[l]);
+    }
+    size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
+    hipLaunchKernelGGL(k_scalar, ELEM_GRID(total2), dim3(256), 0, S(s), a, out, c->primes, t, limbs, c->log_n,
+                       total2, op);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_multiply_scalar(mhe_ctx *c, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys,
+                                   int limbs, void *s)
+{
+    return launch_scalar(c, a, scalars, out, polys, limbs, 0, s);
+}
+
+MHE_EXPORT int mhe_add_scalar(mhe_ctx *c, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys,
+                              int limbs, void *s)
+{
+    return launch_scalar(c, a, scalars, out, polys, limbs, 1, s);
+}
+
+static int launch_tensor(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out3, int L, int square, hipStream_t st)
+{
+    size_t total2 = ((size_t)L << c->log_n) / 2;
+    hipLaunchKernelGGL(k_tensor, ELEM_GRID(total2), dim3(256), 0, st, a, b, out3, c->primes, L, c->log_n, total2,
+                       square);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_ct_multiply(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out3, int limbs, void *s)
+{
+    int r = check_poly_args(c, a, 2, limbs);
+    if (r) return r;
+    if (!b || !out3) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    return launch_tensor(c, a, b, out3, limbs, 0, S(s));
+}
+
+MHE_EXPORT int mhe_ct_square(mhe_ctx *c, const uint64_t *a, uint64_t *out3, int limbs, void *s)
+{
+    int r = check_poly_args(c, a, 2, limbs);
+    if (r) return r;
+    if (!out3) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    return launch_tensor(c, a, a, out3, limbs, 1, S(s));
+}
+
+MHE_EXPORT int mhe_switch_key(mhe_ctx *c, uint64_t *ct, const uint64_t *target, const uint64_t *key, int key_limbs,
+                              int limbs, void *s)
+{
+    int r = check_limbs(c, limbs, 1);
+    if (r) return r;
+    if (!ct || !target || !key) return fail(MHE_ERR_ARG, "target_iter");
+    return run_switch_key(c, ct, target, key, key_limbs, limbs, S(s));
+}
+
+MHE_EXPORT int mhe_relinearize(mhe_ctx *c, uint64_t *ct3, const uint64_t *key, int key_limbs, int limbs, void *s)
+{
+    int r = check_limbs(c, limbs, 1);
+    if (r) return r;
+    if (!ct3 || !key) return fail(MHE_ERR_ARG, "relin_keys is not valid for encryption parameters");
+    return run_switch_key(c, ct3, ct3 + ((size_t)2 * limbs << c->log_n), key, key_limbs, limbs, S(s));
+}
+
+static int launch_galois(mhe_ctx *c, const u64 *in, u32 elt, u64 *out, int polys, int limbs, hipStream_t st)
+{
+    if (!(elt & 1) || elt >= 2 * c->n) return fail(MHE_ERR_ARG, "Galois element is not valid");
+    size_t total = (size_t)polys * limbs << c->log_n;
+    hipLaunchKernelGGL(k_galois, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, out, elt, c->log_n,
+                       total);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_permute_galois(mhe_ctx *c, const uint64_t *in, uint32_t elt, uint64_t *out, int polys, int limbs,
+                                  void *s)
+{
+    int r = check_poly_args(c, in, polys, limbs);
+    if (r) return r;
+    if (!out || out == in) return fail(MHE_ERR_ARG, "result cannot point to the same value as operand");
+    return launch_galois(c, in, elt, out, polys, limbs, S(s));
+}
+
+MHE_EXPORT int mhe_apply_galois(mhe_ctx *c, uint64_t *ct, uint32_t elt, const uint64_t *key, int key_limbs, int limbs,
+                                void *s)
+{
+    int r = check_limbs(c, limbs, 1);
+    if (r) return r;
+    if (!ct || !key) return fail(MHE_ERR_ARG, "Galois key not present");
+    hipStream_t st = S(s);
+    Workspace *w;
+    r = get_ws(c, st, c->K - 1, &w);
+    if (r) return r;
+    const size_t ps = (size_t)limbs << c->log_n;
+    // evaluator.cpp:2193-2214: c0 <- perm(c0) (via tmp), tmp <- perm(c1), c1 <- 0, then KS(tmp)
+    r = launch_galois(c, ct, elt, w->tmp, 1, limbs, st);
+    if (r) return r;
+    HIP_TRY(hipMemcpyAsync(ct, w->tmp, ps * sizeof(u64), hipMemcpyDeviceToDevice, st));
+    r = launch_galois(c, ct + ps, elt, w->tmp, 1, limbs, st);
+    if (r) return r;
+    HIP_TRY(hipMemsetAsync(ct + ps, 0, ps * sizeof(u64), st));
+    return run_switch_key(c, ct, w->tmp, key, key_limbs, limbs, st);
+}
+
+MHE_EXPORT int mhe_rescale_to_next(mhe_ctx *c, const uint64_t *in, uint64_t *out, int size, int limbs, void *s)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (limbs < 2) return fail(MHE_ERR_RANGE, "end of modulus switching chain reached");
+    if (limbs > c->K - 1 || size < 1 || size > 3 || !in || !out)
+        return fail(MHE_ERR_ARG, "encrypted is not valid for encryption parameters");
+    if (in == out) return fail(MHE_ERR_ARG, "rescale output must not alias its input");
+    return run_rescale(c, in, out, size, limbs, S(s));
+}
+
+MHE_EXPORT int mhe_mod_switch_drop(mhe_ctx *c, const uint64_t *in, uint64_t *out, int size, int limbs, void *s)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (limbs < 2) return fail(MHE_ERR_RANGE, "end of modulus switching chain reached");
+    if (!in || !out || size < 1) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    const size_t src_pitch = ((size_t)limbs << c->log_n) * sizeof(u64);
+    const size_t dst_pitch = ((size_t)(limbs - 1) << c->log_n) * sizeof(u64);
+    // Row-by-row ascending copy is safe in place (each destination row starts at or before its source).
+    for (int p = 0; p < size; p++)
+        if (in != out || p > 0)
+            HIP_TRY(hipMemcpyAsync((char *)out + p * dst_pitch, (const char *)in + p * src_pitch, dst_pitch,
+                                   hipMemcpyDeviceToDevice, S(s)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_hmult(mhe_ctx *c, const uint64_t *a, const uint64_t *b, const uint64_t *key, int key_limbs,
+                         uint64_t *out, int limbs, void *s)
+{
+    int r = check_limbs(c, limbs, 2);
+    if (r) return r;
+    if (!a || !b || !key || !out) return fail(MHE_ERR_ARG, "invalid argument");
+    hipStream_t st = S(s);
+    Workspace *w;
+    r = get_ws(c, st, c->K - 1, &w);
+    if (r) return r;
+    if ((r = launch_tensor(c, a, b, w->ct3, limbs, a == b, st))) return r;
+    if ((r = run_switch_key(c, w->ct3, w->ct3 + ((size_t)2 * limbs << c->log_n), key, key_limbs, limbs, st))) return r;
+    return run_rescale(c, w->ct3, out, 2, limbs, st);
+}

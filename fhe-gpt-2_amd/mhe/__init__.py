@@ -1,0 +1,273 @@
+"""Python binding of libmhe.so (include/mhe.h) for tests and bench.
+
+Thin ctypes layer: one method per C-ABI entry point, named after the SEAL evaluator step it
+replaces.  Device memory and streams come from PyTorch (plumbing only); every compute call
+goes through the HIP kernels in libmhe.so.  There is no CPU fallback: if the library or the
+GPU is missing, construction raises.
+
+Device arrays are torch int64 tensors holding the u64 residue bits ([poly][limb][n]).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "libmhe.so")
+_lib = None
+
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/mhe.h
+SIGNATURES = {
+    "mhe_last_error": (ctypes.c_char_p, []),
+    "mhe_version": (ctypes.c_int, []),
+    "mhe_ctx_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, u64p, ctypes.c_int, ctypes.c_int]),
+    "mhe_ctx_destroy": (ctypes.c_int, [vp]),
+    "mhe_ctx_reserve": (ctypes.c_int, [vp, ctypes.c_int, vp]),
+    "mhe_coeff_modulus_create": (ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_int), ctypes.c_int, u64p]),
+    "mhe_galois_elt_from_step": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_int]),
+    "mhe_malloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
+    "mhe_free": (ctypes.c_int, [vp, vp]),
+    "mhe_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
+    "mhe_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
+    "mhe_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
+    "mhe_stream_sync": (ctypes.c_int, [vp, vp]),
+    "mhe_ntt_forward": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_ntt_inverse": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_add": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_sub": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_negate": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_multiply_plain": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_multiply_scalar": (ctypes.c_int, [vp, vp, u64p, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_add_scalar": (ctypes.c_int, [vp, vp, u64p, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_ct_multiply": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, vp]),
+    "mhe_ct_square": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, vp]),
+    "mhe_switch_key": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_relinearize": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_apply_galois": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_permute_galois": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_rescale_to_next": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_mod_switch_drop": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_hmult": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]),
+}
+
+
+class MheError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7.  Importing torch
+        # first makes libmhe.so's libamdhip64.so.7 dependency resolve to that same copy (same
+        # SONAME); loading /opt/rocm's first and torch's second puts two runtimes in the process
+        # and device initialisation fails.
+        import torch  # noqa: F401
+
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise MheError(rc, lib().mhe_last_error().decode())
+
+
+def coeff_modulus_create(n, bit_sizes):
+    """CoeffModulus::Create (modulus.cpp:143-185) -- host-only, no GPU needed."""
+    bs = (ctypes.c_int * len(bit_sizes))(*bit_sizes)
+    out = (ctypes.c_uint64 * len(bit_sizes))()
+    _check(lib().mhe_coeff_modulus_create(n, bs, len(bit_sizes), out))
+    return list(out)
+
+
+def galois_elt_from_step(log_n, step):
+    return int(lib().mhe_galois_elt_from_step(log_n, step))
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Engine:
+    """One mhe_ctx: the key-level modulus chain on one device."""
+
+    def __init__(self, log_n, moduli, device=0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError("mhe.Engine needs a ROCm GPU (no CPU fallback)")
+        self.log_n = log_n
+        self.n = 1 << log_n
+        self.moduli = [int(q) for q in moduli]
+        self.K = len(self.moduli)
+        self.device = device
+        self.torch_device = torch.device("cuda", device)
+        h = vp()
+        arr = (ctypes.c_uint64 * self.K)(*self.moduli)
+        _check(lib().mhe_ctx_create(ctypes.byref(h), log_n, arr, self.K, device))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mhe_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ plumbing
+    def stream(self):
+        return ctypes.c_void_p(_torch().cuda.current_stream(self.torch_device).cuda_stream)
+
+    def to_device(self, arr):
+        torch = _torch()
+        a = np.ascontiguousarray(arr, dtype=np.uint64)
+        return torch.from_numpy(a.view(np.int64)).to(self.torch_device)
+
+    def empty(self, *shape):
+        torch = _torch()
+        return torch.empty(*shape, dtype=torch.int64, device=self.torch_device)
+
+    @staticmethod
+    def to_host(t):
+        return t.detach().cpu().numpy().view(np.uint64)
+
+    def synchronize(self):
+        _check(lib().mhe_stream_sync(self._h, self.stream()))
+
+    def reserve(self, max_limbs):
+        _check(lib().mhe_ctx_reserve(self._h, max_limbs, self.stream()))
+
+    @staticmethod
+    def _pl(t):
+        """(polys, limbs) of a [polys][limbs][n] or [limbs][n] tensor."""
+        return (1, t.shape[0]) if t.dim() == 2 else (t.shape[0], t.shape[1])
+
+    # ----------------------------------------------------------------- kernels
+    def ntt_forward(self, t, lazy=False):
+        p, l = self._pl(t)
+        _check(lib().mhe_ntt_forward(self._h, _ptr(t), p, l, int(lazy), self.stream()))
+        return t
+
+    def ntt_inverse(self, t, lazy=False):
+        p, l = self._pl(t)
+        _check(lib().mhe_ntt_inverse(self._h, _ptr(t), p, l, int(lazy), self.stream()))
+        return t
+
+    def add(self, a, b, out=None):
+        out = self.empty(*a.shape) if out is None else out
+        p, l = self._pl(a)
+        _check(lib().mhe_add(self._h, _ptr(a), _ptr(b), _ptr(out), p, l, self.stream()))
+        return out
+
+    def sub(self, a, b, out=None):
+        out = self.empty(*a.shape) if out is None else out
+        p, l = self._pl(a)
+        _check(lib().mhe_sub(self._h, _ptr(a), _ptr(b), _ptr(out), p, l, self.stream()))
+        return out
+
+    def negate(self, a, out=None):
+        out = self.empty(*a.shape) if out is None else out
+        p, l = self._pl(a)
+        _check(lib().mhe_negate(self._h, _ptr(a), _ptr(out), p, l, self.stream()))
+        return out
+
+    def multiply_plain(self, a, pt, out=None):
+        out = self.empty(*a.shape) if out is None else out
+        p, l = self._pl(a)
+        _check(lib().mhe_multiply_plain(self._h, _ptr(a), _ptr(pt), _ptr(out), p, l, self.stream()))
+        return out
+
+    def _scalar(self, fn, a, scalars, out):
+        out = self.empty(*a.shape) if out is None else out
+        p, l = self._pl(a)
+        s = (ctypes.c_uint64 * l)(*[int(x) for x in scalars])
+        _check(fn(self._h, _ptr(a), s, _ptr(out), p, l, self.stream()))
+        return out
+
+    def multiply_scalar(self, a, scalars, out=None):
+        return self._scalar(lib().mhe_multiply_scalar, a, scalars, out)
+
+    def add_scalar(self, a, scalars, out=None):
+        return self._scalar(lib().mhe_add_scalar, a, scalars, out)
+
+    def multiply(self, a, b, out3=None):
+        L = a.shape[1]
+        out3 = self.empty(3, L, self.n) if out3 is None else out3
+        _check(lib().mhe_ct_multiply(self._h, _ptr(a), _ptr(b), _ptr(out3), L, self.stream()))
+        return out3
+
+    def square(self, a, out3=None):
+        L = a.shape[1]
+        out3 = self.empty(3, L, self.n) if out3 is None else out3
+        _check(lib().mhe_ct_square(self._h, _ptr(a), _ptr(out3), L, self.stream()))
+        return out3
+
+    @staticmethod
+    def _key_limbs(key):
+        return key.shape[2]  # [digits][2][key_limbs][n]
+
+    def switch_key(self, ct, target, key):
+        _check(lib().mhe_switch_key(self._h, _ptr(ct), _ptr(target), _ptr(key), self._key_limbs(key), ct.shape[1],
+                                    self.stream()))
+        return ct
+
+    def relinearize(self, ct3, key):
+        _check(lib().mhe_relinearize(self._h, _ptr(ct3), _ptr(key), self._key_limbs(key), ct3.shape[1],
+                                     self.stream()))
+        return ct3[:2]
+
+    def apply_galois(self, ct, elt, key):
+        _check(lib().mhe_apply_galois(self._h, _ptr(ct), elt, _ptr(key), self._key_limbs(key), ct.shape[1],
+                                      self.stream()))
+        return ct
+
+    def permute_galois(self, a, elt, out=None):
+        out = self.empty(*a.shape) if out is None else out
+        p, l = self._pl(a)
+        _check(lib().mhe_permute_galois(self._h, _ptr(a), elt, _ptr(out), p, l, self.stream()))
+        return out
+
+    def rescale_to_next(self, ct, out=None):
+        size, L = ct.shape[0], ct.shape[1]
+        out = self.empty(size, L - 1, self.n) if out is None else out
+        _check(lib().mhe_rescale_to_next(self._h, _ptr(ct), _ptr(out), size, L, self.stream()))
+        return out
+
+    def mod_switch_drop(self, ct, out=None):
+        size, L = ct.shape[0], ct.shape[1]
+        out = self.empty(size, L - 1, self.n) if out is None else out
+        _check(lib().mhe_mod_switch_drop(self._h, _ptr(ct), _ptr(out), size, L, self.stream()))
+        return out
+
+    def hmult(self, a, b, key, out=None):
+        L = a.shape[1]
+        out = self.empty(2, L - 1, self.n) if out is None else out
+        _check(lib().mhe_hmult(self._h, _ptr(a), _ptr(b), _ptr(key), self._key_limbs(key), _ptr(out), L,
+                               self.stream()))
+        return out
+
+    def hmult_raw(self, a_ptr, b_ptr, key_ptr, key_limbs, out_ptr, L, stream):
+        """Pointer-level HMult for the benchmark loop (no tensor bookkeeping)."""
+        return lib().mhe_hmult(self._h, a_ptr, b_ptr, key_ptr, key_limbs, out_ptr, L, stream)

@@ -1,0 +1,134 @@
+/*
+ * mhe.h -- C ABI of the MI355X-native RNS-CKKS engine (libmhe.so).
+ *
+ * This is the drop-in boundary under the SEAL-compatible C++ surface: every entry point
+ * replaces one step of the modified SEAL 3.6.6 evaluator path in the reference
+ * (paths relative to /root/reference/cnn_ckks/cpu-ckks/single-key/seal-modified-3.6.6/native/src/seal/).
+ *
+ * Conventions
+ *  - Polynomials are u64 residues laid out exactly like SEAL's Ciphertext/Plaintext/
+ *    PublicKey data: [poly][limb][n], limb-major, NTT form for CKKS.  Uploading a SEAL
+ *    object is one memcpy.
+ *  - All data pointers passed to compute calls are DEVICE pointers (from mhe_malloc or any
+ *    HIP allocation on the context's device).  Sizes are in limbs / polys; n = 2^log_n.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).  Every call is
+ *    stream-ordered and asynchronous; concurrent calls on different streams are safe
+ *    (each stream gets its own scratch workspace).
+ *  - Return value: MHE_OK (0) or a negative MHE_ERR_*; mhe_last_error() gives the message,
+ *    worded like SEAL's exceptions so the C++ shim can rethrow them verbatim.
+ *  - The modulus chain passed to mhe_ctx_create is the KEY level chain of a SEALContext
+ *    (context.cpp:422-523): data primes q_0..q_{L-1} then the special prime P.  A ciphertext
+ *    "at L limbs" uses q_0..q_{L-1}.
+ */
+#ifndef MHE_H
+#define MHE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MHE_OK 0
+#define MHE_ERR_ARG (-1)     /* std::invalid_argument in SEAL */
+#define MHE_ERR_DEVICE (-2)  /* HIP runtime failure */
+#define MHE_ERR_RANGE (-3)   /* std::out_of_range / end of modulus switching chain */
+#define MHE_ERR_MEMORY (-4)  /* allocation failure */
+
+typedef struct mhe_ctx mhe_ctx;
+
+/* ---- diagnostics ---------------------------------------------------------------- */
+const char *mhe_last_error(void);
+int mhe_version(void);
+
+/* ---- context ------------------------------------------------------------------------
+ * Replaces SEALContext's per-prime precomputation: NTTTables::initialize
+ * (util/ntt.cpp:30-89), RNSTool::inv_q_last_mod_q (util/rns.cpp:686-693), Modulus::const_ratio
+ * (modulus.cpp:66-98).  log_n in [12,16]; moduli: key-level chain, special prime last;
+ * count in [2,64]; each q < 2^61, q = 1 mod 2n. */
+int mhe_ctx_create(mhe_ctx **ctx, int log_n, const uint64_t *moduli, int count, int device);
+int mhe_ctx_destroy(mhe_ctx *ctx);
+/* Pre-size the scratch workspace of `stream` for ciphertexts of up to max_limbs limbs so
+ * that no allocation happens inside later calls (needed before hipGraph capture). */
+int mhe_ctx_reserve(mhe_ctx *ctx, int max_limbs, void *stream);
+
+/* CoeffModulus::Create (modulus.cpp:143-185 with get_primes, util/numth.cpp:279-317). */
+int mhe_coeff_modulus_create(uint64_t poly_modulus_degree, const int *bit_sizes, int count, uint64_t *out);
+/* GaloisTool::get_elt_from_step (util/galois.cpp:53-95); 0 on invalid step. */
+uint32_t mhe_galois_elt_from_step(int log_n, int step);
+
+/* ---- memory ----------------------------------------------------------------------- */
+int mhe_malloc(mhe_ctx *ctx, void **dptr, size_t bytes);
+int mhe_free(mhe_ctx *ctx, void *dptr);
+int mhe_memcpy_h2d(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int mhe_memcpy_d2h(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int mhe_memcpy_d2d(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+int mhe_stream_sync(mhe_ctx *ctx, void *stream);
+
+/* ---- NTT ---------------------------------------------------------------------------
+ * ntt_negacyclic_harvey(_lazy) / inverse_ntt_negacyclic_harvey(_lazy) on every limb l of
+ * `polys` polynomials of `limbs` limbs each (limb l uses prime l of the chain):
+ * util/ntt.cpp:183-209, util/ntt.h:235-296,336-396; ct version evaluator.cpp:2025-2118.
+ * lazy=1 leaves forward outputs in [0,4q) and inverse outputs in [0,2q). */
+int mhe_ntt_forward(mhe_ctx *ctx, uint64_t *data, int polys, int limbs, int lazy, void *stream);
+int mhe_ntt_inverse(mhe_ctx *ctx, uint64_t *data, int polys, int limbs, int lazy, void *stream);
+
+/* ---- coefficient-wise arithmetic ----------------------------------------------------
+ * add/sub/negate_poly_coeffmod (util/polyarithsmallmod.h:190-300; Evaluator::add_inplace,
+ * sub_inplace, negate_inplace evaluator.cpp:103-246); out may alias a or b. */
+int mhe_add(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs, void *stream);
+int mhe_sub(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs, void *stream);
+int mhe_negate(mhe_ctx *ctx, const uint64_t *a, uint64_t *out, int polys, int limbs, void *stream);
+/* dyadic_product_coeffmod per limb (util/polyarithsmallmod.cpp:111-165); b is [limbs][n] and
+ * is broadcast over the polys of a: this is Evaluator::multiply_plain_ntt
+ * (evaluator.cpp:1891-1930) when a is a ciphertext and b an NTT plaintext. */
+int mhe_multiply_plain(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs,
+                       void *stream);
+/* multiply_poly_scalar_coeffmod with one scalar per limb (scalars[l] < q_l), host array;
+ * used by multiply_const (evaluator.cpp:287-301). */
+int mhe_multiply_scalar(mhe_ctx *ctx, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys,
+                        int limbs, void *stream);
+/* add_poly_scalar_coeffmod with one scalar per limb (add_const, evaluator.cpp:287-301). */
+int mhe_add_scalar(mhe_ctx *ctx, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys, int limbs,
+                   void *stream);
+
+/* ---- ciphertext ops -------------------------------------------------------------------
+ * Evaluator::ckks_multiply, size-2 x size-2 (evaluator.cpp:673-773): out3 = [3][L][n]. */
+int mhe_ct_multiply(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out3, int limbs, void *stream);
+/* Evaluator::ckks_square (evaluator.cpp:1000-1059). */
+int mhe_ct_square(mhe_ctx *ctx, const uint64_t *a, uint64_t *out3, int limbs, void *stream);
+
+/* Key-switching key: one KSwitchKeys entry (vector<PublicKey>, keygenerator.cpp:384-414) laid
+ * out [digit][2][key_limbs][n] on the device; the special prime is limb key_limbs-1 and data
+ * limb i is limb i.  A full SEAL key has key_limbs = chain count and digits = count-1; a
+ * level-truncated slice for L-limb ciphertexts may keep only L digits and L+1 limbs. */
+
+/* Evaluator::switch_key_inplace (evaluator.cpp:2281-2525): ct[2][L][n] += KS(target[L][n]). */
+int mhe_switch_key(mhe_ctx *ctx, uint64_t *ct, const uint64_t *target, const uint64_t *key, int key_limbs,
+                   int limbs, void *stream);
+/* Evaluator::relinearize_internal for size 3 (evaluator.cpp:1061-1116): ct3[3][L][n] ->
+ * first two polys hold the relinearised ciphertext. */
+int mhe_relinearize(mhe_ctx *ctx, uint64_t *ct3, const uint64_t *key, int key_limbs, int limbs, void *stream);
+/* Evaluator::apply_galois_inplace (evaluator.cpp:2120-2222) with GaloisTool::apply_galois_ntt
+ * (util/galois.cpp:192-218): ct[2][L][n] in place. */
+int mhe_apply_galois(mhe_ctx *ctx, uint64_t *ct, uint32_t galois_elt, const uint64_t *key, int key_limbs,
+                     int limbs, void *stream);
+/* GaloisTool::apply_galois_ntt alone on [polys][limbs][n] (out must not alias in). */
+int mhe_permute_galois(mhe_ctx *ctx, const uint64_t *in, uint32_t galois_elt, uint64_t *out, int polys, int limbs,
+                       void *stream);
+/* Evaluator::mod_switch_scale_to_next / RNSTool::divide_and_round_q_last_ntt_inplace
+ * (evaluator.cpp:1118-1181, util/rns.cpp:737-808): in[size][L][n] -> out[size][L-1][n]. */
+int mhe_rescale_to_next(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int size, int limbs, void *stream);
+/* Evaluator::mod_switch_drop_to_next (evaluator.cpp:1183-1281): in[size][L][n] ->
+ * out[size][L-1][n] (limb copy; out may equal in for an in-place compaction). */
+int mhe_mod_switch_drop(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int size, int limbs, void *stream);
+/* One HMult: multiply + relinearize + rescale_to_next:
+ * a, b: [2][L][n] -> out: [2][L-1][n]. */
+int mhe_hmult(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, const uint64_t *relin_key, int key_limbs,
+              uint64_t *out, int limbs, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

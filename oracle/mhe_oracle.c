@@ -41,8 +41,9 @@ typedef struct
 static void or_mod_init(or_mod *m, uint64_t q)
 {
     m->value = q;
-    /* floor(2^128 / q) = floor((2^128 - 1) / q) unless q divides 2^128 (q odd here, q > 1). */
+    /* floor(2^128 / q) = floor((2^128 - 1) / q) unless q divides 2^128 (q a power of two). */
     u128 r = (~(u128)0) / q;
+    if ((q & (q - 1)) == 0) r += 1;
     m->ratio0 = (uint64_t)r;
     m->ratio1 = (uint64_t)(r >> 64);
 }

@@ -1,0 +1,343 @@
+"""GPU parity: the HIP engine (through the C ABI of include/mhe.h) against the CPU oracle,
+bit for bit, on seeded inputs.  Sizes: N=2^12 (fast, every op and edge case), and the full
+N=2^16 chains of the reference -- the 45-prime C2 chain, the ResNet
+chain (cnn/infer_seal.cpp:288-316) and the GPT-2 chain with its 60-bit special prime
+(gpt2/util.h:22-27).  Names follow the reference GoogleTest / evaluator entry points."""
+import numpy as np
+import pytest
+
+import ckks_helpers as H
+import mhe
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+C2_BITS = [51] + [46] * 30 + [51] * 13 + [51]       # 44 data limbs + special
+RESNET_BITS = [51] + [46] * 16 + [51] * 14 + [51]   # 31 data limbs + special
+GPT2_BITS = [49] + [46] * 21 + [49] * 14 + [60]     # 36 data limbs + 60-bit special
+SMALL_BITS = [51] + [46] * 4 + [51] * 2 + [51]      # 7 data limbs + special
+
+
+class Chain:
+    def __init__(self, log_n, bits, seed=0):
+        self.log_n, self.n = log_n, 1 << log_n
+        self.moduli = O.coeff_modulus_create(self.n, bits)
+        self.K = len(self.moduli)
+        self.oc = O.Context(log_n, self.moduli)
+        self.eng = mhe.Engine(log_n, self.moduli)
+        self.rng = np.random.default_rng(seed)
+
+    def rand(self, *shape, limbs=None):
+        """Uniform residues, shape [..., limbs, n] with limb l mod q_l."""
+        L = shape[-2]
+        out = np.empty(shape, np.uint64)
+        for l in range(L):
+            out[..., l, :] = self.rng.integers(0, self.moduli[l], size=shape[:-2] + (self.n,), dtype=np.uint64)
+        return out
+
+    def rand_key(self, digits=None):
+        """Random key-switching key [digits][2][K][n] (uniform residues per key-level prime)."""
+        digits = self.K - 1 if digits is None else digits
+        key = np.empty((digits, 2, self.K, self.n), np.uint64)
+        for l, q in enumerate(self.moduli):
+            key[:, :, l, :] = self.rng.integers(0, q, size=(digits, 2, self.n), dtype=np.uint64)
+        return key
+
+    def up(self, a):
+        return self.eng.to_device(a)
+
+    def down(self, t):
+        self.eng.synchronize()
+        return mhe.Engine.to_host(t)
+
+
+@pytest.fixture(scope="module")
+def small():
+    return Chain(12, SMALL_BITS, seed=1)
+
+
+@pytest.fixture(scope="module")
+def c2():
+    return Chain(16, C2_BITS, seed=2)
+
+
+# ----------------------------------------------------------------------------- NTT
+@pytest.mark.parametrize("lazy", [False, True])
+def test_ntt_negacyclic_harvey(small, lazy):
+    ch = small
+    x = ch.rand(3, ch.K - 1, ch.n)
+    got = ch.down(ch.eng.ntt_forward(ch.up(x), lazy=lazy))
+    want = ch.oc.ntt(x, O.NTT_FWD)
+    if lazy:
+        assert (got < 4 * np.array(ch.moduli[:-1], np.uint64)[None, :, None]).all()
+        got = got % np.array(ch.moduli[:-1], np.uint64)[None, :, None]
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_inverse_ntt_negacyclic_harvey(small, lazy):
+    ch = small
+    x = ch.rand(2, ch.K, ch.n)
+    got = ch.down(ch.eng.ntt_inverse(ch.up(x), lazy=lazy))
+    want = ch.oc.ntt(x, O.NTT_INV)
+    if lazy:
+        got = got % np.array(ch.moduli, np.uint64)[None, :, None]
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("log_n", [12, 13, 14, 15, 16])
+def test_ntt_all_sizes(log_n):
+    """Every supported ring degree (column/row pass split differs for odd log n)."""
+    moduli = O.coeff_modulus_create(1 << log_n, [50, 40, 60])
+    oc = O.Context(log_n, moduli)
+    eng = mhe.Engine(log_n, moduli)
+    rng = np.random.default_rng(log_n)
+    x = np.stack([rng.integers(0, q, size=1 << log_n, dtype=np.uint64) for q in moduli])
+    t = eng.to_device(x)
+    eng.ntt_forward(t)
+    eng.synchronize()
+    got = mhe.Engine.to_host(t)
+    assert np.array_equal(got, oc.ntt(x, O.NTT_FWD))
+    eng.ntt_inverse(t)
+    eng.synchronize()
+    assert np.array_equal(mhe.Engine.to_host(t), x)
+
+
+def test_ntt_kat_vectors():
+    """The reference KAT modulus 0xffffffffffc0001 at N=2^12: GPU == oracle, round trip exact."""
+    q = 0xFFFFFFFFFFC0001
+    # q-1 = 2^18 * ... so q is NTT-friendly for 2n <= 2^18
+    eng = mhe.Engine(12, [q, O.get_primes(1 << 12, 50, 1)[0]])
+    x = np.random.default_rng(7).integers(0, q, size=(1, 1 << 12), dtype=np.uint64)
+    t = eng.to_device(x)
+    eng.ntt_forward(t)
+    eng.synchronize()
+    assert np.array_equal(mhe.Engine.to_host(t), O.ntt(x, 12, q).reshape(1, -1))
+
+
+# ---------------------------------------------------------------- coefficient-wise
+def test_add_sub_negate(small):
+    ch = small
+    a, b = ch.rand(2, ch.K - 1, ch.n), ch.rand(2, ch.K - 1, ch.n)
+    ta, tb = ch.up(a), ch.up(b)
+    assert np.array_equal(ch.down(ch.eng.add(ta, tb)), ch.oc.add(a, b))
+    assert np.array_equal(ch.down(ch.eng.sub(ta, tb)), ch.oc.sub(a, b))
+    assert np.array_equal(ch.down(ch.eng.negate(ta)), ch.oc.negate(a))
+    # in place (out aliases a)
+    ch.eng.add(ta, tb, out=ta)
+    assert np.array_equal(ch.down(ta), ch.oc.add(a, b))
+
+
+def test_multiply_plain_ntt(small):
+    ch = small
+    L = ch.K - 1
+    ct, pt = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+    got = ch.down(ch.eng.multiply_plain(ch.up(ct), ch.up(pt)))
+    assert np.array_equal(got, ch.oc.multiply_plain(ct, pt))
+
+
+def test_multiply_add_scalar(small):
+    ch = small
+    L = ch.K - 1
+    a = ch.rand(2, L, ch.n)
+    s = [int(ch.rng.integers(0, q)) for q in ch.moduli[:L]]
+    got = ch.down(ch.eng.multiply_scalar(ch.up(a), s))
+    want = np.stack([np.stack([(a[p, l].astype(object) * s[l] % ch.moduli[l]).astype(np.uint64) for l in range(L)])
+                     for p in range(2)])
+    assert np.array_equal(got, want)
+    got = ch.down(ch.eng.add_scalar(ch.up(a), s))
+    want = np.stack([np.stack([((a[p, l].astype(object) + s[l]) % ch.moduli[l]).astype(np.uint64) for l in range(L)])
+                     for p in range(2)])
+    assert np.array_equal(got, want)
+
+
+# ----------------------------------------------------------------- ciphertext ops
+@pytest.mark.parametrize("L", [1, 4, 7])
+def test_ckks_multiply(small, L):
+    ch = small
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.multiply(ch.up(a), ch.up(b)))
+    assert np.array_equal(got, ch.oc.multiply(a, b))
+
+
+def test_ckks_square(small):
+    ch = small
+    a = ch.rand(2, 5, ch.n)
+    got = ch.down(ch.eng.square(ch.up(a)))
+    assert np.array_equal(got, ch.oc.square(a))
+
+
+@pytest.mark.parametrize("L", [2, 3, 7])
+@pytest.mark.parametrize("size", [1, 2, 3])
+def test_rescale_to_next(small, L, size):
+    ch = small
+    ct = ch.rand(size, L, ch.n)
+    got = ch.down(ch.eng.rescale_to_next(ch.up(ct)))
+    assert np.array_equal(got, ch.oc.rescale(ct))
+
+
+@pytest.mark.parametrize("L", [1, 2, 5, 7])
+def test_switch_key_inplace(small, L):
+    ch = small
+    key = ch.rand_key()
+    ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+    got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
+    assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
+
+
+def test_switch_key_truncated_key(small):
+    """A level-truncated key slice ([L digits][2][L+1 limbs], special last) gives the same result."""
+    ch = small
+    L = 4
+    key = ch.rand_key()
+    trunc = np.concatenate([key[:L, :, :L], key[:L, :, -1:]], axis=2).copy()
+    ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+    got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(trunc)))
+    assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
+
+
+def test_relinearize(small):
+    ch = small
+    L = 6
+    key = ch.rand_key()
+    ct3 = ch.rand(3, L, ch.n)
+    t = ch.up(ct3)
+    ch.eng.relinearize(t, ch.up(key))
+    got = ch.down(t)[:2]
+    assert np.array_equal(got, ch.oc.relinearize(ct3, key))
+
+
+@pytest.mark.parametrize("step", [1, -1, 3, 100, 0])
+def test_rotate_vector(small, step):
+    """apply_galois_inplace with elt = get_elt_from_step(step) (0 -> conjugation 2N-1)."""
+    ch = small
+    L = 5
+    elt = mhe.galois_elt_from_step(ch.log_n, step)
+    assert elt == O.galois_elt_from_step(ch.n, step)
+    key = ch.rand_key()
+    ct = ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.apply_galois(ch.up(ct), elt, ch.up(key)))
+    assert np.array_equal(got, ch.oc.apply_galois(ct, elt, key))
+
+
+def test_apply_galois_ntt_permutation(small):
+    ch = small
+    a = ch.rand(2, 3, ch.n)
+    for elt in (3, 5, 25, 2 * ch.n - 1):
+        got = ch.down(ch.eng.permute_galois(ch.up(a), elt))
+        want = O.apply_galois_ntt(a.reshape(-1, ch.n), ch.log_n, elt).reshape(a.shape)
+        assert np.array_equal(got, want)
+
+
+def test_mod_switch_drop_to_next(small):
+    ch = small
+    ct = ch.rand(2, 5, ch.n)
+    got = ch.down(ch.eng.mod_switch_drop(ch.up(ct)))
+    assert np.array_equal(got, ct[:, :4])
+
+
+def test_hmult_small(small):
+    ch = small
+    L = ch.K - 1
+    key = ch.rand_key()
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
+    assert np.array_equal(got, ch.oc.hmult(a, b, key))
+
+
+def test_errors_are_reported(small):
+    ch = small
+    key = ch.up(ch.rand_key())
+    ct = ch.up(ch.rand(2, 1, ch.n))
+    with pytest.raises(mhe.MheError, match="end of modulus switching chain"):
+        ch.eng.rescale_to_next(ct)
+    with pytest.raises(mhe.MheError, match="Galois element is not valid"):
+        ch.eng.permute_galois(ch.up(ch.rand(1, 2, ch.n)), 4)
+    too_many = ch.up(ch.rand(2, ch.K, ch.n))  # K limbs > K-1 data limbs
+    with pytest.raises(mhe.MheError):
+        ch.eng.switch_key(too_many, too_many[0], key)
+
+
+# ------------------------------------------------------------ decryptable end-to-end
+def test_CKKSEncryptMultiplyRelinRescaleDecrypt_small():
+    """Mirror of tests/seal/evaluator.cpp:2314 on the GPU: Enc(x)*Enc(x) -> relin -> rescale
+    decrypts to x^2 (SURVEY.md §8(d) input kind (ii))."""
+    log_n = 13
+    moduli = O.coeff_modulus_create(1 << log_n, [51, 46, 46, 46, 51])
+    oc = O.Context(log_n, moduli)
+    eng = mhe.Engine(log_n, moduli)
+    keys = H.keygen(oc, seed=11, hw=64)
+    L, scale = 4, 2.0 ** 46
+    x = 0.5 * np.cos(2 * np.pi * np.arange((1 << log_n) // 2) / 1024)
+    ct = H.encrypt(oc, keys, H.encode(oc, x, scale, L), L)
+    out = mhe.Engine.to_host(eng.hmult(eng.to_device(ct), eng.to_device(ct), eng.to_device(keys.relin)))
+    assert np.array_equal(out, oc.hmult(ct, ct, keys.relin))
+    dec = H.decode(oc, H.decrypt(oc, keys, out), scale * scale / moduli[L - 1])
+    assert np.abs(dec - x * x).max() < 1e-6
+
+
+def test_CKKSEncryptRotateDecrypt_small():
+    """Mirror of tests/seal/evaluator.cpp:3100: rotate_vector by k shifts slots left by k."""
+    log_n = 12
+    moduli = O.coeff_modulus_create(1 << log_n, [51, 46, 46, 51])
+    oc = O.Context(log_n, moduli)
+    eng = mhe.Engine(log_n, moduli)
+    keys = H.keygen(oc, seed=5, hw=64)
+    L, scale = 3, 2.0 ** 40
+    x = np.random.default_rng(3).uniform(-1, 1, size=(1 << log_n) // 2)
+    ct = H.encrypt(oc, keys, H.encode(oc, x, scale, L), L)
+    for step in (1, 7, -2):
+        elt = mhe.galois_elt_from_step(log_n, step)
+        gk = H.galois_key(oc, keys, elt)
+        out = mhe.Engine.to_host(eng.apply_galois(eng.to_device(ct), elt, eng.to_device(gk)))
+        dec = H.decode(oc, H.decrypt(oc, keys, out), scale)
+        assert np.abs(dec - np.roll(x, -step)).max() < 1e-5
+
+
+# ------------------------------------------------------------------- full size (C2)
+@pytest.mark.slow
+def test_hmult_c2_full_bit_exact(c2):
+    """Config 2 workload (N=2^16, 44 data limbs + special): GPU HMult is
+    bit-identical to the oracle on uniform residues and a random relin key."""
+    ch = c2
+    L = ch.K - 1
+    key = ch.rand_key()
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
+    want = ch.oc.hmult(a, b, key)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.slow
+def test_rotate_c2_full_bit_exact(c2):
+    ch = c2
+    L = ch.K - 1
+    key = ch.rand_key()
+    ct = ch.rand(2, L, ch.n)
+    elt = mhe.galois_elt_from_step(16, 5)
+    got = ch.down(ch.eng.apply_galois(ch.up(ct), elt, ch.up(key)))
+    assert np.array_equal(got, ch.oc.apply_galois(ct, elt, key))
+
+
+@pytest.mark.slow
+def test_ntt_roundtrip_c2_all_limbs(c2):
+    """Size-independent property at full size: INTT(NTT(x)) == x for all 45 limbs, 2 polys."""
+    ch = c2
+    x = ch.rand(2, ch.K, ch.n)
+    t = ch.up(x)
+    ch.eng.ntt_forward(t)  # inverse inputs must be < 2q (dwthandler.h:202-233), as in SEAL
+    ch.eng.ntt_inverse(t)
+    assert np.array_equal(ch.down(t), x)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("bits", [RESNET_BITS, GPT2_BITS], ids=["resnet31", "gpt2_60bit_special"])
+def test_hmult_reference_chains(bits):
+    """The ResNet (31+1) and GPT-2 (36+1, 60-bit special) chains at N=2^16, at a reduced
+    level (8 limbs) so the oracle stays in seconds; the key is the full key-level layout."""
+    ch = Chain(16, bits, seed=9)
+    L = 8
+    key = ch.rand_key()
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
+    assert np.array_equal(got, ch.oc.hmult(a, b, key))
