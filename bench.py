@@ -12,6 +12,7 @@ Prints one JSON line (rank 0).  The cpu_baseline leg times the repo's CPU restat
 reference algorithm (oracle/, "port") on the host cores of the same box.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -70,6 +71,23 @@ def cpu_baseline(moduli, L, threads, seconds_hint):
     }
 
 
+def broadcast_key(key, src=0):
+    """One-time evaluation-key broadcast from `src` to every rank (RCCL over xGMI on the GPU
+    box; any backend works).  No-op on a single process."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.broadcast(key, src=src)
+    return key
+
+
+def max_over_ranks(seconds, device):
+    """Max of a per-rank elapsed time (the slowest GPU sets the job time)."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([seconds], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    return seconds
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,8 +124,7 @@ def main():
         g0 = torch.Generator(device=dev)
         g0.manual_seed(7)
         key.copy_(rand_residues((K - 1, 2, K, n), q_t, g0))
-    if world > 1:
-        dist.broadcast(key, src=0)
+    broadcast_key(key, src=0)
     B = args.batch
     a = rand_residues((B, 2, L, n), q_t[:L], gen)
     b = rand_residues((B, 2, L, n), q_t[:L], gen)
@@ -146,11 +163,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     gpu_s = ev0.elapsed_time(ev1) / 1e3
-    elapsed = max(wall, gpu_s)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(max(wall, gpu_s), dev)
+
+    # HBM traffic per HMult from the committed PMC passes of the same workload (rocprofv3
+    # FETCH_SIZE/WRITE_SIZE, gfx950-corrected; scripts/gpu_round.sh + scripts/traffic.py)
+    traffic, traffic_src = None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json"))):
+        try:
+            t = json.load(open(f))
+            if t.get("limbs", L) == L:
+                traffic, traffic_src = t["hbm_bytes_per_hmult"], os.path.relpath(f, ROOT)
+        except (OSError, ValueError, KeyError):
+            pass
 
     hmults_per_gpu = B * args.steps
     value = world * hmults_per_gpu / elapsed
@@ -183,7 +207,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per HMult (L2-miss fabric reads x2 + writes, PMC)",
+            "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": hmult_bytes(L),
             "avg_launch_us": round(per_hmult_s * 1e6, 2),
         },

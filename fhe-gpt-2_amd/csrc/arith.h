@@ -30,15 +30,68 @@ struct PrimeDev
     u64 last_wq;
 };
 
+// 64-bit products built only from v_mad_u64_u32 (32x32+64 -> 64), which gfx950 issues at
+// half rate.  The default lowering of u64 '*' and __umul64hi uses v_mul_lo_u32 / v_mul_hi_u32,
+// which are quarter rate (measured: scripts/ubench_valu.hip, DESIGN.md "Arithmetic"), and
+// LLVM re-forms a wide multiply from any schoolbook expansion written in C.  So the single
+// instruction is pinned with inline asm; the carry-out goes to a scratch SGPR pair that is
+// never read, and operand/pair assembly stays with the compiler.
+__device__ __forceinline__ u64 mad32(u32 a, u32 b, u64 c)
+{
+    u64 d, sc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(sc) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+__device__ __forceinline__ u64 mul32(u32 a, u32 b)
+{
+    u64 d, sc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(sc) : "v"(a), "v"(b));
+    return d;
+}
+
+// floor(a * b / 2^64), exact: 4 v_mad_u64_u32 (b is the possibly-uniform operand).
 __device__ __forceinline__ u64 mulhi64(u64 a, u64 b)
 {
-    return __umul64hi(a, b);
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    const u64 p00 = mul32(b0, a0);
+    const u64 p01 = mad32(b1, a0, p00 >> 32);
+    const u64 p10 = mad32(b0, a1, (u32)p01);
+    return mad32(b1, a1, (p01 >> 32) + (p10 >> 32));
+}
+
+// a * b mod 2^64: 3 v_mad_u64_u32 (the cross terms only feed the high word, so their
+// addends may carry garbage above bit 31).
+__device__ __forceinline__ u64 mullo64(u64 a, u64 b)
+{
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    const u32 cross = (u32)mad32(b0, a1, mul32(b1, a0));
+    return mad32(b0, a0, (u64)cross << 32);
+}
+
+// full 128-bit product (lo, hi): 4 v_mad_u64_u32.
+__device__ __forceinline__ void mul128(u64 a, u64 b, u64 &lo, u64 &hi)
+{
+    const u32 a0 = (u32)a, a1 = (u32)(a >> 32), b0 = (u32)b, b1 = (u32)(b >> 32);
+    const u64 p00 = mul32(a0, b0);
+    const u64 p01 = mad32(a0, b1, p00 >> 32);
+    const u64 p10 = mad32(a1, b0, (u32)p01);
+    lo = ((u64)(u32)p10 << 32) | (u32)p00;
+    hi = mad32(a1, b1, (p01 >> 32) + (p10 >> 32));
 }
 
 // multiply_uint_mod_lazy: x * w mod q in [0, 2q) for any 64-bit x.
 __device__ __forceinline__ u64 mul_shoup_lazy(u64 x, u64 w, u64 wq, u64 q)
 {
-    return w * x - mulhi64(x, wq) * q;
+    const u64 h = mulhi64(x, wq);
+    const u64 nq = 0 - q; // w x - h q = w x + h (2^64 - q) (mod 2^64)
+    const u32 x0 = (u32)x, x1 = (u32)(x >> 32), w0 = (u32)w, w1 = (u32)(w >> 32);
+    const u32 h0 = (u32)h, h1 = (u32)(h >> 32), n0 = (u32)nq, n1 = (u32)(nq >> 32);
+    u64 c = mul32(w0, x1);
+    c = mad32(w1, x0, c);
+    c = mad32(n1, h0, c);
+    c = mad32(n0, h1, c); // low word = cross terms of both products (mod 2^32)
+    return mad32(w0, x0, mul32(n0, h0)) + ((u64)(u32)c << 32);
 }
 
 __device__ __forceinline__ u64 csub(u64 x, u64 m)
@@ -55,26 +108,30 @@ __device__ __forceinline__ u64 mul_shoup(u64 x, u64 w, u64 wq, u64 q)
 __device__ __forceinline__ u64 barrett128(u64 lo, u64 hi, const PrimeDev &p)
 {
     u64 carry = mulhi64(lo, p.r0);
-    u64 t2lo = lo * p.r1, t2hi = mulhi64(lo, p.r1);
+    u64 t2lo, t2hi;
+    mul128(lo, p.r1, t2lo, t2hi);
     u64 tmp1 = t2lo + carry;
     u64 tmp3 = t2hi + (tmp1 < carry);
-    u64 u2lo = hi * p.r0, u2hi = mulhi64(hi, p.r0);
+    u64 u2lo, u2hi;
+    mul128(hi, p.r0, u2lo, u2hi);
     u64 s = tmp1 + u2lo;
     carry = u2hi + (s < u2lo);
-    tmp1 = hi * p.r1 + tmp3 + carry;
-    return csub(lo - tmp1 * p.q, p.q);
+    tmp1 = mullo64(hi, p.r1) + tmp3 + carry;
+    return csub(lo - mullo64(tmp1, p.q), p.q);
 }
 
 // barrett_reduce_64 (util/uintarithsmallmod.h:206-224).
 __device__ __forceinline__ u64 barrett64(u64 x, const PrimeDev &p)
 {
-    return csub(x - mulhi64(x, p.r1) * p.q, p.q);
+    return csub(x - mullo64(mulhi64(x, p.r1), p.q), p.q);
 }
 
 // multiply_uint_mod (util/uintarithsmallmod.h:230-242).
 __device__ __forceinline__ u64 mulmod(u64 a, u64 b, const PrimeDev &p)
 {
-    return barrett128(a * b, mulhi64(a, b), p);
+    u64 lo, hi;
+    mul128(a, b, lo, hi);
+    return barrett128(lo, hi, p);
 }
 
 __device__ __forceinline__ u64 addmod(u64 a, u64 b, u64 q)
@@ -95,7 +152,8 @@ struct Acc128
 
 __device__ __forceinline__ void mac128(Acc128 &acc, u64 a, u64 b)
 {
-    u64 plo = a * b, phi = mulhi64(a, b);
+    u64 plo, phi;
+    mul128(a, b, plo, phi);
     u64 s = acc.lo + plo;
     acc.hi += phi + (s < plo);
     acc.lo = s;

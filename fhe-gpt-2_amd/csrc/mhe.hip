@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -183,6 +184,7 @@ struct mhe_ctx
     Tw *tw = nullptr;
     Tw *itw = nullptr;
     Tw *invq = nullptr;
+    int ks_fused = 0; // MHE_KS_FUSED=1 selects the fused row-pass + key-MAC kernel
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };
@@ -197,7 +199,7 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out)
         w.base = nullptr;
         const size_t n = c->n, L = limbs;
         const size_t Lc = L < 3 ? 3 : L;
-        size_t words = Lc * n + (L + 1) * L * n + 2 * (L + 1) * n + L * n + 3 * L * n;
+        size_t words = Lc * n + (L + 1) * L * n + 4 * 2 * (L + 1) * n + L * n + 3 * L * n;
         HIP_TRY(hipSetDevice(c->device));
         if (hipMalloc(&w.base, words * sizeof(u64)) != hipSuccess)
         {
@@ -207,7 +209,7 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out)
         w.coeff = w.base;
         w.modup = w.coeff + Lc * n;
         w.acc = w.modup + (L + 1) * L * n;
-        w.tmp = w.acc + 2 * (L + 1) * n;
+        w.tmp = w.acc + 4 * 2 * (L + 1) * n; // acc holds up to 4 digit-group partials
         w.ct3 = w.tmp + L * n;
         w.max_limbs = limbs;
     }
@@ -807,15 +809,22 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
         j.mode = 1;
         inv_col(j, log_n, L, st);
     }
-    // 2. ModUp: lift digit J to prime I, NTT (evaluator.cpp:2386-2408)
+    // 2. ModUp: lift digit J to prime I and run the column pass of its NTT
+    //    (evaluator.cpp:2386-2408); I == J jobs are skipped.
     {
         JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n };
         fwd_col(j, log_n, (L + 1) * L, st);
+    }
+    // 3. finish the NTTs and take the inner products with the key (evaluator.cpp:2410-2463)
+    if (c->ks_fused)
+    {
+        // row pass fused with the key MAC: digits never leave registers (experimental)
+        ks_row_mac(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, st);
+    }
+    else
+    {
         JobModUpRow r2{ w->modup, c->primes, c->tw, L, c->K, log_n };
         fwd_row(r2, log_n, (L + 1) * L, st);
-    }
-    // 3. inner products with the key (evaluator.cpp:2410-2463)
-    {
         dim3 grid((unsigned)(n / 512), L + 1);
         hipLaunchKernelGGL(k_ks_mac, grid, dim3(256), 0, st, w->modup, target, key, w->acc, c->primes, L, c->K,
                            key_limbs, log_n);
@@ -933,6 +942,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     c->n = n;
     c->K = count;
     c->q.assign(moduli, moduli + count);
+    if (const char *f = getenv("MHE_KS_FUSED")) c->ks_fused = atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);
     for (int k = 0; k < count; k++)

@@ -292,3 +292,193 @@ template <class Job> static inline void fwd_col(const Job &j, int log_n, int job
 template <class Job> static inline void fwd_row(const Job &j, int log_n, int jobs, hipStream_t st) { launch_row<FWD_ROW>(j, log_n, jobs, st); }
 template <class Job> static inline void inv_row(const Job &j, int log_n, int jobs, hipStream_t st) { launch_row<INV_ROW>(j, log_n, jobs, st); }
 template <class Job> static inline void inv_col(const Job &j, int log_n, int jobs, hipStream_t st) { launch_col<INV_COL>(j, log_n, jobs, st); }
+
+// ============================================================================
+// Fused key-switching ModUp row pass + key inner product (evaluator.cpp:2386-2463).
+//
+// One workgroup owns output prime I (blockIdx.y; I == L is the special prime) and S blocks of
+// R = 2^LOGR coefficients.  For every digit J it loads the column-pass output of (I, J)
+// (or, for I == J, the input target limb, already in NTT form), finishes the forward NTT in
+// registers, and multiply-accumulates with key[J][0][I] and key[J][1][I] into 128-bit
+// accumulators.  The NTT'd digits never touch HBM, and each key residue is read once.
+// 8 residues per lane keep the 2 x 8 x 128-bit accumulators at 64 VGPRs; the 2^LOGR-point
+// row transform is then run as 3-bit phases (in-register radix-8) with LDS transposes.
+template <int LOGR>
+struct RowMacShape
+{
+    static constexpr int R = 1 << LOGR;
+    static constexpr int E = 8;
+    static constexpr int TPS = R / E;      // lanes per block
+    static constexpr int S = 256 / TPS;    // blocks per workgroup
+    static constexpr int LD = R + R / 32;  // padded row: one extra dword pair every 32 residues
+};
+
+__device__ __forceinline__ u32 lds_pad(u32 r)
+{
+    return r + (r >> 5);
+}
+
+// Residue index held in slot e by lane t for a layout whose 3 in-lane bits start at b_lo.
+__device__ __forceinline__ u32 lay(u32 t, int e, int b_lo)
+{
+    return ((t >> b_lo) << (b_lo + 3)) | ((u32)e << b_lo) | (t & ((1u << b_lo) - 1));
+}
+
+// Forward stages [s0, s1) of the local 2^LOGR transform on a layout with in-lane bits at b_lo.
+template <int LOGR>
+__device__ __forceinline__ void row_stages(u64 (&v)[8], u32 t, int b_lo, int s0, int s1, u32 rb, const Tw *tw,
+                                           u64 q, u64 q2)
+{
+#pragma unroll
+    for (int s = s0; s < s1; s++)
+    {
+        const int gap = 1 << (LOGR - 1 - s - b_lo); // in slot units
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+            if (!(e & gap)) fwd_bfly(v[e], v[e + gap], tw[(rb << s) + (lay(t, e, b_lo) >> (LOGR - s))], q, q2);
+    }
+}
+
+template <int LOGR>
+__global__ __launch_bounds__(256) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass output
+                                                    const u64 *__restrict__ target, // [L][n] NTT form
+                                                    const u64 *__restrict__ key,    // [digits][2][key_limbs][n]
+                                                    u64 *__restrict__ acc,          // [G][2][L+1][n]
+                                                    const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all,
+                                                    int L, int K, int key_limbs, int log_n)
+{
+    // digit group blockIdx.z of gridDim.z: J in [j0, j1); partial sums go to acc[z]
+    const int G = gridDim.z, g = blockIdx.z;
+    const int j0 = (L * g) / G, j1 = (L * (g + 1)) / G;
+    using SH = RowMacShape<LOGR>;
+    constexpr int TPS = SH::TPS, S = SH::S, LD = SH::LD;
+    constexpr int B_A = LOGR - 3;               // phase A in-lane bits
+    constexpr int B_B = LOGR >= 6 ? LOGR - 6 : 0; // phase B
+    __shared__ u64 lds[2][S * LD];
+    const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
+    const u32 b = blockIdx.x * S + sl;
+    const u32 base = b << LOGR;
+    const u32 rb = (1u << (log_n - LOGR)) + b;
+    const int I = blockIdx.y;
+    const int pi = (I == L) ? K - 1 : I;
+    const int ki = (I == L) ? key_limbs - 1 : I;
+    const PrimeDev p = primes[pi];
+    const Tw *tw = tw_all + ((size_t)pi << log_n);
+    const size_t n = (size_t)1 << log_n;
+    const size_t kstride = (size_t)key_limbs * n;
+    u64 *l0 = &lds[0][sl * LD], *l1 = &lds[1][sl * LD];
+
+    Acc128 a0[8], a1[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) a0[e] = a1[e] = Acc128{ 0, 0 };
+
+    for (int J = j0; J < j1; J++)
+    {
+        u64 v[8];
+        if (J == I)
+        {
+            // reuse the RNS-NTT form of the input (evaluator.cpp:2380-2384)
+            const u64 *src = target + (size_t)J * n + base;
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = src[lay(t, e, B_A)];
+        }
+        else
+        {
+            const u64 *src = inter + ((size_t)I * L + J) * n + base;
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = src[lay(t, e, B_A)];
+            row_stages<LOGR>(v, t, B_A, 0, 3, rb, tw, p.q, p.two_q);
+#pragma unroll
+            for (int e = 0; e < 8; e++) l0[lds_pad(lay(t, e, B_A))] = v[e];
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = l0[lds_pad(lay(t, e, B_B))];
+            row_stages<LOGR>(v, t, B_B, 3, LOGR < 6 ? LOGR : 6, rb, tw, p.q, p.two_q);
+            if (LOGR > 6)
+            {
+#pragma unroll
+                for (int e = 0; e < 8; e++) l1[lds_pad(lay(t, e, B_B))] = v[e];
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = l1[lds_pad(lay(t, e, 0))];
+                row_stages<LOGR>(v, t, 0, 6, LOGR, rb, tw, p.q, p.two_q);
+            }
+            // back to the coalesced layout for the key stream; canonical digits keep the
+            // 128-bit sums exact for any digit count below 2^8
+            u64 *lo = (LOGR > 6) ? l0 : l1;
+            const int b_last = (LOGR > 6) ? 0 : B_B;
+#pragma unroll
+            for (int e = 0; e < 8; e++) lo[lds_pad(lay(t, e, b_last))] = csub(csub(v[e], p.two_q), p.q);
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = lo[lds_pad(lay(t, e, B_A))];
+        }
+        const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n + base;
+        const u64 *k1 = k0 + kstride;
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+        {
+            const u32 r = lay(t, e, B_A);
+            mac128(a0[e], v[e], k0[r]);
+            mac128(a1[e], v[e], k1[r]);
+        }
+    }
+    u64 *o0 = acc + (size_t)(2 * g * (L + 1) + I) * n + base;
+    u64 *o1 = o0 + (size_t)(L + 1) * n;
+#pragma unroll
+    for (int e = 0; e < 8; e++)
+    {
+        const u32 r = lay(t, e, B_A);
+        o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
+        o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
+    }
+}
+
+// Sum the G partial accumulators: acc[0] += acc[1..G-1] mod q (prime of each limb).
+__global__ void k_acc_reduce(u64 *acc, const PrimeDev *primes, int L, int K, int G, int log_n)
+{
+    const size_t n = (size_t)1 << log_n;
+    const size_t per = (size_t)2 * (L + 1) * n;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= per) return;
+    const int limb = (int)((i >> log_n) % (L + 1));
+    const u64 q = primes[limb == L ? K - 1 : limb].q;
+    u64 s = acc[i];
+    for (int g = 1; g < G; g++) s = addmod(s, acc[g * per + i], q);
+    acc[i] = s;
+}
+
+// Digit groups G: enough workgroups to hide HBM latency (each one walks L/G digits).
+static inline int ks_groups(int L)
+{
+    return L >= 24 ? 4 : (L >= 8 ? 2 : 1);
+}
+
+static inline void ks_row_mac(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
+                              const Tw *tw, int L, int K, int key_limbs, int log_n, hipStream_t st)
+{
+    const int logr = log_n / 2;
+    const int blocks = 1 << (log_n - logr);
+    const int G = ks_groups(L);
+    switch (logr)
+    {
+    case 6:
+        hipLaunchKernelGGL(k_ks_row_mac<6>, dim3(blocks / RowMacShape<6>::S, L + 1, G), dim3(256), 0, st, inter,
+                           target, key, acc, primes, tw, L, K, key_limbs, log_n);
+        break;
+    case 7:
+        hipLaunchKernelGGL(k_ks_row_mac<7>, dim3(blocks / RowMacShape<7>::S, L + 1, G), dim3(256), 0, st, inter,
+                           target, key, acc, primes, tw, L, K, key_limbs, log_n);
+        break;
+    case 8:
+        hipLaunchKernelGGL(k_ks_row_mac<8>, dim3(blocks / RowMacShape<8>::S, L + 1, G), dim3(256), 0, st, inter,
+                           target, key, acc, primes, tw, L, K, key_limbs, log_n);
+        break;
+    }
+    if (G > 1)
+    {
+        const size_t per = (size_t)2 * (L + 1) << log_n;
+        hipLaunchKernelGGL(k_acc_reduce, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, st, acc, primes, L, K, G,
+                           log_n);
+    }
+}

@@ -341,3 +341,40 @@ def test_hmult_reference_chains(bits):
     a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
     got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
     assert np.array_equal(got, ch.oc.hmult(a, b, key))
+
+
+# ------------------------------------------------------ fused key-switch path (MHE_KS_FUSED)
+@pytest.fixture(scope="module")
+def fused_engines():
+    import os
+
+    old = os.environ.get("MHE_KS_FUSED")
+    os.environ["MHE_KS_FUSED"] = "1"
+    try:
+        small_ch = Chain(12, SMALL_BITS, seed=21)
+        full_ch = Chain(16, SMALL_BITS + [51] * 8, seed=22)
+    finally:
+        if old is None:
+            del os.environ["MHE_KS_FUSED"]
+        else:
+            os.environ["MHE_KS_FUSED"] = old
+    return small_ch, full_ch
+
+
+@pytest.mark.parametrize("L", [1, 3, 7])
+def test_switch_key_fused(fused_engines, L):
+    ch = fused_engines[0]
+    key = ch.rand_key()
+    ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+    got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
+    assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
+
+
+@pytest.mark.slow
+def test_hmult_fused_n16(fused_engines):
+    ch = fused_engines[1]
+    L = ch.K - 1
+    key = ch.rand_key()
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
+    assert np.array_equal(got, ch.oc.hmult(a, b, key))
