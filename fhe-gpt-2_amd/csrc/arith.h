@@ -16,6 +16,7 @@
 
 typedef uint64_t u64;
 typedef uint32_t u32;
+typedef ulonglong2 Tw; // (w, floor(w 2^64 / q)): a Shoup operand
 
 // Per-prime constants, one entry per key-level prime, resident in HBM.
 struct PrimeDev
@@ -91,7 +92,56 @@ __device__ __forceinline__ u64 mul_shoup_lazy(u64 x, u64 w, u64 wq, u64 q)
     c = mad32(w1, x0, c);
     c = mad32(n1, h0, c);
     c = mad32(n0, h1, c); // low word = cross terms of both products (mod 2^32)
-    return mad32(w0, x0, mul32(n0, h0)) + ((u64)(u32)c << 32);
+    return mad32(w0, x0, mul32(n0, h0)) + (c << 32); // one v_lshl_add_u64, garbage shifts out
+}
+
+// NB independent Shoup lazy products x[i] * w[i] (mod q, in [0, 2q)), computed step by step
+// across the batch.  The schedule is written out explicitly: hipcc does not know the latency
+// of the inline-asm v_mad_u64_u32, so it would otherwise emit one product's dependent chain
+// back to back (an s_nop per link) instead of interleaving independent products.
+template <int NB>
+__device__ __forceinline__ void mul_shoup_lazy_batch(const u64 (&x)[NB], const Tw *const (&w)[NB], u64 q,
+                                                     u64 (&out)[NB])
+{
+    const u64 nq = 0 - q;
+    const u32 n0 = (u32)nq, n1 = (u32)(nq >> 32);
+    u32 x0[NB], x1[NB], w0[NB], w1[NB], v0[NB], v1[NB];
+    u64 t[NB], u[NB], h[NB], c[NB];
+#pragma unroll
+    for (int i = 0; i < NB; i++)
+    {
+        const Tw tw = *w[i];
+        x0[i] = (u32)x[i];
+        x1[i] = (u32)(x[i] >> 32);
+        w0[i] = (u32)tw.x;
+        w1[i] = (u32)(tw.x >> 32);
+        v0[i] = (u32)tw.y;
+        v1[i] = (u32)(tw.y >> 32);
+    }
+    // h = floor(x * w' / 2^64)
+#pragma unroll
+    for (int i = 0; i < NB; i++) t[i] = mul32(v0[i], x0[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) t[i] = mad32(v1[i], x0[i], t[i] >> 32);
+#pragma unroll
+    for (int i = 0; i < NB; i++) u[i] = mad32(v0[i], x1[i], (u32)t[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) h[i] = mad32(v1[i], x1[i], (t[i] >> 32) + (u[i] >> 32));
+    // w x - h q (mod 2^64): cross terms of both products in one chain, then the low parts
+#pragma unroll
+    for (int i = 0; i < NB; i++) c[i] = mul32(w0[i], x1[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) c[i] = mad32(w1[i], x0[i], c[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) c[i] = mad32(n1, (u32)h[i], c[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) c[i] = mad32(n0, (u32)(h[i] >> 32), c[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) t[i] = mul32(n0, (u32)h[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) t[i] = mad32(w0[i], x0[i], t[i]);
+#pragma unroll
+    for (int i = 0; i < NB; i++) out[i] = t[i] + (c[i] << 32);
 }
 
 __device__ __forceinline__ u64 csub(u64 x, u64 m)

@@ -184,7 +184,8 @@ struct mhe_ctx
     Tw *tw = nullptr;
     Tw *itw = nullptr;
     Tw *invq = nullptr;
-    int ks_fused = 0; // MHE_KS_FUSED=1 selects the fused row-pass + key-MAC kernel
+    int ks_fused = 1; // fused row-pass + key-MAC kernel (MHE_KS_FUSED=0: separate row pass + MAC)
+    int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };
@@ -280,10 +281,10 @@ struct JobInvPlain : JobPlain
 struct JobModUpCol
 {
     const u64 *coeff; // [L][n]
-    u64 *modup;       // [L+1][L][n]
+    u64 *modup;       // [chunk][L][n] for output primes I0 .. I0+chunk-1
     const PrimeDev *primes;
     const Tw *tw;
-    int L, K, log_n;
+    int L, K, log_n, I0;
     struct View
     {
         const u64 *src;
@@ -301,7 +302,7 @@ struct JobModUpCol
     };
     __device__ View view(int y) const
     {
-        const int I = y / L, J = y % L;
+        const int I = I0 + y / L, J = y % L;
         const int pi = (I == L) ? K - 1 : I;
         View v;
         v.src = coeff + ((size_t)J << log_n);
@@ -319,7 +320,7 @@ struct JobModUpRow
     u64 *modup;
     const PrimeDev *primes;
     const Tw *tw;
-    int L, K, log_n;
+    int L, K, log_n, I0;
     struct View
     {
         u64 *buf;
@@ -332,7 +333,7 @@ struct JobModUpRow
     };
     __device__ View view(int y) const
     {
-        const int I = y / L, J = y % L;
+        const int I = I0 + y / L, J = y % L;
         const int pi = (I == L) ? K - 1 : I;
         return View{ modup + ((size_t)y << log_n), primes[pi], tw + ((size_t)pi << log_n), I == J };
     }
@@ -690,10 +691,10 @@ __global__ void k_tensor(const u64 *a, const u64 *b, u64 *out, const PrimeDev *p
 // (modup[I][J]) or, for I == J, the input target limb itself.  128-bit accumulation with a
 // single final Barrett reduction (digits are canonical so < 2^8 terms never overflow).
 __global__ __launch_bounds__(256) void k_ks_mac(const u64 *modup, const u64 *target, const u64 *key, u64 *acc,
-                                                const PrimeDev *primes, int L, int K, int key_limbs, int log_n)
+                                                const PrimeDev *primes, int L, int K, int key_limbs, int log_n, int I0)
 {
     const u32 i = (blockIdx.x * 256 + threadIdx.x) * 2;
-    const int I = blockIdx.y;
+    const int I = I0 + blockIdx.y;
     const int pi = (I == L) ? K - 1 : I;
     const int ki = (I == L) ? key_limbs - 1 : I;
     const size_t n = (size_t)1 << log_n;
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(256) void k_ks_mac(const u64 *modup, const u64 *tar
     const size_t kstride = (size_t)key_limbs * n;
     for (int J = 0; J < L; J++)
     {
-        const u64 *d = (I == J) ? target + (size_t)J * n : modup + ((size_t)I * L + J) * n;
+        const u64 *d = (I == J) ? target + (size_t)J * n : modup + ((size_t)(I - I0) * L + J) * n;
         ulonglong2 x = *(const ulonglong2 *)(d + i);
         const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
         ulonglong2 y0 = *(const ulonglong2 *)(k0 + i);
@@ -809,25 +810,34 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
         j.mode = 1;
         inv_col(j, log_n, L, st);
     }
-    // 2. ModUp: lift digit J to prime I and run the column pass of its NTT
-    //    (evaluator.cpp:2386-2408); I == J jobs are skipped.
-    {
-        JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n };
-        fwd_col(j, log_n, (L + 1) * L, st);
-    }
-    // 3. finish the NTTs and take the inner products with the key (evaluator.cpp:2410-2463)
     if (c->ks_fused)
     {
-        // row pass fused with the key MAC: digits never leave registers (experimental)
+        // 2+3 (experimental): column pass for all output primes, then the row pass fused
+        // with the key MAC so NTT'd digits never leave registers.
+        JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, 0 };
+        fwd_col(j, log_n, (L + 1) * L, st);
         ks_row_mac(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, st);
     }
     else
     {
-        JobModUpRow r2{ w->modup, c->primes, c->tw, L, c->K, log_n };
-        fwd_row(r2, log_n, (L + 1) * L, st);
-        dim3 grid((unsigned)(n / 512), L + 1);
-        hipLaunchKernelGGL(k_ks_mac, grid, dim3(256), 0, st, w->modup, target, key, w->acc, c->primes, L, c->K,
-                           key_limbs, log_n);
+        // 2+3. ModUp + key inner products in chunks of output primes: lift digit J to prime
+        //      I and NTT it (evaluator.cpp:2386-2408; I == J skipped), then
+        //      acc[k][I] = sum_J digit * key[J][k][I] (evaluator.cpp:2410-2463).  The chunk
+        //      scratch is reused, so the column-pass output and the NTT'd digits of a chunk
+        //      stay in the Infinity Cache between the three kernels instead of round-tripping
+        //      through HBM; only the key streams from HBM.
+        const int P = c->ks_chunk > 0 ? c->ks_chunk : L + 1;
+        for (int I0 = 0; I0 <= L; I0 += P)
+        {
+            const int cnt = (I0 + P <= L + 1) ? P : L + 1 - I0;
+            JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
+            fwd_col(j, log_n, cnt * L, st);
+            JobModUpRow r2{ w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
+            fwd_row(r2, log_n, cnt * L, st);
+            dim3 grid((unsigned)(n / 512), cnt);
+            hipLaunchKernelGGL(k_ks_mac, grid, dim3(256), 0, st, w->modup, target, key, w->acc, c->primes, L, c->K,
+                               key_limbs, log_n, I0);
+        }
     }
     // 4. ModDown (evaluator.cpp:2466-2524): INTT_lazy of the special limbs, then fused
     //    lift + NTT + (c + 4q - t) * P^-1 + add.
@@ -943,6 +953,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     c->K = count;
     c->q.assign(moduli, moduli + count);
     if (const char *f = getenv("MHE_KS_FUSED")) c->ks_fused = atoi(f);
+    if (const char *f = getenv("MHE_KS_CHUNK")) c->ks_chunk = atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);
     for (int k = 0; k < count; k++)

@@ -22,7 +22,6 @@
 #pragma once
 #include "arith.h"
 
-typedef ulonglong2 Tw; // (w, floor(w 2^64 / q))
 
 // Forward Harvey butterfly (dwthandler.h:122-125 with ntt.h:34-65 arithmetic).
 __device__ __forceinline__ void fwd_bfly(u64 &x, u64 &y, const Tw w, u64 q, u64 q2)
@@ -47,6 +46,61 @@ __device__ __forceinline__ void inv_bfly_last(u64 &x, u64 &y, const PrimeDev &p)
     u64 u = csub(x, p.two_q), v = y;
     x = mul_shoup_lazy(csub(u + v, p.two_q), p.ninv, p.ninv_q, p.q);
     y = mul_shoup_lazy(u + p.two_q - v, p.last_w, p.last_wq, p.q);
+}
+
+// One forward stage on the E residues of a lane: butterflies (e, e+gap) for every e with the
+// gap bit clear, twiddle pointer tw_of(e).  The E/2 twiddle products are computed as a batch.
+template <int E, class TwOf>
+__device__ __forceinline__ void fwd_stage(u64 (&v)[E], int gap, TwOf tw_of, u64 q, u64 q2)
+{
+    constexpr int NB = E / 2;
+    u64 y[NB], m[NB];
+    const Tw *w[NB];
+    int k = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (!(e & gap))
+        {
+            y[k] = v[e + gap];
+            w[k] = tw_of(e);
+            k++;
+        }
+    mul_shoup_lazy_batch<NB>(y, w, q, m);
+    k = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (!(e & gap))
+        {
+            const u64 u = csub(v[e], q2);
+            v[e] = u + m[k];
+            v[e + gap] = u + q2 - m[k];
+            k++;
+        }
+}
+
+// One inverse (Gentleman-Sande) stage, batched like fwd_stage.
+template <int E, class TwOf>
+__device__ __forceinline__ void inv_stage(u64 (&v)[E], int gap, TwOf tw_of, u64 q, u64 q2)
+{
+    constexpr int NB = E / 2;
+    u64 y[NB], m[NB];
+    const Tw *w[NB];
+    int k = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (!(e & gap))
+        {
+            const u64 a = v[e], b = v[e + gap];
+            v[e] = csub(a + b, q2);
+            y[k] = a + q2 - b;
+            w[k] = tw_of(e);
+            k++;
+        }
+    mul_shoup_lazy_batch<NB>(y, w, q, m);
+    k = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (!(e & gap)) v[e + gap] = m[k++];
 }
 
 template <int LOGR, int LOGT>
@@ -80,12 +134,7 @@ __global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = V.load(c + ((u32)(t + TPS * e) << logC));
 #pragma unroll
     for (int s = 0; s < LOGE; s++)
-    {
-        const int gap = 1 << (LOGE - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) fwd_bfly(v[e], v[e + gap], tw[(1 << s) + (e >> (LOGE - s))], q, q2);
-    }
+        fwd_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(1 << s) + (e >> (LOGE - s))]; }, q, q2);
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
     __syncthreads();
@@ -93,12 +142,8 @@ __global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
     for (int s = LOGE; s < LOGR; s++)
-    {
-        const int gap = 1 << (LOGR - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) fwd_bfly(v[e], v[e + gap], tw[(1 << s) + ((E * t + e) >> (LOGR - s))], q, q2);
-    }
+        fwd_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(1 << s) + ((E * t + e) >> (LOGR - s))]; },
+                     q, q2);
 #pragma unroll
     for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), v[e]);
 }
@@ -123,12 +168,7 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = V.load(base + t + TPS * e);
 #pragma unroll
     for (int s = 0; s < LOGE; s++)
-    {
-        const int gap = 1 << (LOGE - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) fwd_bfly(v[e], v[e + gap], tw[(rb << s) + (e >> (LOGE - s))], q, q2);
-    }
+        fwd_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(rb << s) + (e >> (LOGE - s))]; }, q, q2);
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
     __syncthreads();
@@ -136,12 +176,8 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
     for (int s = LOGE; s < LOGR; s++)
-    {
-        const int gap = 1 << (LOGR - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) fwd_bfly(v[e], v[e + gap], tw[(rb << s) + ((E * t + e) >> (LOGR - s))], q, q2);
-    }
+        fwd_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(rb << s) + ((E * t + e) >> (LOGR - s))]; },
+                     q, q2);
     // transpose back so stores (and epilogue reads) are coalesced
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
@@ -173,12 +209,8 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
     for (int s = LOGR - 1; s >= LOGE; s--)
-    {
-        const int gap = 1 << (LOGR - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) inv_bfly(v[e], v[e + gap], tw[(rb << s) + ((E * t + e) >> (LOGR - s))], q, q2);
-    }
+        inv_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(rb << s) + ((E * t + e) >> (LOGR - s))]; },
+                     q, q2);
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
     __syncthreads();
@@ -186,12 +218,7 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + t + TPS * e];
 #pragma unroll
     for (int s = LOGE - 1; s >= 0; s--)
-    {
-        const int gap = 1 << (LOGE - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) inv_bfly(v[e], v[e + gap], tw[(rb << s) + (e >> (LOGE - s))], q, q2);
-    }
+        inv_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(rb << s) + (e >> (LOGE - s))]; }, q, q2);
 #pragma unroll
     for (int e = 0; e < E; e++) V.store(base + t + TPS * e, v[e]);
 }
@@ -215,12 +242,8 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = V.load(c + ((u32)(E * t + e) << logC));
 #pragma unroll
     for (int s = LOGR - 1; s >= LOGE; s--)
-    {
-        const int gap = 1 << (LOGR - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) inv_bfly(v[e], v[e + gap], tw[(1 << s) + ((E * t + e) >> (LOGR - s))], q, q2);
-    }
+        inv_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(1 << s) + ((E * t + e) >> (LOGR - s))]; },
+                     q, q2);
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
     __syncthreads();
@@ -228,12 +251,7 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + t + TPS * e];
 #pragma unroll
     for (int s = LOGE - 1; s >= 1; s--)
-    {
-        const int gap = 1 << (LOGE - 1 - s);
-#pragma unroll
-        for (int e = 0; e < E; e++)
-            if (!(e & gap)) inv_bfly(v[e], v[e + gap], tw[(1 << s) + (e >> (LOGE - s))], q, q2);
-    }
+        inv_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(1 << s) + (e >> (LOGE - s))]; }, q, q2);
     {
         constexpr int gap = E / 2;
 #pragma unroll
@@ -297,25 +315,33 @@ template <class Job> static inline void inv_col(const Job &j, int log_n, int job
 // Fused key-switching ModUp row pass + key inner product (evaluator.cpp:2386-2463).
 //
 // One workgroup owns output prime I (blockIdx.y; I == L is the special prime) and S blocks of
-// R = 2^LOGR coefficients.  For every digit J it loads the column-pass output of (I, J)
-// (or, for I == J, the input target limb, already in NTT form), finishes the forward NTT in
-// registers, and multiply-accumulates with key[J][0][I] and key[J][1][I] into 128-bit
-// accumulators.  The NTT'd digits never touch HBM, and each key residue is read once.
-// 8 residues per lane keep the 2 x 8 x 128-bit accumulators at 64 VGPRs; the 2^LOGR-point
-// row transform is then run as 3-bit phases (in-register radix-8) with LDS transposes.
+// R = 2^LOGR coefficients; blockIdx.z selects a range of digits J.  For every digit it takes
+// the column-pass output of (I, J) (or, for I == J, the input target limb, already in NTT
+// form), finishes the forward NTT in registers, and multiply-accumulates with key[J][0][I] and
+// key[J][1][I] into 128-bit accumulators.  NTT'd digits never touch HBM; each key residue is
+// read once.
+//   * 8 residues per lane keep the 2 x 8 x 128-bit accumulators at 64 VGPRs; the 2^LOGR-point
+//     row transform runs as radix-8 register phases with swizzled (conflict-free) LDS
+//     transposes.
+//   * The row-pass twiddles depend on (I, block) but not on J, so they are staged in LDS
+//     once per workgroup; no global load is left inside the digit loop except the digit and
+//     key streams, which are issued one digit (digits) / one NTT (key) ahead.
+//   * Barriers wait on LDS only (s_waitcnt lgkmcnt(0) + s_barrier): __syncthreads() would
+//     also drain vmcnt and serialise the prefetch (cdna_hip_programming.md §8).
 template <int LOGR>
 struct RowMacShape
 {
     static constexpr int R = 1 << LOGR;
     static constexpr int E = 8;
-    static constexpr int TPS = R / E;      // lanes per block
-    static constexpr int S = 256 / TPS;    // blocks per workgroup
-    static constexpr int LD = R + R / 32;  // padded row: one extra dword pair every 32 residues
+    static constexpr int TPS = R / E;     // lanes per block
+    static constexpr int S = 256 / TPS;   // blocks per workgroup
 };
 
-__device__ __forceinline__ u32 lds_pad(u32 r)
+// Bijective LDS index swizzle: conflict-free ds_write_b64 / ds_read_b64 for all three
+// transpose layouts (bank model of MI355X_MICROARCH.md §LDS; checked in scripts).
+__device__ __forceinline__ u32 swz(u32 r)
 {
-    return r + (r >> 5);
+    return r ^ ((r >> 3) & 3) ^ (((r >> 5) & 7) << 2);
 }
 
 // Residue index held in slot e by lane t for a layout whose 3 in-lane bits start at b_lo.
@@ -324,104 +350,138 @@ __device__ __forceinline__ u32 lay(u32 t, int e, int b_lo)
     return ((t >> b_lo) << (b_lo + 3)) | ((u32)e << b_lo) | (t & ((1u << b_lo) - 1));
 }
 
-// Forward stages [s0, s1) of the local 2^LOGR transform on a layout with in-lane bits at b_lo.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Forward stages [s0, s1) of the local 2^LOGR transform, twiddles from the block's LDS row
+// (entry (1 << s) + g holds tw[((2^k1 + b) << s) + g]).
 template <int LOGR>
-__device__ __forceinline__ void row_stages(u64 (&v)[8], u32 t, int b_lo, int s0, int s1, u32 rb, const Tw *tw,
-                                           u64 q, u64 q2)
+__device__ __forceinline__ void row_stages(u64 (&v)[8], u32 t, int b_lo, int s0, int s1, const Tw *twl, u64 q,
+                                           u64 q2)
 {
 #pragma unroll
     for (int s = s0; s < s1; s++)
-    {
-        const int gap = 1 << (LOGR - 1 - s - b_lo); // in slot units
-#pragma unroll
-        for (int e = 0; e < 8; e++)
-            if (!(e & gap)) fwd_bfly(v[e], v[e + gap], tw[(rb << s) + (lay(t, e, b_lo) >> (LOGR - s))], q, q2);
-    }
+        fwd_stage<8>(v, 1 << (LOGR - 1 - s - b_lo), // gap in slot units
+                     [&](int e) { return &twl[(1 << s) + (lay(t, e, b_lo) >> (LOGR - s))]; }, q, q2);
 }
 
 template <int LOGR>
-__global__ __launch_bounds__(256) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass output
-                                                    const u64 *__restrict__ target, // [L][n] NTT form
-                                                    const u64 *__restrict__ key,    // [digits][2][key_limbs][n]
-                                                    u64 *__restrict__ acc,          // [G][2][L+1][n]
-                                                    const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all,
-                                                    int L, int K, int key_limbs, int log_n)
+__global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass out
+                                                       const u64 *__restrict__ target, // [L][n] NTT form
+                                                       const u64 *__restrict__ key,    // [digits][2][key_limbs][n]
+                                                       u64 *__restrict__ acc,          // [G][2][L+1][n]
+                                                       const PrimeDev *__restrict__ primes,
+                                                       const Tw *__restrict__ tw_all, int L, int K, int key_limbs,
+                                                       int log_n)
 {
-    // digit group blockIdx.z of gridDim.z: J in [j0, j1); partial sums go to acc[z]
+    using SH = RowMacShape<LOGR>;
+    constexpr int R = SH::R, TPS = SH::TPS, S = SH::S;
+    constexpr int B_A = LOGR - 3, B_B = LOGR - 6;
+    __shared__ u64 xch[2][S * R];
+    __shared__ Tw twl[S * (R + 1)];
     const int G = gridDim.z, g = blockIdx.z;
     const int j0 = (L * g) / G, j1 = (L * (g + 1)) / G;
-    using SH = RowMacShape<LOGR>;
-    constexpr int TPS = SH::TPS, S = SH::S, LD = SH::LD;
-    constexpr int B_A = LOGR - 3;               // phase A in-lane bits
-    constexpr int B_B = LOGR >= 6 ? LOGR - 6 : 0; // phase B
-    __shared__ u64 lds[2][S * LD];
     const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
     const u32 b = blockIdx.x * S + sl;
     const u32 base = b << LOGR;
-    const u32 rb = (1u << (log_n - LOGR)) + b;
+    const u32 R1 = 1u << (log_n - LOGR);
     const int I = blockIdx.y;
     const int pi = (I == L) ? K - 1 : I;
     const int ki = (I == L) ? key_limbs - 1 : I;
     const PrimeDev p = primes[pi];
-    const Tw *tw = tw_all + ((size_t)pi << log_n);
     const size_t n = (size_t)1 << log_n;
     const size_t kstride = (size_t)key_limbs * n;
-    u64 *l0 = &lds[0][sl * LD], *l1 = &lds[1][sl * LD];
+
+    // stage this workgroup's row-pass twiddles (all digits share them)
+    {
+        const Tw *tw = tw_all + ((size_t)pi << log_n);
+        for (u32 idx = tid; idx < (u32)(S * R); idx += 256)
+        {
+            const u32 blk = idx / R, k = idx % R;
+            if (k == 0) continue;
+            const int s = 31 - __builtin_clz(k);
+            twl[blk * (R + 1) + k] = tw[(((R1 + blockIdx.x * S + blk) << s)) + (k - (1u << s))];
+        }
+    }
+    const Tw *mytw = &twl[sl * (R + 1)];
+    u64 *x0 = &xch[0][sl * R], *x1 = &xch[1][sl * R];
 
     Acc128 a0[8], a1[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) a0[e] = a1[e] = Acc128{ 0, 0 };
 
+    auto digit_src = [&](int J) -> const u64 * {
+        return (J == I) ? target + (size_t)J * n + base : inter + ((size_t)I * L + J) * n + base;
+    };
+    u64 vin[8];
+    {
+        const u64 *src = digit_src(j0);
+#pragma unroll
+        for (int e = 0; e < 8; e++) vin[e] = src[lay(t, e, B_A)];
+    }
+    lds_barrier(); // twiddles visible
+
     for (int J = j0; J < j1; J++)
     {
-        u64 v[8];
-        if (J == I)
-        {
-            // reuse the RNS-NTT form of the input (evaluator.cpp:2380-2384)
-            const u64 *src = target + (size_t)J * n + base;
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = src[lay(t, e, B_A)];
-        }
-        else
-        {
-            const u64 *src = inter + ((size_t)I * L + J) * n + base;
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = src[lay(t, e, B_A)];
-            row_stages<LOGR>(v, t, B_A, 0, 3, rb, tw, p.q, p.two_q);
-#pragma unroll
-            for (int e = 0; e < 8; e++) l0[lds_pad(lay(t, e, B_A))] = v[e];
-            __syncthreads();
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = l0[lds_pad(lay(t, e, B_B))];
-            row_stages<LOGR>(v, t, B_B, 3, LOGR < 6 ? LOGR : 6, rb, tw, p.q, p.two_q);
-            if (LOGR > 6)
-            {
-#pragma unroll
-                for (int e = 0; e < 8; e++) l1[lds_pad(lay(t, e, B_B))] = v[e];
-                __syncthreads();
-#pragma unroll
-                for (int e = 0; e < 8; e++) v[e] = l1[lds_pad(lay(t, e, 0))];
-                row_stages<LOGR>(v, t, 0, 6, LOGR, rb, tw, p.q, p.two_q);
-            }
-            // back to the coalesced layout for the key stream; canonical digits keep the
-            // 128-bit sums exact for any digit count below 2^8
-            u64 *lo = (LOGR > 6) ? l0 : l1;
-            const int b_last = (LOGR > 6) ? 0 : B_B;
-#pragma unroll
-            for (int e = 0; e < 8; e++) lo[lds_pad(lay(t, e, b_last))] = csub(csub(v[e], p.two_q), p.q);
-            __syncthreads();
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = lo[lds_pad(lay(t, e, B_A))];
-        }
+        // key for this digit (consumed after the NTT) and the next digit's residues
         const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n + base;
         const u64 *k1 = k0 + kstride;
+        u64 kk0[8], kk1[8], vnext[8];
 #pragma unroll
         for (int e = 0; e < 8; e++)
         {
-            const u32 r = lay(t, e, B_A);
-            mac128(a0[e], v[e], k0[r]);
-            mac128(a1[e], v[e], k1[r]);
+            kk0[e] = k0[lay(t, e, B_A)];
+            kk1[e] = k1[lay(t, e, B_A)];
         }
+        if (J + 1 < j1)
+        {
+            const u64 *src = digit_src(J + 1);
+#pragma unroll
+            for (int e = 0; e < 8; e++) vnext[e] = src[lay(t, e, B_A)];
+        }
+        u64 v[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = vin[e];
+        if (J != I)
+        {
+            row_stages<LOGR>(v, t, B_A, 0, 3, mytw, p.q, p.two_q);
+#pragma unroll
+            for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = v[e];
+            lds_barrier();
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = x0[swz(lay(t, e, B_B))];
+            row_stages<LOGR>(v, t, B_B, 3, 6, mytw, p.q, p.two_q);
+            u64 *xl = x1;
+            int bl = B_B;
+            if (LOGR > 6)
+            {
+#pragma unroll
+                for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = v[e];
+                lds_barrier();
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = x1[swz(lay(t, e, 0))];
+                row_stages<LOGR>(v, t, 0, 6, LOGR, mytw, p.q, p.two_q);
+                xl = x0;
+                bl = 0;
+            }
+            // back to the coalesced layout of the key stream; canonical digits keep the
+            // 128-bit sums exact for any digit count below 2^8
+#pragma unroll
+            for (int e = 0; e < 8; e++) xl[swz(lay(t, e, bl))] = csub(csub(v[e], p.two_q), p.q);
+            lds_barrier();
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = xl[swz(lay(t, e, B_A))];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+        {
+            mac128(a0[e], v[e], kk0[e]);
+            mac128(a1[e], v[e], kk1[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) vin[e] = vnext[e];
     }
     u64 *o0 = acc + (size_t)(2 * g * (L + 1) + I) * n + base;
     u64 *o1 = o0 + (size_t)(L + 1) * n;

@@ -378,3 +378,24 @@ def test_hmult_fused_n16(fused_engines):
     a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
     got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
     assert np.array_equal(got, ch.oc.hmult(a, b, key))
+
+
+@pytest.mark.parametrize("chunk", [1, 3, 0])
+def test_switch_key_chunked_modup(chunk):
+    """ModUp processed in chunks of output primes (MHE_KS_CHUNK) is bit-identical."""
+    import os
+
+    old = os.environ.get("MHE_KS_CHUNK")
+    os.environ["MHE_KS_CHUNK"] = str(chunk)
+    try:
+        ch = Chain(12, SMALL_BITS, seed=30 + chunk)
+    finally:
+        if old is None:
+            del os.environ["MHE_KS_CHUNK"]
+        else:
+            os.environ["MHE_KS_CHUNK"] = old
+    L = ch.K - 1
+    key = ch.rand_key()
+    ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+    got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
+    assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
