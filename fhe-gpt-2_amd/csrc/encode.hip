@@ -1,0 +1,322 @@
+// CKKS encoding for libmhe.
+//
+// CKKSEncoder::encode (SEAL/ckks.h:457-640) is a host double-precision FFT followed by rounding,
+// an RNS reduction and a per-limb NTT.  Bit-exactness with SEAL needs SEAL's exact sequence of
+// non-fused double operations (the reference builds its encoder without FMA), so the FFT and
+// the rounding run here on the host, compiled with -ffp-contract=off, in SEAL's operation order:
+//   * ComplexRoots (util/croots.cpp:17-66): polar(1, 2*PI*i/m) for i <= m/8, 8-fold symmetry;
+//   * index map 5^i (ckks.cpp:34-49), inverse roots conj(root[rev(i-1)+1]) (ckks.cpp:55-60);
+//   * DWTHandler::transform_from_rev over complex<double> with scalar scale/n
+//     (util/dwthandler.h:202-314, ckks.h:46-81).
+// The rounded integer coefficients (sign + 1 or 2 magnitude words) go to HBM once; the RNS
+// reduction and the NTT run on the GPU.  Coefficients wider than 128 bits (scale * |value| >=
+// 2^127) take SEAL's multi-word path (RNSBase::decompose) on the host.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <complex>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mhe.h"
+#include "arith.h"
+
+typedef unsigned __int128 u128;
+typedef std::complex<double> cd;
+
+// shared with mhe.hip
+int mhe_internal_fail(int code, const char *msg);
+int mhe_internal_ntt_forward(mhe_ctx *c, uint64_t *data, int polys, int limbs, int full, hipStream_t st);
+int mhe_internal_primes(mhe_ctx *c, const PrimeDev **dev, const uint64_t **host, int *count, int *log_n);
+
+struct mhe_encoder
+{
+    int log_n = 0;
+    size_t n = 0, slots = 0;
+    std::vector<size_t> index_map;
+    std::vector<cd> inv_root_powers;
+    std::vector<cd> root_powers;
+};
+
+namespace
+{
+u32 rev_bits(u32 x, int bits)
+{
+    return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0;
+}
+
+struct ComplexRoots
+{
+    size_t m;
+    std::vector<cd> roots;
+    explicit ComplexRoots(size_t degree) : m(degree), roots(degree / 8 + 1)
+    {
+        const double PI_ = 3.1415926535897932384626433832795028842;
+        for (size_t i = 0; i <= m / 8; i++)
+            roots[i] = std::polar<double>(1.0, 2 * PI_ * static_cast<double>(i) / static_cast<double>(m));
+    }
+    cd get(size_t index) const
+    {
+        index &= m - 1;
+        if (index <= m / 8) return roots[index];
+        if (index <= m / 4) return cd(roots[m / 4 - index].imag(), roots[m / 4 - index].real());
+        if (index <= m / 2) return -std::conj(get(m / 2 - index));
+        if (index <= 3 * m / 4) return -get(index - m / 2);
+        return std::conj(get(m - index));
+    }
+};
+
+// transform_from_rev with scalar (util/dwthandler.h:202-314)
+void fft_from_rev(cd *values, int log_n, const cd *roots, double scalar)
+{
+    const size_t n = size_t(1) << log_n;
+    size_t gap = 1, m = n >> 1;
+    for (; m > 1; m >>= 1)
+    {
+        size_t offset = 0;
+        for (size_t i = 0; i < m; i++)
+        {
+            const cd r = *++roots;
+            cd *x = values + offset, *y = x + gap;
+            for (size_t j = 0; j < gap; j++)
+            {
+                const cd u = *x, v = *y;
+                *x++ = u + v;
+                *y++ = (u - v) * r;
+            }
+            offset += gap << 1;
+        }
+        gap <<= 1;
+    }
+    const cd r = *++roots;
+    const cd scaled_r = r * scalar;
+    cd *x = values, *y = values + gap;
+    for (size_t j = 0; j < gap; j++)
+    {
+        const cd u = *x, v = *y;
+        *x++ = (u + v) * scalar;
+        *y++ = (u - v) * scaled_r;
+    }
+}
+
+// SEAL's ContextData::total_coeff_modulus_bit_count: bit length of prod q_j.
+int total_bits(const uint64_t *q, int limbs)
+{
+    std::vector<u64> prod(limbs + 1, 0);
+    prod[0] = 1;
+    int words = 1;
+    for (int j = 0; j < limbs; j++)
+    {
+        u64 carry = 0;
+        for (int w = 0; w < words; w++)
+        {
+            u128 t = (u128)prod[w] * q[j] + carry;
+            prod[w] = (u64)t;
+            carry = (u64)(t >> 64);
+        }
+        if (carry) prod[words++] = carry;
+    }
+    return 64 * (words - 1) + (64 - __builtin_clzll(prod[words - 1]));
+}
+
+u64 words_mod(const u64 *w, int nw, u64 q)
+{
+    u128 r = 0;
+    for (int k = nw - 1; k >= 0; k--) r = ((r << 64) | w[k]) % q;
+    return (u64)r;
+}
+} // namespace
+
+// RNS reduction of rounded coefficients: out[j][i] = (+-)(hi:lo mod q_j).
+__global__ void k_encode_reduce(const u64 *lo, const u64 *hi, const unsigned char *neg, u64 *out,
+                                const PrimeDev *primes, int limbs, int log_n)
+{
+    const size_t n = (size_t)1 << log_n;
+    const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= n * limbs) return;
+    const size_t i = g & (n - 1);
+    const int j = (int)(g >> log_n);
+    const PrimeDev p = primes[j];
+    u64 r = hi ? barrett128(lo[i], hi[i], p) : barrett64(lo[i], p);
+    out[g] = (neg[i] && r) ? p.q - r : r;
+}
+
+extern "C" __attribute__((visibility("default"))) int mhe_encoder_create(mhe_encoder **out, int log_n)
+{
+    if (!out || log_n < 2 || log_n > 17) return mhe_internal_fail(MHE_ERR_ARG, "poly_modulus_degree is invalid");
+    mhe_encoder *e = new mhe_encoder;
+    const size_t n = size_t(1) << log_n, m = n << 1;
+    e->log_n = log_n;
+    e->n = n;
+    e->slots = n >> 1;
+    e->index_map.resize(n);
+    u64 pos = 1;
+    for (size_t i = 0; i < e->slots; i++)
+    {
+        const u64 index1 = (pos - 1) >> 1, index2 = (m - pos - 1) >> 1;
+        e->index_map[i] = rev_bits((u32)index1, log_n);
+        e->index_map[e->slots | i] = rev_bits((u32)index2, log_n);
+        pos = (pos * 5) & (m - 1);
+    }
+    e->root_powers.assign(n, cd(0, 0));
+    e->inv_root_powers.assign(n, cd(0, 0));
+    ComplexRoots cr(m);
+    for (size_t i = 1; i < n; i++)
+    {
+        e->root_powers[i] = cr.get(rev_bits((u32)i, log_n));
+        e->inv_root_powers[i] = std::conj(cr.get(rev_bits((u32)(i - 1), log_n) + 1));
+    }
+    *out = e;
+    return MHE_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int mhe_encoder_destroy(mhe_encoder *e)
+{
+    delete e;
+    return MHE_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode(mhe_ctx *c, const mhe_encoder *e,
+                                                                     const double *re, const double *im,
+                                                                     size_t count, double scale, int limbs,
+                                                                     uint64_t *out, void *stream)
+{
+    const PrimeDev *primes;
+    const uint64_t *q;
+    int K, log_n;
+    if (mhe_internal_primes(c, &primes, &q, &K, &log_n)) return mhe_internal_fail(MHE_ERR_ARG, "context is not valid");
+    if (!e || e->log_n != log_n) return mhe_internal_fail(MHE_ERR_ARG, "encoder does not match the context");
+    if (!re && count > 0) return mhe_internal_fail(MHE_ERR_ARG, "values cannot be null");
+    if (count > e->slots) return mhe_internal_fail(MHE_ERR_ARG, "values_size is too large");
+    if (limbs < 1 || limbs > K || !out) return mhe_internal_fail(MHE_ERR_ARG, "parms_id is not valid for encryption parameters");
+    const int tb = total_bits(q, limbs);
+    if (scale <= 0 || (static_cast<int>(std::log2(scale)) + 1 >= tb))
+        return mhe_internal_fail(MHE_ERR_ARG, "scale out of bounds");
+    const size_t n = e->n;
+    std::vector<cd> cv(n, cd(0, 0));
+    for (size_t i = 0; i < count; i++)
+    {
+        const cd v(re[i], im ? im[i] : 0.0);
+        cv[e->index_map[i]] = v;
+        cv[e->index_map[i + e->slots]] = std::conj(v);
+    }
+    const double fix = scale / static_cast<double>(n);
+    fft_from_rev(cv.data(), log_n, e->inv_root_powers.data(), fix);
+    double max_coeff = 0;
+    for (size_t i = 0; i < n; i++) max_coeff = std::max<double>(max_coeff, std::fabs(cv[i].real()));
+    const int max_bits = static_cast<int>(std::ceil(std::log2(std::max<double>(max_coeff, 1.0)))) + 1;
+    if (max_bits >= tb) return mhe_internal_fail(MHE_ERR_ARG, "encoded values are too large");
+
+    const double two64 = std::pow(2.0, 64);
+    std::vector<u64> lo(n), hi(max_bits > 64 ? n : 0);
+    std::vector<unsigned char> neg(n);
+    std::vector<u64> host_out; // multi-word path
+    if (max_bits > 128) host_out.resize(n * limbs);
+    for (size_t i = 0; i < n; i++)
+    {
+        double coeffd = std::round(cv[i].real());
+        neg[i] = std::signbit(coeffd) ? 1 : 0;
+        coeffd = std::fabs(coeffd);
+        if (max_bits <= 64)
+            lo[i] = static_cast<u64>(coeffd);
+        else if (max_bits <= 128)
+        {
+            lo[i] = static_cast<u64>(std::fmod(coeffd, two64));
+            hi[i] = static_cast<u64>(coeffd / two64);
+        }
+        else
+        {
+            u64 w[64] = { 0 };
+            int nw = 0;
+            while (coeffd >= 1)
+            {
+                w[nw++] = static_cast<u64>(std::fmod(coeffd, two64));
+                coeffd /= two64;
+            }
+            for (int j = 0; j < limbs; j++)
+            {
+                const u64 r = words_mod(w, nw ? nw : 1, q[j]);
+                host_out[(size_t)j * n + i] = (neg[i] && r) ? q[j] - r : r;
+            }
+        }
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (max_bits > 128)
+    {
+        if (hipMemcpyAsync(out, host_out.data(), n * limbs * sizeof(u64), hipMemcpyHostToDevice, st) != hipSuccess)
+            return mhe_internal_fail(MHE_ERR_DEVICE, "encode upload failed");
+    }
+    else
+    {
+        u64 *d_lo = nullptr, *d_hi = nullptr;
+        unsigned char *d_neg = nullptr;
+        const size_t bytes = n * sizeof(u64) * (hi.empty() ? 1 : 2) + n;
+        char *buf = nullptr;
+        if (hipMallocAsync((void **)&buf, bytes, st) != hipSuccess)
+            return mhe_internal_fail(MHE_ERR_MEMORY, "encode staging allocation failed");
+        d_lo = (u64 *)buf;
+        if (!hi.empty()) d_hi = d_lo + n;
+        d_neg = (unsigned char *)(d_lo + n * (hi.empty() ? 1 : 2));
+        hipError_t err = hipMemcpyAsync(d_lo, lo.data(), n * sizeof(u64), hipMemcpyHostToDevice, st);
+        if (err == hipSuccess && d_hi) err = hipMemcpyAsync(d_hi, hi.data(), n * sizeof(u64), hipMemcpyHostToDevice, st);
+        if (err == hipSuccess) err = hipMemcpyAsync(d_neg, neg.data(), n, hipMemcpyHostToDevice, st);
+        if (err == hipSuccess)
+        {
+            const size_t total = n * limbs;
+            hipLaunchKernelGGL(k_encode_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_lo, d_hi,
+                               d_neg, out, primes, limbs, log_n);
+            err = hipGetLastError();
+        }
+        // the host staging vectors die at return: finish the copies first
+        if (err == hipSuccess) err = hipStreamSynchronize(st);
+        (void)hipFreeAsync(buf, st);
+        if (err != hipSuccess) return mhe_internal_fail(MHE_ERR_DEVICE, hipGetErrorString(err));
+    }
+    return mhe_internal_ntt_forward(c, out, 1, limbs, 1, st);
+}
+
+extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_scalar(mhe_ctx *c, double value, double scale,
+                                                                            int limbs, uint64_t *residues)
+{
+    const PrimeDev *primes;
+    const uint64_t *q;
+    int K, log_n;
+    if (mhe_internal_primes(c, &primes, &q, &K, &log_n)) return mhe_internal_fail(MHE_ERR_ARG, "context is not valid");
+    if (limbs < 1 || limbs > K || !residues) return mhe_internal_fail(MHE_ERR_ARG, "parms_id is not valid for encryption parameters");
+    const int tb = total_bits(q, limbs);
+    if (scale <= 0 || (static_cast<int>(std::log2(scale)) >= tb)) return mhe_internal_fail(MHE_ERR_ARG, "scale out of bounds");
+    value *= scale;
+    const int coeff_bits = static_cast<int>(std::log2(std::fabs(value))) + 2;
+    if (coeff_bits >= tb) return mhe_internal_fail(MHE_ERR_ARG, "encoded value is too large");
+    const double two64 = std::pow(2.0, 64);
+    double coeffd = std::round(value);
+    const bool is_neg = std::signbit(coeffd);
+    coeffd = std::fabs(coeffd);
+    u64 w[64] = { 0 };
+    int nw = 1;
+    if (coeff_bits <= 64)
+        w[0] = static_cast<u64>(std::fabs(coeffd));
+    else if (coeff_bits <= 128)
+    {
+        w[0] = static_cast<u64>(std::fmod(coeffd, two64));
+        w[1] = static_cast<u64>(coeffd / two64);
+        nw = 2;
+    }
+    else
+    {
+        nw = 0;
+        while (coeffd >= 1)
+        {
+            w[nw++] = static_cast<u64>(std::fmod(coeffd, two64));
+            coeffd /= two64;
+        }
+        if (!nw) nw = 1;
+    }
+    for (int j = 0; j < limbs; j++)
+    {
+        const u64 r = words_mod(w, nw, q[j]);
+        residues[j] = (is_neg && r) ? q[j] - r : r;
+    }
+    return MHE_OK;
+}

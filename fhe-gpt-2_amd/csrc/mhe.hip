@@ -876,6 +876,27 @@ static int run_rescale(mhe_ctx *c, const u64 *in, u64 *out, int size, int L, hip
     return MHE_OK;
 }
 
+// ================================================================ internal (encode.hip)
+int mhe_internal_fail(int code, const char *msg)
+{
+    return fail(code, msg);
+}
+
+int mhe_internal_ntt_forward(mhe_ctx *c, uint64_t *data, int polys, int limbs, int full, hipStream_t st)
+{
+    return run_ntt_fwd(c, data, data, polys, limbs, full, st);
+}
+
+int mhe_internal_primes(mhe_ctx *c, const PrimeDev **dev, const uint64_t **host, int *count, int *log_n)
+{
+    if (!valid_ctx(c)) return MHE_ERR_ARG;
+    *dev = c->primes;
+    *host = c->q.data();
+    *count = c->K;
+    *log_n = c->log_n;
+    return MHE_OK;
+}
+
 // ================================================================================ C ABI
 MHE_EXPORT const char *mhe_last_error(void)
 {

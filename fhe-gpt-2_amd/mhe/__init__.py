@@ -51,6 +51,11 @@ SIGNATURES = {
     "mhe_rescale_to_next": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_mod_switch_drop": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_hmult": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]),
+    "mhe_encoder_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
+    "mhe_encoder_destroy": (ctypes.c_int, [vp]),
+    "mhe_ckks_encode": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                       ctypes.c_size_t, ctypes.c_double, ctypes.c_int, vp, vp]),
+    "mhe_ckks_encode_scalar": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_int, u64p]),
 }
 
 
@@ -126,6 +131,9 @@ class Engine:
         self._h = h
 
     def close(self):
+        if getattr(self, "_enc", None):
+            lib().mhe_encoder_destroy(self._enc)
+            self._enc = None
         if getattr(self, "_h", None):
             lib().mhe_ctx_destroy(self._h)
             self._h = None
@@ -267,6 +275,27 @@ class Engine:
         _check(lib().mhe_hmult(self._h, _ptr(a), _ptr(b), _ptr(key), self._key_limbs(key), _ptr(out), L,
                                self.stream()))
         return out
+
+    def encode(self, values, scale, limbs, out=None):
+        """CKKSEncoder::encode -> NTT-form plaintext [limbs][n] on the device."""
+        if getattr(self, "_enc", None) is None:
+            h = vp()
+            _check(lib().mhe_encoder_create(ctypes.byref(h), self.log_n))
+            self._enc = h
+        v = np.asarray(values)
+        re = np.ascontiguousarray(v.real, np.float64)
+        im = np.ascontiguousarray(v.imag, np.float64) if np.iscomplexobj(v) else None
+        out = self.empty(limbs, self.n) if out is None else out
+        dp = ctypes.POINTER(ctypes.c_double)
+        _check(lib().mhe_ckks_encode(self._h, self._enc, re.ctypes.data_as(dp),
+                                     im.ctypes.data_as(dp) if im is not None else None, re.size, scale, limbs,
+                                     _ptr(out), self.stream()))
+        return out
+
+    def encode_scalar(self, value, scale, limbs):
+        out = (ctypes.c_uint64 * limbs)()
+        _check(lib().mhe_ckks_encode_scalar(self._h, value, scale, limbs, out))
+        return list(out)
 
     def hmult_raw(self, a_ptr, b_ptr, key_ptr, key_limbs, out_ptr, L, stream):
         """Pointer-level HMult for the benchmark loop (no tensor bookkeeping)."""

@@ -128,6 +128,23 @@ int mhe_mod_switch_drop(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int siz
 int mhe_hmult(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, const uint64_t *relin_key, int key_limbs,
               uint64_t *out, int limbs, void *stream);
 
+/* ---- CKKS encoding (SEAL/ckks.cpp:10-200, SEAL/ckks.h:457-640) ---------------------------
+ * An encoder holds CKKSEncoder's constructor tables (index map 5^i, complex roots).  Encoding
+ * is SEAL's host double-precision FFT in SEAL's operation order (no FMA, bit-identical),
+ * then the RNS reduction and the per-limb NTT on the GPU. */
+typedef struct mhe_encoder mhe_encoder;
+int mhe_encoder_create(mhe_encoder **enc, int log_n);
+int mhe_encoder_destroy(mhe_encoder *enc);
+/* CKKSEncoder::encode(vector<double|complex<double>>, parms_id, scale, destination): re/im
+ * host arrays (im may be NULL for real input), count <= n/2 slots; writes the NTT-form
+ * plaintext [limbs][n] at device pointer out (limbs = coeff_modulus_size of the level). */
+int mhe_ckks_encode(mhe_ctx *ctx, const mhe_encoder *enc, const double *re, const double *im, size_t count,
+                    double scale, int limbs, uint64_t *out, void *stream);
+/* CKKSEncoder::encode(double value, parms_id, scale, destination) (ckks.cpp:78-200): the
+ * constant plaintext is one residue per limb, written to the host array residues[limbs]
+ * (multiply_const / add_const feed it to mhe_multiply_scalar / mhe_add_scalar). */
+int mhe_ckks_encode_scalar(mhe_ctx *ctx, double value, double scale, int limbs, uint64_t *residues);
+
 #ifdef __cplusplus
 }
 #endif

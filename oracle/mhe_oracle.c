@@ -927,3 +927,285 @@ OR_API int or_ctx_hmult_batch(const or_ctx *c, const uint64_t *a, const uint64_t
     }
     return used;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * CKKS encoder (ckks.cpp:10-60 constructor tables, ckks.h:457-640 encode_internal,
+ * ckks.cpp:78-200 encode_internal(double), util/croots.cpp ComplexRoots,
+ * util/dwthandler.h:202-314 transform_from_rev over complex<double> with
+ * Arithmetic<complex<double>> (ckks.h:46-81)).  Built with -ffp-contract=off: the reference
+ * encodes without FMA (SEAL library at -O3 for baseline x86-64, cnn driver at -O0), so the
+ * double results here are bit-identical to SEAL's for the same libm.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct
+{
+    double re, im;
+} or_cplx;
+
+static or_cplx or_c(double re, double im)
+{
+    or_cplx z = { re, im };
+    return z;
+}
+static or_cplx or_cmul(or_cplx a, or_cplx b) /* std::complex operator* (finite path) */
+{
+    return or_c(a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re);
+}
+static or_cplx or_cadd(or_cplx a, or_cplx b)
+{
+    return or_c(a.re + b.re, a.im + b.im);
+}
+static or_cplx or_csub(or_cplx a, or_cplx b)
+{
+    return or_c(a.re - b.re, a.im - b.im);
+}
+static or_cplx or_cscale(or_cplx a, double s)
+{
+    return or_c(a.re * s, a.im * s);
+}
+
+/* ComplexRoots (util/croots.cpp:17-66) for degree m = 2n. */
+typedef struct
+{
+    size_t m;
+    or_cplx *roots; /* m/8 + 1 entries */
+} or_croots;
+
+static void or_croots_init(or_croots *c, size_t m)
+{
+    const double PI_ = 3.1415926535897932384626433832795028842;
+    c->m = m;
+    c->roots = (or_cplx *)malloc(sizeof(or_cplx) * (m / 8 + 1));
+    for (size_t i = 0; i <= m / 8; i++)
+    {
+        double th = 2 * PI_ * (double)i / (double)m; /* polar<double>(1.0, theta) */
+        c->roots[i] = or_c(cos(th), sin(th));
+    }
+}
+
+static or_cplx or_croot(const or_croots *c, size_t index)
+{
+    size_t m = c->m;
+    index &= m - 1;
+    if (index <= m / 8) return c->roots[index];
+    if (index <= m / 4)
+    {
+        or_cplx a = c->roots[m / 4 - index];
+        return or_c(a.im, a.re); /* mirror */
+    }
+    if (index <= m / 2)
+    {
+        or_cplx a = or_croot(c, m / 2 - index);
+        return or_c(-a.re, a.im); /* -conj(a) */
+    }
+    if (index <= 3 * m / 4)
+    {
+        or_cplx a = or_croot(c, index - m / 2);
+        return or_c(-a.re, -a.im);
+    }
+    or_cplx a = or_croot(c, m - index);
+    return or_c(a.re, -a.im); /* conj */
+}
+
+/* CKKSEncoder constructor tables: matrix_reps_index_map_ (5^i), root_powers_ (bit-reversed),
+ * inv_root_powers_ (scrambled, conjugated). */
+typedef struct
+{
+    int log_n;
+    size_t n, slots;
+    size_t *index_map;
+    or_cplx *root_powers, *inv_root_powers;
+} or_encoder;
+
+OR_API or_encoder *or_encoder_create(int log_n)
+{
+    or_encoder *e = (or_encoder *)calloc(1, sizeof(or_encoder));
+    size_t n = (size_t)1 << log_n, m = n << 1;
+    e->log_n = log_n;
+    e->n = n;
+    e->slots = n >> 1;
+    e->index_map = (size_t *)malloc(sizeof(size_t) * n);
+    uint64_t pos = 1;
+    for (size_t i = 0; i < e->slots; i++)
+    {
+        uint64_t index1 = (pos - 1) >> 1, index2 = (m - pos - 1) >> 1;
+        e->index_map[i] = or_reverse_bits((uint32_t)index1, log_n);
+        e->index_map[e->slots | i] = or_reverse_bits((uint32_t)index2, log_n);
+        pos *= 5;
+        pos &= (m - 1);
+    }
+    e->root_powers = (or_cplx *)calloc(n, sizeof(or_cplx));
+    e->inv_root_powers = (or_cplx *)calloc(n, sizeof(or_cplx));
+    or_croots cr;
+    or_croots_init(&cr, m);
+    for (size_t i = 1; i < n; i++)
+    {
+        e->root_powers[i] = or_croot(&cr, or_reverse_bits((uint32_t)i, log_n));
+        or_cplx r = or_croot(&cr, or_reverse_bits((uint32_t)(i - 1), log_n) + 1);
+        e->inv_root_powers[i] = or_c(r.re, -r.im);
+    }
+    free(cr.roots);
+    return e;
+}
+
+OR_API void or_encoder_destroy(or_encoder *e)
+{
+    if (!e) return;
+    free(e->index_map);
+    free(e->root_powers);
+    free(e->inv_root_powers);
+    free(e);
+}
+
+/* DWTHandler<complex<double>, complex<double>, double>::transform_from_rev with scalar. */
+static void or_fft_from_rev(or_cplx *values, int log_n, const or_cplx *roots, double scalar)
+{
+    size_t n = (size_t)1 << log_n, gap = 1, m = n >> 1;
+    for (; m > 1; m >>= 1)
+    {
+        size_t offset = 0;
+        for (size_t i = 0; i < m; i++)
+        {
+            or_cplx r = *++roots;
+            or_cplx *x = values + offset, *y = x + gap;
+            for (size_t j = 0; j < gap; j++)
+            {
+                or_cplx u = *x, v = *y;
+                *x++ = or_cadd(u, v);
+                *y++ = or_cmul(or_csub(u, v), r);
+            }
+            offset += gap << 1;
+        }
+        gap <<= 1;
+    }
+    or_cplx r = *++roots;
+    or_cplx scaled_r = or_cscale(r, scalar);
+    or_cplx *x = values, *y = values + gap;
+    for (size_t j = 0; j < gap; j++)
+    {
+        or_cplx u = *x, v = *y;
+        *x++ = or_cscale(or_cadd(u, v), scalar);
+        *y++ = or_cmul(or_csub(u, v), scaled_r);
+    }
+}
+
+/* Multi-word decomposition of a non-negative integer given as little-endian words into RNS
+ * (RNSBase::decompose, util/rns.cpp): value mod q_j by Horner from the top word. */
+static uint64_t or_words_mod(const uint64_t *w, int nw, const or_mod *m)
+{
+    uint64_t r = 0;
+    for (int k = nw - 1; k >= 0; k--) r = or_barrett128(w[k], r, m);
+    return r;
+}
+
+/* encode_internal for complex values (ckks.h:457-640), at a level with `limbs` primes of the
+ * context: writes the NTT-form plaintext [limbs][n].  total_bits = total coeff modulus bit
+ * count of that level (for the SEAL range checks).  Returns 0, -1 scale out of bounds,
+ * -2 values too large. */
+OR_API int or_ckks_encode(const or_encoder *e, const or_ctx *c, const double *re, const double *im, size_t count,
+                          double scale, int limbs, int total_bits, uint64_t *out)
+{
+    size_t n = e->n;
+    if (scale <= 0 || ((int)log2(scale)) + 1 >= total_bits) return -1;
+    or_cplx *cv = (or_cplx *)calloc(n, sizeof(or_cplx));
+    for (size_t i = 0; i < count; i++)
+    {
+        or_cplx v = or_c(re[i], im ? im[i] : 0.0);
+        cv[e->index_map[i]] = v;
+        cv[e->index_map[i + e->slots]] = or_c(v.re, -v.im);
+    }
+    double fix = scale / (double)n;
+    or_fft_from_rev(cv, e->log_n, e->inv_root_powers, fix);
+    double max_coeff = 0;
+    for (size_t i = 0; i < n; i++) max_coeff = fmax(max_coeff, fabs(cv[i].re));
+    int max_bits = (int)ceil(log2(fmax(max_coeff, 1.0))) + 1;
+    if (max_bits >= total_bits)
+    {
+        free(cv);
+        return -2;
+    }
+    const double two64 = pow(2.0, 64);
+    for (size_t i = 0; i < n; i++)
+    {
+        double cd = round(cv[i].re);
+        int neg = signbit(cd) ? 1 : 0;
+        cd = fabs(cd);
+        uint64_t w[64] = { 0 };
+        int nw;
+        if (max_bits <= 64)
+        {
+            w[0] = (uint64_t)cd;
+            nw = 1;
+        }
+        else if (max_bits <= 128)
+        {
+            w[0] = (uint64_t)fmod(cd, two64);
+            w[1] = (uint64_t)(cd / two64);
+            nw = 2;
+        }
+        else
+        {
+            nw = 0;
+            while (cd >= 1)
+            {
+                w[nw++] = (uint64_t)fmod(cd, two64);
+                cd /= two64;
+            }
+            if (!nw) nw = 1;
+        }
+        for (int j = 0; j < limbs; j++)
+        {
+            const or_mod *m = &c->mod[j];
+            uint64_t r = (nw == 1) ? or_barrett64(w[0], m) : or_words_mod(w, nw, m);
+            out[(size_t)j * n + i] = (neg && r) ? m->value - r : r;
+        }
+    }
+    free(cv);
+    for (int j = 0; j < limbs; j++) or_ntt_fwd(out + (size_t)j * n, &c->ntt[j]);
+    return 0;
+}
+
+/* encode_internal(double value, ...) (ckks.cpp:78-200): a constant polynomial, written as
+ * one residue per limb (the plaintext is that residue in every coefficient, NTT of a
+ * constant is the constant).  Returns the SEAL error codes as or_ckks_encode. */
+OR_API int or_ckks_encode_scalar(const or_ctx *c, double value, double scale, int limbs, int total_bits,
+                                 uint64_t *residues)
+{
+    if (scale <= 0 || ((int)log2(scale)) >= total_bits) return -1;
+    value *= scale;
+    int coeff_bits = (int)log2(fabs(value)) + 2;
+    if (coeff_bits >= total_bits) return -2;
+    const double two64 = pow(2.0, 64);
+    double cd = round(value);
+    int neg = signbit(cd) ? 1 : 0;
+    cd = fabs(cd);
+    uint64_t w[64] = { 0 };
+    int nw;
+    if (coeff_bits <= 64)
+    {
+        w[0] = (uint64_t)fabs(cd);
+        nw = 1;
+    }
+    else if (coeff_bits <= 128)
+    {
+        w[0] = (uint64_t)fmod(cd, two64);
+        w[1] = (uint64_t)(cd / two64);
+        nw = 2;
+    }
+    else
+    {
+        nw = 0;
+        while (cd >= 1)
+        {
+            w[nw++] = (uint64_t)fmod(cd, two64);
+            cd /= two64;
+        }
+        if (!nw) nw = 1;
+    }
+    for (int j = 0; j < limbs; j++)
+    {
+        const or_mod *m = &c->mod[j];
+        uint64_t r = (nw == 1) ? or_barrett64(w[0], m) : or_words_mod(w, nw, m);
+        residues[j] = (neg && r) ? m->value - r : r;
+    }
+    return 0;
+}

@@ -58,6 +58,13 @@ def lib():
             "or_ctx_multiply_plain": (None, [ctypes.c_void_p, u64p, u64p, ctypes.c_int, ctypes.c_int]),
             "or_ctx_hmult": (ctypes.c_int, [ctypes.c_void_p, u64p, u64p, u64p, u64p, ctypes.c_int]),
             "or_ctx_hmult_batch": (ctypes.c_int, [ctypes.c_void_p, u64p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+            "or_encoder_create": (ctypes.c_void_p, [ctypes.c_int]),
+            "or_encoder_destroy": (None, [ctypes.c_void_p]),
+            "or_ckks_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_double), ctypes.c_size_t, ctypes.c_double,
+                                              ctypes.c_int, ctypes.c_int, u64p]),
+            "or_ckks_encode_scalar": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                                     ctypes.c_int, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -149,6 +156,9 @@ class Context:
             raise ValueError("invalid modulus chain")
 
     def __del__(self):
+        if getattr(self, "_enc", None):
+            lib().or_encoder_destroy(self._enc)
+            self._enc = None
         if getattr(self, "_h", None):
             lib().or_ctx_destroy(self._h)
             self._h = None
@@ -235,6 +245,38 @@ class Context:
         if lib().or_ctx_hmult(self._h, _p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), _p(key), _p(out), L):
             raise ValueError("hmult failed")
         return out
+
+    def total_bits(self, limbs):
+        """ContextData::total_coeff_modulus_bit_count of the level with `limbs` primes."""
+        p = 1
+        for q in self.moduli[:limbs]:
+            p *= q
+        return p.bit_length()
+
+    def encode(self, values, scale, limbs):
+        """CKKSEncoder::encode (ckks.h:457-640) -> NTT-form plaintext [limbs][n]."""
+        if not hasattr(self, "_enc"):
+            self._enc = lib().or_encoder_create(self.log_n)
+        v = np.asarray(values)
+        re = np.ascontiguousarray(v.real, np.float64)
+        im = np.ascontiguousarray(v.imag, np.float64) if np.iscomplexobj(v) else None
+        out = np.zeros((limbs, self.n), np.uint64)
+        dp = ctypes.POINTER(ctypes.c_double)
+        rc = lib().or_ckks_encode(self._enc, self._h, re.ctypes.data_as(dp), im.ctypes.data_as(dp) if im is not None else None,
+                                  re.size, scale, limbs, self.total_bits(limbs), _p(out))
+        if rc == -1:
+            raise ValueError("scale out of bounds")
+        if rc == -2:
+            raise ValueError("encoded values are too large")
+        return out
+
+    def encode_scalar(self, value, scale, limbs):
+        """CKKSEncoder::encode(double) (ckks.cpp:78-200) -> one residue per limb."""
+        out = np.zeros(limbs, np.uint64)
+        rc = lib().or_ckks_encode_scalar(self._h, value, scale, limbs, self.total_bits(limbs), _p(out))
+        if rc:
+            raise ValueError("scale out of bounds" if rc == -1 else "encoded value is too large")
+        return [int(x) for x in out]
 
     def hmult_batch(self, a, b, key, threads=0):
         """a, b: [B][2][L][n] -> ([B][2][L-1][n], threads used)."""

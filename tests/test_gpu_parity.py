@@ -399,3 +399,52 @@ def test_switch_key_chunked_modup(chunk):
     ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
     got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
     assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
+
+
+# ----------------------------------------------------------------- CKKS encode (A13, A14)
+@pytest.mark.parametrize("kind", ["real", "complex", "partial"])
+def test_ckks_encode_bit_exact(small, kind):
+    """CKKSEncoder::encode on the engine == the oracle restatement, bit for bit."""
+    ch = small
+    rng = np.random.default_rng(40)
+    if kind == "real":
+        v = rng.uniform(-1, 1, ch.n // 2)
+    elif kind == "complex":
+        v = rng.uniform(-1, 1, ch.n // 2) + 1j * rng.uniform(-1, 1, ch.n // 2)
+    else:
+        v = rng.uniform(-4, 4, 37)
+    L = ch.K - 1
+    got = ch.down(ch.eng.encode(v, 2.0 ** 46, L))
+    assert np.array_equal(got, ch.oc.encode(v, 2.0 ** 46, L))
+
+
+@pytest.mark.parametrize("scale", [2.0 ** 20, 2.0 ** 70, 2.0 ** 140])
+def test_ckks_encode_wide_coefficients(small, scale):
+    """<=64-bit, 128-bit and multi-word coefficient paths (ckks.h:560-628)."""
+    ch = small
+    v = np.random.default_rng(41).uniform(-1, 1, ch.n // 2)
+    L = ch.K - 1
+    got = ch.down(ch.eng.encode(v, scale, L))
+    assert np.array_equal(got, ch.oc.encode(v, scale, L))
+
+
+def test_ckks_encode_scalar(small):
+    ch = small
+    for value, scale in [(0.5, 2.0 ** 40), (-3.25, 2.0 ** 46), (1.0, 2.0 ** 90), (0.0, 2.0 ** 30)]:
+        assert ch.eng.encode_scalar(value, scale, ch.K - 1) == ch.oc.encode_scalar(value, scale, ch.K - 1)
+
+
+def test_ckks_encode_errors(small):
+    ch = small
+    with pytest.raises(mhe.MheError, match="scale out of bounds"):
+        ch.eng.encode([1.0], 2.0 ** 400, 2)
+    with pytest.raises(mhe.MheError, match="values_size is too large"):
+        ch.eng.encode(np.zeros(ch.n), 2.0 ** 20, 2)
+
+
+@pytest.mark.slow
+def test_ckks_encode_c2_full(c2):
+    ch = c2
+    v = np.random.default_rng(42).uniform(-1, 1, ch.n // 2) * np.cos(np.arange(ch.n // 2))
+    got = ch.down(ch.eng.encode(v, 2.0 ** 46, ch.K - 1))
+    assert np.array_equal(got, ch.oc.encode(v, 2.0 ** 46, ch.K - 1))
