@@ -1020,6 +1020,15 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
             invq[(size_t)j * count + i].y = host::shoup(inv, moduli[i]);
         }
     hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess)
+    {
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess)
+        {
+            uint64_t threshold = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &threshold);
+        }
+    }
     if (e == hipSuccess) e = hipMalloc(&c->primes, sizeof(PrimeDev) * count);
     if (e == hipSuccess) e = hipMalloc(&c->tw, sizeof(Tw) * tw.size());
     if (e == hipSuccess) e = hipMalloc(&c->itw, sizeof(Tw) * itw.size());
@@ -1071,6 +1080,21 @@ MHE_EXPORT int mhe_malloc(mhe_ctx *c, void **dptr, size_t bytes)
     return MHE_OK;
 }
 
+MHE_EXPORT int mhe_malloc_async(mhe_ctx *c, void **dptr, size_t bytes, void *stream)
+{
+    if (!valid_ctx(c) || !dptr) return fail(MHE_ERR_ARG, "invalid argument");
+    if (hipMallocAsync(dptr, bytes ? bytes : 1, S(stream)) != hipSuccess)
+        return fail(MHE_ERR_MEMORY, "device allocation failed");
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_free_async(mhe_ctx *c, void *dptr, void *stream)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipFreeAsync(dptr, S(stream)));
+    return MHE_OK;
+}
+
 MHE_EXPORT int mhe_free(mhe_ctx *c, void *dptr)
 {
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
@@ -1096,6 +1120,33 @@ MHE_EXPORT int mhe_memcpy_d2d(mhe_ctx *c, void *dst, const void *src, size_t byt
 {
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_stream_create(mhe_ctx *c, void **stream)
+{
+    if (!valid_ctx(c) || !stream) return fail(MHE_ERR_ARG, "invalid argument");
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_stream_destroy(mhe_ctx *c, void *stream)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        auto it = c->ws.find(S(stream));
+        if (it != c->ws.end())
+        {
+            (void)hipStreamSynchronize(S(stream));
+            if (it->second.base) (void)hipFree(it->second.base);
+            c->ws.erase(it);
+        }
+    }
+    HIP_TRY(hipStreamDestroy(S(stream)));
     return MHE_OK;
 }
 
@@ -1285,7 +1336,7 @@ MHE_EXPORT int mhe_rescale_to_next(mhe_ctx *c, const uint64_t *in, uint64_t *out
 {
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
     if (limbs < 2) return fail(MHE_ERR_RANGE, "end of modulus switching chain reached");
-    if (limbs > c->K - 1 || size < 1 || size > 3 || !in || !out)
+    if (limbs > c->K || size < 1 || size > 3 || !in || !out)
         return fail(MHE_ERR_ARG, "encrypted is not valid for encryption parameters");
     if (in == out) return fail(MHE_ERR_ARG, "rescale output must not alias its input");
     return run_rescale(c, in, out, size, limbs, S(s));

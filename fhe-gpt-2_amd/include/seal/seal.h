@@ -1,0 +1,530 @@
+// seal/seal.h -- SEAL-3.6-compatible C++ surface of the MI355X engine (libmhe_seal.so).
+//
+// Drop-in for the subset of the modified Microsoft SEAL 3.6.6 API that the reference's
+// callers use: EncryptionParameters, CoeffModulus, SEALContext (+ chain),
+// Ciphertext / Plaintext, keys, KeyGenerator, CKKSEncoder, Encryptor, Decryptor and the
+// Evaluator, including the modified `Evaluator(context, encoder)` constructor and the
+// `*_const`, `multiply_vector*`, `*_reduced_error` methods (SEAL/evaluator.h:1186-1285).
+//
+// Every ciphertext operation runs on the GPU through the C ABI of include/mhe.h; polynomial
+// data lives in HBM in SEAL's layout ([poly][limb][n] u64, NTT form).  Ciphertext/Plaintext
+// keep a host mirror that is synchronised only when data() is touched, so the usual
+// value-semantics code (copies, temporaries) never crosses PCIe.  Each calling host thread
+// gets its own HIP stream (the reference calls one shared Evaluator from 50 OpenMP threads,
+// cnn/infer_seal.cpp:404).
+//
+// Differences from SEAL, by design:
+//  * randomness: key generation and encryption draw from std::mt19937_64 (seeded from
+//    std::random_device, or from Blake2xbPRNGFactory's seed words), not from Blake2xb, so
+//    keys/ciphertexts are not SEAL's bits -- every *operation* on given inputs is bit-exact;
+//  * SEAL's memory pools (MemoryPoolHandle) are accepted and ignored;
+//  * serialization (save/load) is not provided yet.
+#pragma once
+
+#include <array>
+#include <complex>
+#include <cstddef>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+struct mhe_ctx;
+struct mhe_encoder;
+
+namespace seal
+{
+enum class scheme_type : std::uint8_t
+{
+    none = 0x0,
+    bfv = 0x1,
+    ckks = 0x2
+};
+
+enum class sec_level_type : int
+{
+    none = 0,
+    tc128 = 128,
+    tc192 = 192,
+    tc256 = 256
+};
+
+using parms_id_type = std::array<std::uint64_t, 4>;
+extern const parms_id_type parms_id_zero;
+
+class MemoryPoolHandle
+{
+public:
+    static MemoryPoolHandle Global() { return {}; }
+    static MemoryPoolHandle New(bool = false) { return {}; }
+    explicit operator bool() const noexcept { return true; }
+};
+
+class MemoryManager
+{
+public:
+    static MemoryPoolHandle GetPool() { return {}; }
+};
+
+// Modulus (SEAL/modulus.h)
+class Modulus
+{
+public:
+    Modulus(std::uint64_t value = 0) : value_(value) {}
+    std::uint64_t value() const noexcept { return value_; }
+    int bit_count() const noexcept;
+    bool is_zero() const noexcept { return value_ == 0; }
+    bool operator==(const Modulus &o) const noexcept { return value_ == o.value_; }
+    bool operator!=(const Modulus &o) const noexcept { return value_ != o.value_; }
+    bool operator<(const Modulus &o) const noexcept { return value_ < o.value_; }
+    bool operator<=(const Modulus &o) const noexcept { return value_ <= o.value_; }
+
+private:
+    std::uint64_t value_;
+};
+
+// CoeffModulus::Create (SEAL/modulus.cpp:143-185)
+class CoeffModulus
+{
+public:
+    static std::vector<Modulus> Create(std::size_t poly_modulus_degree, std::vector<int> bit_sizes);
+};
+
+// Seeded PRNG factory: keeps SEAL's construction syntax (SEAL/randomgen.h:553); the words
+// seed std::mt19937_64, not Blake2xb.
+class UniformRandomGeneratorFactory
+{
+public:
+    virtual ~UniformRandomGeneratorFactory() = default;
+    virtual std::uint64_t seed() const = 0;
+};
+
+class Blake2xbPRNGFactory : public UniformRandomGeneratorFactory
+{
+public:
+    Blake2xbPRNGFactory() : seeded_(false), seed_(0) {}
+    explicit Blake2xbPRNGFactory(const std::array<std::uint64_t, 8> &s);
+    std::uint64_t seed() const override;
+
+private:
+    bool seeded_;
+    std::uint64_t seed_;
+};
+
+// EncryptionParameters (SEAL/encryptionparams.h, with the modified hamming weight / sparse slots)
+class EncryptionParameters
+{
+public:
+    EncryptionParameters(scheme_type scheme = scheme_type::none) : scheme_(scheme) {}
+    void set_poly_modulus_degree(std::size_t n) { n_ = n; }
+    void set_coeff_modulus(const std::vector<Modulus> &cm) { coeff_modulus_ = cm; }
+    void set_secret_key_hamming_weight(std::size_t hw) { hamming_weight_ = hw; }
+    void set_sparse_slots(std::size_t s) { sparse_slots_ = s; }
+    void set_random_generator(std::shared_ptr<UniformRandomGeneratorFactory> g) { rng_ = std::move(g); }
+    scheme_type scheme() const noexcept { return scheme_; }
+    std::size_t poly_modulus_degree() const noexcept { return n_; }
+    const std::vector<Modulus> &coeff_modulus() const noexcept { return coeff_modulus_; }
+    std::size_t secret_key_hamming_weight() const noexcept { return hamming_weight_; }
+    std::size_t sparse_slots() const noexcept { return sparse_slots_; }
+    std::shared_ptr<UniformRandomGeneratorFactory> random_generator() const { return rng_; }
+    parms_id_type parms_id() const;
+
+private:
+    scheme_type scheme_;
+    std::size_t n_ = 0;
+    std::vector<Modulus> coeff_modulus_;
+    std::size_t hamming_weight_ = 0;
+    std::size_t sparse_slots_ = 0;
+    std::shared_ptr<UniformRandomGeneratorFactory> rng_;
+};
+
+class Ciphertext;
+class Plaintext;
+
+// SEALContext (SEAL/context.h): the modulus switching chain
+class SEALContext
+{
+public:
+    class ContextData
+    {
+    public:
+        const EncryptionParameters &parms() const noexcept { return parms_; }
+        const parms_id_type &parms_id() const noexcept { return parms_id_; }
+        std::size_t chain_index() const noexcept { return chain_index_; }
+        int total_coeff_modulus_bit_count() const noexcept { return total_bits_; }
+        std::shared_ptr<const ContextData> next_context_data() const noexcept { return next_.lock(); }
+        std::shared_ptr<const ContextData> prev_context_data() const noexcept { return prev_.lock(); }
+
+    private:
+        friend class SEALContext;
+        EncryptionParameters parms_;
+        parms_id_type parms_id_{};
+        std::size_t chain_index_ = 0;
+        int total_bits_ = 0;
+        std::weak_ptr<const ContextData> next_, prev_;
+    };
+
+    SEALContext(const EncryptionParameters &parms, bool expand_mod_chain = true,
+                sec_level_type sec_level = sec_level_type::tc128);
+    std::shared_ptr<const ContextData> get_context_data(const parms_id_type &id) const;
+    std::shared_ptr<const ContextData> key_context_data() const;
+    std::shared_ptr<const ContextData> first_context_data() const;
+    std::shared_ptr<const ContextData> last_context_data() const;
+    const parms_id_type &key_parms_id() const;
+    const parms_id_type &first_parms_id() const;
+    const parms_id_type &last_parms_id() const;
+    bool parameters_set() const noexcept;
+    bool using_keyswitching() const noexcept;
+
+    // engine plumbing (not SEAL API)
+    mhe_ctx *engine() const;
+    void *stream() const;      // this host thread's HIP stream on the engine
+    std::size_t key_size() const; // primes at the key level (data + special)
+
+private:
+    struct Impl;
+    std::shared_ptr<Impl> impl_;
+};
+
+// Device polynomial storage with a lazily synchronised host mirror.
+class PolyStore
+{
+public:
+    PolyStore() = default;
+    PolyStore(const PolyStore &o);
+    PolyStore &operator=(const PolyStore &o);
+    PolyStore(PolyStore &&o) noexcept;
+    PolyStore &operator=(PolyStore &&o) noexcept;
+    ~PolyStore();
+
+    void bind(const SEALContext &ctx);
+    void resize_words(std::size_t words);
+    std::size_t words() const noexcept { return words_; }
+    std::uint64_t *device();                 // device copy, made current (host edits uploaded)
+    const std::uint64_t *device() const;
+    std::uint64_t *host();                   // host mirror, device marked stale
+    const std::uint64_t *host() const;       // host mirror, device stays current
+    void *stream() const;
+
+private:
+    void release();
+    void *stream_now() const;
+    std::shared_ptr<void> hold_; // keeps the SEALContext engine alive
+    mhe_ctx *eng_ = nullptr;
+    std::uint64_t *dev_ = nullptr;
+    std::size_t words_ = 0, cap_ = 0;
+    mutable std::vector<std::uint64_t> host_;
+    mutable bool host_valid_ = true, dev_valid_ = true;
+};
+
+class Ciphertext
+{
+public:
+    Ciphertext(MemoryPoolHandle = {}) {}
+    Ciphertext(const SEALContext &context, MemoryPoolHandle = {});
+    Ciphertext(const SEALContext &context, parms_id_type parms_id, MemoryPoolHandle = {});
+
+    void resize(const SEALContext &context, parms_id_type parms_id, std::size_t size);
+    void resize(const SEALContext &context, std::size_t size);
+    void resize(std::size_t size);
+    std::size_t size() const noexcept { return size_; }
+    std::size_t coeff_modulus_size() const noexcept { return coeff_modulus_size_; }
+    std::size_t poly_modulus_degree() const noexcept { return poly_modulus_degree_; }
+    parms_id_type &parms_id() noexcept { return parms_id_; }
+    const parms_id_type &parms_id() const noexcept { return parms_id_; }
+    double &scale() noexcept { return scale_; }
+    double scale() const noexcept { return scale_; }
+    bool &is_ntt_form() noexcept { return is_ntt_form_; }
+    bool is_ntt_form() const noexcept { return is_ntt_form_; }
+    bool is_transparent() const;
+    std::uint64_t *data() { return store_.host(); }
+    const std::uint64_t *data() const { return store_.host(); }
+    std::uint64_t *data(std::size_t poly) { return store_.host() + poly * coeff_modulus_size_ * poly_modulus_degree_; }
+    const std::uint64_t *data(std::size_t poly) const
+    {
+        return store_.host() + poly * coeff_modulus_size_ * poly_modulus_degree_;
+    }
+    std::size_t dyn_array_size() const noexcept { return store_.words(); }
+
+    // engine plumbing
+    PolyStore &store() noexcept { return store_; }
+    const PolyStore &store() const noexcept { return store_; }
+
+private:
+    PolyStore store_;
+    parms_id_type parms_id_{};
+    std::size_t size_ = 0, coeff_modulus_size_ = 0, poly_modulus_degree_ = 0;
+    double scale_ = 1.0;
+    bool is_ntt_form_ = false;
+};
+
+class Plaintext
+{
+public:
+    Plaintext(MemoryPoolHandle = {}) {}
+    std::size_t coeff_count() const noexcept { return store_.words(); }
+    parms_id_type &parms_id() noexcept { return parms_id_; }
+    const parms_id_type &parms_id() const noexcept { return parms_id_; }
+    double &scale() noexcept { return scale_; }
+    double scale() const noexcept { return scale_; }
+    bool is_ntt_form() const noexcept { return parms_id_ != parms_id_zero; }
+    std::uint64_t *data() { return store_.host(); }
+    const std::uint64_t *data() const { return store_.host(); }
+    std::uint64_t &operator[](std::size_t i) { return store_.host()[i]; }
+    std::size_t limbs() const noexcept { return limbs_; }
+
+    // engine plumbing
+    void set_level(const SEALContext &ctx, const parms_id_type &id, std::size_t limbs);
+    PolyStore &store() noexcept { return store_; }
+    const PolyStore &store() const noexcept { return store_; }
+
+private:
+    PolyStore store_;
+    parms_id_type parms_id_ = parms_id_zero;
+    double scale_ = 1.0;
+    std::size_t limbs_ = 0;
+};
+
+class SecretKey
+{
+public:
+    const Plaintext &data() const noexcept { return sk_; }
+    Plaintext &data() noexcept { return sk_; }
+    const parms_id_type &parms_id() const noexcept { return sk_.parms_id(); }
+
+private:
+    Plaintext sk_; // NTT form over the key level
+};
+
+class PublicKey
+{
+public:
+    const Ciphertext &data() const noexcept { return pk_; }
+    Ciphertext &data() noexcept { return pk_; }
+    const parms_id_type &parms_id() const noexcept { return pk_.parms_id(); }
+
+private:
+    Ciphertext pk_;
+};
+
+// KSwitchKeys (SEAL/kswitchkeys.h): one device buffer [digits][2][key_limbs][n] per key index.
+class KSwitchKeys
+{
+public:
+    std::size_t size() const noexcept { return keys_.size(); }
+    const parms_id_type &parms_id() const noexcept { return parms_id_; }
+    parms_id_type &parms_id() noexcept { return parms_id_; }
+    bool has_index(std::size_t i) const { return keys_.count(i) != 0; }
+    const PolyStore &key(std::size_t i) const;
+    PolyStore &key_mut(std::size_t i) { return keys_[i]; }
+    std::size_t key_limbs() const noexcept { return key_limbs_; }
+    void set_key_limbs(std::size_t k) { key_limbs_ = k; }
+
+private:
+    std::map<std::size_t, PolyStore> keys_;
+    parms_id_type parms_id_ = parms_id_zero;
+    std::size_t key_limbs_ = 0;
+};
+
+class RelinKeys : public KSwitchKeys
+{
+public:
+    static std::size_t get_index(std::size_t key_power) { return key_power - 2; } // relinkeys.h:58
+    bool has_key(std::size_t key_power) const { return has_index(get_index(key_power)); }
+};
+
+class GaloisKeys : public KSwitchKeys
+{
+public:
+    static std::size_t get_index(std::uint32_t galois_elt) { return (galois_elt - 1) >> 1; } // galoiskeys.h:48
+    bool has_key(std::uint32_t galois_elt) const { return has_index(get_index(galois_elt)); }
+};
+
+class KeyGenerator
+{
+public:
+    explicit KeyGenerator(const SEALContext &context);
+    KeyGenerator(const SEALContext &context, const SecretKey &secret_key);
+    const SecretKey &secret_key() const { return sk_; }
+    void create_public_key(PublicKey &destination);
+    PublicKey create_public_key();
+    void create_relin_keys(RelinKeys &destination);
+    void create_galois_keys(const std::vector<int> &steps, GaloisKeys &destination);
+    void create_galois_keys(GaloisKeys &destination);
+    void create_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination);
+
+private:
+    void kswitch_key(const std::uint64_t *new_key_dev, PolyStore &dest);
+    SEALContext ctx_;
+    SecretKey sk_;
+    std::uint64_t rng_state_[2];
+    std::function<std::uint64_t()> rng_;
+};
+
+class CKKSEncoder
+{
+public:
+    explicit CKKSEncoder(const SEALContext &context);
+    ~CKKSEncoder();
+    std::size_t slot_count() const noexcept { return slots_; }
+    void set_sparse_slots(std::size_t sparse_slots) { sparse_slots_ = sparse_slots; }
+    void encode(const std::vector<double> &values, parms_id_type parms_id, double scale, Plaintext &destination,
+                MemoryPoolHandle = {});
+    void encode(const std::vector<std::complex<double>> &values, parms_id_type parms_id, double scale,
+                Plaintext &destination, MemoryPoolHandle = {});
+    void encode(const std::vector<double> &values, double scale, Plaintext &destination, MemoryPoolHandle = {});
+    void encode(const std::vector<std::complex<double>> &values, double scale, Plaintext &destination,
+                MemoryPoolHandle = {});
+    void encode(double value, parms_id_type parms_id, double scale, Plaintext &destination, MemoryPoolHandle = {});
+    void encode(double value, double scale, Plaintext &destination, MemoryPoolHandle = {});
+    void decode(const Plaintext &plain, std::vector<double> &destination, MemoryPoolHandle = {});
+    void decode(const Plaintext &plain, std::vector<std::complex<double>> &destination, MemoryPoolHandle = {});
+
+private:
+    void encode_internal(const double *re, const double *im, std::size_t count, parms_id_type parms_id,
+                         double scale, Plaintext &destination);
+    void decode_internal(const Plaintext &plain, std::vector<std::complex<double>> &out);
+    SEALContext ctx_;
+    mhe_encoder *enc_ = nullptr;
+    std::size_t slots_ = 0, sparse_slots_ = 0;
+    std::vector<std::size_t> index_map_;
+    std::vector<std::complex<double>> root_powers_;
+};
+
+class Encryptor
+{
+public:
+    Encryptor(const SEALContext &context, const PublicKey &public_key);
+    Encryptor(const SEALContext &context, const SecretKey &secret_key);
+    void encrypt(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void encrypt_zero(Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void encrypt_zero(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle = {}) const;
+
+private:
+    void encrypt_zero_at(std::size_t limbs, Ciphertext &dest) const;
+    SEALContext ctx_;
+    PublicKey pk_;
+    SecretKey sk_;
+    bool asymmetric_;
+    mutable std::mutex mu_;
+    mutable std::function<std::uint64_t()> rng_;
+};
+
+class Decryptor
+{
+public:
+    Decryptor(const SEALContext &context, const SecretKey &secret_key);
+    void decrypt(const Ciphertext &encrypted, Plaintext &destination);
+
+private:
+    SEALContext ctx_;
+    SecretKey sk_;
+};
+
+class Evaluator
+{
+public:
+    Evaluator(const SEALContext &context, CKKSEncoder &encoder);
+
+    void negate_inplace(Ciphertext &encrypted) const;
+    void negate(const Ciphertext &encrypted, Ciphertext &destination) const;
+    void add_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
+    void add(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const;
+    void add_many(const std::vector<Ciphertext> &encrypteds, Ciphertext &destination) const;
+    void sub_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
+    void sub(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const;
+    void multiply_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2, MemoryPoolHandle = {}) const;
+    void multiply(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
+                  MemoryPoolHandle = {}) const;
+    void square_inplace(Ciphertext &encrypted, MemoryPoolHandle = {}) const;
+    void square(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void relinearize_inplace(Ciphertext &encrypted, const RelinKeys &relin_keys, MemoryPoolHandle = {}) const;
+    void relinearize(const Ciphertext &encrypted, const RelinKeys &relin_keys, Ciphertext &destination,
+                     MemoryPoolHandle = {}) const;
+    void mod_switch_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle = {}) const;
+    void mod_switch_to_next(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void mod_switch_to_next_inplace(Plaintext &plain) const;
+    void mod_switch_to_inplace(Ciphertext &encrypted, parms_id_type parms_id, MemoryPoolHandle = {}) const;
+    void mod_switch_to(const Ciphertext &encrypted, parms_id_type parms_id, Ciphertext &destination,
+                       MemoryPoolHandle = {}) const;
+    void mod_switch_to_inplace(Plaintext &plain, parms_id_type parms_id) const;
+    void rescale_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle = {}) const;
+    void rescale_to_next(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void rescale_to_inplace(Ciphertext &encrypted, parms_id_type parms_id, MemoryPoolHandle = {}) const;
+    void multiply_plain_inplace(Ciphertext &encrypted, const Plaintext &plain, MemoryPoolHandle = {}) const;
+    void multiply_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination,
+                        MemoryPoolHandle = {}) const;
+    void add_plain_inplace(Ciphertext &encrypted, const Plaintext &plain) const;
+    void add_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination) const;
+    void sub_plain_inplace(Ciphertext &encrypted, const Plaintext &plain) const;
+    void sub_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination) const;
+    void transform_to_ntt_inplace(Ciphertext &encrypted) const;
+    void transform_from_ntt_inplace(Ciphertext &encrypted) const;
+    void apply_galois_inplace(Ciphertext &encrypted, std::uint32_t galois_elt, const GaloisKeys &galois_keys,
+                              MemoryPoolHandle = {}) const;
+    void rotate_vector_inplace(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
+                               MemoryPoolHandle = {}) const;
+    void rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
+                       Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKeys &galois_keys, MemoryPoolHandle = {}) const;
+    void complex_conjugate(const Ciphertext &encrypted, const GaloisKeys &galois_keys, Ciphertext &destination,
+                           MemoryPoolHandle = {}) const;
+
+    // modified SEAL (evaluator.h:1186-1285)
+    void add_const_inplace(Ciphertext &encrypted, double value) const;
+    void add_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const;
+    void multiply_const_inplace(Ciphertext &encrypted, double value) const;
+    void multiply_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const;
+    template <typename T>
+    void multiply_vector_inplace(Ciphertext &encrypted, const std::vector<T> &value) const;
+    template <typename T>
+    void multiply_vector(Ciphertext &encrypted, const std::vector<T> &value, Ciphertext &destination) const
+    {
+        destination = encrypted;
+        multiply_vector_inplace(destination, value);
+    }
+    void add_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
+    void add_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const;
+    void double_inplace(Ciphertext &encrypted) const { add_inplace(encrypted, encrypted); }
+    void sub_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
+    void sub_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const;
+    void multiply_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2,
+                                        const RelinKeys &relin_keys) const;
+    void multiply_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2,
+                                const RelinKeys &relin_keys, Ciphertext &destination) const;
+    template <typename T>
+    void multiply_vector_inplace_reduced_error(Ciphertext &encrypted, const std::vector<T> &value)
+    {
+        multiply_vector_inplace(encrypted, value);
+    }
+    template <typename T>
+    void multiply_vector_reduced_error(Ciphertext &encrypted, const std::vector<T> &value, Ciphertext &destination)
+    {
+        destination = encrypted;
+        multiply_vector_inplace_reduced_error(destination, value);
+    }
+
+private:
+    enum class Rmode
+    {
+        add,
+        sub,
+        mul
+    };
+    void reduced_error_op(Ciphertext &encrypted1, const Ciphertext &encrypted2, Rmode mode) const;
+    void switch_key(Ciphertext &encrypted, const std::uint64_t *target_dev, const KSwitchKeys &keys,
+                    std::size_t index) const;
+    void rotate_internal(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys) const;
+    std::size_t limbs_of(const parms_id_type &id) const;
+    SEALContext context_;
+    CKKSEncoder &encoder_;
+};
+
+extern template void Evaluator::multiply_vector_inplace<double>(Ciphertext &, const std::vector<double> &) const;
+extern template void Evaluator::multiply_vector_inplace<std::complex<double>>(
+    Ciphertext &, const std::vector<std::complex<double>> &) const;
+} // namespace seal

@@ -30,10 +30,14 @@ SIGNATURES = {
     "mhe_galois_elt_from_step": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_int]),
     "mhe_malloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
     "mhe_free": (ctypes.c_int, [vp, vp]),
+    "mhe_malloc_async": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t, vp]),
+    "mhe_free_async": (ctypes.c_int, [vp, vp, vp]),
     "mhe_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
     "mhe_memcpy_d2h": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
     "mhe_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
     "mhe_stream_sync": (ctypes.c_int, [vp, vp]),
+    "mhe_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+    "mhe_stream_destroy": (ctypes.c_int, [vp, vp]),
     "mhe_ntt_forward": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_ntt_inverse": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_add": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),

@@ -61,10 +61,19 @@ uint32_t mhe_galois_elt_from_step(int log_n, int step);
 /* ---- memory ----------------------------------------------------------------------- */
 int mhe_malloc(mhe_ctx *ctx, void **dptr, size_t bytes);
 int mhe_free(mhe_ctx *ctx, void *dptr);
+/* Stream-ordered allocation from the device memory pool (kept cached: Ciphertext temporaries
+ * are created and destroyed constantly by the reference's callers). */
+int mhe_malloc_async(mhe_ctx *ctx, void **dptr, size_t bytes, void *stream);
+int mhe_free_async(mhe_ctx *ctx, void *dptr, void *stream);
 int mhe_memcpy_h2d(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int mhe_memcpy_d2h(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int mhe_memcpy_d2d(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int mhe_stream_sync(mhe_ctx *ctx, void *stream);
+/* A non-blocking HIP stream on the context's device (and its scratch workspace); the SEAL
+ * shim gives every host thread its own, as the reference's OpenMP threads share one
+ * Evaluator (cnn/infer_seal.cpp:404). */
+int mhe_stream_create(mhe_ctx *ctx, void **stream);
+int mhe_stream_destroy(mhe_ctx *ctx, void *stream);
 
 /* ---- NTT ---------------------------------------------------------------------------
  * ntt_negacyclic_harvey(_lazy) / inverse_ntt_negacyclic_harvey(_lazy) on every limb l of
@@ -118,7 +127,8 @@ int mhe_apply_galois(mhe_ctx *ctx, uint64_t *ct, uint32_t galois_elt, const uint
 int mhe_permute_galois(mhe_ctx *ctx, const uint64_t *in, uint32_t galois_elt, uint64_t *out, int polys, int limbs,
                        void *stream);
 /* Evaluator::mod_switch_scale_to_next / RNSTool::divide_and_round_q_last_ntt_inplace
- * (evaluator.cpp:1118-1181, util/rns.cpp:737-808): in[size][L][n] -> out[size][L-1][n]. */
+ * (evaluator.cpp:1118-1181, util/rns.cpp:737-808): in[size][L][n] -> out[size][L-1][n].
+ * L may be the full key level (special prime last), as Encryptor uses it to drop P. */
 int mhe_rescale_to_next(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int size, int limbs, void *stream);
 /* Evaluator::mod_switch_drop_to_next (evaluator.cpp:1183-1281): in[size][L][n] ->
  * out[size][L-1][n] (limb copy; out may equal in for an in-place compaction). */
