@@ -177,10 +177,10 @@ extern "C" __attribute__((visibility("default"))) int mhe_encoder_destroy(mhe_en
     return MHE_OK;
 }
 
-extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode(mhe_ctx *c, const mhe_encoder *e,
-                                                                     const double *re, const double *im,
-                                                                     size_t count, double scale, int limbs,
-                                                                     uint64_t *out, void *stream)
+extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_at(mhe_ctx *c, const mhe_encoder *e,
+                                                                        const double *re, const double *im,
+                                                                        size_t count, double scale, int bound_limbs,
+                                                                        int limbs, uint64_t *out, void *stream)
 {
     const PrimeDev *primes;
     const uint64_t *q;
@@ -189,8 +189,9 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode(mhe_ctx *c
     if (!e || e->log_n != log_n) return mhe_internal_fail(MHE_ERR_ARG, "encoder does not match the context");
     if (!re && count > 0) return mhe_internal_fail(MHE_ERR_ARG, "values cannot be null");
     if (count > e->slots) return mhe_internal_fail(MHE_ERR_ARG, "values_size is too large");
-    if (limbs < 1 || limbs > K || !out) return mhe_internal_fail(MHE_ERR_ARG, "parms_id is not valid for encryption parameters");
-    const int tb = total_bits(q, limbs);
+    if (limbs < 1 || limbs > bound_limbs || bound_limbs > K || !out)
+        return mhe_internal_fail(MHE_ERR_ARG, "parms_id is not valid for encryption parameters");
+    const int tb = total_bits(q, bound_limbs);
     if (scale <= 0 || (static_cast<int>(std::log2(scale)) + 1 >= tb))
         return mhe_internal_fail(MHE_ERR_ARG, "scale out of bounds");
     const size_t n = e->n;
@@ -276,15 +277,25 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode(mhe_ctx *c
     return mhe_internal_ntt_forward(c, out, 1, limbs, 1, st);
 }
 
-extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_scalar(mhe_ctx *c, double value, double scale,
-                                                                            int limbs, uint64_t *residues)
+extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode(mhe_ctx *c, const mhe_encoder *e,
+                                                                     const double *re, const double *im,
+                                                                     size_t count, double scale, int limbs,
+                                                                     uint64_t *out, void *stream)
+{
+    return mhe_ckks_encode_at(c, e, re, im, count, scale, limbs, limbs, out, stream);
+}
+
+extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_scalar_at(mhe_ctx *c, double value, double scale,
+                                                                               int bound_limbs, int limbs,
+                                                                               uint64_t *residues)
 {
     const PrimeDev *primes;
     const uint64_t *q;
     int K, log_n;
     if (mhe_internal_primes(c, &primes, &q, &K, &log_n)) return mhe_internal_fail(MHE_ERR_ARG, "context is not valid");
-    if (limbs < 1 || limbs > K || !residues) return mhe_internal_fail(MHE_ERR_ARG, "parms_id is not valid for encryption parameters");
-    const int tb = total_bits(q, limbs);
+    if (limbs < 1 || limbs > bound_limbs || bound_limbs > K || !residues)
+        return mhe_internal_fail(MHE_ERR_ARG, "parms_id is not valid for encryption parameters");
+    const int tb = total_bits(q, bound_limbs);
     if (scale <= 0 || (static_cast<int>(std::log2(scale)) >= tb)) return mhe_internal_fail(MHE_ERR_ARG, "scale out of bounds");
     value *= scale;
     const int coeff_bits = static_cast<int>(std::log2(std::fabs(value))) + 2;
@@ -317,6 +328,226 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_scalar(mhe
     {
         const u64 r = words_mod(w, nw, q[j]);
         residues[j] = (is_neg && r) ? q[j] - r : r;
+    }
+    return MHE_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_scalar(mhe_ctx *c, double value, double scale,
+                                                                            int limbs, uint64_t *residues)
+{
+    return mhe_ckks_encode_scalar_at(c, value, scale, limbs, limbs, residues);
+}
+
+// ------------------------------------------------------------------------------------ decode
+// CKKSEncoder::decode (ckks.h:644-761).  The inverse NTT runs on the GPU; CRT composition
+// (RNSBase::compose_array, util/rns.cpp:354-400 -- its result is the canonical value in
+// [0, Q), so any exact composition gives SEAL's words), the sparse-slot mask (ckks.h:704-713),
+// SEAL's word-by-word double conversion (ckks.h:715-753) and transform_to_rev
+// (util/dwthandler.h:94-190) run on the host in SEAL's operation order.
+namespace
+{
+void fft_to_rev(cd *values, int log_n, const cd *roots)
+{
+    const size_t n = size_t(1) << log_n;
+    size_t gap = n >> 1, m = 1;
+    for (; m < (n >> 1); m <<= 1)
+    {
+        size_t offset = 0;
+        for (size_t i = 0; i < m; i++)
+        {
+            const cd r = *++roots;
+            cd *x = values + offset, *y = x + gap;
+            for (size_t j = 0; j < gap; j++)
+            {
+                const cd u = *x, v = *y * r;
+                *x++ = u + v;
+                *y++ = u - v;
+            }
+            offset += gap << 1;
+        }
+        gap >>= 1;
+    }
+    for (size_t i = 0; i < m; i++)
+    {
+        const cd r = *++roots;
+        const cd u = values[0], v = values[1] * r;
+        values[0] = u + v;
+        values[1] = u - v;
+        values += 2;
+    }
+}
+
+// a (L words) * s -> out (L words, truncated: every product here is < Q)
+void mp_mul_scalar(const u64 *a, size_t L, u64 s, u64 *out)
+{
+    u64 carry = 0;
+    for (size_t k = 0; k < L; k++)
+    {
+        const u128 p = (u128)a[k] * s + carry;
+        out[k] = (u64)p;
+        carry = (u64)(p >> 64);
+    }
+}
+
+bool mp_geq(const u64 *a, const u64 *b, size_t L)
+{
+    for (size_t k = L; k-- > 0;)
+        if (a[k] != b[k]) return a[k] > b[k];
+    return true;
+}
+
+void mp_sub(u64 *a, const u64 *b, size_t L)
+{
+    u64 borrow = 0;
+    for (size_t k = 0; k < L; k++)
+    {
+        const u128 d = (u128)a[k] - b[k] - borrow;
+        a[k] = (u64)d;
+        borrow = (u64)(d >> 64) & 1;
+    }
+}
+
+u64 inv_mod(u64 a, u64 q)
+{
+    // extended Euclid on signed 128-bit
+    __int128 t = 0, nt = 1, r = q, nr = a % q;
+    while (nr)
+    {
+        const __int128 qq = r / nr, tt = t - qq * nt, rr = r - qq * nr;
+        t = nt;
+        nt = tt;
+        r = nr;
+        nr = rr;
+    }
+    if (t < 0) t += q;
+    return (u64)t;
+}
+} // namespace
+
+extern "C" __attribute__((visibility("default"))) int mhe_ckks_decode(mhe_ctx *c, const mhe_encoder *e,
+                                                                     const uint64_t *plain, int limbs, double scale,
+                                                                     size_t sparse_slots, double *re, double *im,
+                                                                     void *stream)
+{
+    const PrimeDev *primes;
+    const uint64_t *q;
+    int K, log_n;
+    if (mhe_internal_primes(c, &primes, &q, &K, &log_n)) return mhe_internal_fail(MHE_ERR_ARG, "context is not valid");
+    if (!e || e->log_n != log_n) return mhe_internal_fail(MHE_ERR_ARG, "encoder does not match the context");
+    if (limbs < 1 || limbs > K || !plain) return mhe_internal_fail(MHE_ERR_ARG, "plain is not valid for encryption parameters");
+    if (!re) return mhe_internal_fail(MHE_ERR_ARG, "destination cannot be null");
+    if (!sparse_slots) sparse_slots = e->slots;
+    if (sparse_slots > e->slots || (sparse_slots & (sparse_slots - 1)))
+        return mhe_internal_fail(MHE_ERR_ARG, "sparse_slots must be a power of two <= slots");
+    if (scale <= 0 || static_cast<int>(std::log2(scale)) >= total_bits(q, limbs))
+        return mhe_internal_fail(MHE_ERR_ARG, "scale out of bounds");
+    const size_t n = e->n, L = (size_t)limbs;
+    hipStream_t st = (hipStream_t)stream;
+
+    std::vector<u64> x(n * L);
+    {
+        u64 *tmp = nullptr;
+        if (hipMallocAsync((void **)&tmp, n * L * sizeof(u64), st) != hipSuccess)
+            return mhe_internal_fail(MHE_ERR_MEMORY, "decode staging allocation failed");
+        hipError_t err = hipMemcpyAsync(tmp, plain, n * L * sizeof(u64), hipMemcpyDeviceToDevice, st);
+        int rc = err == hipSuccess ? mhe_ntt_inverse(c, tmp, 1, limbs, 0, stream) : MHE_ERR_DEVICE;
+        if (rc == MHE_OK)
+        {
+            err = hipMemcpyAsync(x.data(), tmp, n * L * sizeof(u64), hipMemcpyDeviceToHost, st);
+            if (err == hipSuccess) err = hipStreamSynchronize(st);
+            if (err != hipSuccess) rc = MHE_ERR_DEVICE;
+        }
+        (void)hipFreeAsync(tmp, st);
+        if (rc != MHE_OK) return rc == MHE_ERR_DEVICE ? mhe_internal_fail(rc, "decode transfer failed") : rc;
+    }
+
+    // RNSBase constants: Q, Q/q_j, (Q/q_j)^{-1} mod q_j
+    std::vector<u64> Q(L, 0), punct(L * L, 0), inv_punct(L), tmp(L);
+    Q[0] = 1;
+    for (size_t j = 0; j < L; j++)
+    {
+        mp_mul_scalar(Q.data(), L, q[j], tmp.data());
+        Q = tmp;
+    }
+    for (size_t j = 0; j < L; j++)
+    {
+        u64 *p = &punct[j * L];
+        p[0] = 1;
+        u64 pm = 1;
+        for (size_t k = 0; k < L; k++)
+        {
+            if (k == j) continue;
+            mp_mul_scalar(p, L, q[k], tmp.data());
+            std::memcpy(p, tmp.data(), L * sizeof(u64));
+            pm = (u64)(((u128)pm * (q[k] % q[j])) % q[j]);
+        }
+        inv_punct[j] = inv_mod(pm, q[j]);
+    }
+    std::vector<u64> thr(Q);
+    {
+        thr[0] += 1; // Q is odd: no carry out of word 0
+        for (size_t k = 0; k < L; k++) thr[k] = (thr[k] >> 1) | (k + 1 < L ? thr[k + 1] << 63 : 0);
+    }
+    const size_t sparsity = e->slots / sparse_slots;
+    const double two64 = std::pow(2.0, 64), inv_scale = 1.0 / scale;
+    std::vector<cd> res(n);
+    std::vector<u64> acc(L);
+    for (size_t i = 0; i < n; i++)
+    {
+        if (sparsity > 1 && ((i - 1) & (sparsity - 1)) != sparsity - 1)
+        {
+            res[i] = 0.0;
+            continue;
+        }
+        if (L == 1)
+            acc[0] = x[i];
+        else
+        {
+            std::fill(acc.begin(), acc.end(), 0);
+            for (size_t j = 0; j < L; j++)
+            {
+                const u64 t = (u64)(((u128)x[j * n + i] * inv_punct[j]) % q[j]);
+                mp_mul_scalar(&punct[j * L], L, t, tmp.data());
+                u64 carry = 0;
+                for (size_t k = 0; k < L; k++)
+                {
+                    const u128 s = (u128)acc[k] + tmp[k] + carry;
+                    acc[k] = (u64)s;
+                    carry = (u64)(s >> 64);
+                }
+                if (carry || mp_geq(acc.data(), Q.data(), L)) mp_sub(acc.data(), Q.data(), L);
+            }
+        }
+        double v = 0.0, s64 = inv_scale;
+        if (mp_geq(acc.data(), thr.data(), L))
+        {
+            for (size_t j = 0; j < L; j++, s64 *= two64)
+            {
+                if (acc[j] > Q[j])
+                {
+                    const u64 diff = acc[j] - Q[j];
+                    v += diff ? static_cast<double>(diff) * s64 : 0.0;
+                }
+                else
+                {
+                    const u64 diff = Q[j] - acc[j];
+                    v -= diff ? static_cast<double>(diff) * s64 : 0.0;
+                }
+            }
+        }
+        else
+        {
+            for (size_t j = 0; j < L; j++, s64 *= two64)
+                v += acc[j] ? static_cast<double>(acc[j]) * s64 : 0.0;
+        }
+        res[i] = cd(v, 0.0);
+    }
+    fft_to_rev(res.data(), log_n, e->root_powers.data());
+    for (size_t i = 0; i < sparse_slots; i++)
+    {
+        const cd z = res[e->index_map[i]];
+        re[i] = z.real();
+        if (im) im[i] = z.imag();
     }
     return MHE_OK;
 }

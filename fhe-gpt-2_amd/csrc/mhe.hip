@@ -634,8 +634,14 @@ __global__ void k_scalar(const u64 *a, u64 *out, const PrimeDev *primes, ScalarT
     const size_t i = i2 * 2;
     const int l = (int)((i >> log_n) % limbs);
     const u64 q = primes[l].q;
-    ulonglong2 x = *(const ulonglong2 *)(a + i);
     ulonglong2 r;
+    if (op == 2)
+    {
+        r.x = r.y = s.v[l];
+        *(ulonglong2 *)(out + i) = r;
+        return;
+    }
+    ulonglong2 x = *(const ulonglong2 *)(a + i);
     if (op == 0)
     {
         r.x = mul_shoup(x.x, s.v[l], s.vq[l], q);
@@ -1248,6 +1254,11 @@ MHE_EXPORT int mhe_add_scalar(mhe_ctx *c, const uint64_t *a, const uint64_t *sca
                               int limbs, void *s)
 {
     return launch_scalar(c, a, scalars, out, polys, limbs, 1, s);
+}
+
+MHE_EXPORT int mhe_set_scalar(mhe_ctx *c, const uint64_t *scalars, uint64_t *out, int polys, int limbs, void *s)
+{
+    return launch_scalar(c, out, scalars, out, polys, limbs, 2, s);
 }
 
 static int launch_tensor(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out3, int L, int square, hipStream_t st)

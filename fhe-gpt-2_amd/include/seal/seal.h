@@ -29,6 +29,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -182,8 +183,10 @@ public:
 
     // engine plumbing (not SEAL API)
     mhe_ctx *engine() const;
-    void *stream() const;      // this host thread's HIP stream on the engine
+    void *stream() const;         // this host thread's HIP stream on the engine
     std::size_t key_size() const; // primes at the key level (data + special)
+    std::shared_ptr<void> handle() const;
+    static void *stream_of(void *handle);
 
 private:
     struct Impl;
@@ -191,6 +194,12 @@ private:
 };
 
 // Device polynomial storage with a lazily synchronised host mirror.
+//
+// Cross-thread ordering: every access names the HIP stream it is issued on (the calling
+// thread's stream).  A read waits for the last writer if that was another stream; a write waits
+// for the readers and the writer on other streams.  This keeps the reference's pattern -- one
+// Evaluator shared by an OpenMP team, inputs produced by one thread and consumed by others --
+// correct while every thread's work stays asynchronous on its own stream.
 class PolyStore
 {
 public:
@@ -202,23 +211,32 @@ public:
     ~PolyStore();
 
     void bind(const SEALContext &ctx);
-    void resize_words(std::size_t words);
+    bool bound() const noexcept { return eng_ != nullptr; }
+    // resize to `words` u64; keeps the common prefix when `preserve`
+    void resize_words(std::size_t words, bool preserve = true);
     std::size_t words() const noexcept { return words_; }
-    std::uint64_t *device();                 // device copy, made current (host edits uploaded)
-    const std::uint64_t *device() const;
-    std::uint64_t *host();                   // host mirror, device marked stale
-    const std::uint64_t *host() const;       // host mirror, device stays current
-    void *stream() const;
+    const std::uint64_t *dev_read(void *stream) const;
+    std::uint64_t *dev_write(void *stream, bool overwrite = false);
+    std::uint64_t *host();             // host mirror, device marked stale
+    const std::uint64_t *host() const; // host mirror, device stays current
+    void *thread_stream() const;       // the calling thread's stream on the bound engine
+    mhe_ctx *engine() const noexcept { return eng_; }
 
 private:
     void release();
-    void *stream_now() const;
-    std::shared_ptr<void> hold_; // keeps the SEALContext engine alive
+    void wait_writer(void *stream) const;
+    void wait_all(void *stream) const;
+    void copy_from(const PolyStore &o);
+    std::shared_ptr<void> hold_; // SEALContext::Impl: keeps the engine and its streams alive
     mhe_ctx *eng_ = nullptr;
     std::uint64_t *dev_ = nullptr;
     std::size_t words_ = 0, cap_ = 0;
     mutable std::vector<std::uint64_t> host_;
     mutable bool host_valid_ = true, dev_valid_ = true;
+    mutable std::unique_ptr<std::mutex> mu_ = std::make_unique<std::mutex>();
+    mutable void *writer_ = nullptr;
+    mutable bool writer_done_ = true;
+    mutable std::vector<void *> readers_;
 };
 
 class Ciphertext
@@ -361,8 +379,7 @@ private:
     void kswitch_key(const std::uint64_t *new_key_dev, PolyStore &dest);
     SEALContext ctx_;
     SecretKey sk_;
-    std::uint64_t rng_state_[2];
-    std::function<std::uint64_t()> rng_;
+    std::shared_ptr<std::mt19937_64> rng_;
 };
 
 class CKKSEncoder
@@ -371,6 +388,7 @@ public:
     explicit CKKSEncoder(const SEALContext &context);
     ~CKKSEncoder();
     std::size_t slot_count() const noexcept { return slots_; }
+    const mhe_encoder *handle() const noexcept { return enc_; } // engine plumbing
     void set_sparse_slots(std::size_t sparse_slots) { sparse_slots_ = sparse_slots; }
     void encode(const std::vector<double> &values, parms_id_type parms_id, double scale, Plaintext &destination,
                 MemoryPoolHandle = {});
@@ -411,7 +429,7 @@ private:
     SecretKey sk_;
     bool asymmetric_;
     mutable std::mutex mu_;
-    mutable std::function<std::uint64_t()> rng_;
+    std::shared_ptr<std::mt19937_64> rng_;
 };
 
 class Decryptor
@@ -438,6 +456,10 @@ public:
     void sub_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
     void sub(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const;
     void multiply_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2, MemoryPoolHandle = {}) const;
+    void multiply_many(const std::vector<Ciphertext> &encrypteds, const RelinKeys &relin_keys,
+                       Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void exponentiate_inplace(Ciphertext &encrypted, std::uint64_t exponent, const RelinKeys &relin_keys,
+                              MemoryPoolHandle = {}) const;
     void multiply(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
                   MemoryPoolHandle = {}) const;
     void square_inplace(Ciphertext &encrypted, MemoryPoolHandle = {}) const;
@@ -488,14 +510,44 @@ public:
         multiply_vector_inplace(destination, value);
     }
     void add_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
-    void add_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const;
+    void add_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
+    {
+        // evaluator.h: operands swap when destination aliases encrypted2
+        if (&encrypted2 == &destination)
+            add_inplace_reduced_error(destination, encrypted1);
+        else
+        {
+            destination = encrypted1;
+            add_inplace_reduced_error(destination, encrypted2);
+        }
+    }
     void double_inplace(Ciphertext &encrypted) const { add_inplace(encrypted, encrypted); }
     void sub_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
-    void sub_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const;
+    void sub_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
+    {
+        // As the modified SEAL (evaluator.h): with destination aliasing encrypted2 the result is
+        // encrypted2 - encrypted1.  Kept for drop-in equality of results.
+        if (&encrypted2 == &destination)
+            sub_inplace_reduced_error(destination, encrypted1);
+        else
+        {
+            destination = encrypted1;
+            sub_inplace_reduced_error(destination, encrypted2);
+        }
+    }
     void multiply_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2,
                                         const RelinKeys &relin_keys) const;
     void multiply_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2,
-                                const RelinKeys &relin_keys, Ciphertext &destination) const;
+                                const RelinKeys &relin_keys, Ciphertext &destination) const
+    {
+        if (&encrypted2 == &destination)
+            multiply_inplace_reduced_error(destination, encrypted1, relin_keys);
+        else
+        {
+            destination = encrypted1;
+            multiply_inplace_reduced_error(destination, encrypted2, relin_keys);
+        }
+    }
     template <typename T>
     void multiply_vector_inplace_reduced_error(Ciphertext &encrypted, const std::vector<T> &value)
     {

@@ -46,6 +46,7 @@ SIGNATURES = {
     "mhe_multiply_plain": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_multiply_scalar": (ctypes.c_int, [vp, vp, u64p, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_add_scalar": (ctypes.c_int, [vp, vp, u64p, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_set_scalar": (ctypes.c_int, [vp, u64p, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_ct_multiply": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, vp]),
     "mhe_ct_square": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, vp]),
     "mhe_switch_key": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
@@ -60,6 +61,12 @@ SIGNATURES = {
     "mhe_ckks_encode": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                        ctypes.c_size_t, ctypes.c_double, ctypes.c_int, vp, vp]),
     "mhe_ckks_encode_scalar": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_int, u64p]),
+    "mhe_ckks_encode_at": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.c_size_t, ctypes.c_double, ctypes.c_int, ctypes.c_int, vp, vp]),
+    "mhe_ckks_decode": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_double, ctypes.c_size_t,
+                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), vp]),
+    "mhe_ckks_encode_scalar_at": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                                 u64p]),
 }
 
 
@@ -280,25 +287,44 @@ class Engine:
                                self.stream()))
         return out
 
-    def encode(self, values, scale, limbs, out=None):
-        """CKKSEncoder::encode -> NTT-form plaintext [limbs][n] on the device."""
-        if getattr(self, "_enc", None) is None:
-            h = vp()
-            _check(lib().mhe_encoder_create(ctypes.byref(h), self.log_n))
-            self._enc = h
+    def encode(self, values, scale, limbs, out=None, bound_limbs=None):
+        """CKKSEncoder::encode -> NTT-form plaintext [limbs][n] on the device.  `bound_limbs`
+        (default `limbs`) is the level SEAL's size checks use (encode at the first level then
+        mod_switch_to, evaluator.cpp:287-310)."""
+        self._encoder()
         v = np.asarray(values)
         re = np.ascontiguousarray(v.real, np.float64)
         im = np.ascontiguousarray(v.imag, np.float64) if np.iscomplexobj(v) else None
         out = self.empty(limbs, self.n) if out is None else out
         dp = ctypes.POINTER(ctypes.c_double)
-        _check(lib().mhe_ckks_encode(self._h, self._enc, re.ctypes.data_as(dp),
-                                     im.ctypes.data_as(dp) if im is not None else None, re.size, scale, limbs,
-                                     _ptr(out), self.stream()))
+        _check(lib().mhe_ckks_encode_at(self._h, self._enc, re.ctypes.data_as(dp),
+                                        im.ctypes.data_as(dp) if im is not None else None, re.size, scale,
+                                        limbs if bound_limbs is None else bound_limbs, limbs, _ptr(out),
+                                        self.stream()))
         return out
 
-    def encode_scalar(self, value, scale, limbs):
+    def _encoder(self):
+        if getattr(self, "_enc", None) is None:
+            h = vp()
+            _check(lib().mhe_encoder_create(ctypes.byref(h), self.log_n))
+            self._enc = h
+        return self._enc
+
+    def decode(self, plain, scale, sparse_slots=0):
+        """CKKSEncoder::decode: device NTT-form plaintext [limbs][n] -> complex numpy slots."""
+        limbs = plain.shape[-2]
+        cnt = sparse_slots or self.n // 2
+        re = np.zeros(cnt, np.float64)
+        im = np.zeros(cnt, np.float64)
+        dp = ctypes.POINTER(ctypes.c_double)
+        _check(lib().mhe_ckks_decode(self._h, self._encoder(), _ptr(plain), limbs, scale, sparse_slots,
+                                     re.ctypes.data_as(dp), im.ctypes.data_as(dp), self.stream()))
+        return re + 1j * im
+
+    def encode_scalar(self, value, scale, limbs, bound_limbs=None):
         out = (ctypes.c_uint64 * limbs)()
-        _check(lib().mhe_ckks_encode_scalar(self._h, value, scale, limbs, out))
+        _check(lib().mhe_ckks_encode_scalar_at(self._h, value, scale, limbs if bound_limbs is None else bound_limbs,
+                                               limbs, out))
         return list(out)
 
     def hmult_raw(self, a_ptr, b_ptr, key_ptr, key_limbs, out_ptr, L, stream):

@@ -1,0 +1,1760 @@
+// seal.cpp -- the SEAL-3.6-compatible C++ surface (include/seal/seal.h) over the C ABI of
+// include/mhe.h.  Host code only: every polynomial operation is one or a few libmhe calls on
+// the calling thread's HIP stream; this file owns the bookkeeping SEAL keeps around them
+// (parms_id chain, scales, sizes, argument checks and their exception messages).
+//
+// Reference behaviour followed (modified SEAL 3.6.6 under
+// gpt2_ckks/gpt2-ckks/single-key/seal-modified-3.6.6/native/src/seal/):
+//   context.cpp (modulus switching chain), ciphertext.h, plaintext.h, keygenerator.cpp,
+//   encryptor.cpp:88-166, decryptor.cpp (ckks_decrypt), ckks.h/ckks.cpp (CKKSEncoder),
+//   evaluator.cpp (all Evaluator entry points; line numbers cited per method).
+#include "seal/seal.h"
+
+#include "../../include/mhe.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <thread>
+#include <unordered_map>
+
+namespace seal
+{
+const parms_id_type parms_id_zero = { 0, 0, 0, 0 };
+
+namespace
+{
+[[noreturn]] void raise(int rc)
+{
+    const std::string msg = mhe_last_error();
+    switch (rc)
+    {
+    case MHE_ERR_ARG: throw std::invalid_argument(msg);
+    case MHE_ERR_RANGE:
+        if (msg.find("out of range") != std::string::npos) throw std::out_of_range(msg);
+        throw std::invalid_argument(msg);
+    default: throw std::runtime_error(msg);
+    }
+}
+
+inline void chk(int rc)
+{
+    if (rc != MHE_OK) raise(rc);
+}
+
+// util::are_close (util/common.h): |a-b| < eps * max(|a|, |b|, 1)
+bool are_close(double a, double b)
+{
+    const double scale = std::max({ std::fabs(a), std::fabs(b), 1.0 });
+    return std::fabs(a - b) < std::numeric_limits<double>::epsilon() * scale;
+}
+
+int product_bits(const std::vector<Modulus> &cm, std::size_t count)
+{
+    std::vector<std::uint64_t> prod(count + 1, 0);
+    prod[0] = 1;
+    std::size_t words = 1;
+    for (std::size_t j = 0; j < count; j++)
+    {
+        std::uint64_t carry = 0;
+        for (std::size_t w = 0; w < words; w++)
+        {
+            const unsigned __int128 t = (unsigned __int128)prod[w] * cm[j].value() + carry;
+            prod[w] = (std::uint64_t)t;
+            carry = (std::uint64_t)(t >> 64);
+        }
+        if (carry) prod[words++] = carry;
+    }
+    return (int)(64 * (words - 1)) + (64 - __builtin_clzll(prod[words - 1]));
+}
+
+std::uint64_t splitmix(std::uint64_t &x)
+{
+    std::uint64_t z = (x += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+std::uint64_t fresh_seed(const std::shared_ptr<UniformRandomGeneratorFactory> &f)
+{
+    if (f) return f->seed();
+    std::random_device rd;
+    return ((std::uint64_t)rd() << 32) ^ rd();
+}
+
+// ---- host samplers (util/rlwe.cpp): coefficient vectors, then RNS residues ----------------
+std::uint64_t uniform_below(std::mt19937_64 &g, std::uint64_t q)
+{
+    const std::uint64_t lim = std::numeric_limits<std::uint64_t>::max() - std::numeric_limits<std::uint64_t>::max() % q;
+    std::uint64_t v;
+    do v = g();
+    while (v >= lim);
+    return v % q;
+}
+
+// sample_poly_ternary: uniform {-1, 0, 1}
+std::vector<std::int64_t> sample_ternary(std::mt19937_64 &g, std::size_t n)
+{
+    std::vector<std::int64_t> c(n);
+    for (auto &x : c) x = (std::int64_t)uniform_below(g, 3) - 1;
+    return c;
+}
+
+// sample_poly_sparse_ternary (modified SEAL, keygenerator.cpp:76): exactly hw coefficients +-1
+std::vector<std::int64_t> sample_sparse_ternary(std::mt19937_64 &g, std::size_t n, std::size_t hw)
+{
+    std::vector<std::size_t> pos(n);
+    for (std::size_t i = 0; i < n; i++) pos[i] = i;
+    std::vector<std::int64_t> c(n, 0);
+    hw = std::min(hw, n);
+    for (std::size_t i = 0; i < hw; i++)
+    {
+        const std::size_t j = i + (std::size_t)uniform_below(g, n - i);
+        std::swap(pos[i], pos[j]);
+        c[pos[i]] = (g() & 1) ? 1 : -1;
+    }
+    return c;
+}
+
+// sample_poly_normal: ClippedNormalDistribution(0, 3.2, 6 * 3.2), truncated to int64
+std::vector<std::int64_t> sample_normal(std::mt19937_64 &g, std::size_t n)
+{
+    std::normal_distribution<double> d(0.0, 3.2);
+    std::vector<std::int64_t> c(n);
+    for (auto &x : c)
+    {
+        double v;
+        do v = d(g);
+        while (std::fabs(v) > 6 * 3.2);
+        x = static_cast<std::int64_t>(v);
+    }
+    return c;
+}
+
+void residues(const std::vector<std::int64_t> &c, const std::vector<Modulus> &cm, std::size_t limbs,
+              std::uint64_t *out)
+{
+    const std::size_t n = c.size();
+    for (std::size_t j = 0; j < limbs; j++)
+    {
+        const std::uint64_t q = cm[j].value();
+        for (std::size_t i = 0; i < n; i++)
+        {
+            const std::int64_t v = c[i];
+            out[j * n + i] = v >= 0 ? (std::uint64_t)v % q : (q - ((std::uint64_t)(-v) % q)) % q;
+        }
+    }
+}
+
+void uniform_poly(std::mt19937_64 &g, const std::vector<Modulus> &cm, std::size_t limbs, std::size_t n,
+                  std::uint64_t *out)
+{
+    for (std::size_t j = 0; j < limbs; j++)
+        for (std::size_t i = 0; i < n; i++) out[j * n + i] = uniform_below(g, cm[j].value());
+}
+} // namespace
+
+// ------------------------------------------------------------------------------ Modulus
+int Modulus::bit_count() const noexcept
+{
+    return value_ ? 64 - __builtin_clzll(value_) : 0;
+}
+
+std::vector<Modulus> CoeffModulus::Create(std::size_t poly_modulus_degree, std::vector<int> bit_sizes)
+{
+    std::vector<std::uint64_t> out(bit_sizes.size());
+    chk(mhe_coeff_modulus_create(poly_modulus_degree, bit_sizes.data(), (int)bit_sizes.size(), out.data()));
+    return std::vector<Modulus>(out.begin(), out.end());
+}
+
+Blake2xbPRNGFactory::Blake2xbPRNGFactory(const std::array<std::uint64_t, 8> &s) : seeded_(true), seed_(0)
+{
+    std::uint64_t h = 0x6a09e667f3bcc908ULL;
+    for (auto w : s)
+    {
+        h ^= w;
+        h = splitmix(h);
+    }
+    seed_ = h;
+}
+
+std::uint64_t Blake2xbPRNGFactory::seed() const
+{
+    return seeded_ ? seed_ : fresh_seed(nullptr);
+}
+
+parms_id_type EncryptionParameters::parms_id() const
+{
+    // Opaque 256-bit identifier of (scheme, n, coeff_modulus) (SEAL hashes the same fields).
+    parms_id_type id{};
+    std::uint64_t st = 0x243f6a8885a308d3ULL ^ (std::uint64_t)scheme_;
+    st ^= splitmix(st) ^ n_;
+    for (auto &m : coeff_modulus_) st = splitmix(st) ^ m.value();
+    for (auto &w : id) w = splitmix(st);
+    return id;
+}
+
+// ------------------------------------------------------------------------------ SEALContext
+struct SEALContext::Impl
+{
+    EncryptionParameters parms;
+    std::vector<std::shared_ptr<ContextData>> levels; // by number of primes - 1
+    std::map<parms_id_type, std::shared_ptr<const ContextData>> by_id;
+    std::shared_ptr<const ContextData> key, first, last;
+    mhe_ctx *eng = nullptr;
+    std::size_t K = 0;
+    std::mutex mu;
+    std::unordered_map<std::thread::id, void *> streams;
+
+    void *stream()
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = streams.find(std::this_thread::get_id());
+        if (it != streams.end()) return it->second;
+        void *s = nullptr;
+        chk(mhe_stream_create(eng, &s));
+        streams.emplace(std::this_thread::get_id(), s);
+        return s;
+    }
+
+    ~Impl()
+    {
+        for (auto &kv : streams)
+        {
+            (void)mhe_stream_sync(eng, kv.second);
+            (void)mhe_stream_destroy(eng, kv.second);
+        }
+        if (eng) (void)mhe_ctx_destroy(eng);
+    }
+};
+
+SEALContext::SEALContext(const EncryptionParameters &parms, bool expand_mod_chain, sec_level_type)
+{
+    if (parms.scheme() != scheme_type::ckks) throw std::invalid_argument("unsupported scheme");
+    const auto &cm = parms.coeff_modulus();
+    const std::size_t n = parms.poly_modulus_degree();
+    if (cm.empty()) throw std::invalid_argument("coeff_modulus is not set");
+    if (!n || (n & (n - 1))) throw std::invalid_argument("poly_modulus_degree is not a power of two");
+    int log_n = 0;
+    while ((std::size_t(1) << log_n) < n) log_n++;
+
+    auto impl = std::make_shared<Impl>();
+    impl->parms = parms;
+    impl->K = cm.size();
+    std::vector<std::uint64_t> q;
+    for (auto &m : cm) q.push_back(m.value());
+    int device = 0;
+    if (const char *d = std::getenv("MHE_DEVICE")) device = std::atoi(d);
+    chk(mhe_ctx_create(&impl->eng, log_n, q.data(), (int)q.size(), device));
+
+    // context.cpp: key level (all primes) -> first (drop the special prime) -> ... -> one prime
+    const std::size_t K = impl->K;
+    impl->levels.resize(K);
+    auto make_level = [&](std::size_t count) {
+        auto cd = std::make_shared<ContextData>();
+        cd->parms_ = parms;
+        cd->parms_.set_coeff_modulus(std::vector<Modulus>(cm.begin(), cm.begin() + count));
+        cd->parms_id_ = cd->parms_.parms_id();
+        cd->total_bits_ = product_bits(cm, count);
+        impl->levels[count - 1] = cd;
+        impl->by_id[cd->parms_id_] = cd;
+        return cd;
+    };
+    auto key = make_level(K);
+    impl->key = key;
+    if (K == 1)
+    {
+        key->chain_index_ = 0;
+        impl->first = impl->last = key;
+    }
+    else
+    {
+        key->chain_index_ = K - 1;
+        std::shared_ptr<ContextData> prev = key;
+        const std::size_t lowest = expand_mod_chain ? 1 : K - 1;
+        for (std::size_t c = K - 1; c >= lowest; c--)
+        {
+            auto cd = make_level(c);
+            cd->chain_index_ = c - 1;
+            cd->prev_ = prev;
+            prev->next_ = cd;
+            if (c == K - 1) impl->first = cd;
+            impl->last = cd;
+            prev = cd;
+            if (c == 1) break;
+        }
+    }
+    impl_ = impl;
+}
+
+std::shared_ptr<const SEALContext::ContextData> SEALContext::get_context_data(const parms_id_type &id) const
+{
+    auto it = impl_->by_id.find(id);
+    return it == impl_->by_id.end() ? nullptr : it->second;
+}
+std::shared_ptr<const SEALContext::ContextData> SEALContext::key_context_data() const { return impl_->key; }
+std::shared_ptr<const SEALContext::ContextData> SEALContext::first_context_data() const { return impl_->first; }
+std::shared_ptr<const SEALContext::ContextData> SEALContext::last_context_data() const { return impl_->last; }
+const parms_id_type &SEALContext::key_parms_id() const { return impl_->key->parms_id(); }
+const parms_id_type &SEALContext::first_parms_id() const { return impl_->first->parms_id(); }
+const parms_id_type &SEALContext::last_parms_id() const { return impl_->last->parms_id(); }
+bool SEALContext::parameters_set() const noexcept { return impl_ && impl_->eng; }
+bool SEALContext::using_keyswitching() const noexcept { return impl_ && impl_->K > 1; }
+mhe_ctx *SEALContext::engine() const { return impl_->eng; }
+void *SEALContext::stream() const { return impl_->stream(); }
+std::size_t SEALContext::key_size() const { return impl_->K; }
+std::shared_ptr<void> SEALContext::handle() const { return impl_; }
+void *SEALContext::stream_of(void *handle) { return static_cast<Impl *>(handle)->stream(); }
+
+// ------------------------------------------------------------------------------ PolyStore
+void PolyStore::bind(const SEALContext &ctx)
+{
+    if (eng_ == ctx.engine()) return;
+    release();
+    hold_ = ctx.handle();
+    eng_ = ctx.engine();
+}
+
+void *PolyStore::thread_stream() const
+{
+    if (!hold_) throw std::logic_error("polynomial storage is not bound to a context");
+    return SEALContext::stream_of(hold_.get());
+}
+
+void PolyStore::wait_writer(void *s) const
+{
+    if (writer_ && writer_ != s && !writer_done_)
+    {
+        chk(mhe_stream_sync(eng_, writer_));
+        writer_done_ = true;
+    }
+}
+
+void PolyStore::wait_all(void *s) const
+{
+    wait_writer(s);
+    for (void *r : readers_)
+        if (r != s) chk(mhe_stream_sync(eng_, r));
+    readers_.clear();
+}
+
+void PolyStore::release()
+{
+    if (dev_)
+    {
+        std::lock_guard<std::mutex> g(*mu_);
+        void *s = writer_ ? writer_ : thread_stream();
+        for (void *r : readers_)
+            if (r != s) (void)mhe_stream_sync(eng_, r);
+        (void)mhe_free_async(eng_, dev_, s);
+    }
+    dev_ = nullptr;
+    cap_ = 0;
+    readers_.clear();
+    writer_ = nullptr;
+    writer_done_ = true;
+}
+
+PolyStore::~PolyStore()
+{
+    release();
+}
+
+void PolyStore::resize_words(std::size_t words, bool preserve)
+{
+    if (!eng_) throw std::logic_error("polynomial storage is not bound to a context");
+    if (words <= cap_ || (!dev_valid_ && host_valid_))
+    {
+        words_ = words;
+        if (host_valid_ && host_.size() < words) host_.resize(words, 0);
+        if (!dev_valid_ && host_valid_ && words > cap_ && dev_)
+        {
+            // host is the authority: the device copy is reallocated on the next upload
+            std::lock_guard<std::mutex> g(*mu_);
+            void *s = thread_stream();
+            wait_all(s);
+            (void)mhe_free_async(eng_, dev_, s);
+            dev_ = nullptr;
+            cap_ = 0;
+        }
+        return;
+    }
+    void *s = thread_stream();
+    std::lock_guard<std::mutex> g(*mu_);
+    wait_all(s);
+    void *p = nullptr;
+    chk(mhe_malloc_async(eng_, &p, words * sizeof(std::uint64_t), s));
+    if (preserve && dev_ && words_) chk(mhe_memcpy_d2d(eng_, p, dev_, std::min(words_, words) * 8, s));
+    if (dev_) (void)mhe_free_async(eng_, dev_, s);
+    dev_ = static_cast<std::uint64_t *>(p);
+    cap_ = words;
+    words_ = words;
+    writer_ = s;
+    writer_done_ = false;
+    dev_valid_ = true;
+    if (preserve && host_valid_)
+        host_.resize(words, 0);
+    else
+    {
+        host_valid_ = false;
+        host_.clear();
+    }
+}
+
+const std::uint64_t *PolyStore::dev_read(void *s) const
+{
+    if (!eng_) throw std::logic_error("polynomial storage is not bound to a context");
+    std::lock_guard<std::mutex> g(*mu_);
+    if (!dev_valid_)
+    {
+        auto *self = const_cast<PolyStore *>(this);
+        if (!dev_ || cap_ < words_)
+        {
+            wait_all(s);
+            if (dev_) (void)mhe_free_async(eng_, dev_, s);
+            void *p = nullptr;
+            chk(mhe_malloc_async(eng_, &p, words_ * sizeof(std::uint64_t), s));
+            self->dev_ = static_cast<std::uint64_t *>(p);
+            self->cap_ = words_;
+        }
+        wait_all(s);
+        chk(mhe_memcpy_h2d(eng_, dev_, host_.data(), words_ * 8, s));
+        chk(mhe_stream_sync(eng_, s));
+        dev_valid_ = true;
+        writer_ = s;
+        writer_done_ = true;
+    }
+    wait_writer(s);
+    if (writer_ != s && std::find(readers_.begin(), readers_.end(), s) == readers_.end()) readers_.push_back(s);
+    return dev_;
+}
+
+std::uint64_t *PolyStore::dev_write(void *s, bool overwrite)
+{
+    if (!eng_) throw std::logic_error("polynomial storage is not bound to a context");
+    if (!dev_valid_)
+    {
+        if (overwrite)
+        {
+            std::lock_guard<std::mutex> g(*mu_);
+            if (!dev_ || cap_ < words_)
+            {
+                wait_all(s);
+                if (dev_) (void)mhe_free_async(eng_, dev_, s);
+                void *p = nullptr;
+                chk(mhe_malloc_async(eng_, &p, words_ * sizeof(std::uint64_t), s));
+                dev_ = static_cast<std::uint64_t *>(p);
+                cap_ = words_;
+            }
+            dev_valid_ = true;
+        }
+        else
+            (void)dev_read(s);
+    }
+    std::lock_guard<std::mutex> g(*mu_);
+    wait_all(s);
+    writer_ = s;
+    writer_done_ = false;
+    host_valid_ = false;
+    return dev_;
+}
+
+const std::uint64_t *PolyStore::host() const
+{
+    if (!host_valid_)
+    {
+        std::lock_guard<std::mutex> g(*mu_);
+        void *s = writer_ ? writer_ : thread_stream();
+        host_.resize(words_);
+        if (words_)
+        {
+            chk(mhe_memcpy_d2h(eng_, host_.data(), dev_, words_ * 8, s));
+            chk(mhe_stream_sync(eng_, s));
+        }
+        writer_done_ = true;
+        host_valid_ = true;
+    }
+    return host_.data();
+}
+
+std::uint64_t *PolyStore::host()
+{
+    const PolyStore *c = this;
+    c->host();
+    if (eng_)
+    {
+        std::lock_guard<std::mutex> g(*mu_);
+        for (void *r : readers_) chk(mhe_stream_sync(eng_, r));
+        readers_.clear();
+        dev_valid_ = false;
+    }
+    return host_.data();
+}
+
+void PolyStore::copy_from(const PolyStore &o)
+{
+    hold_ = o.hold_;
+    eng_ = o.eng_;
+    words_ = o.words_;
+    if (!eng_ || (!o.dev_valid_ && o.host_valid_))
+    {
+        host_ = o.host_;
+        host_valid_ = true;
+        dev_valid_ = !eng_;
+        return;
+    }
+    void *s = thread_stream();
+    const std::uint64_t *src = o.dev_read(s);
+    void *p = nullptr;
+    chk(mhe_malloc_async(eng_, &p, std::max<std::size_t>(words_, 1) * 8, s));
+    if (words_) chk(mhe_memcpy_d2d(eng_, p, src, words_ * 8, s));
+    dev_ = static_cast<std::uint64_t *>(p);
+    cap_ = words_;
+    writer_ = s;
+    writer_done_ = false;
+    dev_valid_ = true;
+    host_valid_ = false;
+}
+
+PolyStore::PolyStore(const PolyStore &o)
+{
+    copy_from(o);
+}
+
+PolyStore &PolyStore::operator=(const PolyStore &o)
+{
+    if (this == &o) return *this;
+    if (eng_ && eng_ == o.eng_ && dev_ && cap_ >= o.words_ && (o.dev_valid_ || !o.host_valid_))
+    {
+        // same engine, enough room: copy in place on this thread's stream
+        void *s = thread_stream();
+        const std::uint64_t *src = o.dev_read(s);
+        std::uint64_t *dst = dev_write(s, true);
+        words_ = o.words_;
+        if (words_) chk(mhe_memcpy_d2d(eng_, dst, src, words_ * 8, s));
+        return *this;
+    }
+    release();
+    copy_from(o);
+    return *this;
+}
+
+PolyStore::PolyStore(PolyStore &&o) noexcept
+{
+    *this = std::move(o);
+}
+
+PolyStore &PolyStore::operator=(PolyStore &&o) noexcept
+{
+    if (this == &o) return *this;
+    std::swap(hold_, o.hold_);
+    std::swap(eng_, o.eng_);
+    std::swap(dev_, o.dev_);
+    std::swap(words_, o.words_);
+    std::swap(cap_, o.cap_);
+    std::swap(host_, o.host_);
+    std::swap(host_valid_, o.host_valid_);
+    std::swap(dev_valid_, o.dev_valid_);
+    std::swap(mu_, o.mu_);
+    std::swap(writer_, o.writer_);
+    std::swap(writer_done_, o.writer_done_);
+    std::swap(readers_, o.readers_);
+    return *this;
+}
+
+// ------------------------------------------------------------------------------ Ciphertext
+Ciphertext::Ciphertext(const SEALContext &context, MemoryPoolHandle) : Ciphertext(context, context.first_parms_id())
+{}
+
+Ciphertext::Ciphertext(const SEALContext &context, parms_id_type parms_id, MemoryPoolHandle)
+{
+    auto cd = context.get_context_data(parms_id);
+    if (!cd) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    store_.bind(context);
+    parms_id_ = parms_id;
+    coeff_modulus_size_ = cd->parms().coeff_modulus().size();
+    poly_modulus_degree_ = cd->parms().poly_modulus_degree();
+}
+
+void Ciphertext::resize(const SEALContext &context, parms_id_type parms_id, std::size_t size)
+{
+    auto cd = context.get_context_data(parms_id);
+    if (!cd) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    if (size < 2 && size != 0) throw std::invalid_argument("invalid size");
+    store_.bind(context);
+    parms_id_ = parms_id;
+    coeff_modulus_size_ = cd->parms().coeff_modulus().size();
+    poly_modulus_degree_ = cd->parms().poly_modulus_degree();
+    size_ = size;
+    store_.resize_words(size * coeff_modulus_size_ * poly_modulus_degree_);
+}
+
+void Ciphertext::resize(const SEALContext &context, std::size_t size)
+{
+    resize(context, parms_id_ == parms_id_zero ? context.first_parms_id() : parms_id_, size);
+}
+
+void Ciphertext::resize(std::size_t size)
+{
+    if (size < 2 && size != 0) throw std::invalid_argument("invalid size");
+    size_ = size;
+    store_.resize_words(size * coeff_modulus_size_ * poly_modulus_degree_);
+}
+
+bool Ciphertext::is_transparent() const
+{
+    if (!store_.words() || size_ < 2) return false;
+    const std::uint64_t *p = data(1);
+    const std::size_t cnt = (size_ - 1) * coeff_modulus_size_ * poly_modulus_degree_;
+    return std::all_of(p, p + cnt, [](std::uint64_t x) { return x == 0; });
+}
+
+void Plaintext::set_level(const SEALContext &ctx, const parms_id_type &id, std::size_t limbs)
+{
+    store_.bind(ctx);
+    store_.resize_words(limbs * ctx.key_context_data()->parms().poly_modulus_degree(), false);
+    parms_id_ = id;
+    limbs_ = limbs;
+}
+
+const PolyStore &KSwitchKeys::key(std::size_t i) const
+{
+    auto it = keys_.find(i);
+    if (it == keys_.end()) throw std::out_of_range("kswitch_keys_index");
+    return it->second;
+}
+
+// ------------------------------------------------------------------------------ KeyGenerator
+// keygenerator.cpp: secret key (sparse ternary with the modified hamming weight, else ternary)
+// in NTT form at the key level; public key and key-switching keys are symmetric encryptions of
+// zero at the key level (rlwe.cpp encrypt_zero_symmetric), the latter with
+// (P mod q_i) * s'_i added to digit i's limb i (keygenerator.cpp:384-414).
+namespace
+{
+struct Poly
+{
+    std::vector<std::uint64_t> h;
+};
+
+// temporary device buffer on stream s
+struct DevBuf
+{
+    mhe_ctx *eng;
+    void *s;
+    std::uint64_t *p = nullptr;
+    DevBuf(mhe_ctx *e, void *st, std::size_t words) : eng(e), s(st)
+    {
+        void *q = nullptr;
+        chk(mhe_malloc_async(eng, &q, std::max<std::size_t>(words, 1) * 8, s));
+        p = static_cast<std::uint64_t *>(q);
+    }
+    ~DevBuf() { (void)mhe_free_async(eng, p, s); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+};
+
+void upload(mhe_ctx *eng, void *s, std::uint64_t *dst, const std::vector<std::uint64_t> &h)
+{
+    chk(mhe_memcpy_h2d(eng, dst, h.data(), h.size() * 8, s));
+    chk(mhe_stream_sync(eng, s)); // the host vector is temporary
+}
+
+// c0 = e - c1 * s over `limbs` primes; c1 uniform (already NTT form), e sampled + NTT
+void encrypt_zero_symmetric(const SEALContext &ctx, std::mt19937_64 &g, const std::uint64_t *sk, std::size_t limbs,
+                            std::uint64_t *c0, std::uint64_t *c1, void *s)
+{
+    mhe_ctx *eng = ctx.engine();
+    const auto &cm = ctx.key_context_data()->parms().coeff_modulus();
+    const std::size_t n = ctx.key_context_data()->parms().poly_modulus_degree();
+    std::vector<std::uint64_t> h(limbs * n);
+    uniform_poly(g, cm, limbs, n, h.data());
+    upload(eng, s, c1, h);
+    residues(sample_normal(g, n), cm, limbs, h.data());
+    upload(eng, s, c0, h);
+    chk(mhe_ntt_forward(eng, c0, 1, (int)limbs, 0, s));
+    DevBuf t(eng, s, limbs * n);
+    chk(mhe_multiply_plain(eng, c1, sk, t.p, 1, (int)limbs, s));
+    chk(mhe_sub(eng, c0, t.p, c0, 1, (int)limbs, s));
+}
+} // namespace
+
+KeyGenerator::KeyGenerator(const SEALContext &context) : ctx_(context)
+{
+    const auto &parms = context.key_context_data()->parms();
+    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(parms.random_generator()));
+    const std::size_t K = context.key_size(), n = parms.poly_modulus_degree();
+    const std::size_t hw = parms.secret_key_hamming_weight();
+    auto c = hw ? sample_sparse_ternary(*rng_, n, hw) : sample_ternary(*rng_, n);
+    std::vector<std::uint64_t> h(K * n);
+    residues(c, parms.coeff_modulus(), K, h.data());
+    void *s = context.stream();
+    sk_.data().set_level(context, context.key_parms_id(), K);
+    std::uint64_t *d = sk_.data().store().dev_write(s, true);
+    upload(context.engine(), s, d, h);
+    chk(mhe_ntt_forward(context.engine(), d, 1, (int)K, 0, s));
+}
+
+KeyGenerator::KeyGenerator(const SEALContext &context, const SecretKey &secret_key) : ctx_(context), sk_(secret_key)
+{
+    if (secret_key.parms_id() != context.key_parms_id())
+        throw std::invalid_argument("secret key is not valid for encryption parameters");
+    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(context.key_context_data()->parms().random_generator()));
+}
+
+void KeyGenerator::create_public_key(PublicKey &destination)
+{
+    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    void *s = ctx_.stream();
+    Ciphertext &pk = destination.data();
+    pk.resize(ctx_, ctx_.key_parms_id(), 2);
+    pk.is_ntt_form() = true;
+    pk.scale() = 1.0;
+    std::uint64_t *d = pk.store().dev_write(s, true);
+    encrypt_zero_symmetric(ctx_, *rng_, sk_.data().store().dev_read(s), K, d, d + K * n, s);
+}
+
+PublicKey KeyGenerator::create_public_key()
+{
+    PublicKey pk;
+    create_public_key(pk);
+    return pk;
+}
+
+void KeyGenerator::kswitch_key(const std::uint64_t *new_key, PolyStore &dest)
+{
+    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    const auto &cm = ctx_.key_context_data()->parms().coeff_modulus();
+    if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
+    void *s = ctx_.stream();
+    dest.bind(ctx_);
+    dest.resize_words((K - 1) * 2 * K * n, false);
+    std::uint64_t *d = dest.dev_write(s, true);
+    const std::uint64_t *sk = sk_.data().store().dev_read(s);
+    DevBuf t(ctx_.engine(), s, K * n);
+    const std::uint64_t P = cm[K - 1].value();
+    for (std::size_t j = 0; j + 1 < K; j++)
+    {
+        std::uint64_t *c0 = d + j * 2 * K * n, *c1 = c0 + K * n;
+        encrypt_zero_symmetric(ctx_, *rng_, sk, K, c0, c1, s);
+        std::vector<std::uint64_t> f(K, 0);
+        f[j] = P % cm[j].value();
+        chk(mhe_multiply_scalar(ctx_.engine(), new_key, f.data(), t.p, 1, (int)K, s));
+        chk(mhe_add(ctx_.engine(), c0, t.p, c0, 1, (int)K, s));
+    }
+}
+
+void KeyGenerator::create_relin_keys(RelinKeys &destination)
+{
+    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    void *s = ctx_.stream();
+    DevBuf s2(ctx_.engine(), s, K * n);
+    const std::uint64_t *sk = sk_.data().store().dev_read(s);
+    chk(mhe_multiply_plain(ctx_.engine(), sk, sk, s2.p, 1, (int)K, s));
+    kswitch_key(s2.p, destination.key_mut(RelinKeys::get_index(2)));
+    destination.parms_id() = ctx_.key_parms_id();
+    destination.set_key_limbs(K);
+}
+
+void KeyGenerator::create_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination)
+{
+    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    void *s = ctx_.stream();
+    DevBuf rot(ctx_.engine(), s, K * n);
+    for (std::uint32_t elt : elts)
+    {
+        if (!(elt & 1) || elt >= 2 * n) throw std::invalid_argument("Galois element is not valid");
+        if (destination.has_key(elt)) continue;
+        const std::uint64_t *sk = sk_.data().store().dev_read(s);
+        chk(mhe_permute_galois(ctx_.engine(), sk, elt, rot.p, 1, (int)K, s));
+        kswitch_key(rot.p, destination.key_mut(GaloisKeys::get_index(elt)));
+    }
+    destination.parms_id() = ctx_.key_parms_id();
+    destination.set_key_limbs(K);
+}
+
+void KeyGenerator::create_galois_keys(const std::vector<int> &steps, GaloisKeys &destination)
+{
+    // GaloisTool::get_elts_from_steps (util/galois.cpp:96-104)
+    const int log_n = __builtin_ctzll(ctx_.key_context_data()->parms().poly_modulus_degree());
+    std::vector<std::uint32_t> elts;
+    for (int st : steps)
+    {
+        const std::uint32_t e = mhe_galois_elt_from_step(log_n, st);
+        if (!e) throw std::invalid_argument("step count too large");
+        elts.push_back(e);
+    }
+    create_galois_keys_from_elts(elts, destination);
+}
+
+void KeyGenerator::create_galois_keys(GaloisKeys &destination)
+{
+    // GaloisTool::get_elts_all (util/galois.cpp:106-131), generator 5
+    const std::size_t n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    const std::uint64_t m = 2 * n;
+    int log_n = __builtin_ctzll(n);
+    std::vector<std::uint32_t> elts{ (std::uint32_t)(m - 1) };
+    std::uint64_t pos = 5, neg = 1;
+    // inverse of 5 mod m (m a power of two): 5^(m/4 - 1)
+    for (std::uint64_t k = 0; k < m / 4 - 1; k++) neg = (neg * 5) & (m - 1);
+    for (int i = 0; i < log_n - 1; i++)
+    {
+        elts.push_back((std::uint32_t)pos);
+        pos = (pos * pos) & (m - 1);
+        elts.push_back((std::uint32_t)neg);
+        neg = (neg * neg) & (m - 1);
+    }
+    create_galois_keys_from_elts(elts, destination);
+}
+
+// ------------------------------------------------------------------------------ CKKSEncoder
+CKKSEncoder::CKKSEncoder(const SEALContext &context) : ctx_(context)
+{
+    const auto &parms = context.first_context_data()->parms();
+    const std::size_t n = parms.poly_modulus_degree();
+    slots_ = n >> 1;
+    sparse_slots_ = parms.sparse_slots() ? parms.sparse_slots() : slots_;
+    chk(mhe_encoder_create(&enc_, __builtin_ctzll(n)));
+}
+
+CKKSEncoder::~CKKSEncoder()
+{
+    if (enc_) (void)mhe_encoder_destroy(enc_);
+}
+
+void CKKSEncoder::encode_internal(const double *re, const double *im, std::size_t count, parms_id_type parms_id,
+                                  double scale, Plaintext &destination)
+{
+    auto cd = ctx_.get_context_data(parms_id);
+    if (!cd) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    const std::size_t L = cd->parms().coeff_modulus().size();
+    if (count > slots_) throw std::invalid_argument("values_size is too large");
+    void *s = ctx_.stream();
+    destination.set_level(ctx_, parms_id, L);
+    destination.scale() = scale;
+    chk(mhe_ckks_encode(ctx_.engine(), enc_, re, im, count, scale, (int)L, destination.store().dev_write(s, true),
+                        s));
+}
+
+void CKKSEncoder::encode(const std::vector<double> &values, parms_id_type parms_id, double scale,
+                         Plaintext &destination, MemoryPoolHandle)
+{
+    encode_internal(values.data(), nullptr, values.size(), parms_id, scale, destination);
+}
+
+void CKKSEncoder::encode(const std::vector<std::complex<double>> &values, parms_id_type parms_id, double scale,
+                         Plaintext &destination, MemoryPoolHandle)
+{
+    std::vector<double> re(values.size()), im(values.size());
+    for (std::size_t i = 0; i < values.size(); i++)
+    {
+        re[i] = values[i].real();
+        im[i] = values[i].imag();
+    }
+    encode_internal(re.data(), im.data(), values.size(), parms_id, scale, destination);
+}
+
+void CKKSEncoder::encode(const std::vector<double> &values, double scale, Plaintext &destination, MemoryPoolHandle)
+{
+    encode(values, ctx_.first_parms_id(), scale, destination);
+}
+
+void CKKSEncoder::encode(const std::vector<std::complex<double>> &values, double scale, Plaintext &destination,
+                         MemoryPoolHandle)
+{
+    encode(values, ctx_.first_parms_id(), scale, destination);
+}
+
+void CKKSEncoder::encode(double value, parms_id_type parms_id, double scale, Plaintext &destination, MemoryPoolHandle)
+{
+    auto cd = ctx_.get_context_data(parms_id);
+    if (!cd) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    const std::size_t L = cd->parms().coeff_modulus().size();
+    std::vector<std::uint64_t> r(L);
+    chk(mhe_ckks_encode_scalar(ctx_.engine(), value, scale, (int)L, r.data()));
+    void *s = ctx_.stream();
+    destination.set_level(ctx_, parms_id, L);
+    destination.scale() = scale;
+    chk(mhe_set_scalar(ctx_.engine(), r.data(), destination.store().dev_write(s, true), 1, (int)L, s));
+}
+
+void CKKSEncoder::encode(double value, double scale, Plaintext &destination, MemoryPoolHandle)
+{
+    encode(value, ctx_.first_parms_id(), scale, destination);
+}
+
+void CKKSEncoder::decode_internal(const Plaintext &plain, std::vector<std::complex<double>> &out)
+{
+    if (!plain.is_ntt_form()) throw std::invalid_argument("plain is not in NTT form");
+    auto cd = ctx_.get_context_data(plain.parms_id());
+    if (!cd) throw std::invalid_argument("plain is not valid for encryption parameters");
+    const std::size_t L = cd->parms().coeff_modulus().size();
+    std::vector<double> re(sparse_slots_), im(sparse_slots_);
+    void *s = ctx_.stream();
+    chk(mhe_ckks_decode(ctx_.engine(), enc_, plain.store().dev_read(s), (int)L, plain.scale(),
+                        sparse_slots_ == slots_ ? 0 : sparse_slots_, re.data(), im.data(), s));
+    out.resize(sparse_slots_);
+    for (std::size_t i = 0; i < sparse_slots_; i++) out[i] = { re[i], im[i] };
+}
+
+void CKKSEncoder::decode(const Plaintext &plain, std::vector<std::complex<double>> &destination, MemoryPoolHandle)
+{
+    decode_internal(plain, destination);
+}
+
+void CKKSEncoder::decode(const Plaintext &plain, std::vector<double> &destination, MemoryPoolHandle)
+{
+    std::vector<std::complex<double>> z;
+    decode_internal(plain, z);
+    destination.resize(z.size());
+    for (std::size_t i = 0; i < z.size(); i++) destination[i] = z[i].real();
+}
+
+// ------------------------------------------------------------------------------ Encryptor
+Encryptor::Encryptor(const SEALContext &context, const PublicKey &public_key)
+    : ctx_(context), pk_(public_key), asymmetric_(true)
+{
+    if (public_key.parms_id() != context.key_parms_id())
+        throw std::invalid_argument("public key is not valid for encryption parameters");
+    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(context.key_context_data()->parms().random_generator()));
+}
+
+Encryptor::Encryptor(const SEALContext &context, const SecretKey &secret_key)
+    : ctx_(context), sk_(secret_key), asymmetric_(false)
+{
+    if (secret_key.parms_id() != context.key_parms_id())
+        throw std::invalid_argument("secret key is not valid for encryption parameters");
+    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(context.key_context_data()->parms().random_generator()));
+}
+
+void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
+{
+    // encryptor.cpp:88-166 (encrypt_zero_internal): public-key encryption runs one level up
+    // (the key level for the first data level) and is rescaled down, dividing the noise by the
+    // dropped prime; secret-key encryption runs at the level itself.
+    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    const auto &cm = ctx_.key_context_data()->parms().coeff_modulus();
+    mhe_ctx *eng = ctx_.engine();
+    void *s = ctx_.stream();
+    std::uint64_t *d = dest.store().dev_write(s, true);
+    std::lock_guard<std::mutex> g(mu_);
+    if (!asymmetric_)
+    {
+        encrypt_zero_symmetric(ctx_, *rng_, sk_.data().store().dev_read(s), L, d, d + L * n, s);
+        return;
+    }
+    const std::size_t m = L < K ? L + 1 : L; // prev level (key level for the first level)
+    const std::uint64_t *pk = pk_.data().store().dev_read(s);
+    DevBuf u(eng, s, m * n), c(eng, s, 2 * m * n), e(eng, s, m * n);
+    std::vector<std::uint64_t> h(m * n);
+    residues(sample_ternary(*rng_, n), cm, m, h.data());
+    upload(eng, s, u.p, h);
+    chk(mhe_ntt_forward(eng, u.p, 1, (int)m, 0, s));
+    for (int j = 0; j < 2; j++)
+    {
+        // pk_j restricted to the first m primes: limbs 0..m-1 of poly j ([2][K][n] layout)
+        chk(mhe_multiply_plain(eng, pk + j * K * n, u.p, c.p + j * m * n, 1, (int)m, s));
+        residues(sample_normal(*rng_, n), cm, m, h.data());
+        upload(eng, s, e.p, h);
+        chk(mhe_ntt_forward(eng, e.p, 1, (int)m, 0, s));
+        chk(mhe_add(eng, c.p + j * m * n, e.p, c.p + j * m * n, 1, (int)m, s));
+    }
+    if (m == L)
+        chk(mhe_memcpy_d2d(eng, d, c.p, 2 * L * n * 8, s));
+    else
+        chk(mhe_rescale_to_next(eng, c.p, d, 2, (int)m, s));
+}
+
+void Encryptor::encrypt_zero(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle) const
+{
+    auto cd = ctx_.get_context_data(parms_id);
+    if (!cd) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    destination.resize(ctx_, parms_id, 2);
+    destination.is_ntt_form() = true;
+    destination.scale() = 1.0;
+    encrypt_zero_at(cd->parms().coeff_modulus().size(), destination);
+}
+
+void Encryptor::encrypt_zero(Ciphertext &destination, MemoryPoolHandle pool) const
+{
+    encrypt_zero(ctx_.first_parms_id(), destination, pool);
+}
+
+void Encryptor::encrypt(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle) const
+{
+    if (!plain.is_ntt_form()) throw std::invalid_argument("plain must be in NTT form");
+    auto cd = ctx_.get_context_data(plain.parms_id());
+    if (!cd) throw std::invalid_argument("plain is not valid for encryption parameters");
+    const std::size_t L = cd->parms().coeff_modulus().size();
+    encrypt_zero(plain.parms_id(), destination);
+    void *s = ctx_.stream();
+    std::uint64_t *d = destination.store().dev_write(s);
+    chk(mhe_add(ctx_.engine(), d, plain.store().dev_read(s), d, 1, (int)L, s));
+    destination.scale() = plain.scale();
+}
+
+// ------------------------------------------------------------------------------ Decryptor
+Decryptor::Decryptor(const SEALContext &context, const SecretKey &secret_key) : ctx_(context), sk_(secret_key)
+{
+    if (secret_key.parms_id() != context.key_parms_id())
+        throw std::invalid_argument("secret key is not valid for encryption parameters");
+}
+
+void Decryptor::decrypt(const Ciphertext &encrypted, Plaintext &destination)
+{
+    // decryptor.cpp ckks_decrypt: <(c0, c1, c2, ...), (1, s, s^2, ...)> in NTT form
+    auto cd = ctx_.get_context_data(encrypted.parms_id());
+    if (!cd || encrypted.size() < 2) throw std::invalid_argument("encrypted is not valid for encryption parameters");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+    const std::size_t L = cd->parms().coeff_modulus().size(), n = cd->parms().poly_modulus_degree();
+    mhe_ctx *eng = ctx_.engine();
+    void *s = ctx_.stream();
+    const std::uint64_t *c = encrypted.store().dev_read(s);
+    const std::uint64_t *sk = sk_.data().store().dev_read(s);
+    Plaintext out;
+    out.set_level(ctx_, encrypted.parms_id(), L);
+    std::uint64_t *d = out.store().dev_write(s, true);
+    chk(mhe_memcpy_d2d(eng, d, c, L * n * 8, s));
+    DevBuf t(eng, s, L * n), sp(eng, s, L * n);
+    chk(mhe_memcpy_d2d(eng, sp.p, sk, L * n * 8, s)); // s restricted to the level (first L limbs)
+    for (std::size_t k = 1; k < encrypted.size(); k++)
+    {
+        if (k > 1) chk(mhe_multiply_plain(eng, sp.p, sk, sp.p, 1, (int)L, s));
+        chk(mhe_multiply_plain(eng, c + k * L * n, sp.p, t.p, 1, (int)L, s));
+        chk(mhe_add(eng, d, t.p, d, 1, (int)L, s));
+    }
+    out.scale() = encrypted.scale();
+    destination = std::move(out);
+}
+
+// ------------------------------------------------------------------------------ Evaluator
+namespace
+{
+struct Level
+{
+    std::size_t L, n;
+    double total_bits;
+    std::shared_ptr<const SEALContext::ContextData> cd;
+};
+
+Level level_of(const SEALContext &ctx, const parms_id_type &id, const char *what)
+{
+    auto cd = ctx.get_context_data(id);
+    if (!cd) throw std::invalid_argument(std::string(what) + " is not valid for encryption parameters");
+    return { cd->parms().coeff_modulus().size(), cd->parms().poly_modulus_degree(),
+             (double)cd->total_coeff_modulus_bit_count(), cd };
+}
+
+Level check_ct(const SEALContext &ctx, const Ciphertext &ct, const char *what)
+{
+    Level lv = level_of(ctx, ct.parms_id(), what);
+    if (ct.size() < 2 || ct.coeff_modulus_size() != lv.L || ct.store().words() != ct.size() * lv.L * lv.n ||
+        ct.store().engine() != ctx.engine())
+        throw std::invalid_argument(std::string(what) + " is not valid for encryption parameters");
+    return lv;
+}
+
+// is_scale_within_bounds (evaluator.cpp): 0 < scale and log2(scale) < total bits of the level
+void check_scale(double scale, const Level &lv)
+{
+    if (scale <= 0 || static_cast<int>(std::log2(scale)) >= (int)lv.total_bits)
+        throw std::invalid_argument("scale out of bounds");
+}
+} // namespace
+
+Evaluator::Evaluator(const SEALContext &context, CKKSEncoder &encoder) : context_(context), encoder_(encoder)
+{
+    if (!context.parameters_set()) throw std::invalid_argument("encryption parameters are not set correctly");
+}
+
+std::size_t Evaluator::limbs_of(const parms_id_type &id) const
+{
+    return level_of(context_, id, "parms_id").L;
+}
+
+void Evaluator::negate_inplace(Ciphertext &encrypted) const
+{
+    // evaluator.cpp:78-101
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    void *s = context_.stream();
+    std::uint64_t *p = encrypted.store().dev_write(s);
+    chk(mhe_negate(context_.engine(), p, p, (int)encrypted.size(), (int)lv.L, s));
+}
+
+void Evaluator::negate(const Ciphertext &encrypted, Ciphertext &destination) const
+{
+    destination = encrypted;
+    negate_inplace(destination);
+}
+
+namespace
+{
+void check_pair(const SEALContext &ctx, const Ciphertext &a, const Ciphertext &b, bool scales)
+{
+    check_ct(ctx, a, "encrypted1");
+    check_ct(ctx, b, "encrypted2");
+    if (a.parms_id() != b.parms_id()) throw std::invalid_argument("encrypted1 and encrypted2 parameter mismatch");
+    if (a.is_ntt_form() != b.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+    if (scales && !are_close(a.scale(), b.scale())) throw std::invalid_argument("scale mismatch");
+}
+} // namespace
+
+void Evaluator::add_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
+{
+    // evaluator.cpp:103-164
+    check_pair(context_, encrypted1, encrypted2, true);
+    const std::size_t L = encrypted1.coeff_modulus_size(), n = encrypted1.poly_modulus_degree();
+    const std::size_t s1 = encrypted1.size(), s2 = encrypted2.size(), mn = std::min(s1, s2);
+    void *s = context_.stream();
+    if (s1 < s2) encrypted1.resize(context_, encrypted1.parms_id(), s2);
+    const std::uint64_t *b = encrypted2.store().dev_read(s);
+    std::uint64_t *a = encrypted1.store().dev_write(s);
+    chk(mhe_add(context_.engine(), a, b, a, (int)mn, (int)L, s));
+    if (s1 < s2) chk(mhe_memcpy_d2d(context_.engine(), a + mn * L * n, b + mn * L * n, (s2 - mn) * L * n * 8, s));
+}
+
+void Evaluator::add(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
+{
+    if (&encrypted2 == &destination)
+        add_inplace(destination, encrypted1);
+    else if (&encrypted1 != &destination && encrypted1.size() == encrypted2.size())
+    {
+        // SEAL copies encrypted1 then adds; writing the sum directly saves a pass over HBM
+        check_pair(context_, encrypted1, encrypted2, true);
+        void *s = context_.stream();
+        destination.resize(context_, encrypted1.parms_id(), encrypted1.size());
+        const std::uint64_t *a = encrypted1.store().dev_read(s), *b = encrypted2.store().dev_read(s);
+        chk(mhe_add(context_.engine(), a, b, destination.store().dev_write(s, true), (int)encrypted1.size(),
+                    (int)encrypted1.coeff_modulus_size(), s));
+        destination.scale() = encrypted1.scale();
+        destination.is_ntt_form() = encrypted1.is_ntt_form();
+    }
+    else
+    {
+        destination = encrypted1;
+        add_inplace(destination, encrypted2);
+    }
+}
+
+void Evaluator::add_many(const std::vector<Ciphertext> &encrypteds, Ciphertext &destination) const
+{
+    // evaluator.cpp:166-185
+    if (encrypteds.empty()) throw std::invalid_argument("encrypteds cannot be empty");
+    for (auto &e : encrypteds)
+        if (&e == &destination) throw std::invalid_argument("encrypteds must be different from destination");
+    destination = encrypteds[0];
+    for (std::size_t i = 1; i < encrypteds.size(); i++) add_inplace(destination, encrypteds[i]);
+}
+
+void Evaluator::sub_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
+{
+    // evaluator.cpp:187-246
+    check_pair(context_, encrypted1, encrypted2, true);
+    const std::size_t L = encrypted1.coeff_modulus_size(), n = encrypted1.poly_modulus_degree();
+    const std::size_t s1 = encrypted1.size(), s2 = encrypted2.size(), mn = std::min(s1, s2);
+    void *s = context_.stream();
+    if (s1 < s2) encrypted1.resize(context_, encrypted1.parms_id(), s2);
+    const std::uint64_t *b = encrypted2.store().dev_read(s);
+    std::uint64_t *a = encrypted1.store().dev_write(s);
+    chk(mhe_sub(context_.engine(), a, b, a, (int)mn, (int)L, s));
+    if (s1 < s2)
+        chk(mhe_negate(context_.engine(), b + mn * L * n, a + mn * L * n, (int)(s2 - mn), (int)L, s));
+}
+
+void Evaluator::sub(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
+{
+    if (&encrypted2 == &destination)
+    {
+        sub_inplace(destination, encrypted1);
+        negate_inplace(destination);
+    }
+    else
+    {
+        destination = encrypted1;
+        sub_inplace(destination, encrypted2);
+    }
+}
+
+void Evaluator::multiply_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2, MemoryPoolHandle) const
+{
+    // evaluator.cpp:248-285, ckks_multiply :673-773 (size 2 x size 2 -> 3)
+    check_ct(context_, encrypted1, "encrypted1");
+    check_ct(context_, encrypted2, "encrypted2");
+    if (encrypted1.parms_id() != encrypted2.parms_id())
+        throw std::invalid_argument("encrypted1 and encrypted2 parameter mismatch");
+    if (!encrypted1.is_ntt_form() || !encrypted2.is_ntt_form())
+        throw std::invalid_argument("encrypted1 or encrypted2 must be in NTT form");
+    if (encrypted1.size() != 2 || encrypted2.size() != 2)
+        throw std::logic_error("only size-2 ciphertexts are multiplied (relinearize first)");
+    Level lv = level_of(context_, encrypted1.parms_id(), "encrypted1");
+    const double new_scale = encrypted1.scale() * encrypted2.scale();
+    check_scale(new_scale, lv);
+    void *s = context_.stream();
+    PolyStore out;
+    out.bind(context_);
+    out.resize_words(3 * lv.L * lv.n, false);
+    const std::uint64_t *a = encrypted1.store().dev_read(s), *b = encrypted2.store().dev_read(s);
+    chk(mhe_ct_multiply(context_.engine(), a, b, out.dev_write(s, true), (int)lv.L, s));
+    encrypted1.store() = std::move(out);
+    encrypted1.resize(3);
+    encrypted1.scale() = new_scale;
+}
+
+void Evaluator::multiply(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
+                         MemoryPoolHandle) const
+{
+    if (&encrypted2 == &destination)
+        multiply_inplace(destination, encrypted1);
+    else
+    {
+        destination = encrypted1;
+        multiply_inplace(destination, encrypted2);
+    }
+}
+
+void Evaluator::multiply_many(const std::vector<Ciphertext> &encrypteds, const RelinKeys &, Ciphertext &destination,
+                              MemoryPoolHandle) const
+{
+    // evaluator.cpp:1468-1543: BFV only in SEAL 3.6
+    if (encrypteds.empty()) throw std::invalid_argument("encrypteds vector must not be empty");
+    for (auto &e : encrypteds)
+        if (&e == &destination) throw std::invalid_argument("encrypteds must be different from destination");
+    level_of(context_, encrypteds[0].parms_id(), "encrypteds");
+    throw std::logic_error("unsupported scheme");
+}
+
+void Evaluator::exponentiate_inplace(Ciphertext &encrypted, std::uint64_t exponent, const RelinKeys &relin_keys,
+                                     MemoryPoolHandle) const
+{
+    // evaluator.cpp:1545-1576 (delegates to multiply_many: BFV only)
+    level_of(context_, encrypted.parms_id(), "encrypted");
+    if (!context_.get_context_data(relin_keys.parms_id()))
+        throw std::invalid_argument("relin_keys is not valid for encryption parameters");
+    if (exponent == 0) throw std::invalid_argument("exponent cannot be 0");
+    if (exponent == 1) return;
+    throw std::logic_error("unsupported scheme");
+}
+
+void Evaluator::square_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
+{
+    // evaluator.cpp:816-845, ckks_square :1000-1059
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+    if (encrypted.size() != 2) throw std::logic_error("only size-2 ciphertexts are squared (relinearize first)");
+    const double new_scale = encrypted.scale() * encrypted.scale();
+    check_scale(new_scale, lv);
+    void *s = context_.stream();
+    PolyStore out;
+    out.bind(context_);
+    out.resize_words(3 * lv.L * lv.n, false);
+    chk(mhe_ct_square(context_.engine(), encrypted.store().dev_read(s), out.dev_write(s, true), (int)lv.L, s));
+    encrypted.store() = std::move(out);
+    encrypted.resize(3);
+    encrypted.scale() = new_scale;
+}
+
+void Evaluator::square(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle) const
+{
+    destination = encrypted;
+    square_inplace(destination);
+}
+
+void Evaluator::switch_key(Ciphertext &encrypted, const std::uint64_t *target, const KSwitchKeys &keys,
+                           std::size_t index) const
+{
+    // switch_key_inplace (evaluator.cpp:2281-2525): ct[0..1] += KS(target)
+    const std::size_t L = encrypted.coeff_modulus_size();
+    void *s = context_.stream();
+    const std::uint64_t *key = keys.key(index).dev_read(s);
+    std::uint64_t *ct = encrypted.store().dev_write(s);
+    chk(mhe_switch_key(context_.engine(), ct, target, key, (int)keys.key_limbs(), (int)L, s));
+}
+
+void Evaluator::relinearize_inplace(Ciphertext &encrypted, const RelinKeys &relin_keys, MemoryPoolHandle) const
+{
+    // relinearize_internal (evaluator.cpp:1061-1116)
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (relin_keys.parms_id() != context_.key_parms_id())
+        throw std::invalid_argument("relin_keys is not valid for encryption parameters");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+    void *s = context_.stream();
+    std::size_t size = encrypted.size();
+    if (size == 3)
+    {
+        const std::uint64_t *key = relin_keys.key(RelinKeys::get_index(2)).dev_read(s);
+        std::uint64_t *ct = encrypted.store().dev_write(s);
+        chk(mhe_relinearize(context_.engine(), ct, key, (int)relin_keys.key_limbs(), (int)lv.L, s));
+        size = 2;
+    }
+    while (size > 2)
+    {
+        // fold the last component with the key for s^(size-1)
+        std::uint64_t *ct = encrypted.store().dev_write(s);
+        switch_key(encrypted, ct + (size - 1) * lv.L * lv.n, relin_keys, RelinKeys::get_index(size - 1));
+        size--;
+    }
+    encrypted.resize(size);
+}
+
+void Evaluator::relinearize(const Ciphertext &encrypted, const RelinKeys &relin_keys, Ciphertext &destination,
+                            MemoryPoolHandle) const
+{
+    destination = encrypted;
+    relinearize_inplace(destination, relin_keys);
+}
+
+void Evaluator::mod_switch_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
+{
+    // mod_switch_drop_to_next (evaluator.cpp:1183-1246) -- CKKS mod_switch_to_next
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
+    auto next = lv.cd->next_context_data();
+    if (!next) throw std::invalid_argument("end of modulus switching chain reached");
+    void *s = context_.stream();
+    std::uint64_t *p = encrypted.store().dev_write(s);
+    chk(mhe_mod_switch_drop(context_.engine(), p, p, (int)encrypted.size(), (int)lv.L, s));
+    const double scale = encrypted.scale();
+    encrypted.resize(context_, next->parms_id(), encrypted.size());
+    encrypted.scale() = scale;
+}
+
+void Evaluator::mod_switch_to_next(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle) const
+{
+    destination = encrypted;
+    mod_switch_to_next_inplace(destination);
+}
+
+void Evaluator::mod_switch_to_next_inplace(Plaintext &plain) const
+{
+    // mod_switch_drop_to_next(Plaintext) (evaluator.cpp:1248-1281)
+    if (!plain.is_ntt_form()) throw std::invalid_argument("plain is not in NTT form");
+    Level lv = level_of(context_, plain.parms_id(), "plain");
+    auto next = lv.cd->next_context_data();
+    if (!next) throw std::invalid_argument("end of modulus switching chain reached");
+    const double scale = plain.scale();
+    plain.set_level(context_, next->parms_id(), lv.L - 1); // shrinking keeps the first L-1 limbs
+    plain.scale() = scale;
+}
+
+void Evaluator::mod_switch_to_inplace(Ciphertext &encrypted, parms_id_type parms_id, MemoryPoolHandle) const
+{
+    // evaluator.cpp:1326-1348
+    Level cur = check_ct(context_, encrypted, "encrypted");
+    auto target = context_.get_context_data(parms_id);
+    if (!target) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    if (cur.cd->chain_index() < target->chain_index())
+        throw std::invalid_argument("cannot switch to higher level modulus");
+    if (encrypted.parms_id() == parms_id) return;
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
+    // all dropped limbs at once: copy the kept prefix of every component
+    const std::size_t L2 = target->parms().coeff_modulus().size(), n = cur.n, size = encrypted.size();
+    void *s = context_.stream();
+    PolyStore out;
+    out.bind(context_);
+    out.resize_words(size * L2 * n, false);
+    std::uint64_t *d = out.dev_write(s, true);
+    const std::uint64_t *p = encrypted.store().dev_read(s);
+    for (std::size_t k = 0; k < size; k++)
+        chk(mhe_memcpy_d2d(context_.engine(), d + k * L2 * n, p + k * cur.L * n, L2 * n * 8, s));
+    const double scale = encrypted.scale();
+    encrypted.store() = std::move(out);
+    encrypted.resize(context_, parms_id, size);
+    encrypted.scale() = scale;
+}
+
+void Evaluator::mod_switch_to(const Ciphertext &encrypted, parms_id_type parms_id, Ciphertext &destination,
+                              MemoryPoolHandle) const
+{
+    destination = encrypted;
+    mod_switch_to_inplace(destination, parms_id);
+}
+
+void Evaluator::mod_switch_to_inplace(Plaintext &plain, parms_id_type parms_id) const
+{
+    // evaluator.cpp:1350-1376
+    auto cur = context_.get_context_data(plain.parms_id());
+    auto target = context_.get_context_data(parms_id);
+    if (!cur) throw std::invalid_argument("plain is not valid for encryption parameters");
+    if (!target) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    if (!plain.is_ntt_form()) throw std::invalid_argument("plain is not in NTT form");
+    if (cur->chain_index() < target->chain_index())
+        throw std::invalid_argument("cannot switch to higher level modulus");
+    if (plain.parms_id() == parms_id) return;
+    const std::size_t L2 = target->parms().coeff_modulus().size();
+    const double scale = plain.scale();
+    plain.set_level(context_, parms_id, L2); // shrinking keeps the prefix limbs
+    plain.scale() = scale;
+}
+
+void Evaluator::rescale_to_next(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle) const
+{
+    // evaluator.cpp:1378-1414, mod_switch_scale_to_next :1118-1181
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (context_.last_parms_id() == encrypted.parms_id())
+        throw std::invalid_argument("end of modulus switching chain reached");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
+    auto next = lv.cd->next_context_data();
+    const double q_last = (double)lv.cd->parms().coeff_modulus().back().value();
+    const double new_scale = encrypted.scale() / q_last;
+    Level nl = level_of(context_, next->parms_id(), "parms_id");
+    check_scale(new_scale, nl);
+    void *s = context_.stream();
+    const std::size_t size = encrypted.size();
+    PolyStore out;
+    out.bind(context_);
+    out.resize_words(size * (lv.L - 1) * lv.n, false);
+    chk(mhe_rescale_to_next(context_.engine(), encrypted.store().dev_read(s), out.dev_write(s, true), (int)size,
+                            (int)lv.L, s));
+    const bool ntt = encrypted.is_ntt_form();
+    destination.store() = std::move(out);
+    destination.resize(context_, next->parms_id(), size);
+    destination.scale() = new_scale;
+    destination.is_ntt_form() = ntt;
+}
+
+void Evaluator::rescale_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
+{
+    rescale_to_next(encrypted, encrypted);
+}
+
+void Evaluator::rescale_to_inplace(Ciphertext &encrypted, parms_id_type parms_id, MemoryPoolHandle) const
+{
+    // evaluator.cpp:1416-1466
+    Level cur = check_ct(context_, encrypted, "encrypted");
+    auto target = context_.get_context_data(parms_id);
+    if (!target) throw std::invalid_argument("parms_id is not valid for encryption parameters");
+    if (cur.cd->chain_index() < target->chain_index())
+        throw std::invalid_argument("cannot switch to higher level modulus");
+    while (encrypted.parms_id() != parms_id) rescale_to_next(encrypted, encrypted);
+}
+
+void Evaluator::multiply_plain_inplace(Ciphertext &encrypted, const Plaintext &plain, MemoryPoolHandle) const
+{
+    // evaluator.cpp:1726-1761, multiply_plain_ntt :1891-1930
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (plain.is_ntt_form()) level_of(context_, plain.parms_id(), "plain");
+    if (encrypted.is_ntt_form() != plain.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+    if (encrypted.parms_id() != plain.parms_id())
+        throw std::invalid_argument("encrypted_ntt and plain_ntt parameter mismatch");
+    const double new_scale = encrypted.scale() * plain.scale();
+    check_scale(new_scale, lv);
+    void *s = context_.stream();
+    const std::uint64_t *b = plain.store().dev_read(s);
+    std::uint64_t *a = encrypted.store().dev_write(s);
+    chk(mhe_multiply_plain(context_.engine(), a, b, a, (int)encrypted.size(), (int)lv.L, s));
+    encrypted.scale() = new_scale;
+}
+
+void Evaluator::multiply_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination,
+                               MemoryPoolHandle) const
+{
+    destination = encrypted;
+    multiply_plain_inplace(destination, plain);
+}
+
+namespace
+{
+void add_sub_plain(const SEALContext &ctx, Ciphertext &encrypted, const Plaintext &plain, bool sub)
+{
+    // evaluator.cpp:1578-1724 (CKKS branch): component 0 +-= plain
+    Level lv = check_ct(ctx, encrypted, "encrypted");
+    if (encrypted.is_ntt_form() != plain.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+    if (encrypted.parms_id() != plain.parms_id())
+        throw std::invalid_argument("encrypted and plain parameter mismatch");
+    if (!are_close(encrypted.scale(), plain.scale())) throw std::invalid_argument("scale mismatch");
+    void *s = ctx.stream();
+    const std::uint64_t *b = plain.store().dev_read(s);
+    std::uint64_t *a = encrypted.store().dev_write(s);
+    if (sub)
+        chk(mhe_sub(ctx.engine(), a, b, a, 1, (int)lv.L, s));
+    else
+        chk(mhe_add(ctx.engine(), a, b, a, 1, (int)lv.L, s));
+}
+} // namespace
+
+void Evaluator::add_plain_inplace(Ciphertext &encrypted, const Plaintext &plain) const
+{
+    add_sub_plain(context_, encrypted, plain, false);
+}
+
+void Evaluator::add_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination) const
+{
+    destination = encrypted;
+    add_plain_inplace(destination, plain);
+}
+
+void Evaluator::sub_plain_inplace(Ciphertext &encrypted, const Plaintext &plain) const
+{
+    add_sub_plain(context_, encrypted, plain, true);
+}
+
+void Evaluator::sub_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination) const
+{
+    destination = encrypted;
+    sub_plain_inplace(destination, plain);
+}
+
+void Evaluator::transform_to_ntt_inplace(Ciphertext &encrypted) const
+{
+    // evaluator.cpp:2025-2071
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (encrypted.is_ntt_form()) throw std::invalid_argument("encrypted is already in NTT form");
+    void *s = context_.stream();
+    chk(mhe_ntt_forward(context_.engine(), encrypted.store().dev_write(s), (int)encrypted.size(), (int)lv.L, 0, s));
+    encrypted.is_ntt_form() = true;
+}
+
+void Evaluator::transform_from_ntt_inplace(Ciphertext &encrypted) const
+{
+    // evaluator.cpp:2073-2118
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted is not in NTT form");
+    void *s = context_.stream();
+    chk(mhe_ntt_inverse(context_.engine(), encrypted.store().dev_write(s), (int)encrypted.size(), (int)lv.L, 0, s));
+    encrypted.is_ntt_form() = false;
+}
+
+void Evaluator::apply_galois_inplace(Ciphertext &encrypted, std::uint32_t galois_elt, const GaloisKeys &galois_keys,
+                                     MemoryPoolHandle) const
+{
+    // evaluator.cpp:2120-2222
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (galois_keys.parms_id() != context_.key_parms_id())
+        throw std::invalid_argument("galois_keys is not valid for encryption parameters");
+    if (!(galois_elt & 1) || galois_elt >= 2 * lv.n) throw std::invalid_argument("Galois element is not valid");
+    if (encrypted.size() > 2) throw std::invalid_argument("encrypted size must be 2");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+    if (!galois_keys.has_key(galois_elt)) throw std::invalid_argument("Galois key not present");
+    void *s = context_.stream();
+    const std::uint64_t *key = galois_keys.key(GaloisKeys::get_index(galois_elt)).dev_read(s);
+    chk(mhe_apply_galois(context_.engine(), encrypted.store().dev_write(s), galois_elt, key,
+                         (int)galois_keys.key_limbs(), (int)lv.L, s));
+}
+
+void Evaluator::rotate_internal(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys) const
+{
+    // evaluator.cpp:2224-2279
+    Level lv = level_of(context_, encrypted.parms_id(), "encrypted");
+    if (galois_keys.parms_id() != context_.key_parms_id())
+        throw std::invalid_argument("galois_keys is not valid for encryption parameters");
+    if (steps == 0) return;
+    const int log_n = __builtin_ctzll(lv.n);
+    const std::uint32_t elt = mhe_galois_elt_from_step(log_n, steps);
+    if (!elt) throw std::invalid_argument("step count too large");
+    if (galois_keys.has_key(elt))
+    {
+        apply_galois_inplace(encrypted, elt, galois_keys);
+        return;
+    }
+    // NAF decomposition (util/numth.h:22-42)
+    std::vector<int> naf;
+    {
+        const bool sign = steps < 0;
+        int v = std::abs(steps);
+        for (int i = 0; v; i++)
+        {
+            const int zi = (v & 1) ? 2 - (v & 3) : 0;
+            v = (v - zi) >> 1;
+            if (zi) naf.push_back((sign ? -zi : zi) * (1 << i));
+        }
+    }
+    if (naf.size() == 1) throw std::invalid_argument("Galois key not present");
+    for (int st : naf)
+        if ((std::size_t)std::abs(st) != (lv.n >> 1)) rotate_internal(encrypted, st, galois_keys);
+}
+
+void Evaluator::rotate_vector_inplace(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
+                                      MemoryPoolHandle) const
+{
+    rotate_internal(encrypted, steps, galois_keys);
+}
+
+void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
+                              Ciphertext &destination, MemoryPoolHandle) const
+{
+    destination = encrypted;
+    rotate_vector_inplace(destination, steps, galois_keys);
+}
+
+void Evaluator::complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKeys &galois_keys, MemoryPoolHandle) const
+{
+    const std::size_t n = level_of(context_, encrypted.parms_id(), "encrypted").n;
+    apply_galois_inplace(encrypted, (std::uint32_t)(2 * n - 1), galois_keys);
+}
+
+void Evaluator::complex_conjugate(const Ciphertext &encrypted, const GaloisKeys &galois_keys, Ciphertext &destination,
+                                  MemoryPoolHandle) const
+{
+    destination = encrypted;
+    complex_conjugate_inplace(destination, galois_keys);
+}
+
+// ---- modified SEAL entry points (evaluator.cpp:287-486) ------------------------------------
+// add_const / multiply_const encode the constant at the first level and mod-switch it to the
+// ciphertext's level; the engine produces exactly those residues (its size checks against the
+// first level) and applies them per limb without materialising the constant polynomial.
+void Evaluator::add_const_inplace(Ciphertext &encrypted, double value) const
+{
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
+    std::vector<std::uint64_t> r(lv.L);
+    chk(mhe_ckks_encode_scalar_at(context_.engine(), value, encrypted.scale(), (int)L1, (int)lv.L, r.data()));
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+    void *s = context_.stream();
+    std::uint64_t *a = encrypted.store().dev_write(s);
+    chk(mhe_add_scalar(context_.engine(), a, r.data(), a, 1, (int)lv.L, s));
+}
+
+void Evaluator::add_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const
+{
+    destination = encrypted;
+    add_const_inplace(destination, value);
+}
+
+void Evaluator::multiply_const_inplace(Ciphertext &encrypted, double value) const
+{
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
+    std::vector<std::uint64_t> r(lv.L);
+    chk(mhe_ckks_encode_scalar_at(context_.engine(), value, encrypted.scale(), (int)L1, (int)lv.L, r.data()));
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+    const double new_scale = encrypted.scale() * encrypted.scale();
+    check_scale(new_scale, lv);
+    void *s = context_.stream();
+    std::uint64_t *a = encrypted.store().dev_write(s);
+    chk(mhe_multiply_scalar(context_.engine(), a, r.data(), a, (int)encrypted.size(), (int)lv.L, s));
+    encrypted.scale() = new_scale;
+}
+
+void Evaluator::multiply_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const
+{
+    destination = encrypted;
+    multiply_const_inplace(destination, value);
+}
+
+namespace
+{
+template <typename T>
+void split(const std::vector<T> &v, std::vector<double> &re, std::vector<double> &im);
+template <>
+void split<double>(const std::vector<double> &v, std::vector<double> &re, std::vector<double> &im)
+{
+    re = v;
+    im.clear();
+}
+template <>
+void split<std::complex<double>>(const std::vector<std::complex<double>> &v, std::vector<double> &re,
+                                 std::vector<double> &im)
+{
+    re.resize(v.size());
+    im.resize(v.size());
+    for (std::size_t i = 0; i < v.size(); i++)
+    {
+        re[i] = v[i].real();
+        im[i] = v[i].imag();
+    }
+}
+} // namespace
+
+template <typename T>
+void Evaluator::multiply_vector_inplace(Ciphertext &encrypted, const std::vector<T> &value) const
+{
+    // evaluator.cpp:303-310: encode at the first level, mod_switch_to, multiply_plain
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
+    if (value.size() > lv.n / 2) throw std::invalid_argument("values_size is too large");
+    std::vector<double> re, im;
+    split<T>(value, re, im);
+    void *s = context_.stream();
+    Plaintext plain;
+    plain.set_level(context_, encrypted.parms_id(), lv.L);
+    plain.scale() = encrypted.scale();
+    chk(mhe_ckks_encode_at(context_.engine(), encoder_.handle(), re.data(), im.empty() ? nullptr : im.data(),
+                           re.size(), encrypted.scale(), (int)L1, (int)lv.L, plain.store().dev_write(s, true), s));
+    multiply_plain_inplace(encrypted, plain);
+}
+
+template void Evaluator::multiply_vector_inplace<double>(Ciphertext &, const std::vector<double> &) const;
+template void Evaluator::multiply_vector_inplace<std::complex<double>>(
+    Ciphertext &, const std::vector<std::complex<double>> &) const;
+
+// evaluator.cpp:312-486 (Kim et al., CT-RSA 2022): when the levels differ, the operand at the
+// higher level is multiplied by s_other * q_last / s^2 (multiply_const), its scale forced to
+// s_other * q_last, rescaled and mod-switched down to the other operand's level; equal levels
+// only copy the scale across.  Same operation order and scale assignments as the reference.
+void Evaluator::reduced_error_op(Ciphertext &encrypted1, const Ciphertext &encrypted2, Rmode mode) const
+{
+    auto op_inplace = [&](Ciphertext &a, const Ciphertext &b) {
+        if (mode == Rmode::add)
+            add_inplace(a, b);
+        else if (mode == Rmode::sub)
+            sub_inplace(a, b);
+        else
+            multiply_inplace(a, b);
+    };
+    auto op_out = [&](const Ciphertext &a, const Ciphertext &b, Ciphertext &d) {
+        if (mode == Rmode::add)
+            add(a, b, d);
+        else if (mode == Rmode::sub)
+            sub(a, b, d);
+        else
+            multiply(a, b, d);
+    };
+    const std::size_t l1 = encrypted1.coeff_modulus_size(), l2 = encrypted2.coeff_modulus_size();
+    if (l1 == l2)
+    {
+        encrypted1.scale() = encrypted2.scale();
+        op_inplace(encrypted1, encrypted2);
+    }
+    else if (l1 < l2)
+    {
+        const double q = static_cast<double>(level_of(context_, encrypted2.parms_id(), "encrypted2")
+                                                 .cd->parms()
+                                                 .coeff_modulus()[l2 - 1]
+                                                 .value());
+        Ciphertext adj;
+        const double scale_adjust = encrypted1.scale() * q / (encrypted2.scale() * encrypted2.scale());
+        multiply_const(encrypted2, scale_adjust, adj);
+        adj.scale() = encrypted1.scale() * q;
+        rescale_to_next_inplace(adj);
+        mod_switch_to_inplace(adj, encrypted1.parms_id());
+        encrypted1.scale() = adj.scale();
+        op_inplace(encrypted1, adj);
+    }
+    else
+    {
+        const double q = static_cast<double>(level_of(context_, encrypted1.parms_id(), "encrypted1")
+                                                 .cd->parms()
+                                                 .coeff_modulus()[l1 - 1]
+                                                 .value());
+        Ciphertext adj;
+        const double scale_adjust = encrypted2.scale() * q / (encrypted1.scale() * encrypted1.scale());
+        multiply_const(encrypted1, scale_adjust, adj);
+        adj.scale() = encrypted2.scale() * q;
+        rescale_to_next_inplace(adj);
+        mod_switch_to_inplace(adj, encrypted2.parms_id());
+        adj.scale() = encrypted2.scale();
+        op_out(adj, encrypted2, encrypted1);
+    }
+}
+
+void Evaluator::add_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
+{
+    reduced_error_op(encrypted1, encrypted2, Rmode::add);
+}
+
+void Evaluator::sub_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
+{
+    reduced_error_op(encrypted1, encrypted2, Rmode::sub);
+}
+
+void Evaluator::multiply_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2,
+                                               const RelinKeys &relin_keys) const
+{
+    reduced_error_op(encrypted1, encrypted2, Rmode::mul);
+    relinearize_inplace(encrypted1, relin_keys);
+}
+} // namespace seal

@@ -101,6 +101,9 @@ int mhe_multiply_scalar(mhe_ctx *ctx, const uint64_t *a, const uint64_t *scalars
 /* add_poly_scalar_coeffmod with one scalar per limb (add_const, evaluator.cpp:287-301). */
 int mhe_add_scalar(mhe_ctx *ctx, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys, int limbs,
                    void *stream);
+/* out[p][l][*] = scalars[l]: the NTT form of a constant plaintext (CKKSEncoder::encode(double),
+ * ckks.cpp:78-200, writes the same residue into every coefficient of limb l). */
+int mhe_set_scalar(mhe_ctx *ctx, const uint64_t *scalars, uint64_t *out, int polys, int limbs, void *stream);
 
 /* ---- ciphertext ops -------------------------------------------------------------------
  * Evaluator::ckks_multiply, size-2 x size-2 (evaluator.cpp:673-773): out3 = [3][L][n]. */
@@ -154,6 +157,19 @@ int mhe_ckks_encode(mhe_ctx *ctx, const mhe_encoder *enc, const double *re, cons
  * constant plaintext is one residue per limb, written to the host array residues[limbs]
  * (multiply_const / add_const feed it to mhe_multiply_scalar / mhe_add_scalar). */
 int mhe_ckks_encode_scalar(mhe_ctx *ctx, double value, double scale, int limbs, uint64_t *residues);
+/* The same, with SEAL's size checks made against the first `bound_limbs` primes while only the
+ * first `limbs` residues are produced: encode at the first level followed by
+ * mod_switch_to_inplace(plain, parms_id) (what Evaluator::add_const/multiply_const/
+ * multiply_vector do, evaluator.cpp:287-310) without computing the dropped limbs. */
+int mhe_ckks_encode_at(mhe_ctx *ctx, const mhe_encoder *enc, const double *re, const double *im, size_t count,
+                       double scale, int bound_limbs, int limbs, uint64_t *out_dev, void *stream);
+/* CKKSEncoder::decode (ckks.h:644-761): NTT-form plaintext [limbs][n] on the device ->
+ * `sparse_slots` slot values (0 = n/2; the modified SEAL's sparse decode, ckks.h:704-713).
+ * `im` may be NULL (decode to vector<double>).  Synchronous on `stream`. */
+int mhe_ckks_decode(mhe_ctx *ctx, const mhe_encoder *enc, const uint64_t *plain_dev, int limbs, double scale,
+                    size_t sparse_slots, double *re, double *im, void *stream);
+int mhe_ckks_encode_scalar_at(mhe_ctx *ctx, double value, double scale, int bound_limbs, int limbs,
+                              uint64_t *residues);
 
 #ifdef __cplusplus
 }

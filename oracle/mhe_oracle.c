@@ -1209,3 +1209,205 @@ OR_API int or_ckks_encode_scalar(const or_ctx *c, double value, double scale, in
     }
     return 0;
 }
+
+/* --------------------------------------------------------------------------------------------
+ * CKKS decode (ckks.h:644-761): inverse NTT per limb, CRT compose (RNSBase::compose_array,
+ * util/rns.cpp:354-400), sparse-slot masking (modified SEAL, ckks.h:704-713), SEAL's
+ * word-by-word conversion to double (ckks.h:715-753), transform_to_rev with root_powers_
+ * (util/dwthandler.h:94-190), slot gather through matrix_reps_index_map_.
+ * ------------------------------------------------------------------------------------------ */
+static void or_mp_mul_scalar(const uint64_t *a, int L, uint64_t s, uint64_t *out) /* multiply_uint, truncated to L words */
+{
+    uint64_t carry = 0;
+    for (int k = 0; k < L; k++)
+    {
+        u128 p = (u128)a[k] * s + carry;
+        out[k] = (uint64_t)p;
+        carry = (uint64_t)(p >> 64);
+    }
+}
+
+static int or_mp_geq(const uint64_t *a, const uint64_t *b, int L)
+{
+    for (int k = L - 1; k >= 0; k--)
+        if (a[k] != b[k]) return a[k] > b[k];
+    return 1;
+}
+
+static void or_mp_sub(uint64_t *a, const uint64_t *b, int L) /* a -= b */
+{
+    uint64_t borrow = 0;
+    for (int k = 0; k < L; k++)
+    {
+        uint64_t d = a[k] - b[k];
+        uint64_t b2 = (a[k] < b[k]) | (d < borrow);
+        a[k] = d - borrow;
+        borrow = b2;
+    }
+}
+
+static void or_mp_add_mod(uint64_t *acc, const uint64_t *b, const uint64_t *Q, int L) /* add_uint_uint_mod */
+{
+    uint64_t carry = 0;
+    for (int k = 0; k < L; k++)
+    {
+        u128 s = (u128)acc[k] + b[k] + carry;
+        acc[k] = (uint64_t)s;
+        carry = (uint64_t)(s >> 64);
+    }
+    if (carry || or_mp_geq(acc, Q, L)) or_mp_sub(acc, Q, L);
+}
+
+static void or_fft_to_rev(or_cplx *values, int log_n, const or_cplx *roots)
+{
+    size_t n = (size_t)1 << log_n, gap = n >> 1, m = 1;
+    for (; m < (n >> 1); m <<= 1)
+    {
+        size_t offset = 0;
+        for (size_t i = 0; i < m; i++)
+        {
+            or_cplx r = *++roots;
+            or_cplx *x = values + offset, *y = x + gap;
+            for (size_t j = 0; j < gap; j++)
+            {
+                or_cplx u = *x, v = or_cmul(*y, r);
+                *x++ = or_cadd(u, v);
+                *y++ = or_csub(u, v);
+            }
+            offset += gap << 1;
+        }
+        gap >>= 1;
+    }
+    for (size_t i = 0; i < m; i++)
+    {
+        or_cplx r = *++roots;
+        or_cplx u = values[0], v = or_cmul(values[1], r);
+        values[0] = or_cadd(u, v);
+        values[1] = or_csub(u, v);
+        values += 2;
+    }
+}
+
+/* plain: NTT-form [limbs][n] at a level of `limbs` primes; total_bits of that level; writes
+ * sparse_slots values (sparse_slots = 0 means n/2).  Returns 0 or -1 (scale out of bounds). */
+OR_API int or_ckks_decode(const or_encoder *e, const or_ctx *c, const uint64_t *plain, int limbs, double scale,
+                          int total_bits, size_t sparse_slots, double *re, double *im)
+{
+    const size_t n = e->n, L = (size_t)limbs;
+    if (scale <= 0 || ((int)log2(scale)) >= total_bits) return -1;
+    if (!sparse_slots) sparse_slots = e->slots;
+    uint64_t *x = (uint64_t *)malloc(sizeof(uint64_t) * n * L);
+    memcpy(x, plain, sizeof(uint64_t) * n * L);
+    for (size_t j = 0; j < L; j++) or_ntt_inv(x + j * n, &c->ntt[j]);
+
+    /* base constants (RNSBase::initialize, util/rns.cpp): Q, Q/q_j, (Q/q_j)^{-1} mod q_j */
+    uint64_t *Q = (uint64_t *)calloc(L, sizeof(uint64_t));
+    uint64_t *punct = (uint64_t *)calloc(L * L, sizeof(uint64_t));
+    uint64_t *inv_punct = (uint64_t *)calloc(L, sizeof(uint64_t));
+    uint64_t *tmp = (uint64_t *)calloc(L + 1, sizeof(uint64_t));
+    Q[0] = 1;
+    for (size_t j = 0; j < L; j++)
+    {
+        or_mp_mul_scalar(Q, (int)L, c->mod[j].value, tmp);
+        memcpy(Q, tmp, sizeof(uint64_t) * L);
+    }
+    for (size_t j = 0; j < L; j++)
+    {
+        uint64_t *p = punct + j * L;
+        p[0] = 1;
+        uint64_t pm = 1; /* punctured product mod q_j */
+        for (size_t k = 0; k < L; k++)
+        {
+            if (k == j) continue;
+            or_mp_mul_scalar(p, (int)L, c->mod[k].value, tmp);
+            memcpy(p, tmp, sizeof(uint64_t) * L);
+            pm = or_mulmod(pm, or_barrett64(c->mod[k].value, &c->mod[j]), &c->mod[j]);
+        }
+        if (L == 1) pm = 1;
+        or_invmod(pm, c->mod[j].value, &inv_punct[j]);
+    }
+
+    /* compose: value_i = sum_j [x_ij * inv_j]_{q_j} * (Q/q_j) mod Q */
+    uint64_t *comp = (uint64_t *)calloc(n * L, sizeof(uint64_t));
+    for (size_t i = 0; i < n; i++)
+    {
+        uint64_t *acc = comp + i * L;
+        if (L == 1)
+        {
+            acc[0] = x[i];
+            continue;
+        }
+        for (size_t j = 0; j < L; j++)
+        {
+            uint64_t t = or_mulmod(x[j * n + i], inv_punct[j], &c->mod[j]);
+            or_mp_mul_scalar(punct + j * L, (int)L, t, tmp);
+            or_mp_add_mod(acc, tmp, Q, (int)L);
+        }
+    }
+    if (sparse_slots != e->slots)
+    {
+        size_t sparsity = e->slots / sparse_slots;
+        for (size_t i = 0; i < n; i++)
+            if (((i - 1) & (sparsity - 1)) != sparsity - 1) memset(comp + i * L, 0, sizeof(uint64_t) * L);
+    }
+
+    /* upper_half_threshold = (Q + 1) / 2 */
+    uint64_t *thr = (uint64_t *)calloc(L, sizeof(uint64_t));
+    {
+        uint64_t carry = 1;
+        for (size_t k = 0; k < L; k++)
+        {
+            thr[k] = Q[k] + carry;
+            carry = (carry && thr[k] == 0) ? 1 : 0;
+        }
+        for (size_t k = 0; k < L; k++) thr[k] = (thr[k] >> 1) | ((k + 1 < L) ? (thr[k + 1] << 63) : ((uint64_t)carry << 63));
+    }
+    const double two64 = pow(2.0, 64), inv_scale = 1.0 / scale;
+    or_cplx *res = (or_cplx *)calloc(n, sizeof(or_cplx));
+    for (size_t i = 0; i < n; i++)
+    {
+        const uint64_t *v = comp + i * L;
+        double acc = 0.0, s64 = inv_scale;
+        if (or_mp_geq(v, thr, (int)L))
+        {
+            for (size_t j = 0; j < L; j++, s64 *= two64)
+            {
+                if (v[j] > Q[j])
+                {
+                    uint64_t diff = v[j] - Q[j];
+                    acc += diff ? (double)diff * s64 : 0.0;
+                }
+                else
+                {
+                    uint64_t diff = Q[j] - v[j];
+                    acc -= diff ? (double)diff * s64 : 0.0;
+                }
+            }
+        }
+        else
+        {
+            for (size_t j = 0; j < L; j++, s64 *= two64)
+            {
+                uint64_t cc = v[j];
+                acc += cc ? (double)cc * s64 : 0.0;
+            }
+        }
+        res[i] = or_c(acc, 0.0);
+    }
+    or_fft_to_rev(res, e->log_n, e->root_powers);
+    for (size_t i = 0; i < sparse_slots; i++)
+    {
+        or_cplx z = res[e->index_map[i]];
+        re[i] = z.re;
+        if (im) im[i] = z.im;
+    }
+    free(x);
+    free(Q);
+    free(punct);
+    free(inv_punct);
+    free(tmp);
+    free(comp);
+    free(thr);
+    free(res);
+    return 0;
+}

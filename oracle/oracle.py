@@ -65,6 +65,9 @@ def lib():
                                               ctypes.c_int, ctypes.c_int, u64p]),
             "or_ckks_encode_scalar": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int,
                                                      ctypes.c_int, u64p]),
+            "or_ckks_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u64p, ctypes.c_int, ctypes.c_double,
+                                              ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_double)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -277,6 +280,22 @@ class Context:
         if rc:
             raise ValueError("scale out of bounds" if rc == -1 else "encoded value is too large")
         return [int(x) for x in out]
+
+    def decode(self, plain, scale, sparse_slots=0):
+        """CKKSEncoder::decode (ckks.h:644-761): NTT-form plaintext [limbs][n] -> complex slots."""
+        if not hasattr(self, "_enc"):
+            self._enc = lib().or_encoder_create(self.log_n)
+        plain = np.ascontiguousarray(plain, np.uint64)
+        limbs = plain.shape[0]
+        cnt = sparse_slots or self.n // 2
+        re = np.zeros(cnt, np.float64)
+        im = np.zeros(cnt, np.float64)
+        dp = ctypes.POINTER(ctypes.c_double)
+        rc = lib().or_ckks_decode(self._enc, self._h, _p(plain), limbs, scale, self.total_bits(limbs), sparse_slots,
+                                  re.ctypes.data_as(dp), im.ctypes.data_as(dp))
+        if rc:
+            raise ValueError("scale out of bounds")
+        return re + 1j * im
 
     def hmult_batch(self, a, b, key, threads=0):
         """a, b: [B][2][L][n] -> ([B][2][L-1][n], threads used)."""

@@ -448,3 +448,51 @@ def test_ckks_encode_c2_full(c2):
     v = np.random.default_rng(42).uniform(-1, 1, ch.n // 2) * np.cos(np.arange(ch.n // 2))
     got = ch.down(ch.eng.encode(v, 2.0 ** 46, ch.K - 1))
     assert np.array_equal(got, ch.oc.encode(v, 2.0 ** 46, ch.K - 1))
+
+
+def test_ckks_encode_at_first_level_bound(small):
+    """encode(values, scale, plain) + mod_switch_to_inplace(plain, parms_id) (evaluator.cpp:
+    287-310) == encode directly at the lower level with the first level's size checks."""
+    ch = small
+    v = np.random.default_rng(43).uniform(-1, 1, ch.n // 2)
+    full = ch.oc.encode(v, 2.0 ** 46, ch.K - 1)
+    got = ch.down(ch.eng.encode(v, 2.0 ** 46, 2, bound_limbs=ch.K - 1))
+    assert np.array_equal(got, full[:2])
+    # 2^110 * |v| is too wide for 2 limbs (~97 bits) but fine against the first level
+    big = ch.oc.encode(v, 2.0 ** 110, ch.K - 1)
+    got = ch.down(ch.eng.encode(v, 2.0 ** 110, 2, bound_limbs=ch.K - 1))
+    assert np.array_equal(got, big[:2])
+    with pytest.raises(mhe.MheError, match="too large|out of bounds"):
+        ch.eng.encode(v, 2.0 ** 110, 2)
+    assert ch.eng.encode_scalar(0.75, 2.0 ** 110, 2, bound_limbs=ch.K - 1) == \
+        ch.oc.encode_scalar(0.75, 2.0 ** 110, ch.K - 1)[:2]
+
+
+# ----------------------------------------------------------------- CKKS decode
+@pytest.mark.parametrize("limbs,scale", [(1, 2.0 ** 30), (3, 2.0 ** 46), (7, 2.0 ** 100)])
+def test_ckks_decode_bit_exact(small, limbs, scale):
+    """CKKSEncoder::decode on the engine == the oracle restatement, double for double."""
+    ch = small
+    rng = np.random.default_rng(44 + limbs)
+    z = rng.uniform(-1, 1, ch.n // 2) + 1j * rng.uniform(-1, 1, ch.n // 2)
+    pt = ch.oc.encode(z, scale, limbs)
+    got = ch.eng.decode(ch.up(pt), scale)
+    ref = ch.oc.decode(pt, scale)
+    assert np.array_equal(got, ref)
+    assert np.abs(got - z).max() < 1e-5
+
+
+def test_ckks_decode_sparse(small):
+    ch = small
+    pt = ch.rand(3, ch.n)  # arbitrary plaintext (not a valid encoding): exercises every word path
+    for sparse in (1, 16, ch.n // 2):
+        got = ch.eng.decode(ch.up(pt), 2.0 ** 40, sparse_slots=sparse)
+        assert np.array_equal(got, ch.oc.decode(pt, 2.0 ** 40, sparse_slots=sparse))
+
+
+@pytest.mark.slow
+def test_ckks_decode_c2_full(c2):
+    ch = c2
+    pt = ch.rand(ch.K - 1, ch.n)
+    got = ch.eng.decode(ch.up(pt), 2.0 ** 46)
+    assert np.array_equal(got, ch.oc.decode(pt, 2.0 ** 46))

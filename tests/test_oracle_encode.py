@@ -75,3 +75,65 @@ def test_encode_scalar(ctx):
     r = ctx.encode_scalar(3.0, 2.0 ** 100, 4)  # 128-bit path
     for q, v in zip(ctx.moduli, r):
         assert v == (3 * 2 ** 100) % q
+
+
+# ----------------------------------------------------------------------------- decode
+def test_decode_roundtrip_real_and_complex(ctx):
+    rng = np.random.default_rng(11)
+    x = rng.uniform(-1, 1, ctx.n // 2)
+    assert np.abs(ctx.decode(ctx.encode(x, 2.0 ** 30, 4), 2.0 ** 30).real - x).max() < 1e-6
+    z = rng.uniform(-1, 1, ctx.n // 2) + 1j * rng.uniform(-1, 1, ctx.n // 2)
+    assert np.abs(ctx.decode(ctx.encode(z, 2.0 ** 30, 3), 2.0 ** 30) - z).max() < 1e-6
+
+
+def test_decode_matches_bigint_crt(ctx):
+    """CRT compose + centered lift agrees with an independent Python-int reconstruction on a
+    plaintext whose coefficients span the whole modulus (multi-limb values of both signs)."""
+    L = 3
+    rng = np.random.default_rng(12)
+    x = rng.uniform(-1, 1, ctx.n // 2) * 2.0 ** 40
+    pt = ctx.encode(x, 2.0 ** 60, L)  # |coeff| ~ 2^100: needs all three limbs
+    got = ctx.decode(pt, 2.0 ** 60)
+    c = ctx.ntt(pt, O.NTT_INV)
+    Q = 1
+    for q in ctx.moduli[:L]:
+        Q *= q
+    vals = []
+    for i in range(ctx.n):
+        v = 0
+        for j, q in enumerate(ctx.moduli[:L]):
+            Mj = Q // q
+            v += int(c[j, i]) * pow(Mj, -1, q) * Mj
+        v %= Q
+        vals.append(float(v - Q if v > Q // 2 else v) / 2.0 ** 60)
+    coeff = np.array(vals)
+    n = ctx.n
+    zeta = np.exp(1j * np.pi * np.arange(n) / n)
+    ev = n * np.fft.ifft(coeff * zeta)
+    t1, _ = H._slot_index(n)
+    ref = ev[t1]
+    assert np.abs(got - ref).max() < 1e-6 * np.abs(ref).max()
+    assert np.abs(got.real - x).max() < 1e-6 * 2.0 ** 40
+
+
+def test_decode_single_limb(ctx):
+    x = np.random.default_rng(13).uniform(-1, 1, ctx.n // 2)
+    assert np.abs(ctx.decode(ctx.encode(x, 2.0 ** 30, 1), 2.0 ** 30).real - x).max() < 1e-6
+
+
+def test_decode_sparse_slots(ctx):
+    """Modified SEAL sparse decode (ckks.h:704-713): a vector with period `sparse` in the slots
+    lives on coefficients i = 0 mod (slots/sparse); decode returns the first `sparse` slots."""
+    sparse = 64
+    rng = np.random.default_rng(14)
+    base = rng.uniform(-1, 1, sparse)
+    x = np.tile(base, ctx.n // 2 // sparse)
+    out = ctx.decode(ctx.encode(x, 2.0 ** 30, 2), 2.0 ** 30, sparse_slots=sparse)
+    assert out.shape == (sparse,)
+    assert np.abs(out.real - base).max() < 1e-6
+
+
+def test_decode_scale_bounds(ctx):
+    pt = ctx.encode([0.5], 2.0 ** 30, 1)
+    with pytest.raises(ValueError, match="scale out of bounds"):
+        ctx.decode(pt, 2.0 ** 70)
