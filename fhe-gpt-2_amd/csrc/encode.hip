@@ -54,7 +54,13 @@ struct ComplexRoots
     {
         const double PI_ = 3.1415926535897932384626433832795028842;
         for (size_t i = 0; i <= m / 8; i++)
-            roots[i] = std::polar<double>(1.0, 2 * PI_ * static_cast<double>(i) / static_cast<double>(m));
+        {
+            // std::polar(1, theta) as SEAL's GCC Release build evaluates it: one sincos() call
+            // (separate cos()/sin() differ in the last bit for a few angles)
+            double sn, cs;
+            ::sincos(2 * PI_ * static_cast<double>(i) / static_cast<double>(m), &sn, &cs);
+            roots[i] = cd(cs, sn);
+        }
     }
     cd get(size_t index) const
     {

@@ -1360,10 +1360,21 @@ MHE_EXPORT int mhe_mod_switch_drop(mhe_ctx *c, const uint64_t *in, uint64_t *out
     if (!in || !out || size < 1) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
     const size_t src_pitch = ((size_t)limbs << c->log_n) * sizeof(u64);
     const size_t dst_pitch = ((size_t)(limbs - 1) << c->log_n) * sizeof(u64);
-    // Row-by-row ascending copy is safe in place (each destination row starts at or before its source).
-    for (int p = 0; p < size; p++)
-        if (in != out || p > 0)
+    if (in != out)
+    {
+        for (int p = 0; p < size; p++)
             HIP_TRY(hipMemcpyAsync((char *)out + p * dst_pitch, (const char *)in + p * src_pitch, dst_pitch,
+                                   hipMemcpyDeviceToDevice, S(s)));
+        return MHE_OK;
+    }
+    // In place: component p moves down by p limbs.  One copy per limb, ascending: every copy's
+    // source and destination are disjoint (they are p*n words apart), and a destination never
+    // covers a source that a later copy still has to read.
+    const size_t limb_bytes = sizeof(u64) << c->log_n;
+    for (int p = 1; p < size; p++)
+        for (int l = 0; l + 1 < limbs; l++)
+            HIP_TRY(hipMemcpyAsync((char *)out + p * dst_pitch + l * limb_bytes,
+                                   (const char *)in + p * src_pitch + l * limb_bytes, limb_bytes,
                                    hipMemcpyDeviceToDevice, S(s)));
     return MHE_OK;
 }

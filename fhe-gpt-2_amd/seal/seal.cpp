@@ -1313,10 +1313,15 @@ void Evaluator::mod_switch_to_next_inplace(Ciphertext &encrypted, MemoryPoolHand
     auto next = lv.cd->next_context_data();
     if (!next) throw std::invalid_argument("end of modulus switching chain reached");
     void *s = context_.stream();
-    std::uint64_t *p = encrypted.store().dev_write(s);
-    chk(mhe_mod_switch_drop(context_.engine(), p, p, (int)encrypted.size(), (int)lv.L, s));
+    const std::size_t size = encrypted.size();
+    PolyStore out;
+    out.bind(context_);
+    out.resize_words(size * (lv.L - 1) * lv.n, false);
+    chk(mhe_mod_switch_drop(context_.engine(), encrypted.store().dev_read(s), out.dev_write(s, true), (int)size,
+                            (int)lv.L, s));
     const double scale = encrypted.scale();
-    encrypted.resize(context_, next->parms_id(), encrypted.size());
+    encrypted.store() = std::move(out);
+    encrypted.resize(context_, next->parms_id(), size);
     encrypted.scale() = scale;
 }
 

@@ -18,6 +18,7 @@
  * (native/tests/seal/util/{ntt,galois,rns,uintarithsmallmod,numth}.cpp), replayed in
  * tests/test_oracle_kat.py from the fixtures in tests/golden/.
  */
+#define _GNU_SOURCE /* sincos */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -977,8 +978,13 @@ static void or_croots_init(or_croots *c, size_t m)
     c->roots = (or_cplx *)malloc(sizeof(or_cplx) * (m / 8 + 1));
     for (size_t i = 0; i <= m / 8; i++)
     {
-        double th = 2 * PI_ * (double)i / (double)m; /* polar<double>(1.0, theta) */
-        c->roots[i] = or_c(cos(th), sin(th));
+        /* polar<double>(1.0, theta): SEAL's Release build with GCC lowers the cos/sin pair of
+         * std::polar to one sincos() call, which differs from separate cos()/sin() in the last
+         * bit for a few angles (e.g. i = 487 at m = 8192); sincos is called explicitly so the
+         * tables do not depend on the optimisation level. */
+        double th = 2 * PI_ * (double)i / (double)m, sn, cs;
+        sincos(th, &sn, &cs);
+        c->roots[i] = or_c(cs, sn);
     }
 }
 
@@ -1290,8 +1296,25 @@ static void or_fft_to_rev(or_cplx *values, int log_n, const or_cplx *roots)
 
 /* plain: NTT-form [limbs][n] at a level of `limbs` primes; total_bits of that level; writes
  * sparse_slots values (sparse_slots = 0 means n/2).  Returns 0 or -1 (scale out of bounds). */
+static int or_ckks_decode_impl(const or_encoder *e, const or_ctx *c, const uint64_t *plain, int limbs, double scale,
+                               int total_bits, size_t sparse_slots, double *re, double *im, double *coeffs_out);
+
+/* The real-valued coefficients before transform_to_rev (ckks.h:715-753), for testing the
+ * conversion step alone. */
+OR_API int or_ckks_decode_coeffs(const or_encoder *e, const or_ctx *c, const uint64_t *plain, int limbs, double scale,
+                                 int total_bits, size_t sparse_slots, double *coeffs)
+{
+    return or_ckks_decode_impl(e, c, plain, limbs, scale, total_bits, sparse_slots, NULL, NULL, coeffs);
+}
+
 OR_API int or_ckks_decode(const or_encoder *e, const or_ctx *c, const uint64_t *plain, int limbs, double scale,
                           int total_bits, size_t sparse_slots, double *re, double *im)
+{
+    return or_ckks_decode_impl(e, c, plain, limbs, scale, total_bits, sparse_slots, re, im, NULL);
+}
+
+static int or_ckks_decode_impl(const or_encoder *e, const or_ctx *c, const uint64_t *plain, int limbs, double scale,
+                               int total_bits, size_t sparse_slots, double *re, double *im, double *coeffs_out)
 {
     const size_t n = e->n, L = (size_t)limbs;
     if (scale <= 0 || ((int)log2(scale)) >= total_bits) return -1;
@@ -1393,9 +1416,10 @@ OR_API int or_ckks_decode(const or_encoder *e, const or_ctx *c, const uint64_t *
             }
         }
         res[i] = or_c(acc, 0.0);
+        if (coeffs_out) coeffs_out[i] = acc;
     }
-    or_fft_to_rev(res, e->log_n, e->root_powers);
-    for (size_t i = 0; i < sparse_slots; i++)
+    if (!coeffs_out) or_fft_to_rev(res, e->log_n, e->root_powers);
+    for (size_t i = 0; i < sparse_slots && re; i++)
     {
         or_cplx z = res[e->index_map[i]];
         re[i] = z.re;

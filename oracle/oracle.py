@@ -65,6 +65,9 @@ def lib():
                                               ctypes.c_int, ctypes.c_int, u64p]),
             "or_ckks_encode_scalar": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_double, ctypes.c_double, ctypes.c_int,
                                                      ctypes.c_int, u64p]),
+            "or_ckks_decode_coeffs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u64p, ctypes.c_int,
+                                                     ctypes.c_double, ctypes.c_int, ctypes.c_size_t,
+                                                     ctypes.POINTER(ctypes.c_double)]),
             "or_ckks_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u64p, ctypes.c_int, ctypes.c_double,
                                               ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)]),
@@ -296,6 +299,19 @@ class Context:
         if rc:
             raise ValueError("scale out of bounds")
         return re + 1j * im
+
+    def decode_coeffs(self, plain, scale, sparse_slots=0):
+        """The doubles decode() feeds to transform_to_rev (ckks.h:715-753)."""
+        if not hasattr(self, "_enc"):
+            self._enc = lib().or_encoder_create(self.log_n)
+        plain = np.ascontiguousarray(plain, np.uint64)
+        out = np.zeros(self.n, np.float64)
+        rc = lib().or_ckks_decode_coeffs(self._enc, self._h, _p(plain), plain.shape[0], scale,
+                                         self.total_bits(plain.shape[0]), sparse_slots,
+                                         out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        if rc:
+            raise ValueError("scale out of bounds")
+        return out
 
     def hmult_batch(self, a, b, key, threads=0):
         """a, b: [B][2][L][n] -> ([B][2][L-1][n], threads used)."""

@@ -234,6 +234,13 @@ def test_mod_switch_drop_to_next(small):
     ct = ch.rand(2, 5, ch.n)
     got = ch.down(ch.eng.mod_switch_drop(ch.up(ct)))
     assert np.array_equal(got, ct[:, :4])
+    # in place (out == in): components are compacted downwards
+    for size in (2, 3):
+        ct = ch.rand(size, 7, ch.n)
+        buf = ch.up(ct)
+        ch.eng.mod_switch_drop(buf, out=buf)
+        flat = ch.down(buf).reshape(-1)[: size * 6 * ch.n].reshape(size, 6, ch.n)
+        assert np.array_equal(flat, ct[:, :6])
 
 
 def test_hmult_small(small):
@@ -493,6 +500,8 @@ def test_ckks_decode_sparse(small):
 @pytest.mark.slow
 def test_ckks_decode_c2_full(c2):
     ch = c2
-    pt = ch.rand(ch.K - 1, ch.n)
+    v = np.random.default_rng(45).uniform(-1, 1, ch.n // 2) + 1j * np.random.default_rng(46).uniform(-1, 1, ch.n // 2)
+    pt = ch.oc.encode(v, 2.0 ** 46, ch.K - 1)
     got = ch.eng.decode(ch.up(pt), 2.0 ** 46)
     assert np.array_equal(got, ch.oc.decode(pt, 2.0 ** 46))
+    assert np.abs(got - v).max() < 1e-6
