@@ -38,3 +38,27 @@ def test_seal_api_end_to_end():
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failed" in r.stdout
+
+
+def _consumer(tmp):
+    _build()
+    bdir = os.path.join(tmp, "consumer")
+    subprocess.check_call(["cmake", "-S", os.path.join(ROOT, "tests", "cpp", "consumer"), "-B", bdir,
+                           "-DCMAKE_PREFIX_PATH=" + PKG, "-DCMAKE_BUILD_TYPE=Release"],
+                          stdout=subprocess.DEVNULL)
+    subprocess.check_call(["cmake", "--build", bdir], stdout=subprocess.DEVNULL)
+    return os.path.join(bdir, "consumer")
+
+
+def test_cmake_package_consumer_builds(tmp_path):
+    """find_package(SEAL 3.6 REQUIRED) + SEAL::seal resolves to this package (the reference's
+    CMake integration, cnn_ckks/CMakeLists.txt:11,60) and a caller compiles and links."""
+    exe = _consumer(str(tmp_path))
+    assert os.path.exists(exe)
+
+
+@pytest.mark.gpu
+def test_cmake_package_consumer_runs(tmp_path):
+    exe = _consumer(str(tmp_path))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
