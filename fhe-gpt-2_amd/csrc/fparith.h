@@ -1,0 +1,104 @@
+// FP64-FMA modular arithmetic for primes q < 2^51 (gfx950).
+//
+// gfx950 has no 64x64 integer multiplier: a Shoup product costs 9-10 v_mad_u64_u32 plus
+// 64-bit carries, ~35 VALU instructions per Harvey butterfly.  The FP64 pipe runs v_fma_f64 at
+// the same rate as v_mad_u64_u32, and for q < 2^51 a residue and a 102-bit product are exact
+// in doubles:
+//     h = y*w (rounded), l = fma(y, w, -h)      -> y*w = h + l exactly
+//     k = rint(y * w')  with w' = w/q           -> quotient estimate, |y*w/q - k| <= 1
+//     r = fma(-k, q, h) + l                     -> r = y*w - k*q exactly, |r| <= 1.5q
+// so a butterfly is ~11 full-rate FP64 operations.  Values are kept as doubles in the signed
+// range |v| <= 2q between stages; the first load converts canonical/lazy u64 residues, the last
+// store canonicalises.  Every output that leaves a transform is canonical, so results are the
+// same residues SEAL's integer Harvey butterflies produce.
+//
+// Bounds (q < 2^51, |inputs| <= B = 2q < 2^52):
+//   rint(y*w') errs by at most 2*B*2^-53 + 1/2 <= 1, so |r| <= 1.5q; |h - k*q| <= 1.5q + ulp(h)/2
+//   <= 1.5q + 2^50 < 2^53, so the fma result is exact; a centered reduction x - rint(x/q)*q of
+//   |x| <= 2^53 is within [-q/2 - 1, q/2 + 1].  Forward: x' = red(x) + r, y' = red(x) - r, so
+//   |.| <= 2q + 1 is preserved.  Inverse: x' = red(x + y), y' = mulmod(red(x - y), w), |.| <= q.
+//   (scripts/ubench_bfly.hip checks 1536 random stages at q ~ 2^51 against the integer path.)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// Twiddle as (w, w/q).
+typedef double2 TwF;
+
+__device__ __forceinline__ double fp_rint(double x)
+{
+    return __builtin_rint(x);
+}
+
+// y*w mod q in (-1.5q, 1.5q) for |y| <= 4q, w in [0, q), ws = w/q.
+__device__ __forceinline__ double fp_mulmod(double y, double w, double ws, double q)
+{
+    const double h = y * w;
+    const double l = __builtin_fma(y, w, -h);
+    const double k = fp_rint(y * ws);
+    return __builtin_fma(-k, q, h) + l;
+}
+
+// centered reduction: x - rint(x/q)*q, |result| <= q/2 + 1 for |x| <= 2^52.
+__device__ __forceinline__ double fp_reduce(double x, double q, double qinv)
+{
+    return __builtin_fma(-fp_rint(x * qinv), q, x);
+}
+
+// canonical [0, q) from |x| <= 2^53, as u64.
+__device__ __forceinline__ uint64_t fp_canon(double x, double q, double qinv)
+{
+    double r = fp_reduce(x, q, qinv); // [-q/2 - 1, q/2 + 1]
+    r = r < 0 ? r + q : r;
+    return (uint64_t)r;
+}
+
+// exact double of a u64 < 2^53
+__device__ __forceinline__ double fp_from_u64(uint64_t x)
+{
+    return (double)x;
+}
+
+// Forward Cooley-Tukey butterfly (the mathematics of dwthandler.h:122-125).
+__device__ __forceinline__ void fwd_bfly_f(double &x, double &y, const TwF w, double q, double qinv)
+{
+    const double r = fp_mulmod(y, w.x, w.y, q);
+    const double u = fp_reduce(x, q, qinv);
+    x = u + r;
+    y = u - r;
+}
+
+// Inverse Gentleman-Sande butterfly (dwthandler.h:230-233).  |x|,|y| <= 2q + 1: the
+// difference is reduced first so the product's quotient estimate stays within 1.
+__device__ __forceinline__ void inv_bfly_f(double &x, double &y, const TwF w, double q, double qinv)
+{
+    const double s = x + y, d = x - y;
+    x = fp_reduce(s, q, qinv);
+    y = fp_mulmod(fp_reduce(d, q, qinv), w.x, w.y, q);
+}
+
+// Last inverse stage with n^-1 merged (dwthandler.h:273-314): x' = (u+v) n^-1, y' = (u-v) w_last.
+__device__ __forceinline__ void inv_bfly_last_f(double &x, double &y, double ninv, double ninv_s, double lw,
+                                                double lws, double q, double qinv)
+{
+    const double s = x + y, d = x - y;
+    x = fp_mulmod(fp_reduce(s, q, qinv), ninv, ninv_s, q);
+    y = fp_mulmod(fp_reduce(d, q, qinv), lw, lws, q);
+}
+
+// One forward stage over the E values of a lane (pairs (e, e+gap), gap bit clear).
+template <int E, class TwOf>
+__device__ __forceinline__ void fwd_stage_f(double (&v)[E], int gap, TwOf tw_of, double q, double qinv)
+{
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (!(e & gap)) fwd_bfly_f(v[e], v[e + gap], *tw_of(e), q, qinv);
+}
+
+template <int E, class TwOf>
+__device__ __forceinline__ void inv_stage_f(double (&v)[E], int gap, TwOf tw_of, double q, double qinv)
+{
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (!(e & gap)) inv_bfly_f(v[e], v[e + gap], *tw_of(e), q, qinv);
+}

@@ -184,6 +184,8 @@ struct mhe_ctx
     Tw *tw = nullptr;
     Tw *itw = nullptr;
     Tw *invq = nullptr;
+    TwF *twf = nullptr; // FP64 twiddles (w, w/q), [K][n] forward then [K][n] inverse
+    NttMode nm;         // FP64 butterflies when every prime is < 2^51 (MHE_FP=0 forces integer)
     int ks_fused = 1; // fused row-pass + key-MAC kernel (MHE_KS_FUSED=0: separate row pass + MAC)
     int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
     std::mutex mu;
@@ -772,10 +774,10 @@ static int run_ntt_fwd(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limb
     j.limbs = limbs;
     j.log_n = c->log_n;
     j.mode = 0;
-    fwd_col(j, c->log_n, polys * limbs, st);
+    fwd_col(j, c->log_n, polys * limbs, c->nm, st);
     j.src = dst;
     j.mode = full;
-    fwd_row(j, c->log_n, polys * limbs, st);
+    fwd_row(j, c->log_n, polys * limbs, c->nm, st);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }
@@ -790,10 +792,10 @@ static int run_ntt_inv(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limb
     j.limbs = limbs;
     j.log_n = c->log_n;
     j.mode = 0;
-    inv_row(j, c->log_n, polys * limbs, st);
+    inv_row(j, c->log_n, polys * limbs, c->nm, st);
     j.src = dst;
     j.mode = full;
-    inv_col(j, c->log_n, polys * limbs, st);
+    inv_col(j, c->log_n, polys * limbs, c->nm, st);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }
@@ -811,18 +813,18 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
     // 1. t_target = INTT(target), canonical (evaluator.cpp:2351-2354)
     {
         JobStrided j{ target, w->coeff, n, n, 0, 1, c->primes, c->itw, log_n, 0 };
-        inv_row(j, log_n, L, st);
+        inv_row(j, log_n, L, c->nm, st);
         j.src = w->coeff;
         j.mode = 1;
-        inv_col(j, log_n, L, st);
+        inv_col(j, log_n, L, c->nm, st);
     }
     if (c->ks_fused)
     {
         // 2+3 (experimental): column pass for all output primes, then the row pass fused
         // with the key MAC so NTT'd digits never leave registers.
         JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, 0 };
-        fwd_col(j, log_n, (L + 1) * L, st);
-        ks_row_mac(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, st);
+        fwd_col(j, log_n, (L + 1) * L, c->nm, st);
+        ks_row_mac(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, c->nm, st);
     }
     else
     {
@@ -837,9 +839,9 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
         {
             const int cnt = (I0 + P <= L + 1) ? P : L + 1 - I0;
             JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
-            fwd_col(j, log_n, cnt * L, st);
+            fwd_col(j, log_n, cnt * L, c->nm, st);
             JobModUpRow r2{ w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
-            fwd_row(r2, log_n, cnt * L, st);
+            fwd_row(r2, log_n, cnt * L, c->nm, st);
             dim3 grid((unsigned)(n / 512), cnt);
             hipLaunchKernelGGL(k_ks_mac, grid, dim3(256), 0, st, w->modup, target, key, w->acc, c->primes, L, c->K,
                                key_limbs, log_n, I0);
@@ -850,12 +852,12 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
     {
         JobStrided j{ w->acc + (size_t)L * n, w->acc + (size_t)L * n, (size_t)(L + 1) * n, (size_t)(L + 1) * n,
                       c->K - 1, 0, c->primes, c->itw, log_n, 0 };
-        inv_row(j, log_n, 2, st);
-        inv_col(j, log_n, 2, st);
+        inv_row(j, log_n, 2, c->nm, st);
+        inv_col(j, log_n, 2, c->nm, st);
         JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n };
-        fwd_col(dc, log_n, 2 * L, st);
+        fwd_col(dc, log_n, 2 * L, c->nm, st);
         JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
-        fwd_row(dr, log_n, 2 * L, st);
+        fwd_row(dr, log_n, 2 * L, c->nm, st);
     }
     HIP_LAUNCH_CHECK();
     return MHE_OK;
@@ -869,15 +871,15 @@ static int run_rescale(mhe_ctx *c, const u64 *in, u64 *out, int size, int L, hip
     const int log_n = c->log_n;
     // last[s] = INTT(in[s][L-1]) canonical -> w->coeff (size <= 3 polys)
     JobLastInv li{ in, w->coeff, c->primes, c->itw, L, log_n, 1 };
-    inv_row(li, log_n, size, st);
+    inv_row(li, log_n, size, c->nm, st);
     {
         JobStrided j2{ w->coeff, w->coeff, c->n, c->n, L - 1, 0, c->primes, c->itw, log_n, 1 };
-        inv_col(j2, log_n, size, st);
+        inv_col(j2, log_n, size, c->nm, st);
     }
     JobRescaleCol rc{ w->coeff, w->modup, c->primes, c->tw, L, log_n };
-    fwd_col(rc, log_n, size * (L - 1), st);
+    fwd_col(rc, log_n, size * (L - 1), c->nm, st);
     JobRescaleRow rr{ w->modup, in, out, c->primes, c->tw, c->invq, L, c->K, log_n };
-    fwd_row(rr, log_n, size * (L - 1), st);
+    fwd_row(rr, log_n, size * (L - 1), c->nm, st);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }
@@ -1043,8 +1045,35 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (e == hipSuccess) e = hipMemcpy(c->tw, tw.data(), sizeof(Tw) * tw.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->itw, itw.data(), sizeof(Tw) * itw.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->invq, invq.data(), sizeof(Tw) * invq.size(), hipMemcpyHostToDevice);
+    // FP64 arithmetic (fparith.h) needs q < 2^51 for every prime of the chain
+    bool fp = true;
+    for (int k = 0; k < count; k++) fp = fp && moduli[k] < ((u64)1 << 51);
+    if (const char *f = getenv("MHE_FP")) fp = fp && atoi(f) != 0;
+    if (e == hipSuccess && fp)
+    {
+        std::vector<TwF> twf((size_t)2 * count * n);
+        for (int k = 0; k < count; k++)
+        {
+            const double qd = (double)moduli[k];
+            for (size_t i = 0; i < n; i++)
+            {
+                const size_t o = (size_t)k * n + i;
+                twf[o] = make_double2((double)tw[o].x, (double)tw[o].x / qd);
+                twf[(size_t)count * n + o] = make_double2((double)itw[o].x, (double)itw[o].x / qd);
+            }
+        }
+        e = hipMalloc(&c->twf, sizeof(TwF) * twf.size());
+        if (e == hipSuccess) e = hipMemcpy(c->twf, twf.data(), sizeof(TwF) * twf.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+        {
+            c->nm.fp = 1;
+            c->nm.dfwd = (long long)((const char *)c->twf - (const char *)c->tw);
+            c->nm.dinv = (long long)((const char *)(c->twf + (size_t)count * n) - (const char *)c->itw);
+        }
+    }
     if (e != hipSuccess)
     {
+        (void)hipFree(c->twf);
         (void)hipFree(c->primes);
         (void)hipFree(c->tw);
         (void)hipFree(c->itw);
@@ -1067,6 +1096,7 @@ MHE_EXPORT int mhe_ctx_destroy(mhe_ctx *c)
     (void)hipFree(c->tw);
     (void)hipFree(c->itw);
     (void)hipFree(c->invq);
+    (void)hipFree(c->twf);
     delete c;
     return MHE_OK;
 }

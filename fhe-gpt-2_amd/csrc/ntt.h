@@ -20,7 +20,10 @@
 // and load()/store() hooks.  Key switching and rescale fuse their digit lift / (c - t)*q^-1
 // epilogues into these hooks, so the lifted digits never take an extra HBM round trip.
 #pragma once
+#include <type_traits>
+
 #include "arith.h"
+#include "fparith.h"
 
 
 // Forward Harvey butterfly (dwthandler.h:122-125 with ntt.h:34-65 arithmetic).
@@ -103,6 +106,88 @@ __device__ __forceinline__ void inv_stage(u64 (&v)[E], int gap, TwOf tw_of, u64 
         if (!(e & gap)) v[e + gap] = m[k++];
 }
 
+// Arithmetic policy of a transform pass.  NttArith<false>: SEAL's integer Harvey butterflies
+// (u64 values in lazy ranges).  NttArith<true>: FP64-FMA butterflies (fparith.h) for primes
+// < 2^51, values held as doubles inside the pass; loads convert exact u64 -> double and stores
+// hand canonical u64 to the job's store hook (canonical lies inside every lazy range the hooks
+// accept).  The FP twiddle tables mirror the integer ones entry for entry (16 B each), so the
+// job's integer twiddle pointer plus a fixed byte offset addresses the FP table.
+template <bool FP>
+struct NttArith;
+
+template <>
+struct NttArith<false>
+{
+    using T = u64;
+    using TW = Tw;
+    u64 q, q2;
+    const Tw *tw;
+    __device__ NttArith(const PrimeDev &p, const Tw *t, long long) : q(p.q), q2(p.two_q), tw(t) {}
+    __device__ T in(u64 x) const { return x; }
+    __device__ u64 out(T x) const { return x; }
+    __device__ u64 canon(T x) const { return csub(csub(x, q2), q); }
+    template <int E, class Ix>
+    __device__ void fwd(T (&v)[E], int gap, Ix ix) const
+    {
+        fwd_stage<E>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, q2);
+    }
+    template <int E, class Ix>
+    __device__ void fwd_tab(T (&v)[E], int gap, const TW *tab, Ix ix) const
+    {
+        fwd_stage<E>(v, gap, [&](int e) { return &tab[ix(e)]; }, q, q2);
+    }
+    template <int E, class Ix>
+    __device__ void inv(T (&v)[E], int gap, Ix ix) const
+    {
+        inv_stage<E>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, q2);
+    }
+    __device__ void inv_last(T &x, T &y, const PrimeDev &p) const { inv_bfly_last(x, y, p); }
+};
+
+template <>
+struct NttArith<true>
+{
+    using T = double;
+    using TW = TwF;
+    double q, qinv;
+    const TwF *tw;
+    __device__ NttArith(const PrimeDev &p, const Tw *t, long long delta)
+        : q((double)p.q), qinv(1.0 / (double)p.q), tw(reinterpret_cast<const TwF *>(reinterpret_cast<const char *>(t) + delta))
+    {
+    }
+    __device__ T in(u64 x) const { return (double)x; }
+    __device__ u64 out(T x) const { return fp_canon(x, q, qinv); }
+    __device__ u64 canon(T x) const { return fp_canon(x, q, qinv); }
+    template <int E, class Ix>
+    __device__ void fwd(T (&v)[E], int gap, Ix ix) const
+    {
+        fwd_stage_f<E>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, qinv);
+    }
+    template <int E, class Ix>
+    __device__ void fwd_tab(T (&v)[E], int gap, const TW *tab, Ix ix) const
+    {
+        fwd_stage_f<E>(v, gap, [&](int e) { return &tab[ix(e)]; }, q, qinv);
+    }
+    template <int E, class Ix>
+    __device__ void inv(T (&v)[E], int gap, Ix ix) const
+    {
+        inv_stage_f<E>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, qinv);
+    }
+    __device__ void inv_last(T &x, T &y, const PrimeDev &p) const
+    {
+        const double ni = (double)p.ninv, lw = (double)p.last_w;
+        inv_bfly_last_f(x, y, ni, ni / q, lw, lw / q, q, qinv);
+    }
+};
+
+// Per-launch arithmetic selection: fp = every prime of the context is < 2^51; the deltas are
+// the byte offsets from the integer to the FP forward / inverse twiddle tables.
+struct NttMode
+{
+    int fp = 0;
+    long long dfwd = 0, dinv = 0;
+};
+
 template <int LOGR, int LOGT>
 struct Shape
 {
@@ -116,25 +201,26 @@ struct Shape
 };
 
 // ------------------------------------------------------------------ forward, column pass
-template <int LOGR, int LOGT, class Job>
-__global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n)
+template <int LOGR, int LOGT, class Job, bool FP>
+__global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n, long long twd)
 {
     using SH = Shape<LOGR, LOGT>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
     constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
-    __shared__ u64 lds[S * LD];
+    __shared__ T lds[S * LD];
     const int tid = threadIdx.x, sl = tid % S, t = tid / S;
     const int logC = log_n - LOGR;
     const u32 c = blockIdx.x * S + sl;
     const auto V = job.view(blockIdx.y);
     if (V.skip) return; // uniform per workgroup, before any barrier
-    const u64 q = V.p.q, q2 = V.p.two_q;
-    const Tw *tw = V.tw;
-    u64 v[E];
+    const A ar(V.p, V.tw, twd);
+    T v[E];
 #pragma unroll
-    for (int e = 0; e < E; e++) v[e] = V.load(c + ((u32)(t + TPS * e) << logC));
+    for (int e = 0; e < E; e++) v[e] = ar.in(V.load(c + ((u32)(t + TPS * e) << logC)));
 #pragma unroll
     for (int s = 0; s < LOGE; s++)
-        fwd_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(1 << s) + (e >> (LOGE - s))]; }, q, q2);
+        ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
     __syncthreads();
@@ -142,33 +228,33 @@ __global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
     for (int s = LOGE; s < LOGR; s++)
-        fwd_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(1 << s) + ((E * t + e) >> (LOGR - s))]; },
-                     q, q2);
+        ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
 #pragma unroll
-    for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), v[e]);
+    for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
 }
 
 // --------------------------------------------------------------------- forward, row pass
-template <int LOGR, int LOGT, class Job>
-__global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n)
+template <int LOGR, int LOGT, class Job, bool FP>
+__global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long twd)
 {
     using SH = Shape<LOGR, LOGT>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
     constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
-    __shared__ u64 lds[S * LD];
+    __shared__ T lds[S * LD];
     const int tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
     const u32 b = blockIdx.x * S + sl;
     const u32 base = b << LOGR;
     const u32 rb = (1u << (log_n - LOGR)) + b; // 2^k1 + b
     const auto V = job.view(blockIdx.y);
     if (V.skip) return; // uniform per workgroup, before any barrier
-    const u64 q = V.p.q, q2 = V.p.two_q;
-    const Tw *tw = V.tw;
-    u64 v[E];
+    const A ar(V.p, V.tw, twd);
+    T v[E];
 #pragma unroll
-    for (int e = 0; e < E; e++) v[e] = V.load(base + t + TPS * e);
+    for (int e = 0; e < E; e++) v[e] = ar.in(V.load(base + t + TPS * e));
 #pragma unroll
     for (int s = 0; s < LOGE; s++)
-        fwd_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(rb << s) + (e >> (LOGE - s))]; }, q, q2);
+        ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (rb << s) + (e >> (LOGE - s)); });
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
     __syncthreads();
@@ -176,41 +262,40 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
     for (int s = LOGE; s < LOGR; s++)
-        fwd_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(rb << s) + ((E * t + e) >> (LOGR - s))]; },
-                     q, q2);
+        ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
     // transpose back so stores (and epilogue reads) are coalesced
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; e++) V.store(base + t + TPS * e, lds[sl * LD + t + TPS * e]);
+    for (int e = 0; e < E; e++) V.store(base + t + TPS * e, ar.out(lds[sl * LD + t + TPS * e]));
 }
 
 // --------------------------------------------------------------------- inverse, row pass
-template <int LOGR, int LOGT, class Job>
-__global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n)
+template <int LOGR, int LOGT, class Job, bool FP>
+__global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long twd)
 {
     using SH = Shape<LOGR, LOGT>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
     constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
-    __shared__ u64 lds[S * LD];
+    __shared__ T lds[S * LD];
     const int tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
     const u32 b = blockIdx.x * S + sl;
     const u32 base = b << LOGR;
     const u32 rb = (1u << (log_n - LOGR)) + b;
     const auto V = job.view(blockIdx.y);
     if (V.skip) return; // uniform per workgroup, before any barrier
-    const u64 q = V.p.q, q2 = V.p.two_q;
-    const Tw *tw = V.tw;
-    u64 v[E];
+    const A ar(V.p, V.tw, twd);
+    T v[E];
 #pragma unroll
-    for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = V.load(base + t + TPS * e);
+    for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = ar.in(V.load(base + t + TPS * e));
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
     for (int s = LOGR - 1; s >= LOGE; s--)
-        inv_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(rb << s) + ((E * t + e) >> (LOGR - s))]; },
-                     q, q2);
+        ar.template inv<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
     __syncthreads();
@@ -218,32 +303,32 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + t + TPS * e];
 #pragma unroll
     for (int s = LOGE - 1; s >= 0; s--)
-        inv_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(rb << s) + (e >> (LOGE - s))]; }, q, q2);
+        ar.template inv<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (rb << s) + (e >> (LOGE - s)); });
 #pragma unroll
-    for (int e = 0; e < E; e++) V.store(base + t + TPS * e, v[e]);
+    for (int e = 0; e < E; e++) V.store(base + t + TPS * e, ar.out(v[e]));
 }
 
 // ------------------------------------------------------------------ inverse, column pass
-template <int LOGR, int LOGT, class Job>
-__global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n)
+template <int LOGR, int LOGT, class Job, bool FP>
+__global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long twd)
 {
     using SH = Shape<LOGR, LOGT>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
     constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
-    __shared__ u64 lds[S * LD];
+    __shared__ T lds[S * LD];
     const int tid = threadIdx.x, sl = tid % S, t = tid / S;
     const int logC = log_n - LOGR;
     const u32 c = blockIdx.x * S + sl;
     const auto V = job.view(blockIdx.y);
     if (V.skip) return; // uniform per workgroup, before any barrier
-    const u64 q = V.p.q, q2 = V.p.two_q;
-    const Tw *tw = V.tw;
-    u64 v[E];
+    const A ar(V.p, V.tw, twd);
+    T v[E];
 #pragma unroll
-    for (int e = 0; e < E; e++) v[e] = V.load(c + ((u32)(E * t + e) << logC));
+    for (int e = 0; e < E; e++) v[e] = ar.in(V.load(c + ((u32)(E * t + e) << logC)));
 #pragma unroll
     for (int s = LOGR - 1; s >= LOGE; s--)
-        inv_stage<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return &tw[(1 << s) + ((E * t + e) >> (LOGR - s))]; },
-                     q, q2);
+        ar.template inv<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
     __syncthreads();
@@ -251,14 +336,14 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n)
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + t + TPS * e];
 #pragma unroll
     for (int s = LOGE - 1; s >= 1; s--)
-        inv_stage<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return &tw[(1 << s) + (e >> (LOGE - s))]; }, q, q2);
+        ar.template inv<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
     {
         constexpr int gap = E / 2;
 #pragma unroll
-        for (int e = 0; e < gap; e++) inv_bfly_last(v[e], v[e + gap], V.p);
+        for (int e = 0; e < gap; e++) ar.inv_last(v[e], v[e + gap], V.p);
     }
 #pragma unroll
-    for (int e = 0; e < E; e++) V.store(c + ((u32)(t + TPS * e) << logC), v[e]);
+    for (int e = 0; e < E; e++) V.store(c + ((u32)(t + TPS * e) << logC), ar.out(v[e]));
 }
 
 // --------------------------------------------------------------------------- dispatch
@@ -271,45 +356,55 @@ enum PassKind
     INV_COL
 };
 
-template <int PASS, int LOGR, class Job>
-static inline void launch_pass(const Job &job, int log_n, int jobs, hipStream_t st)
+template <int PASS, int LOGR, class Job, bool FP>
+static inline void launch_pass_a(const Job &job, int log_n, int jobs, long long twd, hipStream_t st)
 {
     constexpr int LOGT = LOGR <= 7 ? 3 : 4;
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
     dim3 grid(subs / SH::S, jobs);
-    if (PASS == FWD_COL) hipLaunchKernelGGL((k_fwd_col<LOGR, LOGT, Job>), grid, dim3(256), 0, st, job, log_n);
-    if (PASS == FWD_ROW) hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job>), grid, dim3(256), 0, st, job, log_n);
-    if (PASS == INV_ROW) hipLaunchKernelGGL((k_inv_row<LOGR, LOGT, Job>), grid, dim3(256), 0, st, job, log_n);
-    if (PASS == INV_COL) hipLaunchKernelGGL((k_inv_col<LOGR, LOGT, Job>), grid, dim3(256), 0, st, job, log_n);
+    if (PASS == FWD_COL) hipLaunchKernelGGL((k_fwd_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if (PASS == FWD_ROW) hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if (PASS == INV_ROW) hipLaunchKernelGGL((k_inv_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if (PASS == INV_COL) hipLaunchKernelGGL((k_inv_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+}
+
+template <int PASS, int LOGR, class Job>
+static inline void launch_pass(const Job &job, int log_n, int jobs, const NttMode &m, hipStream_t st)
+{
+    const long long d = (PASS == FWD_COL || PASS == FWD_ROW) ? m.dfwd : m.dinv;
+    if (m.fp)
+        launch_pass_a<PASS, LOGR, Job, true>(job, log_n, jobs, d, st);
+    else
+        launch_pass_a<PASS, LOGR, Job, false>(job, log_n, jobs, 0, st);
 }
 
 template <int PASS, class Job>
-static inline void launch_col(const Job &job, int log_n, int jobs, hipStream_t st)
+static inline void launch_col(const Job &job, int log_n, int jobs, const NttMode &m, hipStream_t st)
 {
     switch ((log_n + 1) / 2)
     {
-    case 6: launch_pass<PASS, 6>(job, log_n, jobs, st); break;
-    case 7: launch_pass<PASS, 7>(job, log_n, jobs, st); break;
-    case 8: launch_pass<PASS, 8>(job, log_n, jobs, st); break;
+    case 6: launch_pass<PASS, 6>(job, log_n, jobs, m, st); break;
+    case 7: launch_pass<PASS, 7>(job, log_n, jobs, m, st); break;
+    case 8: launch_pass<PASS, 8>(job, log_n, jobs, m, st); break;
     }
 }
 
 template <int PASS, class Job>
-static inline void launch_row(const Job &job, int log_n, int jobs, hipStream_t st)
+static inline void launch_row(const Job &job, int log_n, int jobs, const NttMode &m, hipStream_t st)
 {
     switch (log_n / 2)
     {
-    case 6: launch_pass<PASS, 6>(job, log_n, jobs, st); break;
-    case 7: launch_pass<PASS, 7>(job, log_n, jobs, st); break;
-    case 8: launch_pass<PASS, 8>(job, log_n, jobs, st); break;
+    case 6: launch_pass<PASS, 6>(job, log_n, jobs, m, st); break;
+    case 7: launch_pass<PASS, 7>(job, log_n, jobs, m, st); break;
+    case 8: launch_pass<PASS, 8>(job, log_n, jobs, m, st); break;
     }
 }
 
-template <class Job> static inline void fwd_col(const Job &j, int log_n, int jobs, hipStream_t st) { launch_col<FWD_COL>(j, log_n, jobs, st); }
-template <class Job> static inline void fwd_row(const Job &j, int log_n, int jobs, hipStream_t st) { launch_row<FWD_ROW>(j, log_n, jobs, st); }
-template <class Job> static inline void inv_row(const Job &j, int log_n, int jobs, hipStream_t st) { launch_row<INV_ROW>(j, log_n, jobs, st); }
-template <class Job> static inline void inv_col(const Job &j, int log_n, int jobs, hipStream_t st) { launch_col<INV_COL>(j, log_n, jobs, st); }
+template <class Job> static inline void fwd_col(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_col<FWD_COL>(j, log_n, jobs, m, st); }
+template <class Job> static inline void fwd_row(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_row<FWD_ROW>(j, log_n, jobs, m, st); }
+template <class Job> static inline void inv_row(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_row<INV_ROW>(j, log_n, jobs, m, st); }
+template <class Job> static inline void inv_col(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_col<INV_COL>(j, log_n, jobs, m, st); }
 
 // ============================================================================
 // Fused key-switching ModUp row pass + key inner product (evaluator.cpp:2386-2463).
@@ -357,30 +452,33 @@ __device__ __forceinline__ void lds_barrier()
 
 // Forward stages [s0, s1) of the local 2^LOGR transform, twiddles from the block's LDS row
 // (entry (1 << s) + g holds tw[((2^k1 + b) << s) + g]).
-template <int LOGR>
-__device__ __forceinline__ void row_stages(u64 (&v)[8], u32 t, int b_lo, int s0, int s1, const Tw *twl, u64 q,
-                                           u64 q2)
+template <int LOGR, class A>
+__device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_lo, int s0, int s1,
+                                           const typename A::TW *twl, const A &ar)
 {
 #pragma unroll
     for (int s = s0; s < s1; s++)
-        fwd_stage<8>(v, 1 << (LOGR - 1 - s - b_lo), // gap in slot units
-                     [&](int e) { return &twl[(1 << s) + (lay(t, e, b_lo) >> (LOGR - s))]; }, q, q2);
+        ar.template fwd_tab<8>(v, 1 << (LOGR - 1 - s - b_lo), twl, // gap in slot units
+                               [&](int e) { return (1 << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
 }
 
-template <int LOGR>
+template <int LOGR, bool FP>
 __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass out
                                                        const u64 *__restrict__ target, // [L][n] NTT form
                                                        const u64 *__restrict__ key,    // [digits][2][key_limbs][n]
                                                        u64 *__restrict__ acc,          // [G][2][L+1][n]
                                                        const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int key_limbs,
-                                                       int log_n)
+                                                       int log_n, long long twd)
 {
     using SH = RowMacShape<LOGR>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
+    using TW = typename A::TW;
     constexpr int R = SH::R, TPS = SH::TPS, S = SH::S;
     constexpr int B_A = LOGR - 3, B_B = LOGR - 6;
-    __shared__ u64 xch[2][S * R];
-    __shared__ Tw twl[S * (R + 1)];
+    __shared__ T xch[2][S * R];
+    __shared__ TW twl[S * (R + 1)];
     const int G = gridDim.z, g = blockIdx.z;
     const int j0 = (L * g) / G, j1 = (L * (g + 1)) / G;
     const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
@@ -393,10 +491,11 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     const PrimeDev p = primes[pi];
     const size_t n = (size_t)1 << log_n;
     const size_t kstride = (size_t)key_limbs * n;
+    const A ar(p, tw_all + ((size_t)pi << log_n), twd);
 
     // stage this workgroup's row-pass twiddles (all digits share them)
     {
-        const Tw *tw = tw_all + ((size_t)pi << log_n);
+        const TW *tw = ar.tw;
         for (u32 idx = tid; idx < (u32)(S * R); idx += 256)
         {
             const u32 blk = idx / R, k = idx % R;
@@ -405,8 +504,8 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
             twl[blk * (R + 1) + k] = tw[(((R1 + blockIdx.x * S + blk) << s)) + (k - (1u << s))];
         }
     }
-    const Tw *mytw = &twl[sl * (R + 1)];
-    u64 *x0 = &xch[0][sl * R], *x1 = &xch[1][sl * R];
+    const TW *mytw = &twl[sl * (R + 1)];
+    T *x0 = &xch[0][sl * R], *x1 = &xch[1][sl * R];
 
     Acc128 a0[8], a1[8];
 #pragma unroll
@@ -446,33 +545,37 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
         for (int e = 0; e < 8; e++) v[e] = vin[e];
         if (J != I)
         {
-            row_stages<LOGR>(v, t, B_A, 0, 3, mytw, p.q, p.two_q);
+            T w[8];
 #pragma unroll
-            for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = v[e];
+            for (int e = 0; e < 8; e++) w[e] = ar.in(vin[e]);
+            row_stages<LOGR, A>(w, t, B_A, 0, 3, mytw, ar);
+#pragma unroll
+            for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
             lds_barrier();
 #pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = x0[swz(lay(t, e, B_B))];
-            row_stages<LOGR>(v, t, B_B, 3, 6, mytw, p.q, p.two_q);
-            u64 *xl = x1;
+            for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
+            row_stages<LOGR, A>(w, t, B_B, 3, 6, mytw, ar);
+            T *xl = x1;
             int bl = B_B;
             if (LOGR > 6)
             {
 #pragma unroll
-                for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = v[e];
+                for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
                 lds_barrier();
 #pragma unroll
-                for (int e = 0; e < 8; e++) v[e] = x1[swz(lay(t, e, 0))];
-                row_stages<LOGR>(v, t, 0, 6, LOGR, mytw, p.q, p.two_q);
+                for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
+                row_stages<LOGR, A>(w, t, 0, 6, LOGR, mytw, ar);
                 xl = x0;
                 bl = 0;
             }
             // back to the coalesced layout of the key stream; canonical digits keep the
             // 128-bit sums exact for any digit count below 2^8
+            u64 *xu = reinterpret_cast<u64 *>(xl);
 #pragma unroll
-            for (int e = 0; e < 8; e++) xl[swz(lay(t, e, bl))] = csub(csub(v[e], p.two_q), p.q);
+            for (int e = 0; e < 8; e++) xu[swz(lay(t, e, bl))] = ar.canon(w[e]);
             lds_barrier();
 #pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = xl[swz(lay(t, e, B_A))];
+            for (int e = 0; e < 8; e++) v[e] = xu[swz(lay(t, e, B_A))];
         }
 #pragma unroll
         for (int e = 0; e < 8; e++)
@@ -514,26 +617,36 @@ static inline int ks_groups(int L)
     return L >= 24 ? 4 : (L >= 8 ? 2 : 1);
 }
 
-static inline void ks_row_mac(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
-                              const Tw *tw, int L, int K, int key_limbs, int log_n, hipStream_t st)
+template <int LOGR, bool FP>
+static inline void ks_row_mac_a(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
+                                const Tw *tw, int L, int K, int key_limbs, int log_n, long long twd, int G,
+                                hipStream_t st)
 {
-    const int logr = log_n / 2;
-    const int blocks = 1 << (log_n - logr);
+    const int blocks = 1 << (log_n - LOGR);
+    hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP>), dim3(blocks / RowMacShape<LOGR>::S, L + 1, G), dim3(256), 0, st,
+                       inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, twd);
+}
+
+template <int LOGR>
+static inline void ks_row_mac_m(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
+                                const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, int G,
+                                hipStream_t st)
+{
+    if (m.fp)
+        ks_row_mac_a<LOGR, true>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m.dfwd, G, st);
+    else
+        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, st);
+}
+
+static inline void ks_row_mac(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
+                              const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, hipStream_t st)
+{
     const int G = ks_groups(L);
-    switch (logr)
+    switch (log_n / 2)
     {
-    case 6:
-        hipLaunchKernelGGL(k_ks_row_mac<6>, dim3(blocks / RowMacShape<6>::S, L + 1, G), dim3(256), 0, st, inter,
-                           target, key, acc, primes, tw, L, K, key_limbs, log_n);
-        break;
-    case 7:
-        hipLaunchKernelGGL(k_ks_row_mac<7>, dim3(blocks / RowMacShape<7>::S, L + 1, G), dim3(256), 0, st, inter,
-                           target, key, acc, primes, tw, L, K, key_limbs, log_n);
-        break;
-    case 8:
-        hipLaunchKernelGGL(k_ks_row_mac<8>, dim3(blocks / RowMacShape<8>::S, L + 1, G), dim3(256), 0, st, inter,
-                           target, key, acc, primes, tw, L, K, key_limbs, log_n);
-        break;
+    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, st); break;
+    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, st); break;
+    case 8: ks_row_mac_m<8>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, st); break;
     }
     if (G > 1)
     {
