@@ -188,6 +188,9 @@ struct mhe_ctx
     NttMode nm;         // FP64 butterflies when every prime is < 2^51 (MHE_FP=0 forces integer)
     int ks_fused = 1; // fused row-pass + key-MAC kernel (MHE_KS_FUSED=0: separate row pass + MAC)
     int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
+    int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
+    int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
+    int ks_colgroups = 5; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };
@@ -202,7 +205,7 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out)
         w.base = nullptr;
         const size_t n = c->n, L = limbs;
         const size_t Lc = L < 3 ? 3 : L;
-        size_t words = Lc * n + (L + 1) * L * n + 4 * 2 * (L + 1) * n + L * n + 3 * L * n;
+        size_t words = Lc * n + (L + 1) * L * n + 8 * 2 * (L + 1) * n + L * n + 3 * L * n;
         HIP_TRY(hipSetDevice(c->device));
         if (hipMalloc(&w.base, words * sizeof(u64)) != hipSuccess)
         {
@@ -212,7 +215,7 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out)
         w.coeff = w.base;
         w.modup = w.coeff + Lc * n;
         w.acc = w.modup + (L + 1) * L * n;
-        w.tmp = w.acc + 4 * 2 * (L + 1) * n; // acc holds up to 4 digit-group partials
+        w.tmp = w.acc + 8 * 2 * (L + 1) * n; // acc holds up to 8 digit-group partials
         w.ct3 = w.tmp + L * n;
         w.max_limbs = limbs;
     }
@@ -820,11 +823,28 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
     }
     if (c->ks_fused)
     {
-        // 2+3 (experimental): column pass for all output primes, then the row pass fused
-        // with the key MAC so NTT'd digits never leave registers.
-        JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, 0 };
-        fwd_col(j, log_n, (L + 1) * L, c->nm, st);
-        ks_row_mac(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, c->nm, st);
+        // 2+3. ModUp column pass, then its row pass fused with the key MAC so NTT'd digits
+        //      never leave registers; optionally in chunks of output primes so a chunk's
+        //      column-pass output can stay in the Infinity Cache (MHE_KS_FCHUNK).
+        const int G = c->ks_groups > 0 ? c->ks_groups : ks_groups(L);
+        const int P = c->ks_fchunk > 0 ? c->ks_fchunk : L + 1;
+        for (int I0 = 0; I0 <= L; I0 += P)
+        {
+            const int cnt = (I0 + P <= L + 1) ? P : L + 1 - I0;
+            if (c->ks_colgroups > 0)
+            {
+                const int IG = c->ks_colgroups < cnt ? c->ks_colgroups : cnt;
+                modup_col(w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, IG, st);
+            }
+            else
+            {
+                JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
+                fwd_col(j, log_n, cnt * L, c->nm, st);
+            }
+            ks_row_mac_chunk(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, c->nm, G, I0,
+                             cnt, st);
+        }
+        ks_acc_finish(w->acc, c->primes, L, c->K, G, log_n, st);
     }
     else
     {
@@ -983,6 +1003,9 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     c->q.assign(moduli, moduli + count);
     if (const char *f = getenv("MHE_KS_FUSED")) c->ks_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_CHUNK")) c->ks_chunk = atoi(f);
+    if (const char *f = getenv("MHE_KS_FCHUNK")) c->ks_fchunk = atoi(f);
+    if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
+    if (const char *f = getenv("MHE_KS_GROUPS")) c->ks_groups = atoi(f) > 8 ? 8 : atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);
     for (int k = 0; k < count; k++)

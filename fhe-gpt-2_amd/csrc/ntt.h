@@ -346,6 +346,102 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long t
     for (int e = 0; e < E; e++) V.store(c + ((u32)(t + TPS * e) << logC), ar.out(v[e]));
 }
 
+// ------------------------------------------------- key-switch ModUp, digit-major column pass
+// Column pass of the ModUp (evaluator.cpp:2386-2408) with one workgroup per (column block,
+// digit J, group of output primes): the digit's columns are read once into registers and
+// lifted + transformed for every output prime I of the group (I == J skipped: the MAC reads
+// the input NTT form).  Reading each digit once instead of once per output prime removes
+// L(L+1) - L limb reads (~1 GB at L=44) from the key switch.
+template <int LOGR, int LOGT, bool FP>
+__global__ __launch_bounds__(256) void k_modup_col(const u64 *__restrict__ coeff, u64 *__restrict__ modup,
+                                                   const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all,
+                                                   int L, int K, int log_n, long long twd, int I0, int Icnt)
+{
+    using SH = Shape<LOGR, LOGT>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
+    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
+    __shared__ T lds[S * LD];
+    const int tid = threadIdx.x, sl = tid % S, t = tid / S;
+    const int logC = log_n - LOGR;
+    const u32 c = blockIdx.x * S + sl;
+    const int J = blockIdx.y;
+    const int IG = gridDim.z, g = blockIdx.z;
+    const int i_lo = I0 + (Icnt * g) / IG, i_hi = I0 + (Icnt * (g + 1)) / IG;
+    const u64 *src = coeff + ((size_t)J << log_n);
+    u64 x[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) x[e] = src[c + ((u32)(t + TPS * e) << logC)];
+    const u64 qJ = primes[J].q;
+    for (int I = i_lo; I < i_hi; I++)
+    {
+        if (I == J) continue; // uniform per workgroup
+        const int pi = (I == L) ? K - 1 : I;
+        const PrimeDev p = primes[pi];
+        const A ar(p, tw_all + ((size_t)pi << log_n), twd);
+        T v[E];
+        if constexpr (FP)
+        {
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = fp_reduce((double)x[e], ar.q, ar.qinv);
+        }
+        else
+        {
+            const bool red = qJ > p.q; // key_modulus[J] <= key_modulus[I] -> plain copy
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = red ? barrett64(x[e], p) : x[e];
+        }
+#pragma unroll
+        for (int s = 0; s < LOGE; s++)
+            ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+#pragma unroll
+        for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+#pragma unroll
+        for (int s = LOGE; s < LOGR; s++)
+            ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
+        u64 *dst = modup + (((size_t)(I - I0) * L + J) << log_n);
+#pragma unroll
+        for (int e = 0; e < E; e++) dst[c + ((u32)(E * t + e) << logC)] = ar.out(v[e]);
+        __syncthreads(); // lds is rewritten by the next output prime
+    }
+}
+
+template <int LOGR, bool FP>
+static inline void modup_col_a(const u64 *coeff, u64 *modup, const PrimeDev *primes, const Tw *tw, int L, int K,
+                               int log_n, long long twd, int I0, int Icnt, int IG, hipStream_t st)
+{
+    constexpr int LOGT = LOGR <= 7 ? 3 : 4;
+    using SH = Shape<LOGR, LOGT>;
+    const int subs = 1 << (log_n - LOGR);
+    hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3(subs / SH::S, L, IG), dim3(256), 0, st, coeff, modup,
+                       primes, tw, L, K, log_n, twd, I0, Icnt);
+}
+
+// ModUp column pass for output primes I0 .. I0+Icnt-1 (modup holds exactly those), in IG
+// groups of output primes per digit.
+static inline void modup_col(const u64 *coeff, u64 *modup, const PrimeDev *primes, const Tw *tw, int L, int K,
+                             int log_n, const NttMode &m, int I0, int Icnt, int IG, hipStream_t st)
+{
+    switch ((log_n + 1) / 2)
+    {
+    case 6:
+        if (m.fp) modup_col_a<6, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, st);
+        else modup_col_a<6, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, st);
+        break;
+    case 7:
+        if (m.fp) modup_col_a<7, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, st);
+        else modup_col_a<7, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, st);
+        break;
+    case 8:
+        if (m.fp) modup_col_a<8, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, st);
+        else modup_col_a<8, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, st);
+        break;
+    }
+}
+
 // --------------------------------------------------------------------------- dispatch
 // Pass split: column pass takes ceil(K/2) stages, row pass floor(K/2).
 enum PassKind
@@ -469,7 +565,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                                                        u64 *__restrict__ acc,          // [G][2][L+1][n]
                                                        const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int key_limbs,
-                                                       int log_n, long long twd)
+                                                       int log_n, long long twd, int I0)
 {
     using SH = RowMacShape<LOGR>;
     using A = NttArith<FP>;
@@ -485,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     const u32 b = blockIdx.x * S + sl;
     const u32 base = b << LOGR;
     const u32 R1 = 1u << (log_n - LOGR);
-    const int I = blockIdx.y;
+    const int I = I0 + blockIdx.y; // inter holds output primes I0 .. I0 + gridDim.y - 1
     const int pi = (I == L) ? K - 1 : I;
     const int ki = (I == L) ? key_limbs - 1 : I;
     const PrimeDev p = primes[pi];
@@ -512,7 +608,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     for (int e = 0; e < 8; e++) a0[e] = a1[e] = Acc128{ 0, 0 };
 
     auto digit_src = [&](int J) -> const u64 * {
-        return (J == I) ? target + (size_t)J * n + base : inter + ((size_t)I * L + J) * n + base;
+        return (J == I) ? target + (size_t)J * n + base : inter + ((size_t)(I - I0) * L + J) * n + base;
     };
     u64 vin[8];
     {
@@ -614,40 +710,46 @@ __global__ void k_acc_reduce(u64 *acc, const PrimeDev *primes, int L, int K, int
 // Digit groups G: enough workgroups to hide HBM latency (each one walks L/G digits).
 static inline int ks_groups(int L)
 {
-    return L >= 24 ? 4 : (L >= 8 ? 2 : 1);
+    return L >= 32 ? 1 : (L >= 8 ? 2 : 1); // measured at L=44: G=1 763, 2 738, 4 700 HMult/s
 }
 
 template <int LOGR, bool FP>
 static inline void ks_row_mac_a(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
-                                const Tw *tw, int L, int K, int key_limbs, int log_n, long long twd, int G,
-                                hipStream_t st)
+                                const Tw *tw, int L, int K, int key_limbs, int log_n, long long twd, int G, int I0,
+                                int cnt, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
-    hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP>), dim3(blocks / RowMacShape<LOGR>::S, L + 1, G), dim3(256), 0, st,
-                       inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, twd);
+    hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP>), dim3(blocks / RowMacShape<LOGR>::S, cnt, G), dim3(256), 0, st,
+                       inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, twd, I0);
 }
 
 template <int LOGR>
 static inline void ks_row_mac_m(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
-                                const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, int G,
-                                hipStream_t st)
+                                const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, int G, int I0,
+                                int cnt, hipStream_t st)
 {
     if (m.fp)
-        ks_row_mac_a<LOGR, true>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m.dfwd, G, st);
+        ks_row_mac_a<LOGR, true>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m.dfwd, G, I0, cnt, st);
     else
-        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, st);
+        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, I0, cnt, st);
 }
 
-static inline void ks_row_mac(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
-                              const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, hipStream_t st)
+// Fused row pass + MAC for output primes I0 .. I0+cnt-1 (inter holds exactly those).
+static inline void ks_row_mac_chunk(const u64 *inter, const u64 *target, const u64 *key, u64 *acc,
+                                    const PrimeDev *primes, const Tw *tw, int L, int K, int key_limbs, int log_n,
+                                    const NttMode &m, int G, int I0, int cnt, hipStream_t st)
 {
-    const int G = ks_groups(L);
     switch (log_n / 2)
     {
-    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, st); break;
-    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, st); break;
-    case 8: ks_row_mac_m<8>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, st); break;
+    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, st); break;
+    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, st); break;
+    case 8: ks_row_mac_m<8>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, st); break;
     }
+}
+
+// Sum of the G digit-group partials (after every chunk has run).
+static inline void ks_acc_finish(u64 *acc, const PrimeDev *primes, int L, int K, int G, int log_n, hipStream_t st)
+{
     if (G > 1)
     {
         const size_t per = (size_t)2 * (L + 1) << log_n;

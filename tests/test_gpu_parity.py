@@ -408,6 +408,51 @@ def test_switch_key_chunked_modup(chunk):
     assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
 
 
+# ------------------------------------------- every arithmetic / scheduling variant, bit-exact
+ENGINE_VARIANTS = [
+    {"MHE_FP": "0"},                                  # integer Harvey/Shoup butterflies everywhere
+    {"MHE_FP": "0", "MHE_KS_FUSED": "0"},             # integer, unfused row pass + k_ks_mac
+    {"MHE_KS_FUSED": "0"},                            # FP64, unfused
+    {"MHE_KS_COLGROUPS": "0"},                        # fused, one column-pass job per (I, J)
+    {"MHE_KS_COLGROUPS": "1", "MHE_KS_GROUPS": "3"},  # digit-major column pass, 3 digit groups
+    {"MHE_KS_FCHUNK": "3", "MHE_KS_GROUPS": "2"},     # output primes in chunks of 3
+    {"MHE_FP": "0", "MHE_KS_FCHUNK": "2", "MHE_KS_COLGROUPS": "2"},
+]
+
+
+def _variant_chain(env, seed):
+    import os
+
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Chain(12, SMALL_BITS, seed=seed)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("variant", range(len(ENGINE_VARIANTS)))
+def test_engine_variants_bit_exact(variant):
+    ch = _variant_chain(ENGINE_VARIANTS[variant], 60 + variant)
+    key = ch.rand_key()
+    for L in (1, 3, ch.K - 1):
+        ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+        got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
+        assert np.array_equal(got, ch.oc.switch_key(ct, target, key)), (ENGINE_VARIANTS[variant], L)
+    L = ch.K - 1
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
+    assert np.array_equal(got, ch.oc.hmult(a, b, key))
+    x = ch.rand(2, L, ch.n)
+    assert np.array_equal(ch.down(ch.eng.rescale_to_next(ch.up(x))), ch.oc.rescale(x))
+    assert np.array_equal(ch.down(ch.eng.ntt_forward(ch.up(x))), ch.oc.ntt(x, O.NTT_FWD))
+    assert np.array_equal(ch.down(ch.eng.ntt_inverse(ch.up(x))), ch.oc.ntt(x, O.NTT_INV))
+
+
 # ----------------------------------------------------------------- CKKS encode (A13, A14)
 @pytest.mark.parametrize("kind", ["real", "complex", "partial"])
 def test_ckks_encode_bit_exact(small, kind):
