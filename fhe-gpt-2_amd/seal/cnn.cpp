@@ -1,0 +1,453 @@
+// cnn.cpp -- multiplexed-packing CNN layers (include/mhe_cnn.h) over the seal:: surface.
+//
+// The reference's layers (cnn_ckks/cpu-ckks/single-key/cnn/cnn_seal.cpp) are host loops that
+// build plaintext masks/weights and issue rotations, multiply_vector, add and rescale on one
+// ciphertext.  Here the same operation sequence runs on the GPU engine; the host work (mask and
+// weight vectors) is computed once per call as in the reference.  Packing (Lee et al.,
+// "multiplexed parallel convolution"): slot s of a TensorCipher (k, h, w, c, t, p) is copy
+// s / (n/p); inside a copy, local index = k^2*h*w*u + k*w*R + C encodes channel
+// k^2*u + k*(R%k) + C%k at pixel (R/k, C/k).
+#include "mhe_cnn.h"
+
+#include <cmath>
+#include <iostream>
+#include <stdexcept>
+
+using namespace seal;
+
+long pow2(long n)
+{
+    return 1L << n;
+}
+
+int floor_to_int(double x)
+{
+    return static_cast<int>(std::floor(x) + 0.5);
+}
+
+long log2_long(long n)
+{
+    // -1 unless n is a power of two in [1, 65536] (common/MinicompFunc.cpp:37-46)
+    if (n > 65536 || n <= 0) throw std::out_of_range("n is too large.");
+    for (int i = 0; i <= 16; i++)
+        if ((1L << i) == n) return i;
+    return -1;
+}
+
+namespace
+{
+// Slot decomposition of the multiplexed layout (cnn_seal.cpp:359-360, 551-552, 601-603).
+struct Mux
+{
+    long n;
+    int k, h, w, t, p;
+    long copy_len() const { return n / p; }
+    struct Slot
+    {
+        long copy;    // which of the p replicas
+        long local;   // index inside the replica
+        int u;        // channel group
+        int rb, cb;   // multiplexed row / column (k*h x k*w grid)
+        int channel;  // k^2*u + k*(rb%k) + cb%k
+        int row, col; // pixel
+    };
+    Slot at(long s) const
+    {
+        Slot r;
+        r.copy = s / copy_len();
+        r.local = s % copy_len();
+        const long plane = (long)k * k * h * w;
+        r.u = (int)(r.local / plane);
+        const long rem = r.local % plane;
+        r.rb = (int)(rem / ((long)k * w));
+        r.cb = (int)(rem % ((long)k * w));
+        r.channel = k * k * r.u + k * (r.rb % k) + r.cb % k;
+        r.row = r.rb / k;
+        r.col = r.cb / k;
+        return r;
+    }
+    bool in_tensor(const Slot &r) const { return r.local < (long)k * k * h * w * t; }
+};
+} // namespace
+
+// ------------------------------------------------------------------------ TensorCipher
+TensorCipher::TensorCipher() = default;
+
+TensorCipher::TensorCipher(int logn, int k, int h, int w, int c, int t, int p, std::vector<double> data,
+                           Encryptor &encryptor, CKKSEncoder &encoder, int logp)
+    : k_(k), h_(h), w_(w), c_(c), t_(t), p_(p), logn_(logn)
+{
+    // cnn_seal.cpp:12-48
+    if (k != 1) throw std::invalid_argument("supported k is only 1 right now");
+    if (logn < 1 || logn > 16) throw std::out_of_range("the value of logn is out of range");
+    if (data.size() > static_cast<std::size_t>(1L << logn)) throw std::out_of_range("the size of data is larger than n");
+    data.resize(static_cast<std::size_t>(1L << logn), 0.0); // zero padding to n slots
+    Plaintext plain;
+    encoder.encode(data, std::pow(2.0, logp), plain);
+    encryptor.encrypt(plain, cipher_);
+}
+
+TensorCipher::TensorCipher(int logn, int k, int h, int w, int c, int t, int p, Ciphertext cipher)
+    : k_(k), h_(h), w_(w), c_(c), t_(t), p_(p), logn_(logn), cipher_(std::move(cipher))
+{}
+
+void TensorCipher::print_parms()
+{
+    std::cout << "k: " << k_ << "\nh: " << h_ << "\nw: " << w_ << "\nc: " << c_ << "\nt: " << t_ << "\np: " << p_
+              << std::endl;
+}
+
+// ------------------------------------------------------------------------ rotations
+void memory_save_rotate(const Ciphertext &cipher_in, Ciphertext &cipher_out, int steps, Evaluator &evaluator,
+                        GaloisKeys &gal_keys)
+{
+    // cnn_seal.cpp:788-809: steps in 34..55 and 57..61 go through a first rotation by 33 (the
+    // key set of infer_seal.cpp lacks them); a zero rotation leaves cipher_out untouched.
+    const long slots = static_cast<long>(cipher_in.poly_modulus_degree() / 2);
+    const long s = (steps + slots) % slots; // C++ remainder, as the reference: 0..slots-1 for steps >= -slots
+    if (s == 0) return;
+    Ciphertext temp = cipher_in;
+    const bool split = (s >= 34 && s <= 55) || (s >= 57 && s <= 61);
+    if (split)
+    {
+        evaluator.rotate_vector_inplace(temp, 33, gal_keys);
+        evaluator.rotate_vector_inplace(temp, static_cast<int>(s - 33), gal_keys);
+    }
+    else
+        evaluator.rotate_vector_inplace(temp, static_cast<int>(s), gal_keys);
+    cipher_out = std::move(temp);
+}
+
+// ------------------------------------------------------------------------ convolution
+void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, int co, int st, int fh,
+                                           int fw, const std::vector<double> &data, std::vector<double> running_var,
+                                           std::vector<double> constant_weight, double epsilon, CKKSEncoder &encoder,
+                                           Encryptor &encryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                                           std::vector<Ciphertext> &cipher_pool, bool end)
+{
+    // cnn_seal.cpp:284-530
+    const int ki = cnn_in.k(), hi = cnn_in.h(), wi = cnn_in.w(), ci = cnn_in.c(), ti = cnn_in.t(), pi = cnn_in.p(),
+              logn = cnn_in.logn();
+    if (st != 1 && st != 2) throw std::invalid_argument("supported st is only 1 or 2");
+    if (static_cast<int>(data.size()) != fh * fw * ci * co)
+        throw std::invalid_argument("the size of data vector is not ker x ker x h x h");
+    if (log2_long(ki) == -1) throw std::invalid_argument("ki is not power of two");
+    if (static_cast<int>(running_var.size()) != co || static_cast<int>(constant_weight.size()) != co)
+        throw std::invalid_argument("the size of running_var or weight is not correct");
+    for (double v : running_var)
+        if (v < 1e-16 && v > -1e-16) throw std::invalid_argument("the size of running_var is too small. nearly zero.");
+    if (fh % 2 == 0 || fw % 2 == 0) throw std::invalid_argument("fh and fw should be odd");
+    int ho = hi, wo = wi, ko = ki;
+    if (st == 2)
+    {
+        if (hi % 2 == 1 || wi % 2 == 1) throw std::invalid_argument("hi or wi is not even");
+        ho = hi / 2;
+        wo = wi / 2;
+        ko = 2 * ki;
+    }
+    const long n = 1L << logn;
+    const int to = (co + ko * ko - 1) / (ko * ko);
+    const int po = static_cast<int>(
+        pow2(floor_to_int(std::log(static_cast<double>(n) / static_cast<double>(ko * ko * ho * wo * to)) / std::log(2.0))));
+    const int q = (co + pi - 1) / pi;
+    if (n % pi != 0) throw std::out_of_range("n is not divisible by pi");
+    if (n % po != 0) throw std::out_of_range("n is not divisible by po");
+    if ((long)ki * ki * hi * wi * ti * pi > n) throw std::out_of_range("ki^2 hi wi ti pi is larger than n");
+    if ((long)ko * ko * ho * wo * to * po > n) throw std::out_of_range("ko^2 ho wo to po is larger than n");
+
+    // kernel tap (i1, i2), input channel a, output channel b: data[((b*ci + a)*fh + i1)*fw + i2]
+    auto tap = [&](int i1, int i2, int a, int b) { return data[((size_t)(b * ci + a) * fh + i1) * fw + i2]; };
+    const Mux in{ n, ki, hi, wi, ti, pi };
+    const int ch = (fh - 1) / 2, cw = (fw - 1) / 2;
+
+    // weights of output-channel block i9 for tap (i1, i2): slot of replica i8 carries output
+    // channel i8 + pi*i9 (cnn_seal.cpp:350-368)
+    auto weight_vec = [&](int i1, int i2, int i9) {
+        std::vector<double> v(n, 0.0);
+        for (long s = 0; s < n; s++)
+        {
+            const Mux::Slot r = in.at(s);
+            const int out_ch = static_cast<int>(r.copy) + pi * i9;
+            const int y = r.row - ch + i1, x = r.col - cw + i2;
+            if (!in.in_tensor(r) || out_ch >= co || r.channel >= ci || y < 0 || y > hi - 1 || x < 0 || x > wi - 1)
+                continue;
+            v[s] = tap(i1, i2, r.channel, out_ch);
+        }
+        return v;
+    };
+    // per output channel: BN-folded scale at the slots that hold that channel after the
+    // channel sum (cnn_seal.cpp:370-397)
+    auto select_vec = [&](int j4) {
+        std::vector<double> v(n, 0.0);
+        const double g = constant_weight[j4] / std::sqrt(running_var[j4] + epsilon);
+        for (int u3 = 0; u3 < to; u3++)
+            for (int v1 = 0; v1 < ko * ho; v1++)
+                for (int v2 = 0; v2 < ko * wo; v2++)
+                    if (ko * ko * u3 + ko * (v1 % ko) + v2 % ko == j4) v[(size_t)ko * ko * ho * wo * u3 + ko * wo * v1 + v2] = g;
+        return v;
+    };
+
+    if (cipher_pool.size() < static_cast<size_t>(6 + fh * fw - 1)) cipher_pool.resize(6 + fh * fw - 1);
+    Ciphertext &ctxt_in = cipher_pool[0], &ct_zero = cipher_pool[1], &temp = cipher_pool[2], &sum = cipher_pool[3],
+               &total_sum = cipher_pool[4], &var = cipher_pool[5];
+    ctxt_in = cnn_in.cipher();
+
+    // the fh*fw shifted copies of the input (centre tap is the input itself)
+    std::vector<Ciphertext *> rot((size_t)fh * fw);
+    for (int i1 = 0; i1 < fh; i1++)
+        for (int i2 = 0; i2 < fw; i2++)
+        {
+            const int idx = fw * i1 + i2, centre = fw * ch + cw;
+            rot[idx] = idx == centre ? &ctxt_in : &cipher_pool[6 + (idx > centre ? idx - 1 : idx)];
+        }
+    for (int i1 = 0; i1 < fh; i1++)
+        for (int i2 = 0; i2 < fw; i2++)
+        {
+            Ciphertext &r = *rot[fw * i1 + i2];
+            r = ctxt_in;
+            memory_save_rotate(r, r, ki * ki * wi * (i1 - ch) + ki * (i2 - cw), evaluator, gal_keys);
+        }
+
+    // encryption of zero at the input scale (cnn_seal.cpp:423-427)
+    {
+        Plaintext plain;
+        encoder.encode(std::vector<double>(n, 0.0), ctxt_in.scale(), plain);
+        encryptor.encrypt(plain, ct_zero);
+    }
+
+    const int d = static_cast<int>(log2_long(ki)), c = static_cast<int>(log2_long(ti));
+    for (int i9 = 0; i9 < q; i9++)
+    {
+        // filter taps
+        for (int i1 = 0; i1 < fh; i1++)
+            for (int i2 = 0; i2 < fw; i2++)
+            {
+                evaluator.multiply_vector_reduced_error(*rot[fw * i1 + i2], weight_vec(i1, i2, i9), temp);
+                if (i1 == 0 && i2 == 0)
+                    sum = temp;
+                else
+                    evaluator.add_inplace_reduced_error(sum, temp);
+            }
+        evaluator.rescale_to_next_inplace(sum);
+        var = sum;
+
+        // sum over the input channels held in one replica
+        auto fold = [&](long step) {
+            temp = var;
+            memory_save_rotate(temp, temp, static_cast<int>(step), evaluator, gal_keys);
+            evaluator.add_inplace_reduced_error(var, temp);
+        };
+        for (int x = 0; x < d; x++) fold(pow2(x));
+        for (int x = 0; x < d; x++) fold(pow2(x) * ki * wi);
+        if (c == -1)
+        {
+            sum = ct_zero;
+            for (int x = 0; x < ti; x++)
+            {
+                temp = var;
+                memory_save_rotate(temp, temp, ki * ki * hi * wi * x, evaluator, gal_keys);
+                evaluator.add_inplace_reduced_error(sum, temp);
+            }
+            var = sum;
+        }
+        else
+            for (int x = 0; x < c; x++) fold(pow2(x) * ki * ki * hi * wi);
+
+        // gather each output channel into its slots of the output layout
+        for (int i8 = 0; i8 < pi && pi * i9 + i8 < co; i8++)
+        {
+            const int j4 = pi * i9 + i8;
+            temp = var;
+            memory_save_rotate(temp, temp,
+                               (int)((n / pi) * (j4 % pi) - j4 % ko - (j4 / (ko * ko)) * ko * ko * ho * wo -
+                                     ((j4 % (ko * ko)) / ko) * ko * wo),
+                               evaluator, gal_keys);
+            evaluator.multiply_vector_inplace_reduced_error(temp, select_vec(j4));
+            if (i8 == 0 && i9 == 0)
+                total_sum = temp;
+            else
+                evaluator.add_inplace_reduced_error(total_sum, temp);
+        }
+    }
+    evaluator.rescale_to_next_inplace(total_sum);
+    var = total_sum;
+
+    // po replicas of the output
+    if (!end)
+    {
+        sum = ct_zero;
+        for (int u6 = 0; u6 < po; u6++)
+        {
+            temp = var;
+            memory_save_rotate(temp, temp, static_cast<int>(-u6 * (n / po)), evaluator, gal_keys);
+            evaluator.add_inplace_reduced_error(sum, temp);
+        }
+        var = sum;
+    }
+    cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, var);
+}
+
+// ------------------------------------------------------------------------ batch norm
+void multiplexed_parallel_batch_norm_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, std::vector<double> bias,
+                                          std::vector<double> running_mean, std::vector<double> running_var,
+                                          std::vector<double> weight, double epsilon, CKKSEncoder &encoder,
+                                          Encryptor &encryptor, Evaluator &evaluator, double B, bool)
+{
+    // cnn_seal.cpp:531-576: subtract the encrypted per-channel offset (mean*w/sqrt(var+eps) - bias)/B
+    // (the multiplicative part is folded into the preceding convolution's select vector)
+    const int ki = cnn_in.k(), hi = cnn_in.h(), wi = cnn_in.w(), ci = cnn_in.c(), ti = cnn_in.t(), pi = cnn_in.p(),
+              logn = cnn_in.logn();
+    if (static_cast<int>(bias.size()) != ci || static_cast<int>(running_mean.size()) != ci ||
+        static_cast<int>(running_var.size()) != ci || static_cast<int>(weight.size()) != ci)
+        throw std::invalid_argument("the size of bias, running_mean, running_var, or weight are not correct");
+    for (double v : running_var)
+        if (v < 1e-16 && v > -1e-16) throw std::invalid_argument("the size of running_var is too small. nearly zero.");
+    if ((long)hi * wi * ci > (1L << logn)) throw std::invalid_argument("hi*wi*ci should not be larger than n");
+    const long n = 1L << logn;
+    if (n % pi != 0) throw std::out_of_range("n is not divisible by pi");
+    const Mux in{ n, ki, hi, wi, ti, pi };
+    std::vector<double> g(n, 0.0);
+    for (long s = 0; s < n; s++)
+    {
+        const Mux::Slot r = in.at(s);
+        if (r.channel >= ci || !in.in_tensor(r)) continue;
+        const int i = r.channel;
+        g[s] = (running_mean[i] * weight[i] / std::sqrt(running_var[i] + epsilon) - bias[i]) / B;
+    }
+    Ciphertext temp = cnn_in.cipher(), cipher_g;
+    Plaintext plain;
+    encoder.encode(g, temp.scale(), plain);
+    encryptor.encrypt(plain, cipher_g);
+    evaluator.sub_inplace_reduced_error(temp, cipher_g);
+    cnn_out = TensorCipher(logn, ki, hi, wi, ci, ti, pi, temp);
+}
+
+// ------------------------------------------------------------------------ residual add
+void cnn_add_seal(const TensorCipher &cnn1, const TensorCipher &cnn2, TensorCipher &destination, Evaluator &evaluator)
+{
+    // cnn_seal.cpp:593-609
+    if (cnn1.k() != cnn2.k() || cnn1.h() != cnn2.h() || cnn1.w() != cnn2.w() || cnn1.c() != cnn2.c() ||
+        cnn1.t() != cnn2.t() || cnn1.p() != cnn2.p() || cnn1.logn() != cnn2.logn())
+        throw std::invalid_argument("the parameters of cnn1 and cnn2 are not the same");
+    Ciphertext a = cnn1.cipher();
+    const Ciphertext b = cnn2.cipher();
+    evaluator.add_inplace_reduced_error(a, b);
+    destination = TensorCipher(cnn1.logn(), cnn1.k(), cnn1.h(), cnn1.w(), cnn1.c(), cnn1.t(), cnn1.p(), a);
+}
+
+// ------------------------------------------------------------------------ downsampling
+void multiplexed_parallel_downsampling_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, Evaluator &evaluator,
+                                            GaloisKeys &gal_keys)
+{
+    // cnn_seal.cpp:610-679: keep even pixels, re-multiplex into gap 2k with half the height/width
+    const int ki = cnn_in.k(), hi = cnn_in.h(), wi = cnn_in.w(), ci = cnn_in.c(), ti = cnn_in.t(), logn = cnn_in.logn();
+    const long n = 1L << logn;
+    const int ko = 2 * ki, ho = hi / 2, wo = wi / 2, to = ti / 2, co = 2 * ci;
+    const int po = static_cast<int>(
+        pow2(floor_to_int(std::log(static_cast<double>(n) / static_cast<double>(ko * ko * ho * wo * to)) / std::log(2.0))));
+    if (ti % 8 != 0) throw std::invalid_argument("ti is not multiple of 8");
+    if (hi % 2 != 0) throw std::invalid_argument("hi is not even");
+    if (wi % 2 != 0) throw std::invalid_argument("wi is not even");
+    if (n % po != 0) throw std::out_of_range("n is not divisible by po");
+    const Mux in{ n, ki, hi, wi, ti, 1 };
+    const Ciphertext ct = cnn_in.cipher();
+    Ciphertext sum, temp;
+    for (int w1 = 0; w1 < ki; w1++)
+        for (int w2 = 0; w2 < ti; w2++)
+        {
+            std::vector<double> sel(n, 0.0);
+            for (long s = 0; s < (long)ki * ki * hi * wi * ti; s++)
+            {
+                const Mux::Slot r = in.at(s);
+                if (r.row % 2 == 0 && r.col % 2 == 0 && r.rb % ki == w1 && r.u == w2) sel[s] = 1.0;
+            }
+            temp = ct;
+            evaluator.multiply_vector_inplace_reduced_error(temp, sel);
+            const int w3 = ((ki * w2 + w1) % (2 * ko)) / 2, w4 = (ki * w2 + w1) % 2, w5 = (ki * w2 + w1) / (2 * ko);
+            memory_save_rotate(temp, temp,
+                               ki * ki * hi * wi * w2 + ki * wi * w1 - ko * ko * ho * wo * w5 - ko * wo * w3 - ki * w4 -
+                                   ko * ko * ho * wo * (ti / 8),
+                               evaluator, gal_keys);
+            if (w1 == 0 && w2 == 0)
+                sum = temp;
+            else
+                evaluator.add_inplace_reduced_error(sum, temp);
+        }
+    evaluator.rescale_to_next_inplace(sum);
+    const Ciphertext packed = sum;
+    for (int u6 = 1; u6 < po; u6++)
+    {
+        temp = packed;
+        memory_save_rotate(temp, temp, static_cast<int>(-(n / po) * u6), evaluator, gal_keys);
+        evaluator.add_inplace_reduced_error(sum, temp);
+    }
+    cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, sum);
+}
+
+// ------------------------------------------------------------------------ average pooling
+void averagepooling_seal_scale(const TensorCipher &cnn_in, TensorCipher &cnn_out, Evaluator &evaluator,
+                               GaloisKeys &gal_keys, double B, CKKSEncoder &, Decryptor &, std::ofstream &)
+{
+    // cnn_seal.cpp:680-746: sum the h*w pixels of every channel, then gather channel means
+    // (times B) into consecutive slots
+    const int ki = cnn_in.k(), hi = cnn_in.h(), wi = cnn_in.w(), ci = cnn_in.c(), ti = cnn_in.t(), logn = cnn_in.logn();
+    if (log2_long(hi) == -1) throw std::invalid_argument("hi is not power of two");
+    if (log2_long(wi) == -1) throw std::invalid_argument("wi is not power of two");
+    const long n = 1L << logn;
+    Ciphertext ct = cnn_in.cipher(), temp, sum;
+    for (int x = 0; x < log2_long(wi); x++)
+    {
+        temp = ct;
+        memory_save_rotate(temp, temp, static_cast<int>(pow2(x) * ki), evaluator, gal_keys);
+        evaluator.add_inplace_reduced_error(ct, temp);
+    }
+    for (int x = 0; x < log2_long(hi); x++)
+    {
+        temp = ct;
+        memory_save_rotate(temp, temp, static_cast<int>(pow2(x) * ki * ki * wi), evaluator, gal_keys);
+        evaluator.add_inplace_reduced_error(ct, temp);
+    }
+    for (int s = 0; s < ki; s++)
+        for (int u = 0; u < ti; u++)
+        {
+            const int p = ki * u + s;
+            temp = ct;
+            memory_save_rotate(temp, temp, -p * ki + ki * ki * hi * wi * u + ki * wi * s, evaluator, gal_keys);
+            std::vector<double> sel(n, 0.0);
+            for (int i = 0; i < ki; i++) sel[(size_t)(ki * u + s) * ki + i] = B / static_cast<double>(hi * wi);
+            evaluator.multiply_vector_inplace_reduced_error(temp, sel);
+            if (u == 0 && s == 0)
+                sum = temp;
+            else
+                evaluator.add_inplace_reduced_error(sum, temp);
+        }
+    evaluator.rescale_to_next_inplace(sum);
+    cnn_out = TensorCipher(logn, 1, 1, 1, ci, ti, 1, sum);
+}
+
+// ------------------------------------------------------------------------ fully connected
+void matrix_multiplication_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, std::vector<double> matrix,
+                                std::vector<double> bias, int q, int r, Evaluator &evaluator, GaloisKeys &gal_keys)
+{
+    // cnn_seal.cpp:747-787: diagonal method, q x r matrix over the first r slots
+    if (static_cast<int>(matrix.size()) != q * r) throw std::invalid_argument("the size of matrix is not q*r");
+    if (static_cast<int>(bias.size()) != q) throw std::invalid_argument("the size of bias is not q");
+    const long n = 1L << cnn_in.logn();
+    std::vector<std::vector<double>> diag(q + r - 1, std::vector<double>(n, 0.0));
+    for (int i = 0; i < q; i++)
+        for (int j = 0; j < r; j++) diag[i - j + r - 1][i] = matrix[(size_t)i * r + j];
+    const Ciphertext ct = cnn_in.cipher();
+    Ciphertext temp, sum;
+    for (int s = 0; s < q + r - 1; s++)
+    {
+        temp = ct;
+        memory_save_rotate(temp, temp, r - 1 - s, evaluator, gal_keys);
+        evaluator.multiply_vector_inplace_reduced_error(temp, diag[s]);
+        if (s == 0)
+            sum = temp;
+        else
+            evaluator.add_inplace_reduced_error(sum, temp);
+    }
+    evaluator.rescale_to_next_inplace(sum);
+    cnn_out = TensorCipher(cnn_in.logn(), cnn_in.k(), cnn_in.h(), cnn_in.w(), cnn_in.c(), cnn_in.t(), cnn_in.p(), sum);
+}

@@ -31,6 +31,17 @@ def test_seal_library_loads():
 
 
 @pytest.mark.gpu
+def test_cnn_layers_end_to_end():
+    """Multiplexed-packing CNN layers (include/mhe_cnn.h, cnn_seal.cpp semantics) on encrypted
+    tensors vs the same layers in plain doubles (tests/cpp/cnn_test.cpp)."""
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "cnn_test")], capture_output=True, text=True, timeout=900)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
 def test_seal_api_end_to_end():
     _build()
     r = subprocess.run([DRIVER], capture_output=True, text=True, timeout=600)
