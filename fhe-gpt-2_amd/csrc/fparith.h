@@ -68,6 +68,17 @@ __device__ __forceinline__ void fwd_bfly_f(double &x, double &y, const TwF w, do
     y = u - r;
 }
 
+// Forward butterfly without reducing x, for q < 2^47: within one pass (<= 8 stages) |x| grows
+// from <= 4q by <= 1.5q per stage to <= 16q <= 2^51, which keeps every product's quotient
+// estimate within 1 (|y| <= 2^51) -- so the centered reduction of x can be skipped.
+__device__ __forceinline__ void fwd_bfly_f_lazy(double &x, double &y, const TwF w, double q)
+{
+    const double r = fp_mulmod(y, w.x, w.y, q);
+    const double u = x;
+    x = u + r;
+    y = u - r;
+}
+
 // Inverse Gentleman-Sande butterfly (dwthandler.h:230-233).  |x|,|y| <= 2q + 1: the
 // difference is reduced first so the product's quotient estimate stays within 1.
 __device__ __forceinline__ void inv_bfly_f(double &x, double &y, const TwF w, double q, double qinv)
@@ -86,13 +97,20 @@ __device__ __forceinline__ void inv_bfly_last_f(double &x, double &y, double nin
     y = fp_mulmod(fp_reduce(d, q, qinv), lw, lws, q);
 }
 
-// One forward stage over the E values of a lane (pairs (e, e+gap), gap bit clear).
-template <int E, class TwOf>
+// One forward stage over the E values of a lane (pairs (e, e+gap), gap bit clear); LAZY (only
+// for q < 2^47) drops the reduction of x.
+template <int E, bool LAZY, class TwOf>
 __device__ __forceinline__ void fwd_stage_f(double (&v)[E], int gap, TwOf tw_of, double q, double qinv)
 {
 #pragma unroll
     for (int e = 0; e < E; e++)
-        if (!(e & gap)) fwd_bfly_f(v[e], v[e + gap], *tw_of(e), q, qinv);
+        if (!(e & gap))
+        {
+            if (LAZY)
+                fwd_bfly_f_lazy(v[e], v[e + gap], *tw_of(e), q);
+            else
+                fwd_bfly_f(v[e], v[e + gap], *tw_of(e), q, qinv);
+        }
 }
 
 template <int E, class TwOf>

@@ -190,7 +190,7 @@ struct mhe_ctx
     int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
     int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
     int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
-    int ks_colgroups = 5; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
+    int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };

@@ -144,14 +144,14 @@ struct NttArith<false>
     __device__ void inv_last(T &x, T &y, const PrimeDev &p) const { inv_bfly_last(x, y, p); }
 };
 
-template <>
-struct NttArith<true>
+template <bool LAZY>
+struct NttArithF
 {
     using T = double;
     using TW = TwF;
     double q, qinv;
     const TwF *tw;
-    __device__ NttArith(const PrimeDev &p, const Tw *t, long long delta)
+    __device__ NttArithF(const PrimeDev &p, const Tw *t, long long delta)
         : q((double)p.q), qinv(1.0 / (double)p.q), tw(reinterpret_cast<const TwF *>(reinterpret_cast<const char *>(t) + delta))
     {
     }
@@ -161,12 +161,12 @@ struct NttArith<true>
     template <int E, class Ix>
     __device__ void fwd(T (&v)[E], int gap, Ix ix) const
     {
-        fwd_stage_f<E>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, qinv);
+        fwd_stage_f<E, LAZY>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, qinv);
     }
     template <int E, class Ix>
     __device__ void fwd_tab(T (&v)[E], int gap, const TW *tab, Ix ix) const
     {
-        fwd_stage_f<E>(v, gap, [&](int e) { return &tab[ix(e)]; }, q, qinv);
+        fwd_stage_f<E, LAZY>(v, gap, [&](int e) { return &tab[ix(e)]; }, q, qinv);
     }
     template <int E, class Ix>
     __device__ void inv(T (&v)[E], int gap, Ix ix) const
@@ -178,6 +178,14 @@ struct NttArith<true>
         const double ni = (double)p.ninv, lw = (double)p.last_w;
         inv_bfly_last_f(x, y, ni, ni / q, lw, lw / q, q, qinv);
     }
+};
+
+// FP64 with the reduction of x in every forward stage (any q < 2^51).  The two hot key-switch
+// kernels pick NttArithF<true> per workgroup when q < 2^47 (fparith.h fwd_bfly_f_lazy).
+template <>
+struct NttArith<true> : NttArithF<false>
+{
+    using NttArithF<false>::NttArithF;
 };
 
 // Per-launch arithmetic selection: fp = every prime of the context is < 2^51; the deltas are
@@ -353,7 +361,7 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long t
 // the input NTT form).  Reading each digit once instead of once per output prime removes
 // L(L+1) - L limb reads (~1 GB at L=44) from the key switch.
 template <int LOGR, int LOGT, bool FP>
-__global__ __launch_bounds__(256) void k_modup_col(const u64 *__restrict__ coeff, u64 *__restrict__ modup,
+__global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ coeff, u64 *__restrict__ modup,
                                                    const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all,
                                                    int L, int K, int log_n, long long twd, int I0, int Icnt)
 {
@@ -373,40 +381,56 @@ __global__ __launch_bounds__(256) void k_modup_col(const u64 *__restrict__ coeff
 #pragma unroll
     for (int e = 0; e < E; e++) x[e] = src[c + ((u32)(t + TPS * e) << logC)];
     const u64 qJ = primes[J].q;
-    for (int I = i_lo; I < i_hi; I++)
+    // two sweeps over the group's output primes when FP: first the q < 2^47 ones with the lazy
+    // forward butterflies, then the rest, so each loop body has one arithmetic variant
+    auto sweep = [&](auto mode) {
+        constexpr int M = decltype(mode)::value; // 0 integer, 1 FP lazy, 2 FP full
+        using AA = std::conditional_t<M == 0, NttArith<false>, std::conditional_t<M == 1, NttArithF<true>, NttArithF<false>>>;
+        for (int I = i_lo; I < i_hi; I++)
+        {
+            if (I == J) continue; // uniform per workgroup
+            const int pi = (I == L) ? K - 1 : I;
+            const PrimeDev p = primes[pi];
+            if (M == 1 && !(p.q < (1ull << 47))) continue;
+            if (M == 2 && p.q < (1ull << 47)) continue;
+            const AA ar(p, tw_all + ((size_t)pi << log_n), twd);
+            T v[E];
+            if constexpr (M != 0)
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++) v[e] = fp_reduce((double)x[e], ar.q, ar.qinv);
+            }
+            else
+            {
+                const bool red = qJ > p.q; // key_modulus[J] <= key_modulus[I] -> plain copy
+#pragma unroll
+                for (int e = 0; e < E; e++) v[e] = red ? barrett64(x[e], p) : x[e];
+            }
+#pragma unroll
+            for (int s = 0; s < LOGE; s++)
+                ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+#pragma unroll
+            for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+#pragma unroll
+            for (int s = LOGE; s < LOGR; s++)
+                ar.template fwd<E>(v, 1 << (LOGR - 1 - s),
+                                   [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
+            u64 *dst = modup + (((size_t)(I - I0) * L + J) << log_n);
+#pragma unroll
+            for (int e = 0; e < E; e++) dst[c + ((u32)(E * t + e) << logC)] = ar.out(v[e]);
+            __syncthreads(); // lds is rewritten by the next output prime
+        }
+    };
+    if constexpr (FP)
     {
-        if (I == J) continue; // uniform per workgroup
-        const int pi = (I == L) ? K - 1 : I;
-        const PrimeDev p = primes[pi];
-        const A ar(p, tw_all + ((size_t)pi << log_n), twd);
-        T v[E];
-        if constexpr (FP)
-        {
-#pragma unroll
-            for (int e = 0; e < E; e++) v[e] = fp_reduce((double)x[e], ar.q, ar.qinv);
-        }
-        else
-        {
-            const bool red = qJ > p.q; // key_modulus[J] <= key_modulus[I] -> plain copy
-#pragma unroll
-            for (int e = 0; e < E; e++) v[e] = red ? barrett64(x[e], p) : x[e];
-        }
-#pragma unroll
-        for (int s = 0; s < LOGE; s++)
-            ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
-#pragma unroll
-        for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
-#pragma unroll
-        for (int s = LOGE; s < LOGR; s++)
-            ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
-        u64 *dst = modup + (((size_t)(I - I0) * L + J) << log_n);
-#pragma unroll
-        for (int e = 0; e < E; e++) dst[c + ((u32)(E * t + e) << logC)] = ar.out(v[e]);
-        __syncthreads(); // lds is rewritten by the next output prime
+        sweep(std::integral_constant<int, 1>{});
+        sweep(std::integral_constant<int, 2>{});
     }
+    else
+        sweep(std::integral_constant<int, 0>{});
 }
 
 template <int LOGR, bool FP>
@@ -550,7 +574,7 @@ __device__ __forceinline__ void lds_barrier()
 // (entry (1 << s) + g holds tw[((2^k1 + b) << s) + g]).
 template <int LOGR, class A>
 __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_lo, int s0, int s1,
-                                           const typename A::TW *twl, const A &ar)
+                                           const typename A::TW *twl, const A &ar, int /*deduce*/ = 0)
 {
 #pragma unroll
     for (int s = s0; s < s1; s++)
@@ -558,7 +582,7 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
                                [&](int e) { return (1 << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
 }
 
-template <int LOGR, bool FP>
+template <int LOGR, bool FP, bool KPF>
 __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass out
                                                        const u64 *__restrict__ target, // [L][n] NTT form
                                                        const u64 *__restrict__ key,    // [digits][2][key_limbs][n]
@@ -587,11 +611,11 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     const PrimeDev p = primes[pi];
     const size_t n = (size_t)1 << log_n;
     const size_t kstride = (size_t)key_limbs * n;
-    const A ar(p, tw_all + ((size_t)pi << log_n), twd);
+    const A ar0(p, tw_all + ((size_t)pi << log_n), twd);
 
     // stage this workgroup's row-pass twiddles (all digits share them)
     {
-        const TW *tw = ar.tw;
+        const TW *tw = ar0.tw;
         for (u32 idx = tid; idx < (u32)(S * R); idx += 256)
         {
             const u32 blk = idx / R, k = idx % R;
@@ -603,94 +627,123 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     const TW *mytw = &twl[sl * (R + 1)];
     T *x0 = &xch[0][sl * R], *x1 = &xch[1][sl * R];
 
-    Acc128 a0[8], a1[8];
-#pragma unroll
-    for (int e = 0; e < 8; e++) a0[e] = a1[e] = Acc128{ 0, 0 };
+    auto run = [&](const auto &ar) {
+        Acc128 a0[8], a1[8];
+    #pragma unroll
+        for (int e = 0; e < 8; e++) a0[e] = a1[e] = Acc128{ 0, 0 };
 
-    auto digit_src = [&](int J) -> const u64 * {
-        return (J == I) ? target + (size_t)J * n + base : inter + ((size_t)(I - I0) * L + J) * n + base;
-    };
-    u64 vin[8];
-    {
-        const u64 *src = digit_src(j0);
-#pragma unroll
-        for (int e = 0; e < 8; e++) vin[e] = src[lay(t, e, B_A)];
-    }
-    lds_barrier(); // twiddles visible
+        auto digit_src = [&](int J) -> const u64 * {
+            return (J == I) ? target + (size_t)J * n + base : inter + ((size_t)(I - I0) * L + J) * n + base;
+        };
+        u64 vin[8];
+        {
+            const u64 *src = digit_src(j0);
+    #pragma unroll
+            for (int e = 0; e < 8; e++) vin[e] = src[lay(t, e, B_A)];
+        }
+        lds_barrier(); // twiddles visible
 
-    for (int J = j0; J < j1; J++)
-    {
-        // key for this digit (consumed after the NTT) and the next digit's residues
-        const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n + base;
-        const u64 *k1 = k0 + kstride;
-        u64 kk0[8], kk1[8], vnext[8];
-#pragma unroll
-        for (int e = 0; e < 8; e++)
-        {
-            kk0[e] = k0[lay(t, e, B_A)];
-            kk1[e] = k1[lay(t, e, B_A)];
-        }
-        if (J + 1 < j1)
-        {
-            const u64 *src = digit_src(J + 1);
-#pragma unroll
-            for (int e = 0; e < 8; e++) vnext[e] = src[lay(t, e, B_A)];
-        }
-        u64 v[8];
-#pragma unroll
-        for (int e = 0; e < 8; e++) v[e] = vin[e];
-        if (J != I)
-        {
-            T w[8];
-#pragma unroll
-            for (int e = 0; e < 8; e++) w[e] = ar.in(vin[e]);
-            row_stages<LOGR, A>(w, t, B_A, 0, 3, mytw, ar);
-#pragma unroll
-            for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
-            lds_barrier();
-#pragma unroll
-            for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
-            row_stages<LOGR, A>(w, t, B_B, 3, 6, mytw, ar);
-            T *xl = x1;
-            int bl = B_B;
-            if (LOGR > 6)
+        // key limbs of a digit: issued one digit ahead (KPF) or at the top of the digit (the
+        // fewer-VGPR variant), consumed after the digit's NTT
+        auto load_key = [&](int J, u64 (&a)[8], u64 (&b)[8]) {
+            const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n + base;
+            const u64 *k1 = k0 + kstride;
+    #pragma unroll
+            for (int e = 0; e < 8; e++)
             {
-#pragma unroll
-                for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
-                lds_barrier();
-#pragma unroll
-                for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
-                row_stages<LOGR, A>(w, t, 0, 6, LOGR, mytw, ar);
-                xl = x0;
-                bl = 0;
+                a[e] = k0[lay(t, e, B_A)];
+                b[e] = k1[lay(t, e, B_A)];
             }
-            // back to the coalesced layout of the key stream; canonical digits keep the
-            // 128-bit sums exact for any digit count below 2^8
-            u64 *xu = reinterpret_cast<u64 *>(xl);
-#pragma unroll
-            for (int e = 0; e < 8; e++) xu[swz(lay(t, e, bl))] = ar.canon(w[e]);
-            lds_barrier();
-#pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = xu[swz(lay(t, e, B_A))];
+        };
+        u64 kk0[8], kk1[8];
+        if (KPF) load_key(j0, kk0, kk1);
+        for (int J = j0; J < j1; J++)
+        {
+            u64 kn0[8], kn1[8], vnext[8];
+            if (!KPF)
+                load_key(J, kk0, kk1);
+            else if (J + 1 < j1)
+                load_key(J + 1, kn0, kn1);
+            if (J + 1 < j1)
+            {
+                const u64 *src = digit_src(J + 1);
+    #pragma unroll
+                for (int e = 0; e < 8; e++) vnext[e] = src[lay(t, e, B_A)];
+            }
+            u64 v[8];
+    #pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = vin[e];
+            if (J != I)
+            {
+                T w[8];
+    #pragma unroll
+                for (int e = 0; e < 8; e++) w[e] = ar.in(vin[e]);
+                row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
+    #pragma unroll
+                for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
+                lds_barrier();
+    #pragma unroll
+                for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
+                row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
+                T *xl = x1;
+                int bl = B_B;
+                if (LOGR > 6)
+                {
+    #pragma unroll
+                    for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
+                    lds_barrier();
+    #pragma unroll
+                    for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
+                    row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
+                    xl = x0;
+                    bl = 0;
+                }
+                // back to the coalesced layout of the key stream; canonical digits keep the
+                // 128-bit sums exact for any digit count below 2^8
+                u64 *xu = reinterpret_cast<u64 *>(xl);
+    #pragma unroll
+                for (int e = 0; e < 8; e++) xu[swz(lay(t, e, bl))] = ar.canon(w[e]);
+                lds_barrier();
+    #pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = xu[swz(lay(t, e, B_A))];
+            }
+    #pragma unroll
+            for (int e = 0; e < 8; e++)
+            {
+                mac128(a0[e], v[e], kk0[e]);
+                mac128(a1[e], v[e], kk1[e]);
+            }
+    #pragma unroll
+            for (int e = 0; e < 8; e++) vin[e] = vnext[e];
+            if (KPF)
+            {
+    #pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    kk0[e] = kn0[e];
+                    kk1[e] = kn1[e];
+                }
+            }
         }
-#pragma unroll
+        u64 *o0 = acc + (size_t)(2 * g * (L + 1) + I) * n + base;
+        u64 *o1 = o0 + (size_t)(L + 1) * n;
+    #pragma unroll
         for (int e = 0; e < 8; e++)
         {
-            mac128(a0[e], v[e], kk0[e]);
-            mac128(a1[e], v[e], kk1[e]);
+            const u32 r = lay(t, e, B_A);
+            o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
+            o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
         }
-#pragma unroll
-        for (int e = 0; e < 8; e++) vin[e] = vnext[e];
-    }
-    u64 *o0 = acc + (size_t)(2 * g * (L + 1) + I) * n + base;
-    u64 *o1 = o0 + (size_t)(L + 1) * n;
-#pragma unroll
-    for (int e = 0; e < 8; e++)
+    };
+    if constexpr (FP)
     {
-        const u32 r = lay(t, e, B_A);
-        o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
-        o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
+        if (p.q < (1ull << 47))
+            run(NttArithF<true>(p, tw_all + ((size_t)pi << log_n), twd));
+        else
+            run(ar0);
     }
+    else
+        run(ar0);
 }
 
 // Sum the G partial accumulators: acc[0] += acc[1..G-1] mod q (prime of each limb).
@@ -707,6 +760,16 @@ __global__ void k_acc_reduce(u64 *acc, const PrimeDev *primes, int L, int K, int
     acc[i] = s;
 }
 
+// Key prefetch distance of the fused kernel: none (default; measured equal, fewer VGPRs) or one digit ahead (MHE_KS_KPF=1).
+static inline bool ks_key_prefetch()
+{
+    static const bool v = [] {
+        const char *f = getenv("MHE_KS_KPF");
+        return f && atoi(f) != 0;
+    }();
+    return v;
+}
+
 // Digit groups G: enough workgroups to hide HBM latency (each one walks L/G digits).
 static inline int ks_groups(int L)
 {
@@ -719,8 +782,13 @@ static inline void ks_row_mac_a(const u64 *inter, const u64 *target, const u64 *
                                 int cnt, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
-    hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP>), dim3(blocks / RowMacShape<LOGR>::S, cnt, G), dim3(256), 0, st,
-                       inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, twd, I0);
+    const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, G);
+    if (ks_key_prefetch())
+        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, inter, target, key, acc, primes, tw,
+                           L, K, key_limbs, log_n, twd, I0);
+    else
+        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, inter, target, key, acc, primes,
+                           tw, L, K, key_limbs, log_n, twd, I0);
 }
 
 template <int LOGR>
