@@ -39,6 +39,17 @@ __device__ __forceinline__ double fp_mulmod(double y, double w, double ws, doubl
     return __builtin_fma(-k, q, h) + l;
 }
 
+// a*b mod q in (-1.25q, 1.25q) for a general b in [0, q) (no precomputed b/q) and |a| <= 2^51:
+// the quotient estimate rint(fl(a*b) * fl(1/q)) errs by at most 3*2^-53*|ab/q| + 1/2 <= 0.875.
+// For |a| <= 2^52 (q < 2^51, a not reduced) it errs by at most 2: |result| <= 2q.
+__device__ __forceinline__ double fp_mulmod_gen(double a, double b, double q, double qinv)
+{
+    const double h = a * b;
+    const double l = __builtin_fma(a, b, -h);
+    const double k = fp_rint(h * qinv);
+    return __builtin_fma(-k, q, h) + l;
+}
+
 // centered reduction: x - rint(x/q)*q, |result| <= q/2 + 1 for |x| <= 2^52.
 __device__ __forceinline__ double fp_reduce(double x, double q, double qinv)
 {

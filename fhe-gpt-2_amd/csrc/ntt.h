@@ -628,9 +628,21 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     T *x0 = &xch[0][sl * R], *x1 = &xch[1][sl * R];
 
     auto run = [&](const auto &ar) {
-        Acc128 a0[8], a1[8];
-    #pragma unroll
-        for (int e = 0; e < 8; e++) a0[e] = a1[e] = Acc128{ 0, 0 };
+        // FP: the key inner products run in FP64 as well (fp_mulmod_gen); with q < 2^47 (LZ)
+        // the digits stay unreduced and 44 products (|.| <= 1.1q each) sum exactly below 2^53,
+        // otherwise digits are reduced and the sums every second digit.  Integer: 128-bit
+        // accumulation, one Barrett reduction at the end (evaluator.cpp:2412-2462).
+        constexpr bool LZ = std::is_same<typename std::decay<decltype(ar)>::type, NttArithF<true>>::value;
+        using AccT = typename std::conditional<FP, double, Acc128>::type;
+        AccT a0[8], a1[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+        {
+            if constexpr (FP)
+                a0[e] = a1[e] = 0.0;
+            else
+                a0[e] = a1[e] = Acc128{ 0, 0 };
+        }
 
         auto digit_src = [&](int J) -> const u64 * {
             return (J == I) ? target + (size_t)J * n + base : inter + ((size_t)(I - I0) * L + J) * n + base;
@@ -638,21 +650,21 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
         u64 vin[8];
         {
             const u64 *src = digit_src(j0);
-    #pragma unroll
+#pragma unroll
             for (int e = 0; e < 8; e++) vin[e] = src[lay(t, e, B_A)];
         }
         lds_barrier(); // twiddles visible
 
         // key limbs of a digit: issued one digit ahead (KPF) or at the top of the digit (the
         // fewer-VGPR variant), consumed after the digit's NTT
-        auto load_key = [&](int J, u64 (&a)[8], u64 (&b)[8]) {
+        auto load_key = [&](int J, u64 (&ka)[8], u64 (&kb)[8]) {
             const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n + base;
             const u64 *k1 = k0 + kstride;
-    #pragma unroll
+#pragma unroll
             for (int e = 0; e < 8; e++)
             {
-                a[e] = k0[lay(t, e, B_A)];
-                b[e] = k1[lay(t, e, B_A)];
+                ka[e] = k0[lay(t, e, B_A)];
+                kb[e] = k1[lay(t, e, B_A)];
             }
         };
         u64 kk0[8], kk1[8];
@@ -667,57 +679,83 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
             if (J + 1 < j1)
             {
                 const u64 *src = digit_src(J + 1);
-    #pragma unroll
+#pragma unroll
                 for (int e = 0; e < 8; e++) vnext[e] = src[lay(t, e, B_A)];
             }
-            u64 v[8];
-    #pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = vin[e];
+            T d[8]; // the digit in the coalesced layout, NTT form
             if (J != I)
             {
                 T w[8];
-    #pragma unroll
+#pragma unroll
                 for (int e = 0; e < 8; e++) w[e] = ar.in(vin[e]);
                 row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
-    #pragma unroll
+#pragma unroll
                 for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
                 lds_barrier();
-    #pragma unroll
+#pragma unroll
                 for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
                 row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
                 T *xl = x1;
                 int bl = B_B;
                 if (LOGR > 6)
                 {
-    #pragma unroll
+#pragma unroll
                     for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
                     lds_barrier();
-    #pragma unroll
+#pragma unroll
                     for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
                     row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
                     xl = x0;
                     bl = 0;
                 }
-                // back to the coalesced layout of the key stream; canonical digits keep the
-                // 128-bit sums exact for any digit count below 2^8
-                u64 *xu = reinterpret_cast<u64 *>(xl);
-    #pragma unroll
-                for (int e = 0; e < 8; e++) xu[swz(lay(t, e, bl))] = ar.canon(w[e]);
+                // back to the coalesced layout of the key stream (integer: canonical digits
+                // keep the 128-bit sums exact for any digit count below 2^8)
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    if constexpr (FP)
+                        xl[swz(lay(t, e, bl))] = w[e];
+                    else
+                        xl[swz(lay(t, e, bl))] = ar.canon(w[e]);
+                }
                 lds_barrier();
-    #pragma unroll
-                for (int e = 0; e < 8; e++) v[e] = xu[swz(lay(t, e, B_A))];
+#pragma unroll
+                for (int e = 0; e < 8; e++) d[e] = xl[swz(lay(t, e, B_A))];
             }
-    #pragma unroll
-            for (int e = 0; e < 8; e++)
+            else
             {
-                mac128(a0[e], v[e], kk0[e]);
-                mac128(a1[e], v[e], kk1[e]);
+#pragma unroll
+                for (int e = 0; e < 8; e++) d[e] = ar.in(vin[e]);
             }
-    #pragma unroll
+            if constexpr (FP)
+            {
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    const double dv = LZ ? d[e] : fp_reduce(d[e], ar.q, ar.qinv);
+                    a0[e] += fp_mulmod_gen(dv, (double)kk0[e], ar.q, ar.qinv);
+                    a1[e] += fp_mulmod_gen(dv, (double)kk1[e], ar.q, ar.qinv);
+                    if (!LZ && ((J - j0) & 1))
+                    {
+                        a0[e] = fp_reduce(a0[e], ar.q, ar.qinv);
+                        a1[e] = fp_reduce(a1[e], ar.q, ar.qinv);
+                    }
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    mac128(a0[e], d[e], kk0[e]);
+                    mac128(a1[e], d[e], kk1[e]);
+                }
+            }
+#pragma unroll
             for (int e = 0; e < 8; e++) vin[e] = vnext[e];
             if (KPF)
             {
-    #pragma unroll
+#pragma unroll
                 for (int e = 0; e < 8; e++)
                 {
                     kk0[e] = kn0[e];
@@ -727,12 +765,20 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
         }
         u64 *o0 = acc + (size_t)(2 * g * (L + 1) + I) * n + base;
         u64 *o1 = o0 + (size_t)(L + 1) * n;
-    #pragma unroll
+#pragma unroll
         for (int e = 0; e < 8; e++)
         {
             const u32 r = lay(t, e, B_A);
-            o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
-            o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
+            if constexpr (FP)
+            {
+                o0[r] = fp_canon(a0[e], ar.q, ar.qinv);
+                o1[r] = fp_canon(a1[e], ar.q, ar.qinv);
+            }
+            else
+            {
+                o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
+                o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
+            }
         }
     };
     if constexpr (FP)
