@@ -549,6 +549,7 @@ struct RowMacShape
     static constexpr int R = 1 << LOGR;
     static constexpr int E = 8;
     static constexpr int TPS = R / E;     // lanes per block
+    static_assert(TPS <= 64, "a block's transposes must stay inside one wave");
     static constexpr int S = 256 / TPS;   // blocks per workgroup
 };
 
@@ -568,6 +569,14 @@ __device__ __forceinline__ u32 lay(u32 t, int e, int b_lo)
 __device__ __forceinline__ void lds_barrier()
 {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// A block of R = 2^LOGR residues is held by TPS = R/8 <= 32 lanes, i.e. inside one wave, so
+// its LDS transposes never cross waves: a wave's LDS accesses execute in program order, and
+// only the compiler must be kept from moving them across each other.
+__device__ __forceinline__ void wave_lds_fence()
+{
+    asm volatile("" ::: "memory");
 }
 
 // Forward stages [s0, s1) of the local 2^LOGR transform, twiddles from the block's LDS row
@@ -691,7 +700,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                 row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
 #pragma unroll
                 for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
-                lds_barrier();
+                wave_lds_fence();
 #pragma unroll
                 for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
                 row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
@@ -701,7 +710,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                 {
 #pragma unroll
                     for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
-                    lds_barrier();
+                    wave_lds_fence();
 #pragma unroll
                     for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
                     row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
@@ -718,7 +727,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                     else
                         xl[swz(lay(t, e, bl))] = ar.canon(w[e]);
                 }
-                lds_barrier();
+                wave_lds_fence();
 #pragma unroll
                 for (int e = 0; e < 8; e++) d[e] = xl[swz(lay(t, e, B_A))];
             }
