@@ -196,6 +196,14 @@ struct NttMode
     long long dfwd = 0, dinv = 0;
 };
 
+// A block of R = 2^LOGR residues is held by TPS = R/8 <= 32 lanes, i.e. inside one wave, so
+// its LDS transposes never cross waves: a wave's LDS accesses execute in program order, and
+// only the compiler must be kept from moving them across each other.
+__device__ __forceinline__ void wave_lds_fence()
+{
+    asm volatile("" ::: "memory");
+}
+
 template <int LOGR, int LOGT>
 struct Shape
 {
@@ -265,7 +273,7 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long t
         ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (rb << s) + (e >> (LOGE - s)); });
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
-    __syncthreads();
+    wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long t
     // transpose back so stores (and epilogue reads) are coalesced
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
-    __syncthreads();
+    wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
     for (int e = 0; e < E; e++) V.store(base + t + TPS * e, ar.out(lds[sl * LD + t + TPS * e]));
 }
@@ -298,7 +306,7 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long t
     T v[E];
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = ar.in(V.load(base + t + TPS * e));
-    __syncthreads();
+    wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
@@ -306,7 +314,7 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long t
         ar.template inv<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
 #pragma unroll
     for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
-    __syncthreads();
+    wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + t + TPS * e];
 #pragma unroll
@@ -571,13 +579,6 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// A block of R = 2^LOGR residues is held by TPS = R/8 <= 32 lanes, i.e. inside one wave, so
-// its LDS transposes never cross waves: a wave's LDS accesses execute in program order, and
-// only the compiler must be kept from moving them across each other.
-__device__ __forceinline__ void wave_lds_fence()
-{
-    asm volatile("" ::: "memory");
-}
 
 // Forward stages [s0, s1) of the local 2^LOGR transform, twiddles from the block's LDS row
 // (entry (1 << s) + g holds tw[((2^k1 + b) << s) + g]).
