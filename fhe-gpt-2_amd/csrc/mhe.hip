@@ -188,6 +188,7 @@ struct mhe_ctx
     NttMode nm;         // FP64 butterflies when every prime is < 2^51 (MHE_FP=0 forces integer)
     int ks_fused = 1; // fused row-pass + key-MAC kernel (MHE_KS_FUSED=0: separate row pass + MAC)
     int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
+    int hmult_fused = 1; // HMult: ModDown fused with the rescale (MHE_HMULT_FUSED=0: separate)
     int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
     int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
@@ -354,6 +355,7 @@ struct JobModDownCol
     const PrimeDev *primes;
     const Tw *tw;
     int L, K, log_n;
+    int fixed_i = -1; // >= 0: one job per poly, all on limb fixed_i
     struct View
     {
         const u64 *src;
@@ -374,7 +376,7 @@ struct JobModDownCol
     };
     __device__ View view(int y) const
     {
-        const int k = y / L, i = y % L;
+        const int k = fixed_i >= 0 ? y : y / L, i = fixed_i >= 0 ? fixed_i : y % L;
         View v;
         v.src = acc + ((size_t)(k * (L + 1) + L) << log_n);
         v.dst = scratch + ((size_t)y << log_n);
@@ -398,6 +400,7 @@ struct JobModDownRow
     const Tw *tw;
     const Tw *invq; // [K][K]
     int L, K, log_n;
+    int fixed_i = -1; // >= 0: one job per poly, all on limb fixed_i
     struct View
     {
         u64 *buf;
@@ -416,7 +419,7 @@ struct JobModDownRow
     };
     __device__ View view(int y) const
     {
-        const int k = y / L, i = y % L;
+        const int k = fixed_i >= 0 ? y : y / L, i = fixed_i >= 0 ? fixed_i : y % L;
         View v;
         v.buf = scratch + ((size_t)y << log_n);
         v.accp = acc + ((size_t)(k * (L + 1) + i) << log_n);
@@ -504,6 +507,112 @@ struct JobRescaleRow
         v.p = primes[i];
         v.tw = tw + ((size_t)i << log_n);
         v.inv = invq[(size_t)(L - 1) * K + i];
+        v.skip = false;
+        return v;
+    }
+};
+
+// ModDown fused with the following rescale (one HMult = multiply + relinearize + rescale).
+// With t_i the ModDown lift of INTT(acc_P) and r_i the rescale lift of last = INTT(ct'_{L-1})
+// (ct' = ct after ModDown), SEAL computes
+//     out_i = ((c_i + (acc_i + 4q - NTT(t_i)) P^-1) + 4q - NTT(r_i)) q_{L-1}^-1   (mod q_i),
+// and NTT is linear mod q_i, so the same residues come from ONE forward NTT per limb:
+//     out_i = (c_i + acc_i P^-1 - NTT(t_i P^-1 + r_i)) q_{L-1}^-1.
+// Column pass job y = k*(L-1) + i builds u_i = t_i P^-1 + r_i (evaluator.cpp:2466-2524 and
+// util/rns.cpp:737-808 lifts), the row pass epilogue forms out_i.
+struct JobMDRCol
+{
+    const u64 *acc;  // [2][L+1][n], limb L = INTT_lazy(acc_P) in [0, 2P)
+    const u64 *last; // [2][n] = INTT(ct'[k][L-1]), canonical
+    u64 *scratch;    // [2][L-1][n]
+    const PrimeDev *primes;
+    const Tw *tw;
+    const Tw *invq; // [K][K]
+    int L, K, log_n;
+    struct View
+    {
+        const u64 *accP, *lastp;
+        u64 *dst;
+        PrimeDev p, P;
+        const Tw *tw;
+        Tw pinv;
+        u64 halfP, fixP, ql, halfL, neg_halfL;
+        bool redP, redL, skip;
+        __device__ u64 load(u32 x) const
+        {
+            u64 t = barrett64(accP[x] + halfP, P);
+            if (redP) t = barrett64(t, p);
+            t += fixP;                                  // ModDown lift, [0, 2q)
+            u64 r = csub(lastp[x] + halfL, ql);
+            if (redL) r = barrett64(r, p);
+            r += neg_halfL;                             // rescale lift, [0, 2q)
+            const u64 u = mul_shoup(t, pinv.x, pinv.y, p.q) + r; // [0, 3q)
+            return csub(csub(u, p.two_q), p.q);
+        }
+        __device__ void store(u32 x, u64 v) const { dst[x] = v; }
+    };
+    __device__ View view(int y) const
+    {
+        const int k = y / (L - 1), i = y % (L - 1);
+        View v;
+        v.accP = acc + ((size_t)(k * (L + 1) + L) << log_n);
+        v.lastp = last + ((size_t)k << log_n);
+        v.dst = scratch + ((size_t)y << log_n);
+        v.p = primes[i];
+        v.P = primes[K - 1];
+        v.tw = tw + ((size_t)i << log_n);
+        v.pinv = invq[(size_t)(K - 1) * K + i];
+        v.halfP = v.P.q >> 1;
+        v.fixP = v.p.q - barrett64(v.halfP, v.p);
+        v.redP = v.P.q > v.p.q;
+        v.ql = primes[L - 1].q;
+        v.halfL = v.ql >> 1;
+        v.neg_halfL = v.p.q - barrett64(v.halfL, v.p);
+        v.redL = v.p.q < v.ql;
+        v.skip = false;
+        return v;
+    }
+};
+
+struct JobMDRRow
+{
+    u64 *scratch;
+    const u64 *acc; // [2][L+1][n]
+    const u64 *ct;  // [2][L][n], limbs < L-1 before ModDown
+    u64 *out;       // [2][L-1][n]
+    const PrimeDev *primes;
+    const Tw *tw;
+    const Tw *invq;
+    int L, K, log_n;
+    struct View
+    {
+        u64 *buf;
+        const u64 *accp, *ctp;
+        u64 *outp;
+        PrimeDev p;
+        const Tw *tw;
+        Tw pinv, qlinv;
+        bool skip;
+        __device__ u64 load(u32 x) const { return buf[x]; }
+        __device__ void store(u32 x, u64 U) const
+        {
+            const u64 a = mul_shoup(accp[x], pinv.x, pinv.y, p.q);  // acc_i P^-1
+            const u64 v = ctp[x] + a + p.four_q - U;                // < 6q
+            outp[x] = mul_shoup(v, qlinv.x, qlinv.y, p.q);
+        }
+    };
+    __device__ View view(int y) const
+    {
+        const int k = y / (L - 1), i = y % (L - 1);
+        View v;
+        v.buf = scratch + ((size_t)y << log_n);
+        v.accp = acc + ((size_t)(k * (L + 1) + i) << log_n);
+        v.ctp = ct + ((size_t)(k * L + i) << log_n);
+        v.outp = out + ((size_t)(k * (L - 1) + i) << log_n);
+        v.p = primes[i];
+        v.tw = tw + ((size_t)i << log_n);
+        v.pinv = invq[(size_t)(K - 1) * K + i];
+        v.qlinv = invq[(size_t)(L - 1) * K + i];
         v.skip = false;
         return v;
     }
@@ -804,8 +913,11 @@ static int run_ntt_inv(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limb
 }
 
 // switch_key_inplace: ct[2][L][n] += KS(target[L][n]) (evaluator.cpp:2281-2525).
+// rescale_out != nullptr (HMult): ct is the first two polys of a product, and instead of
+// ct += KS(target) the result of rescale_to_next(ct + KS(target)) goes to rescale_out
+// [2][L-1][n] (JobMDRCol / JobMDRRow); ct limb L-1 is overwritten on the way.
 static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key, int key_limbs, int L,
-                          hipStream_t st)
+                          hipStream_t st, u64 *rescale_out = nullptr)
 {
     if (key_limbs < L + 1 || key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
     Workspace *w;
@@ -874,10 +986,30 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
                       c->K - 1, 0, c->primes, c->itw, log_n, 0 };
         inv_row(j, log_n, 2, c->nm, st);
         inv_col(j, log_n, 2, c->nm, st);
-        JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n };
-        fwd_col(dc, log_n, 2 * L, c->nm, st);
-        JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
-        fwd_row(dr, log_n, 2 * L, c->nm, st);
+        if (!rescale_out || L < 2)
+        {
+            JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n };
+            fwd_col(dc, log_n, 2 * L, c->nm, st);
+            JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
+            fwd_row(dr, log_n, 2 * L, c->nm, st);
+        }
+        else
+        {
+            // ModDown of limb L-1 only, its INTT (the rescale's "last"), then ModDown and
+            // rescale of the other limbs through one forward NTT each
+            JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n, L - 1 };
+            fwd_col(dc, log_n, 2, c->nm, st);
+            JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n, L - 1 };
+            fwd_row(dr, log_n, 2, c->nm, st);
+            JobLastInv li{ ct, w->coeff, c->primes, c->itw, L, log_n, 1 };
+            inv_row(li, log_n, 2, c->nm, st);
+            JobStrided j2{ w->coeff, w->coeff, n, n, L - 1, 0, c->primes, c->itw, log_n, 1 };
+            inv_col(j2, log_n, 2, c->nm, st);
+            JobMDRCol mc{ w->acc, w->coeff, w->modup, c->primes, c->tw, c->invq, L, c->K, log_n };
+            fwd_col(mc, log_n, 2 * (L - 1), c->nm, st);
+            JobMDRRow mr{ w->modup, w->acc, ct, rescale_out, c->primes, c->tw, c->invq, L, c->K, log_n };
+            fwd_row(mr, log_n, 2 * (L - 1), c->nm, st);
+        }
     }
     HIP_LAUNCH_CHECK();
     return MHE_OK;
@@ -1004,6 +1136,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_KS_FUSED")) c->ks_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_CHUNK")) c->ks_chunk = atoi(f);
     if (const char *f = getenv("MHE_KS_FCHUNK")) c->ks_fchunk = atoi(f);
+    if (const char *f = getenv("MHE_HMULT_FUSED")) c->hmult_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
     if (const char *f = getenv("MHE_KS_GROUPS")) c->ks_groups = atoi(f) > 8 ? 8 : atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
@@ -1443,6 +1576,8 @@ MHE_EXPORT int mhe_hmult(mhe_ctx *c, const uint64_t *a, const uint64_t *b, const
     r = get_ws(c, st, c->K - 1, &w);
     if (r) return r;
     if ((r = launch_tensor(c, a, b, w->ct3, limbs, a == b, st))) return r;
+    if (c->hmult_fused)
+        return run_switch_key(c, w->ct3, w->ct3 + ((size_t)2 * limbs << c->log_n), key, key_limbs, limbs, st, out);
     if ((r = run_switch_key(c, w->ct3, w->ct3 + ((size_t)2 * limbs << c->log_n), key, key_limbs, limbs, st))) return r;
     return run_rescale(c, w->ct3, out, 2, limbs, st);
 }

@@ -417,6 +417,8 @@ ENGINE_VARIANTS = [
     {"MHE_KS_COLGROUPS": "1", "MHE_KS_GROUPS": "3"},  # digit-major column pass, 3 digit groups
     {"MHE_KS_FCHUNK": "3", "MHE_KS_GROUPS": "2"},     # output primes in chunks of 3
     {"MHE_FP": "0", "MHE_KS_FCHUNK": "2", "MHE_KS_COLGROUPS": "2"},
+    {"MHE_HMULT_FUSED": "0"},                         # HMult: separate ModDown and rescale
+    {"MHE_FP": "0", "MHE_KS_GROUPS": "2"},            # integer, fused ModDown + rescale, 2 groups
 ]
 
 
