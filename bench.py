@@ -3,7 +3,9 @@ on config 2 -- N=2^16, 45-prime chain (44 data limbs + 1 special prime), one HMu
 multiply_inplace + relinearize_inplace + rescale_to_next_inplace.
 
 One step = BATCH independent HMults per GPU (same relin key, different ciphertexts), inputs
-resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun), each
+resident in HBM before the timed region, spread round-robin over 4 HIP streams (the hardware
+queues of one process) so one HMult's small ModDown/rescale kernels overlap the next one's
+key-switch kernels.  Multi-GPU: one process per GPU (torchrun), each
 rank runs its own ciphertexts (images are independent in the reference), the relin key is
 generated on rank 0 and broadcast over RCCL/xGMI once at setup; no collective in the data
 path -> weak scaling.
@@ -97,6 +99,8 @@ def main():
     ap.add_argument("--limbs", type=int, default=44)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--streams", type=int, default=4,
+                    help="HIP streams the batch is spread over (round robin; 4 = the hardware queues per process)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,9 +133,11 @@ def main():
     a = rand_residues((B, 2, L, n), q_t[:L], gen)
     b = rand_residues((B, 2, L, n), q_t[:L], gen)
     out = torch.empty((B, 2, L - 1, n), dtype=torch.int64, device=dev)
-    eng.reserve(K - 1)
     stream = torch.cuda.current_stream(dev)
-    sp = mhe.ctypes.c_void_p(stream.cuda_stream)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
+    sps = [mhe.ctypes.c_void_p(s_.cuda_stream) for s_ in streams]
+    for s_ in sps:
+        mhe.lib().mhe_ctx_reserve(eng._h, K - 1, s_)
     ptr = lambda t: mhe.ctypes.c_void_p(t.data_ptr())  # noqa: E731
     a_p = [ptr(a[i]) for i in range(B)]
     b_p = [ptr(b[i]) for i in range(B)]
@@ -139,10 +145,20 @@ def main():
     k_p = ptr(key)
 
     def step():
+        if len(streams) > 1:  # the extra streams start after the main stream's prior work
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            for s_ in streams[1:]:
+                s_.wait_event(ev)
         for i in range(B):
-            rc = eng.hmult_raw(a_p[i], b_p[i], k_p, K, o_p[i], L, sp)
+            rc = eng.hmult_raw(a_p[i], b_p[i], k_p, K, o_p[i], L, sps[i % len(sps)])
             if rc:
                 raise mhe.MheError(rc, mhe.lib().mhe_last_error().decode())
+        if len(streams) > 1:  # join back so the timing events on the main stream cover all
+            for s_ in streams[1:]:
+                ev = torch.cuda.Event()
+                ev.record(s_)
+                stream.wait_event(ev)
 
     for _ in range(args.warmup):
         step()
@@ -198,6 +214,7 @@ def main():
             "log_n": LOG_N,
             "limbs": L,
             "batch_per_gpu": B,
+            "streams": args.streams,
             "parallelism": f"replicas{world} (independent ciphertexts per GPU, key broadcast over RCCL)",
         },
         "roofline": {
