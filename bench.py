@@ -41,6 +41,13 @@ def hmult_bytes(L):
     return (L * L + 4 * L - 1) * MIB
 
 
+def ks_row_mac_key_bytes(L, n):
+    """Algorithmic HBM bytes of one k_ks_row_mac launch (SURVEY.md §8(d) key slice): every key
+    limb it multiplies against is read once, 2 polys x L digits x (L+1) primes x n x 8 B; the
+    ModUp intermediate it also reads is not algorithmic (it is what fusion should remove)."""
+    return 2 * L * (L + 1) * n * 8
+
+
 def rand_residues(shape, moduli_t, gen):
     """Uniform residues on device: last two dims [limbs][n], limb l uniform in [0, q_l)."""
     hi = torch.randint(0, 2**62, shape, generator=gen, device=moduli_t.device, dtype=torch.int64)
@@ -160,9 +167,13 @@ def main():
                 ev.record(s_)
                 stream.wait_event(ev)
 
+    lib = mhe.lib()
+    lib.mhe_ctx_set_timing(eng._h, 1)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    km_ms, km_n = mhe.ctypes.c_double(), mhe.ctypes.c_int()
+    lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))  # drop the warmup launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -180,22 +191,42 @@ def main():
     torch.cuda.synchronize(dev)
     gpu_s = ev0.elapsed_time(ev1) / 1e3
     elapsed = max_over_ranks(max(wall, gpu_s), dev)
+    # HIP-event time of the dominant kernel, recorded by the engine on the stream each launch
+    # ran on (mhe_ctx_set_timing / mhe_kernel_time).  With several streams the launches of
+    # different HMults overlap, so the kernel's own duration is taken from a short
+    # single-stream pass after the timed region (the rocprofv3 summary under profiles/ is of
+    # the same single-stream command: bench.py --streams 1).
+    lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))
+    if len(sps) > 1:
+        for _ in range(min(args.steps, 4)):
+            for i in range(B):
+                rc = eng.hmult_raw(a_p[i], b_p[i], k_p, K, o_p[i], L, sps[0])
+                if rc:
+                    raise mhe.MheError(rc, lib.mhe_last_error().decode())
+        torch.cuda.synchronize(dev)
+        lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))
+    km_avg_us = km_ms.value * 1e3 / max(km_n.value, 1)
 
     # HBM traffic per HMult from the committed PMC passes of the same workload (rocprofv3
     # FETCH_SIZE/WRITE_SIZE, gfx950-corrected; scripts/gpu_round.sh + scripts/traffic.py)
-    traffic, traffic_src = None, None
+    traffic, traffic_src, km_traffic = None, None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json"))):
         try:
             t = json.load(open(f))
             if t.get("limbs", L) == L:
                 traffic, traffic_src = t["hbm_bytes_per_hmult"], os.path.relpath(f, ROOT)
+                pk = {k.split("<")[0]: v for k, v in t.get("per_kernel_GB_per_hmult", {}).items()}
+                km_traffic = pk.get("k_ks_row_mac")
+                km_traffic = None if km_traffic is None else km_traffic * 1e9  # one launch per HMult
         except (OSError, ValueError, KeyError):
             pass
 
     hmults_per_gpu = B * args.steps
     value = world * hmults_per_gpu / elapsed
-    per_hmult_s = gpu_s / hmults_per_gpu  # HIP-event time of one HMult on this GPU's stream
+    per_hmult_s = gpu_s / hmults_per_gpu  # HIP-event time per HMult (batch over its streams)
     achieved = hmult_bytes(L) / per_hmult_s / 1e9
+    km_bytes = ks_row_mac_key_bytes(L, n)
+    km_achieved = km_bytes / (km_avg_us * 1e-6) / 1e9 if km_avg_us > 0 else 0.0
     result = {
         "metric": "homomorphic ciphertext mults/sec (N=2^16, L limbs)",
         "value": round(value, 3),
@@ -207,7 +238,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64",
+        "dtype": "u64 residues, exact fp64-FMA modular arithmetic",
         "data": "synthetic: uniform RNS residues (mt-style seeded) + random relin key, NTT form",
         "config": {
             "workload": "C2: N=2^16 45-prime chain (44 data limbs + special), HMult = multiply+relinearize+rescale",
@@ -219,16 +250,30 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "hmult (tensor + key-switch + rescale kernel sequence, one launch group per HMult)",
+            "kernel": "k_ks_row_mac (fused ModUp row pass + key inner products; 1 launch per HMult)",
+            "achieved": round(km_achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(km_achieved / HBM_PEAK_GBS, 4),
+            "traffic": km_traffic,
+            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": km_bytes,
+            "avg_launch_us": round(km_avg_us, 2),
+            "launches_timed": km_n.value,
+            "timing": "HIP events around each launch on its stream; single-stream pass when --streams > 1",
+        },
+        "hmult_roofline": {
+            "bound": "hbm",
+            "unit_of_work": "one HMult (tensor + key switch + rescale kernel sequence)",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "traffic_unit": "bytes per HMult (L2-miss fabric reads x2 + writes, PMC)",
-            "traffic_source": traffic_src,
-            "algorithmic_bytes_per_launch": hmult_bytes(L),
-            "avg_launch_us": round(per_hmult_s * 1e6, 2),
+            "traffic_unit": "HBM bytes per HMult (PMC)",
+            "algorithmic_bytes_per_hmult": hmult_bytes(L),
+            "us_per_hmult": round(per_hmult_s * 1e6, 2),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:

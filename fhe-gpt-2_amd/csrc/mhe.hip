@@ -170,6 +170,16 @@ struct Workspace
     u64 *acc = nullptr;   // [2][L+1][n]   key inner products
     u64 *tmp = nullptr;   // [L][n]        permuted c1 for Galois
     u64 *ct3 = nullptr;   // [3][L][n]     tensor output for hmult
+    // kernel timing (mhe_ctx_set_timing): event pairs recorded around the two dominant
+    // key-switch kernels on this stream, read back by mhe_kernel_time
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
+    size_t ev_used[2] = { 0, 0 };
+};
+
+enum TimedKernel
+{
+    TK_KS_ROW_MAC = 0, // k_ks_row_mac: fused ModUp row pass + key inner products
+    TK_MODUP_COL = 1   // k_modup_col / ModUp column pass
 };
 
 struct mhe_ctx
@@ -188,6 +198,7 @@ struct mhe_ctx
     NttMode nm;         // FP64 butterflies when every prime is < 2^51 (MHE_FP=0 forces integer)
     int ks_fused = 1; // fused row-pass + key-MAC kernel (MHE_KS_FUSED=0: separate row pass + MAC)
     int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
+    int timing = 0;      // record HIP events around the key-switch kernels (mhe_ctx_set_timing)
     int hmult_fused = 1; // HMult: ModDown fused with the rescale (MHE_HMULT_FUSED=0: separate)
     int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
     int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
@@ -195,6 +206,27 @@ struct mhe_ctx
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };
+
+// Events around a launch of kernel kind k on stream st when timing is on.
+static hipEvent_t *timing_slot(mhe_ctx *c, Workspace *w, int k, hipStream_t st)
+{
+    if (!c->timing) return nullptr;
+    auto &v = w->ev[k];
+    if (w->ev_used[k] == v.size())
+    {
+        std::pair<hipEvent_t, hipEvent_t> e{};
+        if (hipEventCreate(&e.first) != hipSuccess || hipEventCreate(&e.second) != hipSuccess) return nullptr;
+        v.push_back(e);
+    }
+    hipEvent_t *pair = &v[w->ev_used[k]++].first;
+    (void)hipEventRecord(pair[0], st);
+    return pair;
+}
+
+static void timing_end(hipEvent_t *pair, hipStream_t st)
+{
+    if (pair) (void)hipEventRecord(pair[1], st);
+}
 
 static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out)
 {
@@ -943,6 +975,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
         for (int I0 = 0; I0 <= L; I0 += P)
         {
             const int cnt = (I0 + P <= L + 1) ? P : L + 1 - I0;
+            hipEvent_t *tc = timing_slot(c, w, TK_MODUP_COL, st);
             if (c->ks_colgroups > 0)
             {
                 const int IG = c->ks_colgroups < cnt ? c->ks_colgroups : cnt;
@@ -953,8 +986,11 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
                 JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
                 fwd_col(j, log_n, cnt * L, c->nm, st);
             }
+            timing_end(tc, st);
+            hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
             ks_row_mac_chunk(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, c->nm, G, I0,
                              cnt, st);
+            timing_end(tm, st);
         }
         ks_acc_finish(w->acc, c->primes, L, c->K, G, log_n, st);
     }
@@ -1247,7 +1283,15 @@ MHE_EXPORT int mhe_ctx_destroy(mhe_ctx *c)
     if (!c) return MHE_OK;
     (void)hipSetDevice(c->device);
     for (auto &kv : c->ws)
+    {
         if (kv.second.base) (void)hipFree(kv.second.base);
+        for (auto &v : kv.second.ev)
+            for (auto &e : v)
+            {
+                (void)hipEventDestroy(e.first);
+                (void)hipEventDestroy(e.second);
+            }
+    }
     (void)hipFree(c->primes);
     (void)hipFree(c->tw);
     (void)hipFree(c->itw);
@@ -1312,6 +1356,37 @@ MHE_EXPORT int mhe_memcpy_d2d(mhe_ctx *c, void *dst, const void *src, size_t byt
 {
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
     HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_ctx_set_timing(mhe_ctx *c, int on)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    c->timing = on ? 1 : 0;
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_kernel_time(mhe_ctx *c, int kernel, double *total_ms, int *launches)
+{
+    if (!valid_ctx(c) || kernel < 0 || kernel > 1 || !total_ms || !launches) return fail(MHE_ERR_ARG, "invalid argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    double ms = 0;
+    int cnt = 0;
+    for (auto &kv : c->ws)
+    {
+        Workspace &w = kv.second;
+        for (size_t i = 0; i < w.ev_used[kernel]; i++)
+        {
+            float t = 0;
+            HIP_TRY(hipEventSynchronize(w.ev[kernel][i].second));
+            HIP_TRY(hipEventElapsedTime(&t, w.ev[kernel][i].first, w.ev[kernel][i].second));
+            ms += t;
+            cnt++;
+        }
+        w.ev_used[kernel] = 0;
+    }
+    *total_ms = ms;
+    *launches = cnt;
     return MHE_OK;
 }
 

@@ -30,6 +30,8 @@ SIGNATURES = {
     "mhe_galois_elt_from_step": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_int]),
     "mhe_malloc": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t]),
     "mhe_free": (ctypes.c_int, [vp, vp]),
+    "mhe_ctx_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
+    "mhe_kernel_time": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
     "mhe_malloc_async": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t, vp]),
     "mhe_free_async": (ctypes.c_int, [vp, vp, vp]),
     "mhe_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),

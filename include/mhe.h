@@ -72,6 +72,12 @@ int mhe_stream_sync(mhe_ctx *ctx, void *stream);
 /* A non-blocking HIP stream on the context's device (and its scratch workspace); the SEAL
  * shim gives every host thread its own, as the reference's OpenMP threads share one
  * Evaluator (cnn/infer_seal.cpp:404). */
+/* Kernel timing for the benchmark: when on, HIP events are recorded on the launching stream
+ * around every launch of the dominant key-switch kernels; mhe_kernel_time sums their durations
+ * since the last call (kernel 0 = fused ModUp row pass + key inner products, 1 = ModUp column
+ * pass) and resets. */
+int mhe_ctx_set_timing(mhe_ctx *ctx, int on);
+int mhe_kernel_time(mhe_ctx *ctx, int kernel, double *total_ms, int *launches);
 int mhe_stream_create(mhe_ctx *ctx, void **stream);
 int mhe_stream_destroy(mhe_ctx *ctx, void *stream);
 
