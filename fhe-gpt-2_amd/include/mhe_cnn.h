@@ -1,15 +1,17 @@
 // mhe_cnn.h -- the reference's multiplexed-packing CNN layers (TensorCipher and the linear
-// layers of cnn_ckks/cpu-ckks/single-key/cnn/cnn_seal.h) over the MI355X seal:: surface.
+// layers of cnn_ckks/cpu-ckks/single-key/cnn/cnn_seal.h, plus the approximate ReLU) over the
+// MI355X seal:: surface.
 //
 // Same class, function names, signatures and operation sequences as the reference
 // (cnn_seal.cpp:3-100, 284-809), so a caller that builds against these gets the same
-// ciphertext-operation trace, run on the GPU.  The non-linear layers (ReLU_seal -> minimax
-// composite polynomials, bootstrap -> Bootstrapper) are not part of this header yet.
+// ciphertext-operation trace, run on the GPU.  Bootstrapping (Bootstrapper) is not part of this
+// header yet.
 #pragma once
 
 #include <fstream>
 #include <vector>
 
+#include "mhe_comp.h"
 #include "seal/seal.h"
 
 class TensorCipher
@@ -47,6 +49,12 @@ void multiplexed_parallel_batch_norm_seal(const TensorCipher &cnn_in, TensorCiph
                                           std::vector<double> weight, double epsilon, seal::CKKSEncoder &encoder,
                                           seal::Encryptor &encryptor, seal::Evaluator &evaluator, double B,
                                           bool end = false);
+// cnn_seal.cpp:577-592: approximate ReLU (minimax composite polynomial, mhe_comp.h) of the tensor
+void ReLU_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, long comp_no, std::vector<int> deg, long alpha,
+               std::vector<Tree> &tree, double scaled_val, long scalingfactor, seal::Encryptor &encryptor,
+               seal::Evaluator &evaluator, seal::Decryptor &decryptor, seal::CKKSEncoder &encoder,
+               seal::PublicKey &public_key, seal::SecretKey &secret_key, seal::RelinKeys &relin_keys,
+               double scale = 1.0);
 void cnn_add_seal(const TensorCipher &cnn1, const TensorCipher &cnn2, TensorCipher &destination,
                   seal::Evaluator &evaluator);
 void multiplexed_parallel_downsampling_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out,

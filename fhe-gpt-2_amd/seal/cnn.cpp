@@ -322,6 +322,21 @@ void multiplexed_parallel_batch_norm_seal(const TensorCipher &cnn_in, TensorCiph
     cnn_out = TensorCipher(logn, ki, hi, wi, ci, ti, pi, temp);
 }
 
+// ------------------------------------------------------------------------ ReLU
+void ReLU_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, long comp_no, std::vector<int> deg, long alpha,
+               std::vector<Tree> &tree, double scaled_val, long scalingfactor, Encryptor &encryptor,
+               Evaluator &evaluator, Decryptor &decryptor, CKKSEncoder &encoder, PublicKey &public_key,
+               SecretKey &secret_key, RelinKeys &relin_keys, double)
+{
+    // cnn_seal.cpp:577-592
+    if ((long)cnn_in.h() * cnn_in.w() * cnn_in.c() > (1L << cnn_in.logn()))
+        throw std::invalid_argument("hi*wi*ci should not be larger than n");
+    Ciphertext temp = cnn_in.cipher();
+    minimax_ReLU_seal(comp_no, deg, alpha, tree, scaled_val, scalingfactor, encryptor, evaluator, decryptor, encoder,
+                      public_key, secret_key, relin_keys, temp, temp);
+    cnn_out = TensorCipher(cnn_in.logn(), cnn_in.k(), cnn_in.h(), cnn_in.w(), cnn_in.c(), cnn_in.t(), cnn_in.p(), temp);
+}
+
 // ------------------------------------------------------------------------ residual add
 void cnn_add_seal(const TensorCipher &cnn1, const TensorCipher &cnn2, TensorCipher &destination, Evaluator &evaluator)
 {

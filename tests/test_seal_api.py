@@ -42,6 +42,19 @@ def test_cnn_layers_end_to_end():
 
 
 @pytest.mark.gpu
+def test_approx_relu_end_to_end():
+    """Approximate ReLU by the reference's minimax composite polynomial (alpha 13, degrees
+    {15,15,27}, odd baby-step trees; include/mhe_comp.h) on the GPU vs max(x, 0)."""
+    _build()
+    env = dict(os.environ, MHE_COMP_DIR=os.path.join(ROOT, "tests", "golden", "comp"))
+    r = subprocess.run([os.path.join(ROOT, "build", "comp_test")], capture_output=True, text=True, timeout=900,
+                       env=env)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
 def test_seal_api_end_to_end():
     _build()
     r = subprocess.run([DRIVER], capture_output=True, text=True, timeout=600)
