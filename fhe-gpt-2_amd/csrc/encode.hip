@@ -1,21 +1,29 @@
 // CKKS encoding for libmhe.
 //
-// CKKSEncoder::encode (SEAL/ckks.h:457-640) is a host double-precision FFT followed by rounding,
-// an RNS reduction and a per-limb NTT.  Bit-exactness with SEAL needs SEAL's exact sequence of
-// non-fused double operations (the reference builds its encoder without FMA), so the FFT and
-// the rounding run here on the host, compiled with -ffp-contract=off, in SEAL's operation order:
-//   * ComplexRoots (util/croots.cpp:17-66): polar(1, 2*PI*i/m) for i <= m/8, 8-fold symmetry;
-//   * index map 5^i (ckks.cpp:34-49), inverse roots conj(root[rev(i-1)+1]) (ckks.cpp:55-60);
+// CKKSEncoder::encode (SEAL/ckks.h:457-640) is a double-precision FFT followed by rounding, an
+// RNS reduction and a per-limb NTT.  Bit-exactness with SEAL needs SEAL's exact sequence of
+// non-fused double operations (the reference builds its encoder without FMA); IEEE double
+// arithmetic is the same on the host and on the GPU, so the whole encode runs on the device,
+// compiled with -ffp-contract=off, in SEAL's operation order:
+//   * ComplexRoots (util/croots.cpp:17-66): polar(1, 2*PI*i/m) for i <= m/8, 8-fold symmetry,
+//     computed once on the host (sincos) and kept in HBM per device;
+//   * index map 5^i (ckks.cpp:34-49) computed per slot on the device;
 //   * DWTHandler::transform_from_rev over complex<double> with scalar scale/n
-//     (util/dwthandler.h:202-314, ckks.h:46-81).
-// The rounded integer coefficients (sign + 1 or 2 magnitude words) go to HBM once; the RNS
-// reduction and the NTT run on the GPU.  Coefficients wider than 128 bits (scale * |value| >=
-// 2^127) take SEAL's multi-word path (RNSBase::decompose) on the host.
+//     (util/dwthandler.h:202-314, ckks.h:46-81): the first 12 stages in LDS (4096-point blocks),
+//     the remaining stages one launch each;
+//   * std::round, then the coefficient's integer value mod q_j (SEAL's 1-word, 2-word and
+//     multi-word paths all reduce the same integer, so one per-coefficient decomposition gives
+//     their residues).
+// The slot values travel through a pinned staging ring, so encode never waits for the device.
+// SEAL's "encoded values are too large" check needs max |coeff|: a host bound
+// (scale / n) * 2 * sum |v_i| settles it for every ordinary input; only when the bound comes
+// within a bit of the limit is the exact device maximum read back (one stream sync).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <complex>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -37,6 +45,27 @@ struct mhe_encoder
     std::vector<size_t> index_map;
     std::vector<cd> inv_root_powers;
     std::vector<cd> root_powers;
+
+    // device state (lazily created on the first encode of each device)
+    static constexpr int kRing = 8;
+    struct DevRoots
+    {
+        int dev;
+        double2 *roots;
+    };
+    mutable std::mutex mu;
+    mutable std::vector<DevRoots> dev_roots;
+    mutable double *ring = nullptr; // kRing slots of 2 * slots doubles (re, im), pinned
+    mutable hipEvent_t ring_ev[kRing] = {};
+    mutable int ring_dev = -1;
+    mutable unsigned ring_next = 0;
+    ~mhe_encoder()
+    {
+        for (auto &d : dev_roots) (void)hipFree(d.roots);
+        if (ring) (void)hipHostFree(ring);
+        for (auto &ev : ring_ev)
+            if (ev) (void)hipEventDestroy(ev);
+    }
 };
 
 namespace
@@ -73,39 +102,6 @@ struct ComplexRoots
     }
 };
 
-// transform_from_rev with scalar (util/dwthandler.h:202-314)
-void fft_from_rev(cd *values, int log_n, const cd *roots, double scalar)
-{
-    const size_t n = size_t(1) << log_n;
-    size_t gap = 1, m = n >> 1;
-    for (; m > 1; m >>= 1)
-    {
-        size_t offset = 0;
-        for (size_t i = 0; i < m; i++)
-        {
-            const cd r = *++roots;
-            cd *x = values + offset, *y = x + gap;
-            for (size_t j = 0; j < gap; j++)
-            {
-                const cd u = *x, v = *y;
-                *x++ = u + v;
-                *y++ = (u - v) * r;
-            }
-            offset += gap << 1;
-        }
-        gap <<= 1;
-    }
-    const cd r = *++roots;
-    const cd scaled_r = r * scalar;
-    cd *x = values, *y = values + gap;
-    for (size_t j = 0; j < gap; j++)
-    {
-        const cd u = *x, v = *y;
-        *x++ = (u + v) * scalar;
-        *y++ = (u - v) * scaled_r;
-    }
-}
-
 // SEAL's ContextData::total_coeff_modulus_bit_count: bit length of prod q_j.
 int total_bits(const uint64_t *q, int limbs)
 {
@@ -134,19 +130,118 @@ u64 words_mod(const u64 *w, int nw, u64 q)
 }
 } // namespace
 
-// RNS reduction of rounded coefficients: out[j][i] = (+-)(hi:lo mod q_j).
-__global__ void k_encode_reduce(const u64 *lo, const u64 *hi, const unsigned char *neg, u64 *out,
-                                const PrimeDev *primes, int limbs, int log_n)
+// ---- device encode kernels -------------------------------------------------------------
+namespace
+{
+__device__ __forceinline__ u32 rev_bits_dev(u32 x, int bits)
+{
+    return __builtin_bitreverse32(x) >> (32 - bits);
+}
+
+// cv[index_map[i]] = v_i, cv[index_map[i + slots]] = conj(v_i) (ckks.h:488-497); cv pre-zeroed
+__global__ void k_enc_scatter(const double *vals, size_t count, int has_im, double2 *cv, int log_n)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= count) return;
+    const u64 m = (u64)2 << log_n;
+    u64 pos = 1, b = 5;
+    for (u64 e = i; e; e >>= 1)
+    {
+        if (e & 1) pos = (pos * b) & (m - 1);
+        b = (b * b) & (m - 1);
+    }
+    const double re = vals[i], im = has_im ? vals[count + i] : 0.0;
+    cv[rev_bits_dev((u32)((pos - 1) >> 1), log_n)] = double2{ re, im };
+    cv[rev_bits_dev((u32)((m - pos - 1) >> 1), log_n)] = double2{ re, -im };
+}
+
+// one butterfly of transform_from_rev in SEAL's operation order (complex products as
+// (ac - bd, ad + bc), no contraction); the last stage folds in the scalar
+__device__ __forceinline__ void enc_bfly(double2 &x, double2 &y, double2 r, bool last, double scalar)
+{
+    const double2 u = x, v = y;
+    const double2 s = double2{ u.x + v.x, u.y + v.y }, d = double2{ u.x - v.x, u.y - v.y };
+    if (last)
+    {
+        r = double2{ r.x * scalar, r.y * scalar };
+        x = double2{ s.x * scalar, s.y * scalar };
+    }
+    else
+        x = s;
+    y = double2{ d.x * r.x - d.y * r.y, d.x * r.y + d.y * r.x };
+}
+
+constexpr int kEncLogBlock = 12;
+
+// stages 0 .. lb-1 (gap 1 .. 2^(lb-1)) of one 2^lb-point block in LDS
+__global__ __launch_bounds__(256) void k_enc_fft_block(double2 *cv, const double2 *roots, int log_n, int lb,
+                                                       double scalar)
+{
+    __shared__ double2 sh[1 << kEncLogBlock];
+    const size_t n = (size_t)1 << log_n, B = (size_t)1 << lb, base = (size_t)blockIdx.x << lb;
+    for (size_t t = threadIdx.x; t < B; t += 256) sh[t] = cv[base + t];
+    __syncthreads();
+    for (int st = 0; st < lb; st++)
+    {
+        const size_t m = n >> (st + 1), gap = (size_t)1 << st;
+        for (size_t t = threadIdx.x; t < B / 2; t += 256)
+        {
+            const size_t k = t >> st, x = (k << (st + 1)) + (t & (gap - 1));
+            const double2 r = roots[n - 2 * m + 1 + (base >> (st + 1)) + k];
+            enc_bfly(sh[x], sh[x + gap], r, m == 1, scalar);
+        }
+        __syncthreads();
+    }
+    for (size_t t = threadIdx.x; t < B; t += 256) cv[base + t] = sh[t];
+}
+
+// one later stage (gap 2^st) over the whole vector
+__global__ void k_enc_fft_stage(double2 *cv, const double2 *roots, int log_n, int st, double scalar)
+{
+    const size_t n = (size_t)1 << log_n, t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n / 2) return;
+    const size_t m = n >> (st + 1), gap = (size_t)1 << st, k = t >> st, x = (k << (st + 1)) + (t & (gap - 1));
+    enc_bfly(cv[x], cv[x + gap], roots[n - 2 * m + 1 + k], m == 1, scalar);
+}
+
+// max |Re cv_i| as ordered bit patterns (non-negative doubles order like their u64 bits)
+__global__ void k_enc_absmax(const double2 *cv, size_t n, unsigned long long *mx)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned long long v = i < n ? (unsigned long long)__double_as_longlong(fabs(cv[i].x)) : 0ull;
+    for (int o = 32; o; o >>= 1) v = max(v, (unsigned long long)__shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(mx, v);
+}
+
+// out[j][i] = round(Re cv_i) mod q_j, sign applied (ckks.h:545-640)
+__global__ void k_enc_round_reduce(const double2 *cv, u64 *out, const PrimeDev *primes, int limbs, int log_n)
 {
     const size_t n = (size_t)1 << log_n;
     const size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (g >= n * limbs) return;
     const size_t i = g & (n - 1);
-    const int j = (int)(g >> log_n);
-    const PrimeDev p = primes[j];
-    u64 r = hi ? barrett128(lo[i], hi[i], p) : barrett64(lo[i], p);
-    out[g] = (neg[i] && r) ? p.q - r : r;
+    const PrimeDev p = primes[g >> log_n];
+    double c = round(cv[i].x);
+    const bool neg = signbit(c);
+    c = fabs(c);
+    u64 r;
+    if (c < 0x1p64)
+        r = barrett64((u64)c, p);
+    else
+    {
+        u64 w[17];
+        int nw = 0;
+        while (c >= 1 && nw < 17)
+        {
+            w[nw++] = (u64)fmod(c, 0x1p64);
+            c /= 0x1p64;
+        }
+        r = 0;
+        for (int k = nw - 1; k >= 0; k--) r = barrett128(w[k], r, p);
+    }
+    out[g] = (neg && r) ? p.q - r : r;
 }
+} // namespace
 
 extern "C" __attribute__((visibility("default"))) int mhe_encoder_create(mhe_encoder **out, int log_n)
 {
@@ -201,85 +296,125 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_at(mhe_ctx
     if (scale <= 0 || (static_cast<int>(std::log2(scale)) + 1 >= tb))
         return mhe_internal_fail(MHE_ERR_ARG, "scale out of bounds");
     const size_t n = e->n;
-    std::vector<cd> cv(n, cd(0, 0));
-    for (size_t i = 0; i < count; i++)
-    {
-        const cd v(re[i], im ? im[i] : 0.0);
-        cv[e->index_map[i]] = v;
-        cv[e->index_map[i + e->slots]] = std::conj(v);
-    }
-    const double fix = scale / static_cast<double>(n);
-    fft_from_rev(cv.data(), log_n, e->inv_root_powers.data(), fix);
-    double max_coeff = 0;
-    for (size_t i = 0; i < n; i++) max_coeff = std::max<double>(max_coeff, std::fabs(cv[i].real()));
-    const int max_bits = static_cast<int>(std::ceil(std::log2(std::max<double>(max_coeff, 1.0)))) + 1;
-    if (max_bits >= tb) return mhe_internal_fail(MHE_ERR_ARG, "encoded values are too large");
+    hipStream_t st = (hipStream_t)stream;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return mhe_internal_fail(MHE_ERR_DEVICE, "no device");
 
-    const double two64 = std::pow(2.0, 64);
-    std::vector<u64> lo(n), hi(max_bits > 64 ? n : 0);
-    std::vector<unsigned char> neg(n);
-    std::vector<u64> host_out; // multi-word path
-    if (max_bits > 128) host_out.resize(n * limbs);
-    for (size_t i = 0; i < n; i++)
+    // host bound on max |coeff| (each value and its conjugate enter with unit-modulus weights)
+    double l1 = 0;
+    for (size_t i = 0; i < count; i++) l1 += std::fabs(re[i]) + (im ? std::fabs(im[i]) : 0.0);
+    const double fix = scale / static_cast<double>(n);
+    const double bound = fix * 2 * l1 * (1 + 1e-6) + 1;
+    const bool exact_check = !(std::isfinite(bound) &&
+                               static_cast<int>(std::ceil(std::log2(std::max<double>(bound, 1.0)))) + 1 < tb);
+
+    std::unique_lock<std::mutex> lk(e->mu);
+    const double2 *roots = nullptr;
+    for (auto &d : e->dev_roots)
+        if (d.dev == dev) roots = d.roots;
+    if (!roots)
     {
-        double coeffd = std::round(cv[i].real());
-        neg[i] = std::signbit(coeffd) ? 1 : 0;
-        coeffd = std::fabs(coeffd);
-        if (max_bits <= 64)
-            lo[i] = static_cast<u64>(coeffd);
-        else if (max_bits <= 128)
+        double2 *r = nullptr;
+        if (hipMalloc((void **)&r, n * sizeof(double2)) != hipSuccess)
+            return mhe_internal_fail(MHE_ERR_MEMORY, "encoder roots allocation failed");
+        if (hipMemcpy(r, e->inv_root_powers.data(), n * sizeof(double2), hipMemcpyHostToDevice) != hipSuccess)
         {
-            lo[i] = static_cast<u64>(std::fmod(coeffd, two64));
-            hi[i] = static_cast<u64>(coeffd / two64);
+            (void)hipFree(r);
+            return mhe_internal_fail(MHE_ERR_DEVICE, "encoder roots upload failed");
+        }
+        e->dev_roots.push_back({ dev, r });
+        roots = r;
+    }
+    // staging: [cv: n double2][values: 2 * count doubles][max word]
+    const size_t vwords = count * (im ? 2 : 1);
+    char *buf = nullptr;
+    const size_t bytes = n * sizeof(double2) + vwords * sizeof(double) + sizeof(u64);
+    if (hipMallocAsync((void **)&buf, bytes, st) != hipSuccess)
+        return mhe_internal_fail(MHE_ERR_MEMORY, "encode staging allocation failed");
+    double2 *cv = (double2 *)buf;
+    double *vals = (double *)(cv + n);
+    unsigned long long *mx = (unsigned long long *)(vals + vwords);
+    hipError_t err = hipMemsetAsync(cv, 0, n * sizeof(double2), st);
+    if (err == hipSuccess && vwords)
+    {
+        if (e->ring_dev < 0)
+        {
+            if (hipHostMalloc((void **)&e->ring, mhe_encoder::kRing * 2 * e->slots * sizeof(double)) == hipSuccess)
+            {
+                e->ring_dev = dev;
+                for (auto &ev : e->ring_ev)
+                    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) e->ring_dev = -2;
+            }
+            else
+                e->ring_dev = -2;
+        }
+        if (e->ring_dev == dev)
+        {
+            const unsigned slot = e->ring_next++ % mhe_encoder::kRing;
+            double *h = e->ring + (size_t)slot * 2 * e->slots;
+            err = hipEventSynchronize(e->ring_ev[slot]); // the slot's previous upload is done
+            if (err == hipSuccess)
+            {
+                std::memcpy(h, re, count * sizeof(double));
+                if (im) std::memcpy(h + count, im, count * sizeof(double));
+                err = hipMemcpyAsync(vals, h, vwords * sizeof(double), hipMemcpyHostToDevice, st);
+            }
+            if (err == hipSuccess) err = hipEventRecord(e->ring_ev[slot], st);
         }
         else
         {
-            u64 w[64] = { 0 };
-            int nw = 0;
-            while (coeffd >= 1)
-            {
-                w[nw++] = static_cast<u64>(std::fmod(coeffd, two64));
-                coeffd /= two64;
-            }
-            for (int j = 0; j < limbs; j++)
-            {
-                const u64 r = words_mod(w, nw ? nw : 1, q[j]);
-                host_out[(size_t)j * n + i] = (neg[i] && r) ? q[j] - r : r;
-            }
+            // another device than the ring's: synchronous upload from the caller's arrays
+            err = hipMemcpyAsync(vals, re, count * sizeof(double), hipMemcpyHostToDevice, st);
+            if (err == hipSuccess && im)
+                err = hipMemcpyAsync(vals + count, im, count * sizeof(double), hipMemcpyHostToDevice, st);
+            if (err == hipSuccess) err = hipStreamSynchronize(st);
         }
     }
-    hipStream_t st = (hipStream_t)stream;
-    if (max_bits > 128)
+    lk.unlock();
+    if (err == hipSuccess && count)
+        hipLaunchKernelGGL(k_enc_scatter, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, vals, count,
+                           im ? 1 : 0, cv, log_n);
+    if (err == hipSuccess)
     {
-        if (hipMemcpyAsync(out, host_out.data(), n * limbs * sizeof(u64), hipMemcpyHostToDevice, st) != hipSuccess)
-            return mhe_internal_fail(MHE_ERR_DEVICE, "encode upload failed");
+        const int lb = std::min(log_n, kEncLogBlock);
+        hipLaunchKernelGGL(k_enc_fft_block, dim3((unsigned)(n >> lb)), dim3(256), 0, st, cv, roots, log_n, lb, fix);
+        for (int s2 = lb; s2 < log_n; s2++)
+            hipLaunchKernelGGL(k_enc_fft_stage, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, st, cv, roots,
+                               log_n, s2, fix);
+        err = hipGetLastError();
     }
-    else
+    if (err == hipSuccess && exact_check)
     {
-        u64 *d_lo = nullptr, *d_hi = nullptr;
-        unsigned char *d_neg = nullptr;
-        const size_t bytes = n * sizeof(u64) * (hi.empty() ? 1 : 2) + n;
-        char *buf = nullptr;
-        if (hipMallocAsync((void **)&buf, bytes, st) != hipSuccess)
-            return mhe_internal_fail(MHE_ERR_MEMORY, "encode staging allocation failed");
-        d_lo = (u64 *)buf;
-        if (!hi.empty()) d_hi = d_lo + n;
-        d_neg = (unsigned char *)(d_lo + n * (hi.empty() ? 1 : 2));
-        hipError_t err = hipMemcpyAsync(d_lo, lo.data(), n * sizeof(u64), hipMemcpyHostToDevice, st);
-        if (err == hipSuccess && d_hi) err = hipMemcpyAsync(d_hi, hi.data(), n * sizeof(u64), hipMemcpyHostToDevice, st);
-        if (err == hipSuccess) err = hipMemcpyAsync(d_neg, neg.data(), n, hipMemcpyHostToDevice, st);
+        // SEAL's check on the exact maximum (ckks.h:525-540)
+        unsigned long long h_mx = 0;
+        err = hipMemsetAsync(mx, 0, sizeof(u64), st);
         if (err == hipSuccess)
         {
-            const size_t total = n * limbs;
-            hipLaunchKernelGGL(k_encode_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d_lo, d_hi,
-                               d_neg, out, primes, limbs, log_n);
-            err = hipGetLastError();
+            hipLaunchKernelGGL(k_enc_absmax, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cv, n, mx);
+            err = hipMemcpyAsync(&h_mx, mx, sizeof(u64), hipMemcpyDeviceToHost, st);
         }
-        // the host staging vectors die at return: finish the copies first
         if (err == hipSuccess) err = hipStreamSynchronize(st);
-        (void)hipFreeAsync(buf, st);
-        if (err != hipSuccess) return mhe_internal_fail(MHE_ERR_DEVICE, hipGetErrorString(err));
+        if (err == hipSuccess)
+        {
+            double max_coeff;
+            std::memcpy(&max_coeff, &h_mx, sizeof(double));
+            const int max_bits = static_cast<int>(std::ceil(std::log2(std::max<double>(max_coeff, 1.0)))) + 1;
+            if (!(max_bits < tb)) // NaN compares false: rejected as well
+            {
+                (void)hipFreeAsync(buf, st);
+                return mhe_internal_fail(MHE_ERR_ARG, "encoded values are too large");
+            }
+        }
     }
+    if (err == hipSuccess)
+    {
+        const size_t total = n * limbs;
+        hipLaunchKernelGGL(k_enc_round_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cv, out,
+                           primes, limbs, log_n);
+        err = hipGetLastError();
+    }
+    (void)hipFreeAsync(buf, st);
+    if (err != hipSuccess) return mhe_internal_fail(MHE_ERR_DEVICE, hipGetErrorString(err));
     return mhe_internal_ntt_forward(c, out, 1, limbs, 1, st);
 }
 

@@ -69,6 +69,7 @@ SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), vp]),
     "mhe_ckks_encode_scalar_at": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                                  u64p]),
+    "mhe_sample_poly": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]),
 }
 
 
@@ -186,6 +187,14 @@ class Engine:
         return (1, t.shape[0]) if t.dim() == 2 else (t.shape[0], t.shape[1])
 
     # ----------------------------------------------------------------- kernels
+    SAMPLE_KINDS = {"uniform": 0, "ternary": 1, "normal": 2}
+
+    def sample(self, kind, limbs, seed, tag=0, out=None):
+        """[limbs][n] residues of a random polynomial (mhe_sample_poly; util/rlwe.cpp:21,72,135)."""
+        out = self.empty(limbs, self.n) if out is None else out
+        _check(lib().mhe_sample_poly(self._h, _ptr(out), limbs, self.SAMPLE_KINDS[kind], seed, tag, self.stream()))
+        return out
+
     def ntt_forward(self, t, lazy=False):
         p, l = self._pl(t)
         _check(lib().mhe_ntt_forward(self._h, _ptr(t), p, l, int(lazy), self.stream()))

@@ -119,21 +119,6 @@ std::vector<std::int64_t> sample_sparse_ternary(std::mt19937_64 &g, std::size_t 
     return c;
 }
 
-// sample_poly_normal: ClippedNormalDistribution(0, 3.2, 6 * 3.2), truncated to int64
-std::vector<std::int64_t> sample_normal(std::mt19937_64 &g, std::size_t n)
-{
-    std::normal_distribution<double> d(0.0, 3.2);
-    std::vector<std::int64_t> c(n);
-    for (auto &x : c)
-    {
-        double v;
-        do v = d(g);
-        while (std::fabs(v) > 6 * 3.2);
-        x = static_cast<std::int64_t>(v);
-    }
-    return c;
-}
-
 void residues(const std::vector<std::int64_t> &c, const std::vector<Modulus> &cm, std::size_t limbs,
               std::uint64_t *out)
 {
@@ -149,11 +134,19 @@ void residues(const std::vector<std::int64_t> &c, const std::vector<Modulus> &cm
     }
 }
 
-void uniform_poly(std::mt19937_64 &g, const std::vector<Modulus> &cm, std::size_t limbs, std::size_t n,
-                  std::uint64_t *out)
+// util/rlwe.cpp sample_poly_{uniform,ternary,normal}: drawn on the device (csrc/sample.hip) straight
+// into RNS form on stream s; the host generator only supplies the Philox key and counter domain
+enum SampleKind
 {
-    for (std::size_t j = 0; j < limbs; j++)
-        for (std::size_t i = 0; i < n; i++) out[j * n + i] = uniform_below(g, cm[j].value());
+    kUniform = 0,
+    kTernary = 1,
+    kNormal = 2
+};
+
+void sample_poly(mhe_ctx *eng, std::mt19937_64 &g, SampleKind kind, std::uint64_t *out, std::size_t limbs, void *s)
+{
+    const std::uint64_t seed = g(), tag = g();
+    chk(mhe_sample_poly(eng, out, (int)limbs, (int)kind, seed, tag, s));
 }
 } // namespace
 
@@ -667,13 +660,9 @@ void encrypt_zero_symmetric(const SEALContext &ctx, std::mt19937_64 &g, const st
                             std::uint64_t *c0, std::uint64_t *c1, void *s)
 {
     mhe_ctx *eng = ctx.engine();
-    const auto &cm = ctx.key_context_data()->parms().coeff_modulus();
     const std::size_t n = ctx.key_context_data()->parms().poly_modulus_degree();
-    std::vector<std::uint64_t> h(limbs * n);
-    uniform_poly(g, cm, limbs, n, h.data());
-    upload(eng, s, c1, h);
-    residues(sample_normal(g, n), cm, limbs, h.data());
-    upload(eng, s, c0, h);
+    sample_poly(eng, g, kUniform, c1, limbs, s);
+    sample_poly(eng, g, kNormal, c0, limbs, s);
     chk(mhe_ntt_forward(eng, c0, 1, (int)limbs, 0, s));
     DevBuf t(eng, s, limbs * n);
     chk(mhe_multiply_plain(eng, c1, sk, t.p, 1, (int)limbs, s));
@@ -935,7 +924,6 @@ void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
     // (the key level for the first data level) and is rescaled down, dividing the noise by the
     // dropped prime; secret-key encryption runs at the level itself.
     const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
-    const auto &cm = ctx_.key_context_data()->parms().coeff_modulus();
     mhe_ctx *eng = ctx_.engine();
     void *s = ctx_.stream();
     std::uint64_t *d = dest.store().dev_write(s, true);
@@ -948,16 +936,13 @@ void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
     const std::size_t m = L < K ? L + 1 : L; // prev level (key level for the first level)
     const std::uint64_t *pk = pk_.data().store().dev_read(s);
     DevBuf u(eng, s, m * n), c(eng, s, 2 * m * n), e(eng, s, m * n);
-    std::vector<std::uint64_t> h(m * n);
-    residues(sample_ternary(*rng_, n), cm, m, h.data());
-    upload(eng, s, u.p, h);
+    sample_poly(eng, *rng_, kTernary, u.p, m, s);
     chk(mhe_ntt_forward(eng, u.p, 1, (int)m, 0, s));
     for (int j = 0; j < 2; j++)
     {
         // pk_j restricted to the first m primes: limbs 0..m-1 of poly j ([2][K][n] layout)
         chk(mhe_multiply_plain(eng, pk + j * K * n, u.p, c.p + j * m * n, 1, (int)m, s));
-        residues(sample_normal(*rng_, n), cm, m, h.data());
-        upload(eng, s, e.p, h);
+        sample_poly(eng, *rng_, kNormal, e.p, m, s);
         chk(mhe_ntt_forward(eng, e.p, 1, (int)m, 0, s));
         chk(mhe_add(eng, c.p + j * m * n, e.p, c.p + j * m * n, 1, (int)m, s));
     }

@@ -177,6 +177,13 @@ int mhe_ckks_decode(mhe_ctx *ctx, const mhe_encoder *enc, const uint64_t *plain_
 int mhe_ckks_encode_scalar_at(mhe_ctx *ctx, double value, double scale, int bound_limbs, int limbs,
                               uint64_t *residues);
 
+/* Random polynomials of key generation / encryption (util/rlwe.cpp:135 sample_poly_uniform, :21
+ * sample_poly_ternary, :72 sample_poly_normal), drawn on the device into out[limbs][n] (coefficient
+ * form for kinds 1-2; kind 0 is uniform mod each q_l and serves as NTT form directly).
+ * kind: 0 uniform, 1 ternary {-1,0,1}, 2 normal sigma 3.2 clipped at 6 sigma, truncated.
+ * Deterministic in (seed, tag); Philox4x32-10, not SEAL's Blake2xb stream.  Async on stream. */
+int mhe_sample_poly(mhe_ctx *ctx, uint64_t *out, int limbs, int kind, uint64_t seed, uint64_t tag, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
