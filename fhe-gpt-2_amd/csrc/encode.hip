@@ -25,6 +25,10 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+
+extern "C" hipError_t mhe_internal_copy_d2d(void *dst, const void *src, size_t bytes, hipStream_t st);
+extern "C" hipError_t mhe_internal_alloc(void **p, size_t bytes, hipStream_t st);
+extern "C" hipError_t mhe_internal_free(void *p, hipStream_t st);
 #include <vector>
 
 #include "../../include/mhe.h"
@@ -329,7 +333,7 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_at(mhe_ctx
     const size_t vwords = count * (im ? 2 : 1);
     char *buf = nullptr;
     const size_t bytes = n * sizeof(double2) + vwords * sizeof(double) + sizeof(u64);
-    if (hipMallocAsync((void **)&buf, bytes, st) != hipSuccess)
+    if (mhe_internal_alloc((void **)&buf, bytes, st) != hipSuccess)
         return mhe_internal_fail(MHE_ERR_MEMORY, "encode staging allocation failed");
     double2 *cv = (double2 *)buf;
     double *vals = (double *)(cv + n);
@@ -401,7 +405,7 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_at(mhe_ctx
             const int max_bits = static_cast<int>(std::ceil(std::log2(std::max<double>(max_coeff, 1.0)))) + 1;
             if (!(max_bits < tb)) // NaN compares false: rejected as well
             {
-                (void)hipFreeAsync(buf, st);
+                (void)mhe_internal_free(buf, st);
                 return mhe_internal_fail(MHE_ERR_ARG, "encoded values are too large");
             }
         }
@@ -413,7 +417,7 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_at(mhe_ctx
                            primes, limbs, log_n);
         err = hipGetLastError();
     }
-    (void)hipFreeAsync(buf, st);
+    (void)mhe_internal_free(buf, st);
     if (err != hipSuccess) return mhe_internal_fail(MHE_ERR_DEVICE, hipGetErrorString(err));
     return mhe_internal_ntt_forward(c, out, 1, limbs, 1, st);
 }
@@ -588,9 +592,9 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_decode(mhe_ctx *c
     std::vector<u64> x(n * L);
     {
         u64 *tmp = nullptr;
-        if (hipMallocAsync((void **)&tmp, n * L * sizeof(u64), st) != hipSuccess)
+        if (mhe_internal_alloc((void **)&tmp, n * L * sizeof(u64), st) != hipSuccess)
             return mhe_internal_fail(MHE_ERR_MEMORY, "decode staging allocation failed");
-        hipError_t err = hipMemcpyAsync(tmp, plain, n * L * sizeof(u64), hipMemcpyDeviceToDevice, st);
+        hipError_t err = mhe_internal_copy_d2d(tmp, plain, n * L * sizeof(u64), st);
         int rc = err == hipSuccess ? mhe_ntt_inverse(c, tmp, 1, limbs, 0, stream) : MHE_ERR_DEVICE;
         if (rc == MHE_OK)
         {
@@ -598,7 +602,7 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_decode(mhe_ctx *c
             if (err == hipSuccess) err = hipStreamSynchronize(st);
             if (err != hipSuccess) rc = MHE_ERR_DEVICE;
         }
-        (void)hipFreeAsync(tmp, st);
+        (void)mhe_internal_free(tmp, st);
         if (rc != MHE_OK) return rc == MHE_ERR_DEVICE ? mhe_internal_fail(rc, "decode transfer failed") : rc;
     }
 

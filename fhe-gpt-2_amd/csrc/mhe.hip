@@ -889,6 +889,187 @@ __global__ void k_galois(const u64 *in, u64 *out, u32 elt, int log_n, size_t tot
     out[g] = in[base + src];
 }
 
+// Bootstrapper::modraise_inplace (ckks_bootstrapping/Bootstrapper.cpp:2894-2948): the single-limb
+// coefficient-form polynomial x (mod q_0, canonical) is lifted centered, v = x - q_0 if
+// x > q_0/2, and reduced mod every prime of the target level.
+__global__ void k_modraise(const u64 *in, u64 *out, const PrimeDev *primes, int limbs, int log_n, size_t total)
+{
+    size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    const size_t n = (size_t)1 << log_n;
+    const size_t per_poly = (size_t)limbs << log_n;
+    const size_t p = g / per_poly, r = g - p * per_poly;
+    const int j = (int)(r >> log_n);
+    const size_t i = r & (n - 1);
+    const u64 x = in[p * n + i];
+    const u64 q0 = primes[0].q, q = primes[j].q;
+    u64 v = x % q;
+    if (x > (q0 >> 1))
+    {
+        const u64 mq0 = q - q0 % q; // -q_0 mod q (q for j = 0 reduces to 0 below)
+        v += mq0;
+        v -= (v >= q) ? q : 0;
+    }
+    out[g] = v;
+}
+
+// ============================================================== caching device allocator
+// Stream-ordered allocation for the engine's transient buffers (every Ciphertext temporary of the
+// SEAL surface).  The runtime's stream-ordered pool (hipMallocAsync/hipFreeAsync) was observed on
+// this image to hand out memory that was still live: bootstrapping's cached plaintexts and guard
+// regions were overwritten even with kernels serialised, and disappeared with plain hipMalloc.
+// So the engine keeps its own cache: a freed block records an event on the freeing stream and goes
+// to a free list by size; an allocation reuses a block of the same rounded size (waiting on its
+// event when it comes from another stream) or calls hipMalloc.  Memory is returned to the device
+// only when hipMalloc fails (then every cached block is released and the call retried).
+namespace
+{
+struct CachedBlock
+{
+    void *p;
+    size_t size;
+    hipStream_t st;
+    hipEvent_t ev;
+};
+struct DevAlloc
+{
+    std::mutex mu;
+    std::map<void *, size_t> live;
+    std::multimap<size_t, CachedBlock> free_blocks;
+    std::vector<hipEvent_t> ev_pool;
+    size_t cached = 0, in_use = 0;
+};
+DevAlloc &dev_alloc()
+{
+    static DevAlloc a[64];
+    int d = 0;
+    (void)hipGetDevice(&d);
+    return a[d & 63];
+}
+size_t round_size(size_t b)
+{
+    if (b == 0) b = 1;
+    if (b < ((size_t)1 << 20)) return (b + 4095) & ~(size_t)4095;
+    return (b + ((size_t)1 << 20) - 1) & ~(((size_t)1 << 20) - 1);
+}
+void release_cached(DevAlloc &a)
+{
+    // caller holds a.mu
+    (void)hipDeviceSynchronize();
+    for (auto &kv : a.free_blocks)
+    {
+        (void)hipFree(kv.second.p);
+        a.ev_pool.push_back(kv.second.ev);
+    }
+    a.free_blocks.clear();
+    a.cached = 0;
+}
+} // namespace
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t mhe_internal_alloc(void **p, size_t bytes, hipStream_t st)
+{
+    DevAlloc &a = dev_alloc();
+    const size_t sz = round_size(bytes);
+    std::lock_guard<std::mutex> g(a.mu);
+    auto it = a.free_blocks.lower_bound(sz);
+    auto best = a.free_blocks.end();
+    for (auto j = it; j != a.free_blocks.end() && j->first <= sz + sz / 4; ++j)
+        if (best == a.free_blocks.end() || j->second.st == st)
+        {
+            best = j;
+            if (j->second.st == st) break;
+        }
+    if (best != a.free_blocks.end())
+    {
+        CachedBlock b = best->second;
+        a.free_blocks.erase(best);
+        a.cached -= b.size;
+        if (b.st != st)
+        {
+            hipError_t e = hipStreamWaitEvent(st, b.ev, 0);
+            if (e != hipSuccess) return e;
+        }
+        a.ev_pool.push_back(b.ev);
+        a.live[b.p] = b.size;
+        a.in_use += b.size;
+        *p = b.p;
+        return hipSuccess;
+    }
+    hipError_t e = hipMalloc(p, sz);
+    if (e != hipSuccess)
+    {
+        (void)hipGetLastError();
+        release_cached(a);
+        e = hipMalloc(p, sz);
+        if (e != hipSuccess) return e;
+    }
+    a.live[*p] = sz;
+    a.in_use += sz;
+    return hipSuccess;
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t mhe_internal_free(void *p, hipStream_t st)
+{
+    if (!p) return hipSuccess;
+    DevAlloc &a = dev_alloc();
+    std::lock_guard<std::mutex> g(a.mu);
+    auto it = a.live.find(p);
+    if (it == a.live.end()) return hipErrorInvalidValue;
+    const size_t sz = it->second;
+    a.live.erase(it);
+    a.in_use -= sz;
+    hipEvent_t ev = nullptr;
+    if (!a.ev_pool.empty())
+    {
+        ev = a.ev_pool.back();
+        a.ev_pool.pop_back();
+    }
+    else
+    {
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipEventRecord(ev, st);
+    if (e != hipSuccess) return e;
+    a.free_blocks.emplace(sz, CachedBlock{ p, sz, st, ev });
+    a.cached += sz;
+    return hipSuccess;
+}
+
+// Device-to-device copies run as a kernel on the caller's stream (ordered with the stream's other
+// kernels by construction, at HBM speed) rather than hipMemcpyAsync's copy engines.
+__global__ void k_copy16(uint4 *__restrict__ dst, const uint4 *__restrict__ src, size_t count)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+__global__ void k_copy8(u64 *__restrict__ dst, const u64 *__restrict__ src, size_t count)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+extern "C" __attribute__((visibility("hidden"))) hipError_t mhe_internal_copy_d2d(void *dst, const void *src,
+                                                                                  size_t bytes, hipStream_t st)
+{
+    if (!bytes || dst == src) return hipSuccess;
+    const uintptr_t a = (uintptr_t)dst | (uintptr_t)src;
+    if ((a & 15) == 0 && (bytes & 15) == 0)
+    {
+        const size_t cnt = bytes / 16;
+        const unsigned grid = (unsigned)std::min<size_t>((cnt + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, st, (uint4 *)dst, (const uint4 *)src, cnt);
+        return hipGetLastError();
+    }
+    if ((a & 7) == 0 && (bytes & 7) == 0)
+    {
+        const size_t cnt = bytes / 8;
+        const unsigned grid = (unsigned)std::min<size_t>((cnt + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_copy8, dim3(grid), dim3(256), 0, st, (u64 *)dst, (const u64 *)src, cnt);
+        return hipGetLastError();
+    }
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st);
+}
+
 // ======================================================================= dispatch helpers
 static bool valid_ctx(mhe_ctx *c)
 {
@@ -1316,18 +1497,130 @@ MHE_EXPORT int mhe_malloc(mhe_ctx *c, void **dptr, size_t bytes)
     return MHE_OK;
 }
 
+// MHE_ALLOC_TRACE=1: track live stream-ordered allocations and report double frees, frees of
+// unknown pointers and overlapping live ranges (debugging aid)
+static std::mutex g_trace_mu;
+static std::map<uintptr_t, size_t> g_live;
+static int trace_on()
+{
+    static int on = -1;
+    if (on < 0)
+    {
+        const char *e = getenv("MHE_ALLOC_TRACE");
+        on = e && e[0] >= '1';
+    }
+    return on;
+}
+
+
+// trace mode: the range [p, p + words) must lie inside one live stream-ordered allocation
+static void trace_range(const char *fn, const char *what, const void *p, size_t words)
+{
+    if (!trace_on() || !p) return;
+    std::lock_guard<std::mutex> g(g_trace_mu);
+    const uintptr_t a = (uintptr_t)p, e = a + words * 8;
+    auto it = g_live.upper_bound(a);
+    if (it == g_live.begin()) return; // not a tracked allocation (workspace, hipMalloc)
+    --it;
+    if (it->first + it->second < a) return;
+    if (e > it->first + it->second)
+        fprintf(stderr, "[alloc-trace] %s: %s range [%p, +%zu words) exceeds allocation %p of %zu words by %zu words\n",
+                fn, what, p, words, (void *)it->first, it->second / 8, (size_t)(e - (it->first + it->second)) / 8);
+}
+// trace level 2: at every instrumented entry, synchronise and check the first 4 KiB of every live
+// allocation's guard; a hit names the previous instrumented call as the writer
+static const char *g_prev_fn = "(none)";
+static size_t g_prev_info[4];
+static void trace_check_all(const char *fn, size_t i0, size_t i1, size_t i2, size_t i3)
+{
+    static int lvl = -1;
+    if (lvl < 0)
+    {
+        const char *e = getenv("MHE_ALLOC_TRACE");
+        lvl = e ? atoi(e) : 0;
+    }
+    if (lvl < 2) return;
+    (void)hipDeviceSynchronize();
+    std::lock_guard<std::mutex> g(g_trace_mu);
+    std::vector<unsigned char> buf(4096);
+    for (auto &kv : g_live)
+    {
+        (void)hipMemcpy(buf.data(), (const char *)kv.first + kv.second, 4096, hipMemcpyDeviceToHost);
+        bool bad = false;
+        for (unsigned char b : buf) bad |= b != 0xAB;
+        if (bad)
+        {
+            fprintf(stderr, "[alloc-trace] guard of %#lx (%zu words) hit before %s; previous call %s(%zu, %zu, %zu, %zu)\n",
+                    (unsigned long)kv.first, kv.second / 8, fn, g_prev_fn, g_prev_info[0], g_prev_info[1],
+                    g_prev_info[2], g_prev_info[3]);
+            (void)hipMemset((char *)kv.first + kv.second, 0xAB, (size_t)16 << 20); // re-arm
+        }
+    }
+    g_prev_fn = fn;
+    g_prev_info[0] = i0;
+    g_prev_info[1] = i1;
+    g_prev_info[2] = i2;
+    g_prev_info[3] = i3;
+}
+#define TR(what, p, words) trace_range(__func__, what, p, (size_t)(words))
+#define TRC(a, b, cc, d) trace_check_all(__func__, (size_t)(a), (size_t)(b), (size_t)(cc), (size_t)(d))
+
 MHE_EXPORT int mhe_malloc_async(mhe_ctx *c, void **dptr, size_t bytes, void *stream)
 {
     if (!valid_ctx(c) || !dptr) return fail(MHE_ERR_ARG, "invalid argument");
-    if (hipMallocAsync(dptr, bytes ? bytes : 1, S(stream)) != hipSuccess)
+    const size_t kGuard = trace_on() ? ((size_t)16 << 20) : 0;
+    if (mhe_internal_alloc(dptr, (bytes ? bytes : 1) + kGuard, S(stream)) != hipSuccess)
         return fail(MHE_ERR_MEMORY, "device allocation failed");
+    if (trace_on())
+    {
+        (void)hipMemsetAsync((char *)*dptr + (bytes ? bytes : 1), 0xAB, kGuard, S(stream));
+        std::lock_guard<std::mutex> g(g_trace_mu);
+        const uintptr_t a = (uintptr_t)*dptr, e = a + (bytes ? bytes : 1);
+        auto it = g_live.upper_bound(a);
+        if (it != g_live.begin())
+        {
+            auto pv = std::prev(it);
+            if (pv->first + pv->second > a)
+                fprintf(stderr, "[alloc-trace] overlap: new [%#lx,+%zu) inside live [%#lx,+%zu)\n", (unsigned long)a,
+                        bytes, (unsigned long)pv->first, pv->second);
+        }
+        if (it != g_live.end() && it->first < e)
+            fprintf(stderr, "[alloc-trace] overlap: new [%#lx,+%zu) covers live [%#lx,+%zu)\n", (unsigned long)a, bytes,
+                    (unsigned long)it->first, it->second);
+        g_live[a] = bytes ? bytes : 1;
+    }
     return MHE_OK;
 }
 
 MHE_EXPORT int mhe_free_async(mhe_ctx *c, void *dptr, void *stream)
 {
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
-    HIP_TRY(hipFreeAsync(dptr, S(stream)));
+    if (trace_on() && dptr)
+    {
+        std::lock_guard<std::mutex> g(g_trace_mu);
+        auto it = g_live.find((uintptr_t)dptr);
+        if (it == g_live.end())
+            fprintf(stderr, "[alloc-trace] free of unknown or already freed pointer %p\n", dptr);
+        else
+        {
+            const size_t kGuard = (size_t)16 << 20;
+            std::vector<unsigned char> gbuf(kGuard);
+            (void)hipStreamSynchronize(S(stream));
+            (void)hipMemcpy(gbuf.data(), (char *)dptr + it->second, kGuard, hipMemcpyDeviceToHost);
+            size_t first = kGuard, last = 0;
+            for (size_t i = 0; i < kGuard; i++)
+                if (gbuf[i] != 0xAB)
+                {
+                    first = std::min(first, i);
+                    last = i;
+                }
+            if (first < kGuard)
+                fprintf(stderr, "[alloc-trace] OVERRUN of allocation %p (%zu bytes = %zu words): guard bytes [%zu, %zu] written\n",
+                        dptr, it->second, it->second / 8, first, last);
+            g_live.erase(it);
+        }
+    }
+    HIP_TRY(mhe_internal_free(dptr, S(stream)));
     return MHE_OK;
 }
 
@@ -1354,8 +1647,10 @@ MHE_EXPORT int mhe_memcpy_d2h(mhe_ctx *c, void *dst, const void *src, size_t byt
 
 MHE_EXPORT int mhe_memcpy_d2d(mhe_ctx *c, void *dst, const void *src, size_t bytes, void *stream)
 {
+    TR("dst", dst, bytes / 8); TR("src", src, bytes / 8);
+    TRC(0, 0, 0, 0);
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)));
+    HIP_TRY(mhe_internal_copy_d2d(dst, src, bytes, S(stream)));
     return MHE_OK;
 }
 
@@ -1433,6 +1728,8 @@ static int check_poly_args(mhe_ctx *c, const void *a, int polys, int limbs)
 
 MHE_EXPORT int mhe_ntt_forward(mhe_ctx *c, uint64_t *data, int polys, int limbs, int lazy, void *stream)
 {
+    TR("data", data, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_poly_args(c, data, polys, limbs);
     if (r) return r;
     return run_ntt_fwd(c, data, data, polys, limbs, lazy ? 0 : 1, S(stream));
@@ -1440,6 +1737,8 @@ MHE_EXPORT int mhe_ntt_forward(mhe_ctx *c, uint64_t *data, int polys, int limbs,
 
 MHE_EXPORT int mhe_ntt_inverse(mhe_ctx *c, uint64_t *data, int polys, int limbs, int lazy, void *stream)
 {
+    TR("data", data, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_poly_args(c, data, polys, limbs);
     if (r) return r;
     return run_ntt_inv(c, data, data, polys, limbs, lazy ? 0 : 1, S(stream));
@@ -1459,22 +1758,30 @@ static int launch_addsub(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out, int p
 
 MHE_EXPORT int mhe_add(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs, void *s)
 {
+    TR("out", out, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("b", b, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     return launch_addsub(c, a, b, out, polys, limbs, 0, s);
 }
 
 MHE_EXPORT int mhe_sub(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs, void *s)
 {
+    TR("out", out, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("b", b, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     return launch_addsub(c, a, b, out, polys, limbs, 1, s);
 }
 
 MHE_EXPORT int mhe_negate(mhe_ctx *c, const uint64_t *a, uint64_t *out, int polys, int limbs, void *s)
 {
+    TR("out", out, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     return launch_addsub(c, a, nullptr, out, polys, limbs, 2, s);
 }
 
 MHE_EXPORT int mhe_multiply_plain(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys,
                                   int limbs, void *s)
 {
+    TR("out", out, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("b", b, (size_t)limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!b || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
@@ -1508,12 +1815,16 @@ static int launch_scalar(mhe_ctx *c, const u64 *a, const u64 *scalars, u64 *out,
 MHE_EXPORT int mhe_multiply_scalar(mhe_ctx *c, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys,
                                    int limbs, void *s)
 {
+    TR("out", out, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     return launch_scalar(c, a, scalars, out, polys, limbs, 0, s);
 }
 
 MHE_EXPORT int mhe_add_scalar(mhe_ctx *c, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys,
                               int limbs, void *s)
 {
+    TR("out", out, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     return launch_scalar(c, a, scalars, out, polys, limbs, 1, s);
 }
 
@@ -1533,6 +1844,8 @@ static int launch_tensor(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out3, int 
 
 MHE_EXPORT int mhe_ct_multiply(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *out3, int limbs, void *s)
 {
+    TR("out3", out3, (size_t)3 * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)2 * limbs * ((size_t)1 << c->log_n)); TR("b", b, (size_t)2 * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_poly_args(c, a, 2, limbs);
     if (r) return r;
     if (!b || !out3) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
@@ -1541,6 +1854,8 @@ MHE_EXPORT int mhe_ct_multiply(mhe_ctx *c, const uint64_t *a, const uint64_t *b,
 
 MHE_EXPORT int mhe_ct_square(mhe_ctx *c, const uint64_t *a, uint64_t *out3, int limbs, void *s)
 {
+    TR("out3", out3, (size_t)3 * limbs * ((size_t)1 << c->log_n)); TR("a", a, (size_t)2 * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_poly_args(c, a, 2, limbs);
     if (r) return r;
     if (!out3) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
@@ -1550,6 +1865,8 @@ MHE_EXPORT int mhe_ct_square(mhe_ctx *c, const uint64_t *a, uint64_t *out3, int 
 MHE_EXPORT int mhe_switch_key(mhe_ctx *c, uint64_t *ct, const uint64_t *target, const uint64_t *key, int key_limbs,
                               int limbs, void *s)
 {
+    TR("ct", ct, (size_t)2 * limbs * ((size_t)1 << c->log_n)); TR("target", target, (size_t)limbs * ((size_t)1 << c->log_n)); TR("key", key, (size_t)limbs * 2 * key_limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_limbs(c, limbs, 1);
     if (r) return r;
     if (!ct || !target || !key) return fail(MHE_ERR_ARG, "target_iter");
@@ -1558,6 +1875,8 @@ MHE_EXPORT int mhe_switch_key(mhe_ctx *c, uint64_t *ct, const uint64_t *target, 
 
 MHE_EXPORT int mhe_relinearize(mhe_ctx *c, uint64_t *ct3, const uint64_t *key, int key_limbs, int limbs, void *s)
 {
+    TR("ct3", ct3, (size_t)3 * limbs * ((size_t)1 << c->log_n)); TR("key", key, (size_t)limbs * 2 * key_limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_limbs(c, limbs, 1);
     if (r) return r;
     if (!ct3 || !key) return fail(MHE_ERR_ARG, "relin_keys is not valid for encryption parameters");
@@ -1577,6 +1896,8 @@ static int launch_galois(mhe_ctx *c, const u64 *in, u32 elt, u64 *out, int polys
 MHE_EXPORT int mhe_permute_galois(mhe_ctx *c, const uint64_t *in, uint32_t elt, uint64_t *out, int polys, int limbs,
                                   void *s)
 {
+    TR("out", out, (size_t)polys * limbs * ((size_t)1 << c->log_n)); TR("in", in, (size_t)polys * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_poly_args(c, in, polys, limbs);
     if (r) return r;
     if (!out || out == in) return fail(MHE_ERR_ARG, "result cannot point to the same value as operand");
@@ -1586,6 +1907,8 @@ MHE_EXPORT int mhe_permute_galois(mhe_ctx *c, const uint64_t *in, uint32_t elt, 
 MHE_EXPORT int mhe_apply_galois(mhe_ctx *c, uint64_t *ct, uint32_t elt, const uint64_t *key, int key_limbs, int limbs,
                                 void *s)
 {
+    TR("ct", ct, (size_t)2 * limbs * ((size_t)1 << c->log_n)); TR("key", key, (size_t)limbs * 2 * key_limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     int r = check_limbs(c, limbs, 1);
     if (r) return r;
     if (!ct || !key) return fail(MHE_ERR_ARG, "Galois key not present");
@@ -1597,7 +1920,7 @@ MHE_EXPORT int mhe_apply_galois(mhe_ctx *c, uint64_t *ct, uint32_t elt, const ui
     // evaluator.cpp:2193-2214: c0 <- perm(c0) (via tmp), tmp <- perm(c1), c1 <- 0, then KS(tmp)
     r = launch_galois(c, ct, elt, w->tmp, 1, limbs, st);
     if (r) return r;
-    HIP_TRY(hipMemcpyAsync(ct, w->tmp, ps * sizeof(u64), hipMemcpyDeviceToDevice, st));
+    HIP_TRY(mhe_internal_copy_d2d(ct, w->tmp, ps * sizeof(u64), st));
     r = launch_galois(c, ct + ps, elt, w->tmp, 1, limbs, st);
     if (r) return r;
     HIP_TRY(hipMemsetAsync(ct + ps, 0, ps * sizeof(u64), st));
@@ -1606,6 +1929,8 @@ MHE_EXPORT int mhe_apply_galois(mhe_ctx *c, uint64_t *ct, uint32_t elt, const ui
 
 MHE_EXPORT int mhe_rescale_to_next(mhe_ctx *c, const uint64_t *in, uint64_t *out, int size, int limbs, void *s)
 {
+    TR("out", out, (size_t)size * (limbs - 1) * ((size_t)1 << c->log_n)); TR("in", in, (size_t)size * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
     if (limbs < 2) return fail(MHE_ERR_RANGE, "end of modulus switching chain reached");
     if (limbs > c->K || size < 1 || size > 3 || !in || !out)
@@ -1614,8 +1939,23 @@ MHE_EXPORT int mhe_rescale_to_next(mhe_ctx *c, const uint64_t *in, uint64_t *out
     return run_rescale(c, in, out, size, limbs, S(s));
 }
 
+MHE_EXPORT int mhe_modraise(mhe_ctx *c, const uint64_t *in, uint64_t *out, int size, int limbs, void *s)
+{
+    TR("out", out, (size_t)size * limbs * ((size_t)1 << c->log_n)); TR("in", in, (size_t)size * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (!in || !out || size < 1 || limbs < 1 || limbs > c->K) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    const size_t total = ((size_t)size * limbs) << c->log_n;
+    hipLaunchKernelGGL(k_modraise, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, S(s), in, out, c->primes,
+                       limbs, c->log_n, total);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
 MHE_EXPORT int mhe_mod_switch_drop(mhe_ctx *c, const uint64_t *in, uint64_t *out, int size, int limbs, void *s)
 {
+    TR("out", out, (size_t)size * (limbs - 1) * ((size_t)1 << c->log_n)); TR("in", in, (size_t)size * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
     if (limbs < 2) return fail(MHE_ERR_RANGE, "end of modulus switching chain reached");
     if (!in || !out || size < 1) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
@@ -1624,8 +1964,8 @@ MHE_EXPORT int mhe_mod_switch_drop(mhe_ctx *c, const uint64_t *in, uint64_t *out
     if (in != out)
     {
         for (int p = 0; p < size; p++)
-            HIP_TRY(hipMemcpyAsync((char *)out + p * dst_pitch, (const char *)in + p * src_pitch, dst_pitch,
-                                   hipMemcpyDeviceToDevice, S(s)));
+            HIP_TRY(mhe_internal_copy_d2d((char *)out + p * dst_pitch, (const char *)in + p * src_pitch, dst_pitch,
+                                          S(s)));
         return MHE_OK;
     }
     // In place: component p moves down by p limbs.  One copy per limb, ascending: every copy's
@@ -1634,9 +1974,8 @@ MHE_EXPORT int mhe_mod_switch_drop(mhe_ctx *c, const uint64_t *in, uint64_t *out
     const size_t limb_bytes = sizeof(u64) << c->log_n;
     for (int p = 1; p < size; p++)
         for (int l = 0; l + 1 < limbs; l++)
-            HIP_TRY(hipMemcpyAsync((char *)out + p * dst_pitch + l * limb_bytes,
-                                   (const char *)in + p * src_pitch + l * limb_bytes, limb_bytes,
-                                   hipMemcpyDeviceToDevice, S(s)));
+            HIP_TRY(mhe_internal_copy_d2d((char *)out + p * dst_pitch + l * limb_bytes,
+                                          (const char *)in + p * src_pitch + l * limb_bytes, limb_bytes, S(s)));
     return MHE_OK;
 }
 

@@ -330,22 +330,42 @@ private:
 };
 
 // KSwitchKeys (SEAL/kswitchkeys.h): one device buffer [digits][2][key_limbs][n] per key index.
+//
+// Deferred materialisation (Galois keys, MI355X memory budget): the reference's ResNet driver asks
+// for 284 Galois keys at the key level, 284 x 1.04 GB = 295 GB, more than one GPU's 288 GB HBM.
+// Most of them are only ever used at <= 3 limbs (the convolutions), where a key needs only L
+// digits over L+1 primes.  A deferred key set keeps the secret key and, per index, a seed; the
+// first rotation at L limbs materialises the level-truncated key (L digits, primes q_0..q_{L-1}
+// and P) and a later use at a higher level re-materialises it larger.  The evaluator sees the
+// same key-switching formula; only the key's random parts differ from an eager key.
+struct KeyMaker;
 class KSwitchKeys
 {
 public:
-    std::size_t size() const noexcept { return keys_.size(); }
+    std::size_t size() const;
     const parms_id_type &parms_id() const noexcept { return parms_id_; }
     parms_id_type &parms_id() noexcept { return parms_id_; }
-    bool has_index(std::size_t i) const { return keys_.count(i) != 0; }
+    bool has_index(std::size_t i) const;
     const PolyStore &key(std::size_t i) const;
     PolyStore &key_mut(std::size_t i) { return keys_[i]; }
     std::size_t key_limbs() const noexcept { return key_limbs_; }
     void set_key_limbs(std::size_t k) { key_limbs_ = k; }
+    // device key for index i usable by an L-limb ciphertext, materialising a deferred key on
+    // demand (thread-safe); key_limbs receives the key's limb stride
+    const std::uint64_t *key_for(std::size_t i, std::size_t L, void *stream, std::size_t &key_limbs) const;
+    bool deferred() const noexcept { return maker_ != nullptr; }
+    void set_maker(std::shared_ptr<KeyMaker> m) { maker_ = std::move(m); }
+    const std::shared_ptr<KeyMaker> &maker() const noexcept { return maker_; }
+    // bytes of device memory held by materialised keys
+    std::size_t device_bytes() const;
 
 private:
-    std::map<std::size_t, PolyStore> keys_;
+    mutable std::map<std::size_t, PolyStore> keys_;
+    mutable std::map<std::size_t, std::size_t> limbs_of_; // deferred keys: limb stride per index
+    mutable std::vector<PolyStore> retired_;               // outgrown deferred keys (may be in flight)
     parms_id_type parms_id_ = parms_id_zero;
     std::size_t key_limbs_ = 0;
+    std::shared_ptr<KeyMaker> maker_;
 };
 
 class RelinKeys : public KSwitchKeys
@@ -503,6 +523,10 @@ public:
     void multiply_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const;
     template <typename T>
     void multiply_vector_inplace(Ciphertext &encrypted, const std::vector<T> &value) const;
+    // (not SEAL API) the plaintext multiply_vector_inplace multiplies by: value encoded at the
+    // first level with scale encrypted.scale(), kept at the ciphertext's level
+    template <typename T>
+    void encode_vector_for(const Ciphertext &encrypted, const std::vector<T> &value, Plaintext &plain) const;
     template <typename T>
     void multiply_vector(Ciphertext &encrypted, const std::vector<T> &value, Ciphertext &destination) const
     {

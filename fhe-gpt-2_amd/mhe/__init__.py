@@ -57,6 +57,7 @@ SIGNATURES = {
     "mhe_permute_galois": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_rescale_to_next": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_mod_switch_drop": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_modraise": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_hmult": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]),
     "mhe_encoder_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
     "mhe_encoder_destroy": (ctypes.c_int, [vp]),
@@ -289,6 +290,13 @@ class Engine:
         size, L = ct.shape[0], ct.shape[1]
         out = self.empty(size, L - 1, self.n) if out is None else out
         _check(lib().mhe_mod_switch_drop(self._h, _ptr(ct), _ptr(out), size, L, self.stream()))
+        return out
+
+    def modraise(self, ct1, L, out=None):
+        """Bootstrapper::modraise_inplace lift: ct1 [size][1][n] coefficient form -> [size][L][n]."""
+        size = ct1.shape[0]
+        out = self.empty(size, L, self.n) if out is None else out
+        _check(lib().mhe_modraise(self._h, _ptr(ct1), _ptr(out), size, L, self.stream()))
         return out
 
     def hmult(self, a, b, key, out=None):

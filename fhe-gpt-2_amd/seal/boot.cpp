@@ -1,0 +1,1277 @@
+// boot.cpp -- CKKS bootstrapping over the seal:: surface (include/mhe_boot.h).
+//
+// Ciphertext-operation sequences follow cnn_ckks/cpu-ckks/single-key/ckks_bootstrapping/
+// Bootstrapper.cpp and ModularReducer.cpp and cnn_ckks/common/Polynomial.cpp (cited per
+// function); the host-side coefficient generation is this build's own (see the header).
+#include "mhe_boot.h"
+
+#include <quadmath.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <mutex>
+#include <stdexcept>
+
+#include "../../include/mhe.h"
+
+using namespace seal;
+using cd = std::complex<double>;
+
+// ============================================================================ common/func.cpp
+void oddbabycount(long &mink, long &minm, long deg)
+{
+    // common/func.cpp:90-115: the (k, m) minimising the odd baby-step cost estimate among
+    // shapes of minimal depth ceil(log2 k) + m = ceil(log2 deg)
+    long m, mind = 0;
+    double mineval = 100000;
+    for (long k = 2; k <= deg; k += 2)
+    {
+        m = 1;
+        while ((1L << m) * k < deg) m++;
+        if (std::ceil(std::log(k) / std::log(2)) + m == std::ceil(std::log(deg) / std::log(2)))
+        {
+            const double eval = std::ceil((deg + 0.0) / (k + 0.0)) + k / 2 - 5 + m + std::ceil(std::log(k)) +
+                                std::max(3.0 - m, std::ceil((deg + 0.0) / (1.5 * (1L << (m - 1)) * k)));
+            if (mineval > eval)
+            {
+                mineval = eval;
+                mink = k;
+                minm = m;
+                mind = (long)(std::ceil(std::log(k) / std::log(2)) + m);
+            }
+            else if (mineval == eval && mind > std::ceil(std::log(k) / std::log(2)) + m)
+            {
+                mink = k;
+                minm = m;
+                mind = (long)(std::ceil(std::log(k) / std::log(2)) + m);
+            }
+        }
+    }
+}
+
+void babycount(long &mink, long &minm, long deg)
+{
+    // common/func.cpp:117-140: minimise log2(d/k) + k + d/k - 3 non-scalar products
+    mink = 2;
+    double d_over_k = static_cast<double>(deg) / mink;
+    int log2_d_over_k = (int)std::ceil(std::log2(d_over_k));
+    int ceil_d_over_k = (int)std::ceil(d_over_k);
+    int min_mul = log2_d_over_k + (int)mink + ceil_d_over_k - 3;
+    minm = log2_d_over_k;
+    for (int i = 3; i < 2 * std::sqrt((double)deg); i++)
+    {
+        d_over_k = static_cast<double>(deg) / i;
+        log2_d_over_k = (int)std::ceil(std::log2(d_over_k));
+        ceil_d_over_k = (int)std::ceil(d_over_k);
+        const int curr_mul = log2_d_over_k + i + ceil_d_over_k - 3;
+        if (min_mul > curr_mul)
+        {
+            mink = i;
+            min_mul = curr_mul;
+            minm = log2_d_over_k;
+        }
+    }
+}
+
+int giantstep(int M)
+{
+    // common/func.cpp:203-213: k minimising ceil(M/k) + k - 1
+    int minval = M, mink = 1;
+    for (int k = 1; k <= 3 * std::sqrt((double)M); k++)
+    {
+        const int currval = (int)std::ceil((M + 0.0) / (k + 0.0)) + k - 1;
+        if (currval < minval)
+        {
+            minval = currval;
+            mink = k;
+        }
+    }
+    return mink;
+}
+
+void rotation(int logslot, int Nh, int shiftcount, const std::vector<cd> &vec, std::vector<cd> &rtnvec)
+{
+    // common/func.cpp:215-224
+    const int slotlen = 1 << logslot, repeatcount = Nh / slotlen;
+    rtnvec.clear();
+    rtnvec.reserve(Nh);
+    for (int j = 0; j < repeatcount; j++)
+        for (int i = 0; i < slotlen; i++) rtnvec.push_back(vec[((slotlen + i + shiftcount) % slotlen + slotlen) % slotlen]);
+}
+
+// ======================================================================== boot::Polynomial
+namespace boot
+{
+Polynomial::Polynomial(long d) : coeff(d + 1, 0.0), chebcoeff(d + 1, 0.0), deg(d) {}
+
+void Polynomial::set_zero_polynomial(long d)
+{
+    deg = d;
+    coeff.assign(d + 1, 0.0);
+    chebcoeff.assign(d + 1, 0.0);
+}
+
+void Polynomial::set_chebyshev(const std::vector<double> &cheb)
+{
+    deg = (long)cheb.size() - 1;
+    chebcoeff = cheb;
+    cheb_to_power();
+}
+
+void Polynomial::cheb_to_power()
+{
+    // Polynomial.cpp:110-123 (T_i by the three-term recurrence, summed in the power basis); only
+    // meaningful in double precision for small degrees, which is where `coeff` is read
+    coeff.assign(deg + 1, 0.0);
+    std::vector<double> t0(deg + 1, 0.0), t1(deg + 1, 0.0), t2(deg + 1, 0.0);
+    t0[0] = 1.0;
+    if (deg >= 1) t1[1] = 1.0;
+    for (long i = 0; i <= deg; i++)
+    {
+        const std::vector<double> &ti = i == 0 ? t0 : t1;
+        for (long j = 0; j <= i; j++) coeff[j] += chebcoeff[i] * ti[j];
+        if (i >= 1 && i < deg)
+        {
+            std::fill(t2.begin(), t2.end(), 0.0);
+            for (long j = 0; j <= i; j++) t2[j + 1] += 2 * t1[j];
+            for (long j = 0; j <= i - 1; j++) t2[j] -= t0[j];
+            t0.swap(t1);
+            t1.swap(t2);
+        }
+    }
+}
+
+void Polynomial::constmul(double c)
+{
+    for (auto &v : coeff) v *= c;
+    for (auto &v : chebcoeff) v *= c;
+}
+
+double Polynomial::evaluate(double x) const
+{
+    // Clenshaw
+    double b1 = 0, b2 = 0;
+    for (long j = deg; j >= 1; j--)
+    {
+        const double b0 = 2 * x * b1 - b2 + chebcoeff[j];
+        b2 = b1;
+        b1 = b0;
+    }
+    return x * b1 - b2 + chebcoeff[0];
+}
+
+void divide_poly(Polynomial &quotient, Polynomial &remainder, const Polynomial &target, long m)
+{
+    // p = q T_m + r, deg r < m, using T_j = 2 T_{j-m} T_m - T_{|j-2m|} (j > m) and T_m = T_0 T_m.
+    // Same polynomials as the reference's power-basis long division (Polynomial.cpp:890-916).
+    if (target.deg < m)
+    {
+        quotient.set_zero_polynomial(0);
+        remainder = target;
+        return;
+    }
+    std::vector<double> r = target.chebcoeff, q(target.deg - m + 1, 0.0);
+    for (long j = target.deg; j >= m; j--)
+    {
+        const double a = r[j];
+        r[j] = 0;
+        if (j == m)
+            q[0] += a;
+        else
+        {
+            q[j - m] += 2 * a;
+            r[std::labs(j - 2 * m)] -= a;
+        }
+    }
+    r.resize(m);
+    quotient.set_chebyshev(q);
+    remainder.set_chebyshev(r);
+}
+
+void Polynomial::generate_poly_heap_manual(long k, long m)
+{
+    // Polynomial.cpp:169-206: node j splits into quotient 2(j+1)-1 and remainder 2(j+1) by
+    // T_{k 2^(m-1-level)}; a node below that degree passes on as the remainder only
+    heap_k = k;
+    heap_m = m;
+    heaplen = (1L << (heap_m + 1)) - 1;
+    poly_heap.assign(heaplen, nullptr);
+    poly_heap[0] = std::make_shared<Polynomial>(*this);
+    poly_heap[0]->poly_heap.clear();
+    long chebdeg = heap_k << heap_m;
+    for (long i = 0; i < heap_m; i++)
+    {
+        chebdeg >>= 1;
+        const long first = (1L << i) - 1, last = (1L << (i + 1)) - 1;
+        for (long j = first; j < last; j++)
+        {
+            if (!poly_heap[j]) continue;
+            if (poly_heap[j]->deg < chebdeg)
+                poly_heap[2 * (j + 1)] = std::make_shared<Polynomial>(*poly_heap[j]);
+            else
+            {
+                auto qn = std::make_shared<Polynomial>(), rn = std::make_shared<Polynomial>();
+                divide_poly(*qn, *rn, *poly_heap[j], chebdeg);
+                poly_heap[2 * (j + 1) - 1] = qn;
+                poly_heap[2 * (j + 1)] = rn;
+            }
+        }
+    }
+}
+
+void Polynomial::generate_poly_heap_odd()
+{
+    oddbabycount(heap_k, heap_m, deg);
+    generate_poly_heap_manual(heap_k, heap_m);
+}
+
+void Polynomial::generate_poly_heap()
+{
+    babycount(heap_k, heap_m, deg);
+    generate_poly_heap_manual(heap_k, heap_m);
+}
+
+void Polynomial::write_heap_to_file(std::ostream &out) const
+{
+    // Polynomial.cpp:217-230 layout: heaplen, then "index deg" and deg+1 Chebyshev coefficients
+    out.precision(17);
+    out << heaplen << "\n";
+    for (long index = 0; index < heaplen; index++)
+        if (poly_heap[index])
+        {
+            out << index << " " << poly_heap[index]->deg << "\n";
+            for (long i = 0; i <= poly_heap[index]->deg; i++) out << poly_heap[index]->chebcoeff[i] << "\n";
+            out << "\n";
+        }
+}
+
+void Polynomial::read_heap_from_file(std::istream &in)
+{
+    // Polynomial.cpp:232-253
+    long index = 0, in_deg = 0;
+    in >> heaplen;
+    poly_heap.assign(heaplen, nullptr);
+    while (index < heaplen - 1 && (in >> index >> in_deg))
+    {
+        std::vector<double> c(in_deg + 1);
+        for (auto &v : c) in >> v;
+        poly_heap[index] = std::make_shared<Polynomial>();
+        poly_heap[index]->set_chebyshev(c);
+    }
+    heap_m = 0;
+    while ((1L << (heap_m + 1)) - 1 < heaplen) heap_m++;
+    if (poly_heap[0])
+    {
+        set_chebyshev(poly_heap[0]->chebcoeff);
+        // heap_k from the top split degree: deg < k 2^m
+        heap_k = 1;
+        while ((heap_k << heap_m) <= deg) heap_k++;
+    }
+}
+
+void Polynomial::homomorphic_poly_evaluation(SEALContext &, CKKSEncoder &, Encryptor &, Evaluator &evaluator,
+                                             RelinKeys &relin_keys, Ciphertext &rtn, Ciphertext &cipher, Decryptor &)
+{
+    // Polynomial.cpp:256-560
+    const double zero = 1. / cipher.scale();
+    if (deg == 1)
+    {
+        evaluator.multiply_const(cipher, coeff[1], rtn);
+        evaluator.rescale_to_next_inplace(rtn);
+        evaluator.add_const(rtn, coeff[0], rtn);
+        return;
+    }
+    if (deg == 2)
+    {
+        Ciphertext squared;
+        evaluator.square(cipher, squared);
+        evaluator.relinearize_inplace(squared, relin_keys);
+        evaluator.rescale_to_next_inplace(squared);
+        evaluator.multiply_const_inplace(squared, coeff[2]);
+        evaluator.rescale_to_next_inplace(squared);
+        if (std::abs(coeff[1]) >= zero)
+        {
+            evaluator.multiply_const(cipher, coeff[1], rtn);
+            evaluator.rescale_to_next_inplace(rtn);
+            evaluator.add_reduced_error(rtn, squared, rtn);
+        }
+        else
+            rtn = squared;
+        evaluator.add_const_inplace(rtn, coeff[0]);
+        return;
+    }
+    if (deg == 3)
+    {
+        Ciphertext squared, cubic;
+        evaluator.square(cipher, squared);
+        evaluator.relinearize_inplace(squared, relin_keys);
+        evaluator.rescale_to_next_inplace(squared);
+        evaluator.multiply_const(cipher, coeff[3], cubic);
+        evaluator.rescale_to_next_inplace(cubic);
+        evaluator.multiply_inplace_reduced_error(cubic, squared, relin_keys);
+        evaluator.rescale_to_next_inplace(cubic);
+        if (std::abs(coeff[1]) >= zero)
+        {
+            evaluator.multiply_const(cipher, coeff[1], rtn);
+            evaluator.rescale_to_next_inplace(rtn);
+            evaluator.add_reduced_error(rtn, cubic, rtn);
+        }
+        else
+            rtn = cubic;
+        if (std::abs(coeff[2]) >= zero)
+        {
+            evaluator.multiply_const_inplace(squared, coeff[2]);
+            evaluator.rescale_to_next_inplace(squared);
+            evaluator.add_reduced_error(rtn, squared, rtn);
+        }
+        evaluator.add_const_inplace(rtn, coeff[0]);
+        return;
+    }
+    if (poly_heap.empty()) throw std::logic_error("polynomial heap is not generated");
+
+    // baby steps T_1 .. T_{k-1}: T_2i = 2 T_i^2 - 1, T_i = 2 T_{2^a} T_{i-2^a} - T_{|2^(a+1) - i|}
+    std::vector<Ciphertext> baby(heap_k);
+    std::vector<bool> babybool(heap_k, false);
+    baby[1] = cipher;
+    babybool[1] = true;
+    for (long i = 2; i < heap_k; i *= 2)
+    {
+        evaluator.square(baby[i / 2], baby[i]);
+        evaluator.relinearize_inplace(baby[i], relin_keys);
+        evaluator.rescale_to_next_inplace(baby[i]);
+        evaluator.double_inplace(baby[i]);
+        evaluator.add_const(baby[i], -1.0, baby[i]);
+        babybool[i] = true;
+    }
+    for (long i = 1; i < heap_k; i++)
+    {
+        if (babybool[i]) continue;
+        const long lpow2 = 1L << (int)std::floor(std::log(i) / std::log(2));
+        const long res = i - lpow2, diff = std::labs(lpow2 - res);
+        evaluator.multiply_reduced_error(baby[lpow2], baby[res], relin_keys, baby[i]);
+        evaluator.rescale_to_next_inplace(baby[i]);
+        evaluator.double_inplace(baby[i]);
+        evaluator.sub_reduced_error(baby[i], baby[diff], baby[i]);
+        babybool[i] = true;
+    }
+
+    // giant steps T_k, T_2k, T_4k, ...
+    std::vector<Ciphertext> giant(heap_m);
+    {
+        const long lpow2 = 1L << ((int)std::ceil(std::log(heap_k) / std::log(2)) - 1);
+        const long res = heap_k - lpow2, diff = std::labs(lpow2 - res);
+        if (res == 0)
+            giant[0] = baby[lpow2];
+        else if (diff == 0)
+        {
+            evaluator.square(baby[lpow2], giant[0]);
+            evaluator.relinearize_inplace(giant[0], relin_keys);
+            evaluator.rescale_to_next_inplace(giant[0]);
+            evaluator.double_inplace(giant[0]);
+            evaluator.add_const(giant[0], -1.0, giant[0]);
+        }
+        else
+        {
+            evaluator.multiply_reduced_error(baby[lpow2], baby[res], relin_keys, giant[0]);
+            evaluator.rescale_to_next_inplace(giant[0]);
+            evaluator.double_inplace(giant[0]);
+            evaluator.sub_reduced_error(giant[0], baby[diff], giant[0]);
+        }
+    }
+    for (long i = 1; i < heap_m; i++)
+    {
+        evaluator.square(giant[i - 1], giant[i]);
+        evaluator.relinearize_inplace(giant[i], relin_keys);
+        evaluator.rescale_to_next_inplace(giant[i]);
+        evaluator.double_inplace(giant[i]);
+        evaluator.add_const_inplace(giant[i], -1.0);
+    }
+
+    // leaves: sum_j c_j T_j by multiply_const + rescale
+    std::vector<Ciphertext> cipherheap(heaplen);
+    std::vector<bool> cipherheapbool(heaplen, false);
+    Ciphertext tmp;
+    long heapfirst = (1L << heap_m) - 1, heaplast = (1L << (heap_m + 1)) - 1;
+    for (long i = heapfirst; i < heaplast; i++)
+    {
+        if (!poly_heap[i]) continue;
+        const Polynomial &p = *poly_heap[i];
+        cipherheapbool[i] = true;
+        evaluator.multiply_const(baby[1], p.chebcoeff[1], cipherheap[i]);
+        evaluator.rescale_to_next_inplace(cipherheap[i]);
+        if (!(std::abs(p.chebcoeff[1]) <= zero)) evaluator.add_const_inplace(cipherheap[i], p.chebcoeff[0]);
+        for (long j = 2; j <= p.deg; j++)
+        {
+            if (std::abs(p.chebcoeff[j]) <= zero) continue;
+            evaluator.multiply_const(j < heap_k ? baby[j] : giant[0], p.chebcoeff[j], tmp);
+            evaluator.rescale_to_next_inplace(tmp);
+            evaluator.add_reduced_error(cipherheap[i], tmp, cipherheap[i]);
+        }
+    }
+    // combine: node = quotient * T_{k 2^g} + remainder
+    long depth = heap_m, gindex = 0;
+    while (depth != 0)
+    {
+        depth--;
+        heapfirst = (1L << depth) - 1;
+        heaplast = (1L << (depth + 1)) - 1;
+        for (long i = heapfirst; i < heaplast; i++)
+        {
+            if (!poly_heap[i]) continue;
+            cipherheapbool[i] = true;
+            if (!cipherheapbool[2 * (i + 1) - 1])
+                cipherheap[i] = cipherheap[2 * (i + 1)];
+            else
+            {
+                evaluator.multiply_reduced_error(cipherheap[2 * (i + 1) - 1], giant[gindex], relin_keys,
+                                                 cipherheap[i]);
+                evaluator.rescale_to_next_inplace(cipherheap[i]);
+                evaluator.add_reduced_error(cipherheap[i], cipherheap[2 * (i + 1)], cipherheap[i]);
+            }
+        }
+        gindex++;
+    }
+    rtn = cipherheap[0];
+}
+} // namespace boot
+
+// ===================================================================== coefficient generation
+namespace
+{
+using f128 = __float128;
+
+// least squares  min |A c - b|_2  by Householder QR in binary128 (A: rows x cols, row-major)
+std::vector<f128> lstsq(std::vector<f128> A, std::vector<f128> b, std::size_t rows, std::size_t cols)
+{
+    for (std::size_t k = 0; k < cols; k++)
+    {
+        f128 norm = 0;
+        for (std::size_t i = k; i < rows; i++) norm += A[i * cols + k] * A[i * cols + k];
+        norm = sqrtq(norm);
+        if (norm == 0) continue;
+        const f128 alpha = A[k * cols + k] > 0 ? -norm : norm;
+        std::vector<f128> v(rows - k);
+        for (std::size_t i = k; i < rows; i++) v[i - k] = A[i * cols + k];
+        v[0] -= alpha;
+        f128 vv = 0;
+        for (auto x : v) vv += x * x;
+        if (vv == 0) continue;
+        for (std::size_t j = k; j < cols; j++)
+        {
+            f128 d = 0;
+            for (std::size_t i = k; i < rows; i++) d += v[i - k] * A[i * cols + j];
+            d = 2 * d / vv;
+            for (std::size_t i = k; i < rows; i++) A[i * cols + j] -= d * v[i - k];
+        }
+        f128 d = 0;
+        for (std::size_t i = k; i < rows; i++) d += v[i - k] * b[i];
+        d = 2 * d / vv;
+        for (std::size_t i = k; i < rows; i++) b[i] -= d * v[i - k];
+    }
+    std::vector<f128> c(cols, 0);
+    for (std::size_t k = cols; k-- > 0;)
+    {
+        f128 s = b[k];
+        for (std::size_t j = k + 1; j < cols; j++) s -= A[k * cols + j] * c[j];
+        c[k] = A[k * cols + k] != 0 ? s / A[k * cols + k] : 0;
+    }
+    return c;
+}
+
+void cheb_row(f128 u, std::size_t deg, f128 *row)
+{
+    row[0] = 1;
+    if (deg >= 1) row[1] = u;
+    for (std::size_t j = 2; j <= deg; j++) row[j] = 2 * u * row[j - 1] - row[j - 2];
+}
+
+const f128 kPi = acosq(-1);
+} // namespace
+
+RemezCos::RemezCos(long K, double lw, long d, long sf) : boundary_K(K), deg(d), scale_factor(sf), log_width(lw) {}
+
+static f128 cos_target(f128 x, long scale_factor)
+{
+    // RemezCos.h:11-14
+    if (scale_factor % 2 == 0) return cosq(2 * kPi * (x - (f128)0.25) / scale_factor);
+    return sinq(2 * kPi * x / scale_factor);
+}
+
+void RemezCos::generate_optimal_poly(boot::Polynomial &poly) const
+{
+    // Target set of Remez::initialize (common/Remez.cpp:95-175): the intervals
+    // [i - w, i + w], |i| <= K-1, w = 2^-log_width; basis T_j(x / K).  Least squares on
+    // Chebyshev nodes of every interval, in binary128.
+    const int M = 10;
+    const f128 w = powq(2, -(f128)log_width);
+    std::vector<f128> xs;
+    for (long i = -(boundary_K - 1); i <= boundary_K - 1; i++)
+        for (int j = 0; j < M; j++) xs.push_back((f128)i + w * cosq((2 * j + 1) * kPi / (2 * M)));
+    const std::size_t rows = xs.size(), cols = deg + 1;
+    std::vector<f128> A(rows * cols), b(rows);
+    for (std::size_t r = 0; r < rows; r++)
+    {
+        cheb_row(xs[r] / boundary_K, deg, &A[r * cols]);
+        b[r] = cos_target(xs[r], scale_factor);
+    }
+    auto c = lstsq(std::move(A), std::move(b), rows, cols);
+    std::vector<double> cheb(cols);
+    for (std::size_t j = 0; j < cols; j++) cheb[j] = (double)c[j];
+    poly.set_chebyshev(cheb);
+}
+
+double RemezCos::max_error(const boot::Polynomial &poly) const
+{
+    const double w = std::pow(2.0, -log_width);
+    double err = 0;
+    for (long i = -(boundary_K - 1); i <= boundary_K - 1; i++)
+        for (int j = 0; j <= 64; j++)
+        {
+            const double x = i - w + 2 * w * j / 64.0;
+            err = std::max(err, std::abs(poly.evaluate(x / boundary_K) - (double)cos_target(x, scale_factor)));
+        }
+    return err;
+}
+
+RemezArcsin::RemezArcsin(double lw, long d) : log_width(lw), deg(d) {}
+
+void RemezArcsin::generate_optimal_poly(boot::Polynomial &poly) const
+{
+    // RemezArcsin.h: arcsin(x) / (2 pi) on [-a, a], a = 2^-log_width (boundary_K = 1)
+    const f128 a = powq(2, -(f128)log_width);
+    auto g = [](f128 x) { return asinq(x) / (2 * kPi); };
+    if (deg == 1)
+    {
+        // odd linear minimax c x: equioscillation between x1 (g'(x1) = c) and a:
+        // c x1 - g(x1) = g(a) - c a, solved by bisection on c in [g(a)/a, 1/(2 pi)]... ordered
+        f128 lo = 1 / (2 * kPi), hi = g(a) / a;
+        if (lo > hi) std::swap(lo, hi);
+        for (int it = 0; it < 200; it++)
+        {
+            const f128 c = (lo + hi) / 2;
+            const f128 s = 1 / (2 * kPi * c);
+            const f128 x1 = sqrtq(1 - s * s);
+            const f128 F = c * (x1 + a) - g(x1) - g(a);
+            if (F > 0)
+                hi = c;
+            else
+                lo = c;
+        }
+        const double c1 = (double)((lo + hi) / 2);
+        poly.set_chebyshev({ 0.0, c1 });
+        return;
+    }
+    const int rows = 8 * (int)(deg + 1);
+    const std::size_t cols = deg + 1;
+    std::vector<f128> A(rows * cols), b(rows);
+    for (int r = 0; r < rows; r++)
+    {
+        const f128 x = a * cosq((2 * r + 1) * kPi / (2 * rows));
+        cheb_row(x, deg, &A[r * cols]);
+        b[r] = g(x);
+    }
+    auto c = lstsq(std::move(A), std::move(b), rows, cols);
+    std::vector<double> cheb(cols);
+    for (std::size_t j = 0; j < cols; j++) cheb[j] = (double)c[j];
+    poly.set_chebyshev(cheb);
+}
+
+// =========================================================================== ModularReducer
+ModularReducer::ModularReducer(long K, double lw, long d, long ndf, long ideg, SEALContext &ctx, CKKSEncoder &enc,
+                               Encryptor &encr, Evaluator &ev, RelinKeys &rk, Decryptor &dec)
+    : boundary_K(K), log_width(lw), deg(d), num_double_formula(ndf),
+      inverse_log_width(-std::log2(std::sin(2 * M_PI * std::pow(2.0, -lw)))), inverse_deg(ideg), context(ctx),
+      encoder(enc), encryptor(encr), evaluator(ev), relin_keys(rk), decryptor(dec),
+      poly_generator(K, lw, d, 1L << ndf), inverse_poly_generator(inverse_log_width, ideg)
+{
+    // ModularReducer.cpp:3-20
+}
+
+void ModularReducer::double_angle_formula(Ciphertext &cipher)
+{
+    // ModularReducer.cpp:22-28: cos 2t = 2 cos^2 t - 1
+    evaluator.square_inplace(cipher);
+    evaluator.relinearize_inplace(cipher, relin_keys);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.double_inplace(cipher);
+    evaluator.add_const(cipher, -1.0, cipher);
+}
+
+void ModularReducer::double_angle_formula_scaled(Ciphertext &cipher, double scale_coeff)
+{
+    // ModularReducer.cpp:30-36
+    evaluator.square_inplace(cipher);
+    evaluator.relinearize_inplace(cipher, relin_keys);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.double_inplace(cipher);
+    evaluator.add_const(cipher, -scale_coeff, cipher);
+}
+
+void ModularReducer::generate_sin_cos_polynomial()
+{
+    poly_generator.generate_optimal_poly(sin_cos_polynomial);
+    sin_cos_polynomial.generate_poly_heap();
+}
+
+void ModularReducer::generate_inverse_sine_polynomial()
+{
+    // ModularReducer.cpp:43-53
+    inverse_poly_generator.generate_optimal_poly(inverse_sin_polynomial);
+    if (inverse_deg > 3) inverse_sin_polynomial.generate_poly_heap_odd();
+    if (inverse_deg == 1)
+    {
+        scale_inverse_coeff = inverse_sin_polynomial.coeff[1];
+        for (int i = 0; i < num_double_formula; i++) scale_inverse_coeff = std::sqrt(scale_inverse_coeff);
+        sin_cos_polynomial.constmul(scale_inverse_coeff);
+        sin_cos_polynomial.generate_poly_heap();
+    }
+}
+
+void ModularReducer::write_polynomials()
+{
+    std::ofstream sin_cos_out("cosine.txt"), inverse_out("inverse_sine.txt");
+    sin_cos_polynomial.write_heap_to_file(sin_cos_out);
+    inverse_sin_polynomial.write_heap_to_file(inverse_out);
+}
+
+void ModularReducer::modular_reduction(Ciphertext &rtn, Ciphertext &cipher)
+{
+    // ModularReducer.cpp:62-80
+    Ciphertext tmp1, tmp2;
+    tmp1 = cipher;
+    sin_cos_polynomial.homomorphic_poly_evaluation(context, encoder, encryptor, evaluator, relin_keys, tmp2, tmp1,
+                                                   decryptor);
+    if (inverse_deg == 1)
+    {
+        double curr_scale = scale_inverse_coeff;
+        for (int i = 0; i < num_double_formula; i++)
+        {
+            curr_scale = curr_scale * curr_scale;
+            double_angle_formula_scaled(tmp2, curr_scale);
+        }
+        rtn = tmp2;
+    }
+    else
+    {
+        for (int i = 0; i < num_double_formula; i++) double_angle_formula(tmp2);
+        inverse_sin_polynomial.homomorphic_poly_evaluation(context, encoder, encryptor, evaluator, relin_keys, rtn,
+                                                           tmp2, decryptor);
+    }
+}
+
+// ============================================================================= Bootstrapper
+Bootstrapper::Bootstrapper(long _loge, long _logn, long _logNh, long _L, double _final_scale, long _boundary_K,
+                           long _sin_cos_deg, long _scale_factor, long _inverse_deg, SEALContext &_context,
+                           KeyGenerator &_keygen, CKKSEncoder &_encoder, Encryptor &_encryptor, Decryptor &_decryptor,
+                           Evaluator &_evaluator, RelinKeys &_relin_keys, GaloisKeys &_gal_keys)
+    : loge(_loge), logn(_logn), n(1L << _logn), logNh(_logNh), Nh(1L << _logNh), L(_L), final_scale(_final_scale),
+      boundary_K(_boundary_K), sin_cos_deg(_sin_cos_deg), scale_factor(_scale_factor), inverse_deg(_inverse_deg),
+      context(_context), keygen(_keygen), encoder(_encoder), encryptor(_encryptor), decryptor(_decryptor),
+      evaluator(_evaluator), relin_keys(_relin_keys), gal_keys(_gal_keys)
+{
+    // Bootstrapper.cpp:3-17
+    mod_reducer = std::make_unique<ModularReducer>(boundary_K, (double)loge, sin_cos_deg, scale_factor, inverse_deg,
+                                                   context, encoder, encryptor, evaluator, relin_keys, decryptor);
+}
+
+void Bootstrapper::addLeftRotKeys_Linear_to_vector_3(std::vector<int> &gal_steps_vector)
+{
+    // Bootstrapper.cpp:82-176: the baby and giant steps of the three CoeffToSlot BSGS levels
+    const int div_part1 = (int)std::floor(logn / 3.0);
+    const int div_part2 = (int)std::floor((logn - div_part1) / 2.0);
+    const int div_part3 = (int)logn - div_part1 - div_part2;
+    const int totlen1 = (1 << div_part1) - 1, totlen2 = (1 << div_part2) - 1, totlen3 = (1 << div_part3) - 1;
+    const int basicstep1 = 1 << (logn - div_part1), basicstep2 = 1 << (logn - div_part1 - div_part2),
+              basicstep3 = 1;
+    const int gs1 = giantstep(totlen1 + 1);
+    const int gs1_e = logn != logNh ? giantstep(2 * totlen1 + 1) : 0;
+    const int gs2 = giantstep(2 * totlen2 + 1), gs3 = giantstep(2 * totlen3 + 1);
+    const int basicstart1 = -totlen1 + gs1 * (int)std::floor((totlen1 + 0.0) / (gs1 + 0.0));
+    const int giantfirst1 = -(int)std::floor((totlen1 + 0.0) / (gs1 + 0.0));
+    const int giantlast1 = (int)std::floor((2 * totlen1 + 0.0) / (gs1 + 0.0)) + giantfirst1;
+    const int giantlast1_e = logn != logNh ? (int)std::floor((totlen1 + 0.0) / (gs1 + 0.0)) : 0;
+    const int basicstart2 = -totlen2 + gs2 * (int)std::floor((totlen2 + 0.0) / (gs2 + 0.0));
+    const int giantfirst2 = -(int)std::floor((totlen2 + 0.0) / (gs2 + 0.0));
+    const int giantlast2 = (int)std::floor((2 * totlen2 + 0.0) / (gs2 + 0.0)) + giantfirst2;
+    const int basicstart3 = -totlen3 + gs3 * (int)std::floor((totlen3 + 0.0) / (gs3 + 0.0));
+    const int giantfirst3 = -(int)std::floor((totlen3 + 0.0) / (gs3 + 0.0));
+    const int giantlast3 = (int)std::floor((2 * totlen3 + 0.0) / (gs3 + 0.0)) + giantfirst3;
+    const int nh = (int)Nh;
+    auto add = [&](int st) {
+        if (std::find(gal_steps_vector.begin(), gal_steps_vector.end(), st) == gal_steps_vector.end())
+            gal_steps_vector.push_back(st);
+    };
+    for (int i = basicstart1; i < basicstart1 + gs1; i++)
+        if (i != 0) add((nh + i * basicstep1) % nh);
+    for (int i = 1; i < gs1_e; i++) add(i * basicstep1);
+    for (int i = basicstart2; i < basicstart2 + gs2; i++)
+        if (i != 0) add((nh + i * basicstep2) % nh);
+    for (int i = basicstart3; i < basicstart3 + gs3; i++)
+        if (i != 0) add((nh + i * basicstep3) % nh);
+    for (int i = giantfirst1; i <= giantlast1; i++)
+        if (i != 0) add((nh + i * gs1 * basicstep1) % nh);
+    for (int i = 1; i <= giantlast1_e; i++) add(i * gs1_e * basicstep1);
+    for (int i = giantfirst2; i <= giantlast2; i++)
+        if (i != 0) add((nh + i * gs2 * basicstep2) % nh);
+    for (int i = giantfirst3; i <= giantlast3; i++)
+        if (i != 0) add((nh + i * gs3 * basicstep3) % nh);
+}
+
+void Bootstrapper::addBootKeys_3(GaloisKeys &keys)
+{
+    // Bootstrapper.cpp:367-385
+    std::vector<int> gal_steps_vector{ 0 };
+    for (int i = 0; i < logNh; i++) gal_steps_vector.push_back(1 << i);
+    addLeftRotKeys_Linear_to_vector_3(gal_steps_vector);
+    keygen.create_galois_keys(gal_steps_vector, keys);
+    slot_vec.push_back(logn);
+    change_logn(logn);
+}
+
+void Bootstrapper::change_logn(long new_logn)
+{
+    // Bootstrapper.cpp:499-510
+    logn = new_logn;
+    n = 1L << logn;
+    slot_index = -1;
+    for (std::size_t i = 0; i < slot_vec.size(); i++)
+        if (slot_vec[i] == logn)
+        {
+            slot_index = (long)i;
+            break;
+        }
+    if (slot_index == -1) throw std::logic_error("LT coefficients were not generated for this logn");
+}
+
+namespace
+{
+// A linear map on n-slot vectors as diagonals: out[x] = sum_d D_d[x] * v[(x + d) mod n].
+using Diags = std::map<int, std::vector<cd>>;
+
+// Butterfly stage i of the special FFT without bit reversal (the decoding direction; the
+// stages orig_coeffvec of Bootstrapper.cpp:512-553): blocks of 2^(i+1), twiddle
+// zeta_j = exp(i pi 5^j / 2^(i+2)) for j < 2^i: (a, b) -> (a + zeta b, a - zeta b).
+Diags fft_stage(int logn, int i)
+{
+    const int n = 1 << logn, b = 1 << (i + 1), h = b / 2;
+    Diags D;
+    for (int d : { -h, 0, h }) D[d].assign(n, 0.0);
+    const double theta = M_PI / (2 * n) * (1 << (logn - 1 - i));
+    long power = 1;
+    for (int j = 0; j < h; j++)
+    {
+        const cd zeta = std::polar(1.0, theta * power);
+        for (int k = 0; k < n / b; k++)
+        {
+            const int x = k * b + j;
+            D[0][x] = 1.0;
+            D[h][x] = zeta;
+            D[-h][x + h] = 1.0;
+            D[0][x + h] = -zeta;
+        }
+        power = (5 * power) % (1L << (i + 3));
+    }
+    return D;
+}
+
+// Inverse butterfly stage i (orig_invcoeffvec, Bootstrapper.cpp:555-590): blocks of n / 2^i,
+// (x, y) -> ((x + y) / 2, zeta^-1 (x - y) / 2) -- the inverse of fft_stage(logn - 1 - i).
+Diags ifft_stage(int logn, int i)
+{
+    const int n = 1 << logn, b = n >> i, h = b / 2;
+    Diags D;
+    for (int d : { -h, 0, h }) D[d].assign(n, 0.0);
+    const double theta = -M_PI / (2 * n) * (1 << i);
+    long power = 1;
+    for (int j = 0; j < h; j++)
+    {
+        const cd zeta = std::polar(1.0, theta * power);
+        for (int k = 0; k < n / b; k++)
+        {
+            const int x = k * b + j;
+            D[0][x] = 0.5;
+            D[h][x] = 0.5;
+            D[-h][x + h] = 0.5 * zeta;
+            D[0][x + h] = -0.5 * zeta;
+        }
+        power = (5 * power) % (1L << ((logn - 1 - i) + 3));
+    }
+    return D;
+}
+
+// A o B (B applied first): (A B)_{a+b}[x] = A_a[x] B_b[x + a]
+Diags compose(const Diags &A, const Diags &B, int n)
+{
+    Diags R;
+    for (const auto &a : A)
+        for (const auto &bb : B)
+        {
+            auto &r = R[a.first + bb.first];
+            if (r.empty()) r.assign(n, 0.0);
+            for (int x = 0; x < n; x++) r[x] += a.second[x] * bb.second[((x + a.first) % n + n) % n];
+        }
+    return R;
+}
+
+Diags merge_stages(bool inverse, int logn, int first, int last)
+{
+    const int n = 1 << logn;
+    Diags M = inverse ? ifft_stage(logn, first) : fft_stage(logn, first);
+    for (int s = first + 1; s < last; s++) M = compose(inverse ? ifft_stage(logn, s) : fft_stage(logn, s), M, n);
+    return M;
+}
+
+// BSGS layout: index offset/step + totlen (bsgs_linear_transform), or offset/step mod (totlen+1)
+// (rotated_bsgs_linear_transform, for a level whose offsets wrap around the n-slot period)
+std::vector<std::vector<cd>> layout(const Diags &M, int n, int step, int totlen, bool cyclic)
+{
+    std::vector<std::vector<cd>> out(cyclic ? totlen + 1 : 2 * totlen + 1, std::vector<cd>(n, 0.0));
+    for (const auto &d : M)
+    {
+        if (d.first % step) throw std::logic_error("LT diagonal off the BSGS grid");
+        const int k = d.first / step;
+        const int idx = cyclic ? ((k % (totlen + 1)) + (totlen + 1)) % (totlen + 1) : k + totlen;
+        if (idx < 0 || idx >= (int)out.size()) throw std::logic_error("LT diagonal outside the BSGS range");
+        for (int x = 0; x < n; x++) out[idx][x] += d.second[x];
+    }
+    return out;
+}
+} // namespace
+
+namespace boot
+{
+void lt_coefficients_3(int ln, long logNh, long boundary_K, LTDiags &f1, LTDiags &f2, LTDiags &f3, LTDiags &i1,
+                       LTDiags &i2, LTDiags &i3)
+{
+    // genorigcoeff + genfftcoeff_3 + geninvfftcoeff_3 (Bootstrapper.cpp:512-590, 1116-1908), sparse
+    // slots: three merged groups each way, with the reference's scalings and 2n-slot extensions.
+    const int cn = 1 << ln;
+    if (ln >= logNh) throw std::logic_error("full-slot bootstrapping (logn == logNh) is not supported");
+    const cd I(0, 1);
+    {
+        // SlotToCoeff: stages 0.. in groups of div1 (step 1), div2 (step 2^div1), div3
+        const int d3 = (int)std::floor(ln / 3.0), d2 = (int)std::floor((ln - d3) / 2.0), d1 = ln - d3 - d2;
+        const int t1 = (1 << d1) - 1, t2 = (1 << d2) - 1, t3 = (1 << d3) - 1;
+        f1 = layout(merge_stages(false, ln, 0, d1), cn, 1, t1, false);
+        f2 = layout(merge_stages(false, ln, d1, d1 + d2), cn, 1 << d1, t2, false);
+        f3 = layout(merge_stages(false, ln, d1 + d2, ln), cn, 1 << (d1 + d2), t3, false);
+        for (auto *g : { &f1, &f2 })
+            for (auto &v : *g)
+            {
+                v.resize(2 * cn);
+                for (int j = 0; j < cn; j++) v[j + cn] = v[j];
+            }
+        for (auto &v : f3)
+        {
+            v.resize(2 * cn);
+            for (int j = 0; j < cn; j++) v[j + cn] = I * v[j];
+        }
+    }
+    {
+        // CoeffToSlot: inverse stages in groups of div1 (step 2^(logn-div1), cyclic), div2, div3 (step 1)
+        const int d1 = (int)std::floor(ln / 3.0), d2 = (int)std::floor((ln - d1) / 2.0), d3 = ln - d1 - d2;
+        const int t1 = (1 << d1) - 1, t2 = (1 << d2) - 1, t3 = (1 << d3) - 1;
+        i1 = layout(merge_stages(true, ln, 0, d1), cn, 1 << (ln - d1), t1, true);
+        i2 = layout(merge_stages(true, ln, d1, d1 + d2), cn, 1 << (ln - d1 - d2), t2, false);
+        i3 = layout(merge_stages(true, ln, d1 + d2, ln), cn, 1, t3, false);
+        const double s1 = 1.0 / ((double)boundary_K * (double)(1L << (logNh - ln)));
+        for (auto &v : i1)
+            for (auto &x : v) x *= s1;
+        for (auto &v : i3)
+        {
+            v.resize(2 * cn);
+            for (int j = 0; j < cn; j++)
+            {
+                v[j] *= 0.5;
+                v[j + cn] = -I * v[j];
+            }
+        }
+    }
+}
+} // namespace boot
+
+void Bootstrapper::generate_LT_coefficient_3()
+{
+    const std::size_t U = slot_vec.size();
+    fftcoeff1.assign(U, {});
+    fftcoeff2.assign(U, {});
+    fftcoeff3.assign(U, {});
+    invfftcoeff1.assign(U, {});
+    invfftcoeff2.assign(U, {});
+    invfftcoeff3.assign(U, {});
+    for (std::size_t u = 0; u < U; u++)
+        boot::lt_coefficients_3((int)slot_vec[u], logNh, boundary_K, fftcoeff1[u], fftcoeff2[u], fftcoeff3[u],
+                                invfftcoeff1[u], invfftcoeff2[u], invfftcoeff3[u]);
+}
+
+void Bootstrapper::prepare_mod_polynomial()
+{
+    mod_reducer->generate_sin_cos_polynomial();
+    mod_reducer->generate_inverse_sine_polynomial();
+}
+
+bool Bootstrapper::PtKey::operator<(const PtKey &o) const
+{
+    if (diag != o.diag) return diag < o.diag;
+    if (shift != o.shift) return shift < o.shift;
+    if (limbs != o.limbs) return limbs < o.limbs;
+    if (scale != o.scale) return scale < o.scale;
+    if (coeff_logn != o.coeff_logn) return coeff_logn < o.coeff_logn;
+    return coeff_scale < o.coeff_scale;
+}
+
+namespace
+{
+std::mutex g_pt_mu;
+bool pt_cache_on()
+{
+    const char *e = std::getenv("MHE_BOOT_PT_CACHE");
+    return !(e && e[0] == '0');
+}
+} // namespace
+
+void Bootstrapper::multiply_diag(Ciphertext &ct, const std::vector<cd> &diag, int coeff_logn, int shift,
+                                 Ciphertext &dest, double coeff_scale)
+{
+    // rotation(coeff_logn, Nh, shift, diag) + multiply_vector_reduced_error (Bootstrapper.cpp:1983-1984):
+    // the diagonal is encoded at ct.scale() on the first level and kept at ct's level
+    const PtKey key{ &diag, shift, ct.coeff_modulus_size(), ct.scale(), coeff_scale, coeff_logn };
+    const Plaintext *pt = nullptr;
+    Plaintext local;
+    if (pt_cache_on())
+    {
+        std::lock_guard<std::mutex> lk(g_pt_mu);
+        auto it = pt_cache_.find(key);
+        if (it != pt_cache_.end()) pt = &it->second;
+    }
+    if (!pt)
+    {
+        std::vector<cd> rc;
+        rotation(coeff_logn, (int)Nh, shift, diag, rc);
+        if (coeff_scale != 1.0)
+            for (auto &x : rc) x *= coeff_scale;
+        evaluator.encode_vector_for(ct, rc, local);
+        if (pt_cache_on())
+        {
+            std::lock_guard<std::mutex> lk(g_pt_mu);
+            pt = &pt_cache_.emplace(key, std::move(local)).first->second;
+        }
+        else
+            pt = &local;
+    }
+    evaluator.multiply_plain(ct, *pt, dest);
+}
+
+std::size_t Bootstrapper::verify_cache()
+{
+    // re-encode every cached diagonal and compare (debugging aid; synchronises)
+    std::lock_guard<std::mutex> lk(g_pt_mu);
+    std::size_t bad_entries = 0;
+    for (const auto &kv : pt_cache_)
+    {
+        const PtKey &k = kv.first;
+        auto cdp = context.first_context_data();
+        while (cdp && cdp->parms().coeff_modulus().size() != k.limbs) cdp = cdp->next_context_data();
+        if (!cdp) continue;
+        Ciphertext dummy(context, cdp->parms_id());
+        dummy.resize(context, cdp->parms_id(), 2);
+        dummy.scale() = k.scale;
+        std::vector<cd> rc;
+        rotation(k.coeff_logn, (int)Nh, k.shift, *static_cast<const std::vector<cd> *>(k.diag), rc);
+        if (k.coeff_scale != 1.0)
+            for (auto &x : rc) x *= k.coeff_scale;
+        Plaintext fresh;
+        evaluator.encode_vector_for(dummy, rc, fresh);
+        const std::uint64_t *a = fresh.store().host(), *b = kv.second.store().host();
+        std::size_t bad = 0;
+        for (std::size_t i = 0; i < fresh.store().words(); i++) bad += a[i] != b[i];
+        if (bad)
+        {
+            bad_entries++;
+            std::fprintf(stderr, "pt cache entry corrupt: diag %p shift %d limbs %zu scale 2^%.3f logn %d: %zu words\n",
+                         k.diag, k.shift, k.limbs, std::log2(k.scale), k.coeff_logn, bad);
+        }
+    }
+    std::fprintf(stderr, "pt cache check: %zu entries, %zu corrupt\n", pt_cache_.size(), bad_entries);
+    return bad_entries;
+}
+
+void Bootstrapper::bsgs_linear_transform(Ciphertext &rtncipher, Ciphertext &cipher, int totlen, int basicstep,
+                                         int coeff_logn, const std::vector<std::vector<cd>> &fftcoeff,
+                                         double coeff_scale)
+{
+    // Bootstrapper.cpp:1952-2016 (coeff_scale: sfl_half_3's fftcoeff3_scale factor)
+    const int gs1 = giantstep(2 * totlen + 1);
+    const int basicstart1 = -totlen + gs1 * (int)std::floor((totlen + 0.0) / (gs1 + 0.0));
+    const int giantfirst1 = -(int)std::floor((totlen + 0.0) / (gs1 + 0.0));
+    const int giantlast1 = (int)std::floor((2 * totlen + 0.0) / (gs1 + 0.0)) + giantfirst1;
+    const int nh = (int)Nh;
+    std::vector<Ciphertext> babyct(gs1);
+    Ciphertext giantct, tmpct, tmptmpct;
+    bool tmpctbool = false;
+    for (int i = basicstart1; i < basicstart1 + gs1; i++)
+    {
+        if (i == 0)
+            babyct[i - basicstart1] = cipher;
+        else
+            evaluator.rotate_vector(cipher, (nh + i * basicstep) % nh, gal_keys, babyct[i - basicstart1]);
+    }
+    for (int i = giantfirst1; i <= giantlast1; i++)
+    {
+        bool giantbool = false;
+        const int jlast = i != giantlast1 ? basicstart1 + gs1 - 1 : totlen - i * gs1;
+        for (int j = basicstart1; j <= jlast; j++)
+        {
+            multiply_diag(babyct[j - basicstart1], fftcoeff[(i * gs1 + j) + totlen], coeff_logn,
+                          (-i) * gs1 * basicstep, tmptmpct, coeff_scale);
+            if (!giantbool)
+            {
+                giantct = tmptmpct;
+                giantbool = true;
+            }
+            else
+                evaluator.add_inplace_reduced_error(giantct, tmptmpct);
+        }
+        if (i != 0)
+        {
+            evaluator.rotate_vector(giantct, (nh + i * gs1 * basicstep) % nh, gal_keys, tmptmpct);
+            if (!tmpctbool)
+            {
+                tmpct = tmptmpct;
+                tmpctbool = true;
+            }
+            else
+                evaluator.add_inplace_reduced_error(tmpct, tmptmpct);
+        }
+        else
+        {
+            if (!tmpctbool)
+            {
+                tmpct = giantct;
+                tmpctbool = true;
+            }
+            else
+                evaluator.add_inplace_reduced_error(tmpct, giantct);
+        }
+    }
+    rtncipher = tmpct;
+}
+
+void Bootstrapper::rotated_bsgs_linear_transform(Ciphertext &rtncipher, Ciphertext &cipher, int totlen,
+                                                 int basicstep, int coeff_logn,
+                                                 const std::vector<std::vector<cd>> &fftcoeff, double coeff_scale)
+{
+    // Bootstrapper.cpp:2018-2085
+    const int gs2 = giantstep(totlen + 1);
+    const int giantlast2 = (int)std::floor((totlen + 0.0) / (gs2 + 0.0));
+    const int nh = (int)Nh;
+    std::vector<Ciphertext> babyct(gs2);
+    Ciphertext giantct, tmpct, tmptmpct;
+    bool tmpctbool = false;
+    for (int i = 0; i < gs2; i++)
+    {
+        if (i == 0)
+            babyct[i] = cipher;
+        else
+            evaluator.rotate_vector(cipher, (nh + i * basicstep) % nh, gal_keys, babyct[i]);
+    }
+    for (int i = 0; i <= giantlast2; i++)
+    {
+        bool giantbool = false;
+        const int jlast = i != giantlast2 ? gs2 - 1 : totlen - i * gs2;
+        for (int j = 0; j <= jlast; j++)
+        {
+            multiply_diag(babyct[j], fftcoeff[i * gs2 + j], coeff_logn, (-i) * gs2 * basicstep, tmptmpct,
+                          coeff_scale);
+            if (!giantbool)
+            {
+                giantct = tmptmpct;
+                giantbool = true;
+            }
+            else
+                evaluator.add_inplace_reduced_error(giantct, tmptmpct);
+        }
+        if (i != 0)
+        {
+            evaluator.rotate_vector(giantct, (nh + i * gs2 * basicstep) % nh, gal_keys, tmptmpct);
+            if (!tmpctbool)
+            {
+                tmpct = tmptmpct;
+                tmpctbool = true;
+            }
+            else
+                evaluator.add_inplace_reduced_error(tmpct, tmptmpct);
+        }
+        else
+        {
+            if (!tmpctbool)
+            {
+                tmpct = giantct;
+                tmpctbool = true;
+            }
+            else
+                evaluator.add_inplace_reduced_error(tmpct, giantct);
+        }
+    }
+    rtncipher = tmpct;
+}
+
+void Bootstrapper::sfl_half_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:2453-2490
+    const int div_part3 = (int)std::floor(logn / 3.0);
+    const int div_part2 = (int)std::floor((logn - div_part3) / 2.0);
+    const int div_part1 = (int)logn - div_part3 - div_part2;
+    const int totlen1 = (1 << div_part1) - 1, totlen2 = (1 << div_part2) - 1, totlen3 = (1 << div_part3) - 1;
+    const int basicstep1 = 1, basicstep2 = 1 << div_part1, basicstep3 = 1 << (div_part1 + div_part2);
+
+    Ciphertext tmpct;
+    bsgs_linear_transform(tmpct, cipher, totlen1, basicstep1, (int)logn + 1, fftcoeff1[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct);
+    Ciphertext tmpct2;
+    bsgs_linear_transform(tmpct2, tmpct, totlen2, basicstep2, (int)logn + 1, fftcoeff2[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct2);
+
+    const auto &modulus = context.first_context_data()->parms().coeff_modulus();
+    const auto curr_level = context.get_context_data(tmpct2.parms_id())->chain_index();
+    const double mod_zero = (double)modulus[0].value();
+    const double curr_mod = (double)modulus[curr_level].value();
+    // fftcoeff3_scale = fftcoeff3 * curr_mod * q0 * final_scale / (2 s^2 initial_scale)
+    const double coeff_scale =
+        curr_mod * mod_zero * final_scale / (2 * tmpct2.scale() * tmpct2.scale() * initial_scale);
+    bsgs_linear_transform(rtncipher, tmpct2, totlen3, basicstep3, (int)logn + 1, fftcoeff3[slot_index],
+                          coeff_scale);
+    evaluator.rescale_to_next_inplace(rtncipher);
+}
+
+void Bootstrapper::sflinv_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:2531-2552
+    const int div_part1 = (int)std::floor(logn / 3.0);
+    const int div_part2 = (int)std::floor((logn - div_part1) / 2.0);
+    const int div_part3 = (int)logn - div_part1 - div_part2;
+    const int totlen1 = (1 << div_part1) - 1, totlen2 = (1 << div_part2) - 1, totlen3 = (1 << div_part3) - 1;
+    const int basicstep1 = 1 << (logn - div_part1), basicstep2 = 1 << (logn - div_part1 - div_part2),
+              basicstep3 = 1;
+
+    Ciphertext tmpct;
+    rotated_bsgs_linear_transform(tmpct, cipher, totlen1, basicstep1, (int)logn, invfftcoeff1[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct);
+    Ciphertext tmpct2;
+    bsgs_linear_transform(tmpct2, tmpct, totlen2, basicstep2, (int)logn, invfftcoeff2[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct2);
+    bsgs_linear_transform(rtncipher, tmpct2, totlen3, basicstep3, (int)logn + 1, invfftcoeff3[slot_index]);
+    evaluator.rescale_to_next_inplace(rtncipher);
+}
+
+void Bootstrapper::coefftoslot_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:2675-2680
+    Ciphertext tmpct1, tmpct2;
+    sflinv_3(tmpct1, cipher);
+    evaluator.complex_conjugate(tmpct1, gal_keys, tmpct2);
+    evaluator.add_reduced_error(tmpct1, tmpct2, rtncipher);
+}
+
+void Bootstrapper::slottocoeff_half_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:2689-2694
+    Ciphertext tmpct1, tmpct2;
+    sfl_half_3(tmpct1, cipher);
+    evaluator.rotate_vector(tmpct1, (int)n, gal_keys, tmpct2);
+    evaluator.add_reduced_error(tmpct1, tmpct2, rtncipher);
+}
+
+void Bootstrapper::modraise_inplace(Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:2894-2948; the centered lift runs on the GPU (mhe_modraise)
+    if (cipher.size() != 2) throw std::invalid_argument("Ciphertexts of size 2 are supported only!");
+    if (cipher.coeff_modulus_size() != 1)
+        throw std::invalid_argument("Ciphertexts in the lowest level are supported only!");
+    if (cipher.is_ntt_form()) evaluator.transform_from_ntt_inplace(cipher);
+    Ciphertext encrypted_copy(cipher);
+    cipher.resize(context, context.first_parms_id(), 2);
+    const std::size_t limbs = cipher.coeff_modulus_size();
+    void *s = context.stream();
+    const std::uint64_t *src = encrypted_copy.store().dev_read(s);
+    std::uint64_t *dst = cipher.store().dev_write(s, true);
+    if (mhe_modraise(context.engine(), src, dst, 2, (int)limbs, s) != MHE_OK) throw std::runtime_error(mhe_last_error());
+    cipher.is_ntt_form() = false;
+    evaluator.transform_to_ntt_inplace(cipher);
+}
+
+void Bootstrapper::bootstrap_sparse_real_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:3166-3236
+    modraise_inplace(cipher);
+    const auto &modulus = context.first_context_data()->parms().coeff_modulus();
+    cipher.scale() = (double)modulus[0].value();
+
+    Ciphertext rot;
+    for (long i = logn; i < logNh; ++i)
+    {
+        evaluator.rotate_vector(cipher, (int)(1L << i), gal_keys, rot);
+        evaluator.add_inplace(cipher, rot);
+    }
+
+    Ciphertext rtn;
+    if (logn == 0)
+    {
+        std::vector<cd> cts_vec(Nh, 0.0);
+        for (long i = 0; i < Nh; i++)
+            cts_vec[i] = i % 2 == 0 ? cd(1.0 / (2.0 * boundary_K * (1L << logNh)))
+                                    : -cd(0, 1.0) / (2.0 * boundary_K * (1L << logNh));
+        evaluator.multiply_vector_reduced_error(cipher, cts_vec, rtn);
+        evaluator.rescale_to_next_inplace(rtn);
+        Ciphertext conjrtn;
+        evaluator.complex_conjugate(rtn, gal_keys, conjrtn);
+        evaluator.add_inplace_reduced_error(rtn, conjrtn);
+    }
+    else
+        coefftoslot_3(rtn, cipher);
+
+    Ciphertext modrtn;
+    mod_reducer->modular_reduction(modrtn, rtn);
+
+    if (logn == 0)
+    {
+        const auto curr_level = context.get_context_data(modrtn.parms_id())->chain_index();
+        const double mod_zero = (double)modulus[0].value(), curr_mod = (double)modulus[curr_level].value();
+        const double scale_adj = curr_mod * mod_zero * final_scale / (modrtn.scale() * modrtn.scale() * initial_scale);
+        std::vector<cd> stc_vec(Nh, 0.0);
+        for (long i = 0; i < Nh; i++) stc_vec[i] = i % 2 == 0 ? cd(scale_adj) : cd(0, 1.0) * scale_adj;
+        evaluator.multiply_vector_reduced_error(modrtn, stc_vec, rtncipher);
+        evaluator.rescale_to_next_inplace(rtncipher);
+        Ciphertext rotrtncipher;
+        evaluator.rotate_vector(rtncipher, 1, gal_keys, rotrtncipher);
+        evaluator.add_inplace_reduced_error(rtncipher, rotrtncipher);
+    }
+    else
+        slottocoeff_half_3(rtncipher, modrtn);
+
+    if (const char *v = std::getenv("MHE_BOOT_PT_CHECK"); v && v[0] == '1') verify_cache();
+    rtncipher.scale() = final_scale;
+    Ciphertext conjct;
+    evaluator.complex_conjugate(rtncipher, gal_keys, conjct);
+    evaluator.add_inplace_reduced_error(rtncipher, conjct);
+}
+
+void Bootstrapper::bootstrap_real_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:3421-3425
+    initial_scale = cipher.scale();
+    if (logn == logNh) throw std::logic_error("full-slot bootstrapping (logn == logNh) is not supported");
+    bootstrap_sparse_real_3(rtncipher, cipher);
+}
+
+void Bootstrapper::bootstrap_inplace_real_3(Ciphertext &cipher)
+{
+    Ciphertext rtncipher;
+    bootstrap_real_3(rtncipher, cipher);
+    cipher = rtncipher;
+}

@@ -613,13 +613,6 @@ void Plaintext::set_level(const SEALContext &ctx, const parms_id_type &id, std::
     limbs_ = limbs;
 }
 
-const PolyStore &KSwitchKeys::key(std::size_t i) const
-{
-    auto it = keys_.find(i);
-    if (it == keys_.end()) throw std::out_of_range("kswitch_keys_index");
-    return it->second;
-}
-
 // ------------------------------------------------------------------------------ KeyGenerator
 // keygenerator.cpp: secret key (sparse ternary with the modified hamming weight, else ternary)
 // in NTT form at the key level; public key and key-switching keys are symmetric encryptions of
@@ -668,7 +661,129 @@ void encrypt_zero_symmetric(const SEALContext &ctx, std::mt19937_64 &g, const st
     chk(mhe_multiply_plain(eng, c1, sk, t.p, 1, (int)limbs, s));
     chk(mhe_sub(eng, c0, t.p, c0, 1, (int)limbs, s));
 }
+
+// generate_one_kswitch_key (keygenerator.cpp:384-414) truncated to `digits` digits: digit j is an
+// encryption of zero over the key level with (P mod q_j) * new_key added to limb j of c0; the
+// stored key keeps primes q_0..q_{digits-1} and P ([digits][2][digits+1][n]).  digits = K-1 is
+// SEAL's full key.
+void make_kswitch_key(const SEALContext &ctx, std::mt19937_64 &g, const std::uint64_t *sk, const std::uint64_t *new_key,
+                      std::size_t digits, PolyStore &dest)
+{
+    const std::size_t K = ctx.key_size(), n = ctx.key_context_data()->parms().poly_modulus_degree();
+    const auto &cm = ctx.key_context_data()->parms().coeff_modulus();
+    if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
+    if (digits < 1 || digits > K - 1) throw std::invalid_argument("key digits out of range");
+    mhe_ctx *eng = ctx.engine();
+    void *s = ctx.stream();
+    const std::size_t KL = digits + 1; // stored limbs
+    dest.bind(ctx);
+    dest.resize_words(digits * 2 * KL * n, false);
+    std::uint64_t *d = dest.dev_write(s, true);
+    DevBuf t(eng, s, K * n);
+    const bool full = KL == K;
+    DevBuf tmp(eng, s, full ? 1 : 2 * K * n);
+    const std::uint64_t P = cm[K - 1].value();
+    for (std::size_t j = 0; j < digits; j++)
+    {
+        std::uint64_t *c0 = full ? d + j * 2 * K * n : tmp.p, *c1 = c0 + K * n;
+        encrypt_zero_symmetric(ctx, g, sk, K, c0, c1, s);
+        std::vector<std::uint64_t> f(K, 0);
+        f[j] = P % cm[j].value();
+        chk(mhe_multiply_scalar(eng, new_key, f.data(), t.p, 1, (int)K, s));
+        chk(mhe_add(eng, c0, t.p, c0, 1, (int)K, s));
+        if (!full)
+            for (int c = 0; c < 2; c++)
+            {
+                const std::uint64_t *src = tmp.p + c * K * n;
+                std::uint64_t *dst = d + (j * 2 + c) * KL * n;
+                chk(mhe_memcpy_d2d(eng, dst, src, digits * n * 8, s));
+                chk(mhe_memcpy_d2d(eng, dst + digits * n, src + (K - 1) * n, n * 8, s));
+            }
+    }
+}
 } // namespace
+
+// Deferred Galois keys (see seal.h): the secret key, and per key index its Galois element and seed.
+struct KeyMaker
+{
+    std::mutex mu;
+    SEALContext ctx;
+    PolyStore sk; // NTT form over the key level
+    std::map<std::size_t, std::pair<std::uint32_t, std::uint64_t>> elts;
+    explicit KeyMaker(const SEALContext &c) : ctx(c) {}
+};
+
+std::size_t KSwitchKeys::size() const
+{
+    if (!maker_) return keys_.size();
+    std::lock_guard<std::mutex> lk(maker_->mu);
+    std::size_t c = maker_->elts.size();
+    for (const auto &kv : keys_)
+        if (!maker_->elts.count(kv.first)) c++;
+    return c;
+}
+
+bool KSwitchKeys::has_index(std::size_t i) const
+{
+    if (maker_)
+    {
+        std::lock_guard<std::mutex> lk(maker_->mu);
+        if (maker_->elts.count(i)) return true;
+    }
+    return keys_.count(i) != 0;
+}
+
+const PolyStore &KSwitchKeys::key(std::size_t i) const
+{
+    auto it = keys_.find(i);
+    if (it == keys_.end()) throw std::out_of_range("kswitch_keys_index");
+    return it->second;
+}
+
+const std::uint64_t *KSwitchKeys::key_for(std::size_t i, std::size_t L, void *stream, std::size_t &key_limbs) const
+{
+    if (maker_)
+    {
+        std::lock_guard<std::mutex> lk(maker_->mu);
+        auto e = maker_->elts.find(i);
+        if (e != maker_->elts.end())
+        {
+            auto lt = limbs_of_.find(i);
+            if (lt == limbs_of_.end() || lt->second < L + 1)
+            {
+                // materialise (or grow) the level-truncated key on the maker's context stream
+                const SEALContext &ctx = maker_->ctx;
+                const std::size_t K = ctx.key_size();
+                const std::size_t digits = std::min(K - 1, std::max<std::size_t>(L, 1));
+                void *s = ctx.stream();
+                const std::size_t n = ctx.key_context_data()->parms().poly_modulus_degree();
+                DevBuf rot(ctx.engine(), s, K * n);
+                const std::uint64_t *sk = maker_->sk.dev_read(s);
+                chk(mhe_permute_galois(ctx.engine(), sk, e->second.first, rot.p, 1, (int)K, s));
+                std::mt19937_64 g(e->second.second ^ (0x9e3779b97f4a7c15ULL * digits));
+                PolyStore fresh;
+                make_kswitch_key(ctx, g, sk, rot.p, digits, fresh);
+                auto kt = keys_.find(i);
+                if (kt != keys_.end()) retired_.push_back(std::move(kt->second));
+                keys_[i] = std::move(fresh);
+                limbs_of_[i] = digits + 1;
+            }
+            key_limbs = limbs_of_[i];
+            return keys_.find(i)->second.dev_read(stream);
+        }
+    }
+    key_limbs = key_limbs_;
+    return key(i).dev_read(stream);
+}
+
+std::size_t KSwitchKeys::device_bytes() const
+{
+    std::size_t b = 0;
+    for (const auto &kv : keys_) b += kv.second.words() * 8;
+    for (const auto &r : retired_) b += r.words() * 8;
+    return b;
+}
+
 
 KeyGenerator::KeyGenerator(const SEALContext &context) : ctx_(context)
 {
@@ -714,25 +829,7 @@ PublicKey KeyGenerator::create_public_key()
 
 void KeyGenerator::kswitch_key(const std::uint64_t *new_key, PolyStore &dest)
 {
-    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
-    const auto &cm = ctx_.key_context_data()->parms().coeff_modulus();
-    if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
-    void *s = ctx_.stream();
-    dest.bind(ctx_);
-    dest.resize_words((K - 1) * 2 * K * n, false);
-    std::uint64_t *d = dest.dev_write(s, true);
-    const std::uint64_t *sk = sk_.data().store().dev_read(s);
-    DevBuf t(ctx_.engine(), s, K * n);
-    const std::uint64_t P = cm[K - 1].value();
-    for (std::size_t j = 0; j + 1 < K; j++)
-    {
-        std::uint64_t *c0 = d + j * 2 * K * n, *c1 = c0 + K * n;
-        encrypt_zero_symmetric(ctx_, *rng_, sk, K, c0, c1, s);
-        std::vector<std::uint64_t> f(K, 0);
-        f[j] = P % cm[j].value();
-        chk(mhe_multiply_scalar(ctx_.engine(), new_key, f.data(), t.p, 1, (int)K, s));
-        chk(mhe_add(ctx_.engine(), c0, t.p, c0, 1, (int)K, s));
-    }
+    make_kswitch_key(ctx_, *rng_, sk_.data().store().dev_read(ctx_.stream()), new_key, ctx_.key_size() - 1, dest);
 }
 
 void KeyGenerator::create_relin_keys(RelinKeys &destination)
@@ -751,6 +848,31 @@ void KeyGenerator::create_galois_keys_from_elts(const std::vector<std::uint32_t>
 {
     const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
     void *s = ctx_.stream();
+    // Deferred by default (seal.h, KSwitchKeys); MHE_EAGER_GALOIS=1 builds SEAL's full keys now.
+    const char *eager_env = std::getenv("MHE_EAGER_GALOIS");
+    const bool eager = eager_env && eager_env[0] == '1';
+    if (!eager)
+    {
+        if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
+        auto maker = destination.maker();
+        if (!maker)
+        {
+            maker = std::make_shared<KeyMaker>(ctx_);
+            maker->sk = sk_.data().store();
+            destination.set_maker(maker);
+        }
+        std::lock_guard<std::mutex> lk(maker->mu);
+        for (std::uint32_t elt : elts)
+        {
+            if (!(elt & 1) || elt >= 2 * n) throw std::invalid_argument("Galois element is not valid");
+            const std::size_t idx = GaloisKeys::get_index(elt);
+            const std::uint64_t seed = (*rng_)();
+            if (!maker->elts.count(idx)) maker->elts[idx] = { elt, seed };
+        }
+        destination.parms_id() = ctx_.key_parms_id();
+        destination.set_key_limbs(K);
+        return;
+    }
     DevBuf rot(ctx_.engine(), s, K * n);
     for (std::uint32_t elt : elts)
     {
@@ -1252,9 +1374,10 @@ void Evaluator::switch_key(Ciphertext &encrypted, const std::uint64_t *target, c
     // switch_key_inplace (evaluator.cpp:2281-2525): ct[0..1] += KS(target)
     const std::size_t L = encrypted.coeff_modulus_size();
     void *s = context_.stream();
-    const std::uint64_t *key = keys.key(index).dev_read(s);
+    std::size_t kl = 0;
+    const std::uint64_t *key = keys.key_for(index, L, s, kl);
     std::uint64_t *ct = encrypted.store().dev_write(s);
-    chk(mhe_switch_key(context_.engine(), ct, target, key, (int)keys.key_limbs(), (int)L, s));
+    chk(mhe_switch_key(context_.engine(), ct, target, key, (int)kl, (int)L, s));
 }
 
 void Evaluator::relinearize_inplace(Ciphertext &encrypted, const RelinKeys &relin_keys, MemoryPoolHandle) const
@@ -1268,9 +1391,10 @@ void Evaluator::relinearize_inplace(Ciphertext &encrypted, const RelinKeys &reli
     std::size_t size = encrypted.size();
     if (size == 3)
     {
-        const std::uint64_t *key = relin_keys.key(RelinKeys::get_index(2)).dev_read(s);
+        std::size_t kl = 0;
+        const std::uint64_t *key = relin_keys.key_for(RelinKeys::get_index(2), lv.L, s, kl);
         std::uint64_t *ct = encrypted.store().dev_write(s);
-        chk(mhe_relinearize(context_.engine(), ct, key, (int)relin_keys.key_limbs(), (int)lv.L, s));
+        chk(mhe_relinearize(context_.engine(), ct, key, (int)kl, (int)lv.L, s));
         size = 2;
     }
     while (size > 2)
@@ -1519,9 +1643,9 @@ void Evaluator::apply_galois_inplace(Ciphertext &encrypted, std::uint32_t galois
     if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
     if (!galois_keys.has_key(galois_elt)) throw std::invalid_argument("Galois key not present");
     void *s = context_.stream();
-    const std::uint64_t *key = galois_keys.key(GaloisKeys::get_index(galois_elt)).dev_read(s);
-    chk(mhe_apply_galois(context_.engine(), encrypted.store().dev_write(s), galois_elt, key,
-                         (int)galois_keys.key_limbs(), (int)lv.L, s));
+    std::size_t kl = 0;
+    const std::uint64_t *key = galois_keys.key_for(GaloisKeys::get_index(galois_elt), lv.L, s, kl);
+    chk(mhe_apply_galois(context_.engine(), encrypted.store().dev_write(s), galois_elt, key, (int)kl, (int)lv.L, s));
 }
 
 void Evaluator::rotate_internal(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys) const
@@ -1653,19 +1777,33 @@ template <typename T>
 void Evaluator::multiply_vector_inplace(Ciphertext &encrypted, const std::vector<T> &value) const
 {
     // evaluator.cpp:303-310: encode at the first level, mod_switch_to, multiply_plain
+    Plaintext plain;
+    encode_vector_for(encrypted, value, plain);
+    multiply_plain_inplace(encrypted, plain);
+}
+
+template <typename T>
+void Evaluator::encode_vector_for(const Ciphertext &encrypted, const std::vector<T> &value, Plaintext &plain) const
+{
+    // CKKSEncoder::encode(value, encrypted.scale()) at the first level, then mod_switch_to the
+    // ciphertext's level: only the kept limbs are produced (SEAL's bounds are checked at the
+    // first level)
     Level lv = check_ct(context_, encrypted, "encrypted");
     const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
     if (value.size() > lv.n / 2) throw std::invalid_argument("values_size is too large");
     std::vector<double> re, im;
     split<T>(value, re, im);
     void *s = context_.stream();
-    Plaintext plain;
     plain.set_level(context_, encrypted.parms_id(), lv.L);
     plain.scale() = encrypted.scale();
     chk(mhe_ckks_encode_at(context_.engine(), encoder_.handle(), re.data(), im.empty() ? nullptr : im.data(),
                            re.size(), encrypted.scale(), (int)L1, (int)lv.L, plain.store().dev_write(s, true), s));
-    multiply_plain_inplace(encrypted, plain);
 }
+
+template void Evaluator::encode_vector_for<double>(const Ciphertext &, const std::vector<double> &, Plaintext &) const;
+template void Evaluator::encode_vector_for<std::complex<double>>(const Ciphertext &,
+                                                                 const std::vector<std::complex<double>> &,
+                                                                 Plaintext &) const;
 
 template void Evaluator::multiply_vector_inplace<double>(Ciphertext &, const std::vector<double> &) const;
 template void Evaluator::multiply_vector_inplace<std::complex<double>>(

@@ -142,6 +142,10 @@ int mhe_rescale_to_next(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int siz
 /* Evaluator::mod_switch_drop_to_next (evaluator.cpp:1183-1281): in[size][L][n] ->
  * out[size][L-1][n] (limb copy; out may equal in for an in-place compaction). */
 int mhe_mod_switch_drop(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int size, int limbs, void *stream);
+/* Bootstrapper::modraise_inplace (cnn_ckks/cpu-ckks/single-key/ckks_bootstrapping/Bootstrapper.cpp:
+ * 2894-2948): in[size][1][n] in COEFFICIENT form mod q_0 -> out[size][limbs][n] coefficient form,
+ * the centered lift of each coefficient reduced mod q_0..q_{limbs-1} (out must not alias in). */
+int mhe_modraise(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int size, int limbs, void *stream);
 /* One HMult: multiply + relinearize + rescale_to_next:
  * a, b: [2][L][n] -> out: [2][L-1][n]. */
 int mhe_hmult(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, const uint64_t *relin_key, int key_limbs,

@@ -245,6 +245,25 @@ class Context:
         lib().or_ctx_multiply_plain(self._h, _p(ct), _p(np.ascontiguousarray(pt, np.uint64)), size, L)
         return ct
 
+    def modraise(self, ct1, L):
+        """Bootstrapper::modraise_inplace lift (ckks_bootstrapping/Bootstrapper.cpp:2929-2945):
+        poly_dest[i] = x % q; if x > q0/2: += q - q0 % q, conditional subtract.  ct1 is the
+        coefficient-form [size][1][n] polynomial mod q0; returns [size][L][n] (coefficient form)."""
+        import numpy as np
+
+        q0 = int(self.moduli[0])
+        x = np.asarray(ct1[:, 0, :], dtype=np.uint64)
+        out = np.empty((x.shape[0], L, x.shape[1]), dtype=np.uint64)
+        hi = x > np.uint64(q0 >> 1)
+        for j in range(L):
+            q = int(self.moduli[j])
+            v = x % np.uint64(q)
+            mq0 = np.uint64(q - q0 % q)
+            w = v + mq0
+            w = np.where(w >= np.uint64(q), w - np.uint64(q), w)
+            out[:, j, :] = np.where(hi, w, v)
+        return out
+
     def hmult(self, a, b, key):
         L = a.shape[1]
         out = np.empty((2, L - 1, self.n), np.uint64)

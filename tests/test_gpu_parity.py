@@ -243,6 +243,18 @@ def test_mod_switch_drop_to_next(small):
         assert np.array_equal(flat, ct[:, :6])
 
 
+@pytest.mark.parametrize("L", [1, 3, 8])
+def test_modraise(small, L):
+    """Bootstrapper::modraise_inplace lift (Bootstrapper.cpp:2894-2948): centered lift of a q_0
+    polynomial to L primes; edge coefficients 0, q0/2, q0/2+1, q0-1 included."""
+    ch = small
+    q0 = ch.moduli[0]
+    x = ch.rand(2, 1, ch.n)
+    x[0, 0, :4] = [0, q0 >> 1, (q0 >> 1) + 1, q0 - 1]
+    got = ch.down(ch.eng.modraise(ch.up(x), L))
+    assert np.array_equal(got, ch.oc.modraise(x, L))
+
+
 def test_hmult_small(small):
     ch = small
     L = ch.K - 1

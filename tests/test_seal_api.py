@@ -54,6 +54,28 @@ def test_approx_relu_end_to_end():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_bootstrapping_host_math():
+    """CPU: merged CoeffToSlot/SlotToCoeff diagonals vs the sparse canonical embedding, cosine fit
+    error on the union of intervals, Chebyshev heap identities (tests/cpp/boot_host_test.cpp)."""
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "boot_host_test")], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_bootstrapping_end_to_end():
+    """CKKS bootstrapping (include/mhe_boot.h, ckks_bootstrapping/Bootstrapper.cpp semantics) in the
+    reference ResNet setting: N=2^16, 31 data limbs, logn 14 sparse slots, 1 limb -> refreshed;
+    decrypted output within 1e-3 of the message (tests/cpp/boot_test.cpp)."""
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "boot_test"), "14", "2"], capture_output=True, text=True,
+                       timeout=900)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 @pytest.mark.gpu
 def test_seal_api_end_to_end():
     _build()
