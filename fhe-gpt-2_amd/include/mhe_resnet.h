@@ -1,0 +1,66 @@
+// mhe_resnet.h -- encrypted ResNet-20/32/44/56/110 CIFAR-10 inference of the reference
+// (cnn_ckks/cpu-ckks/single-key/cnn/infer_seal.cpp: import_parameters_cifar10 :3-100,
+// ResNet_cifar10_seal_sparse :234-577) over the MI355X seal:: surface, with the multiplexed
+// layers of mhe_cnn.h, the approximate ReLU of mhe_comp.h and the bootstrapping of mhe_boot.h.
+//
+// ResNetRunner is the one-time setup of ResNet_cifar10_seal_sparse (parameters, keys, three
+// sparse-slot bootstrappers, LT coefficients, ReLU trees) and infer() the per-image body, in the
+// reference's operation order.  Galois keys are registered for every rotation step and
+// materialised on first use at the level of that use (seal.h, KSwitchKeys), which replaces the
+// reference's hand-listed rotation_kinds table (infer_seal.cpp:345-360).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "mhe_boot.h"
+#include "mhe_cnn.h"
+
+struct ResNetParams
+{
+    std::vector<double> linear_weight, linear_bias;
+    std::vector<std::vector<double>> conv_weight, bn_bias, bn_running_mean, bn_running_var, bn_weight;
+};
+
+// infer_seal.cpp:3-100: text files of the reference layout under <dir>/resnet<L>_new/
+void import_parameters_cifar10(std::vector<double> &linear_weight, std::vector<double> &linear_bias,
+                               std::vector<std::vector<double>> &conv_weight,
+                               std::vector<std::vector<double>> &bn_bias,
+                               std::vector<std::vector<double>> &bn_running_mean,
+                               std::vector<std::vector<double>> &bn_running_var,
+                               std::vector<std::vector<double>> &bn_weight, std::size_t layer_num,
+                               std::size_t end_num, const std::string &dir = "../../pretrained_parameters");
+// The same values from one float64 file in import order (tests/golden/make_resnet_params.py).
+ResNetParams load_resnet_params_bin(const std::string &path, std::size_t layer_num);
+
+struct ResNetResult
+{
+    std::vector<double> logits; // 10 scores (real parts of the first 10 slots)
+    std::size_t label = 0;      // argmax
+    double seconds = 0;         // total_time of the reference: encryption excluded, decryption excluded
+    double boot_seconds = 0, relu_seconds = 0, linear_seconds = 0;
+    int bootstraps = 0;
+};
+
+class ResNetRunner
+{
+public:
+    // comp_dir: directory holding d<alpha>.txt of the approximate ReLU (mhe_comp.h)
+    ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir);
+    ~ResNetRunner();
+    // one image: 3 x 32 x 32 values (channel-major, the test_values.txt order), before /B
+    ResNetResult infer(const std::vector<double> &image);
+    double setup_seconds() const { return setup_s_; }
+    double galois_key_gb() const;
+
+private:
+    struct Impl;
+    std::unique_ptr<Impl> impl_;
+    double setup_s_ = 0;
+};
+
+// infer_seal.cpp:234-577 entry point: images [start, end] from ../../../testFile/test_values.txt
+// when present, else seeded synthetic images (uniform [-2.5, 2.5], seed = image id); parameters
+// from ../../pretrained_parameters (or $MHE_RESNET_PARAMS, a .bin from make_resnet_params.py).
+void ResNet_cifar10_seal_sparse(std::size_t layer_num, std::size_t start_image_id, std::size_t end_image_id);

@@ -1,0 +1,414 @@
+// resnet.cpp -- encrypted ResNet CIFAR-10 inference (include/mhe_resnet.h), restating
+// cnn_ckks/cpu-ckks/single-key/cnn/infer_seal.cpp over the seal:: surface.
+#include "mhe_resnet.h"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <random>
+#include <stdexcept>
+
+#include "../../include/mhe.h"
+
+using namespace seal;
+
+namespace
+{
+std::size_t end_num_of(std::size_t layer_num)
+{
+    // infer_seal.cpp:393-400
+    switch (layer_num)
+    {
+    case 20: return 2;
+    case 32: return 4;
+    case 44: return 6;
+    case 56: return 8;
+    case 110: return 17;
+    default: throw std::invalid_argument("layer_num is not correct");
+    }
+}
+
+// conv / bn channel counts in import order (infer_seal.cpp:31-99)
+void shapes(std::size_t layer_num, std::vector<std::size_t> &conv_sizes, std::vector<std::size_t> &bn_sizes)
+{
+    const std::size_t end_num = end_num_of(layer_num);
+    conv_sizes = { 9 * 3 * 16 };
+    for (int j = 1; j <= 3; j++)
+        for (std::size_t k = 0; k <= end_num; k++)
+        {
+            const int co = j == 1 ? 16 : j == 2 ? 32 : 64;
+            int ci;
+            if (j == 1 || (j == 2 && k == 0))
+                ci = 16;
+            else if ((j == 2 && k != 0) || (j == 3 && k == 0))
+                ci = 32;
+            else
+                ci = 64;
+            conv_sizes.push_back((std::size_t)9 * ci * co);
+            conv_sizes.push_back((std::size_t)9 * co * co);
+        }
+    bn_sizes = { 16 };
+    for (int j = 1; j <= 3; j++)
+        for (std::size_t k = 0; k <= end_num; k++)
+        {
+            const std::size_t ci = j == 1 ? 16 : j == 2 ? 32 : 64;
+            bn_sizes.push_back(ci);
+            bn_sizes.push_back(ci);
+        }
+}
+
+void read_text(const std::string &path, std::size_t count, std::vector<double> &out)
+{
+    std::ifstream in(path);
+    if (!in.is_open()) throw std::runtime_error("file is not open");
+    double v;
+    for (std::size_t i = 0; i < count; i++)
+    {
+        in >> v;
+        out.emplace_back(v);
+    }
+}
+} // namespace
+
+void import_parameters_cifar10(std::vector<double> &linear_weight, std::vector<double> &linear_bias,
+                               std::vector<std::vector<double>> &conv_weight, std::vector<std::vector<double>> &bn_bias,
+                               std::vector<std::vector<double>> &bn_running_mean,
+                               std::vector<std::vector<double>> &bn_running_var,
+                               std::vector<std::vector<double>> &bn_weight, std::size_t layer_num, std::size_t end_num,
+                               const std::string &root)
+{
+    // infer_seal.cpp:3-100
+    if (layer_num != 20 && layer_num != 32 && layer_num != 44 && layer_num != 56 && layer_num != 110)
+        throw std::invalid_argument("layer number is not valid");
+    const std::string dir = root + "/resnet" + std::to_string(layer_num) + "_new/";
+    std::vector<std::size_t> cs, bs;
+    shapes(layer_num, cs, bs);
+    (void)end_num;
+    conv_weight.assign(layer_num - 1, {});
+    bn_bias.assign(layer_num - 1, {});
+    bn_running_mean.assign(layer_num - 1, {});
+    bn_running_var.assign(layer_num - 1, {});
+    bn_weight.assign(layer_num - 1, {});
+    const std::size_t E = end_num_of(layer_num);
+    std::size_t c = 0;
+    read_text(dir + "conv1_weight.txt", cs[c], conv_weight[c]);
+    c++;
+    for (int j = 1; j <= 3; j++)
+        for (std::size_t k = 0; k <= E; k++)
+            for (int i = 1; i <= 2; i++, c++)
+                read_text(dir + "layer" + std::to_string(j) + "_" + std::to_string(k) + "_conv" + std::to_string(i) +
+                              "_weight.txt",
+                          cs[c], conv_weight[c]);
+    std::size_t b = 0;
+    auto bn = [&](const std::string &prefix) {
+        read_text(dir + prefix + "_bias.txt", bs[b], bn_bias[b]);
+        read_text(dir + prefix + "_running_mean.txt", bs[b], bn_running_mean[b]);
+        read_text(dir + prefix + "_running_var.txt", bs[b], bn_running_var[b]);
+        read_text(dir + prefix + "_weight.txt", bs[b], bn_weight[b]);
+        b++;
+    };
+    bn("bn1");
+    for (int j = 1; j <= 3; j++)
+        for (std::size_t k = 0; k <= E; k++)
+            for (int i = 1; i <= 2; i++)
+                bn("layer" + std::to_string(j) + "_" + std::to_string(k) + "_bn" + std::to_string(i));
+    read_text(dir + "linear_weight.txt", 10 * 64, linear_weight);
+    read_text(dir + "linear_bias.txt", 10, linear_bias);
+}
+
+ResNetParams load_resnet_params_bin(const std::string &path, std::size_t layer_num)
+{
+    std::vector<std::size_t> cs, bs;
+    shapes(layer_num, cs, bs);
+    std::ifstream in(path, std::ios::binary);
+    if (!in.is_open()) throw std::runtime_error("parameter file is not open: " + path);
+    auto take = [&](std::size_t count) {
+        std::vector<double> v(count);
+        in.read(reinterpret_cast<char *>(v.data()), (std::streamsize)(count * sizeof(double)));
+        if (!in) throw std::runtime_error("parameter file is truncated: " + path);
+        return v;
+    };
+    ResNetParams p;
+    for (std::size_t c : cs) p.conv_weight.push_back(take(c));
+    for (std::size_t b : bs)
+    {
+        p.bn_bias.push_back(take(b));
+        p.bn_running_mean.push_back(take(b));
+        p.bn_running_var.push_back(take(b));
+        p.bn_weight.push_back(take(b));
+    }
+    p.linear_weight = take(10 * 64);
+    p.linear_bias = take(10);
+    return p;
+}
+
+// ------------------------------------------------------------------------------------ runner
+struct ResNetRunner::Impl
+{
+    std::size_t layer_num, end_num;
+    ResNetParams prm;
+    // infer_seal.cpp:236-310
+    const double B = 40.0;
+    const long alpha = 13, comp_no = 3;
+    std::vector<int> deg{ 15, 15, 27 };
+    const double scaled_val = 1.7;
+    std::vector<Tree> tree;
+    const long boundary_K = 25, boot_deg = 59, scale_factor = 2, inverse_deg = 1;
+    const long logN = 16, loge = 10, logn = 15, logn_1 = 14, logn_2 = 13, logn_3 = 12;
+    const int logp = 46, logq = 51, log_special_prime = 51;
+    const int remaining_level = 16, boot_level = 14, total_level = remaining_level + boot_level;
+
+    EncryptionParameters parms{ scheme_type::ckks };
+    std::unique_ptr<SEALContext> context;
+    std::unique_ptr<KeyGenerator> keygen;
+    PublicKey public_key;
+    SecretKey secret_key;
+    RelinKeys relin_keys;
+    GaloisKeys gal_keys;
+    std::unique_ptr<CKKSEncoder> encoder;
+    std::unique_ptr<Encryptor> encryptor;
+    std::unique_ptr<Evaluator> evaluator;
+    std::unique_ptr<Decryptor> decryptor;
+    std::unique_ptr<Bootstrapper> boot[3];
+};
+
+ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir)
+    : impl_(std::make_unique<Impl>())
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    Impl &m = *impl_;
+    m.layer_num = layer_num;
+    m.end_num = end_num_of(layer_num);
+    m.prm = params;
+    if (!comp_dir.empty()) setenv("MHE_COMP_DIR", comp_dir.c_str(), 1);
+    for (int i = 0; i < m.comp_no; i++)
+    {
+        Tree tr;
+        upgrade_oddbaby(m.deg[i], tr); // ev_type oddbaby (infer_seal.cpp:245-276)
+        m.tree.emplace_back(tr);
+    }
+    std::vector<int> coeff_bit_vec{ m.logq };
+    for (int i = 0; i < m.remaining_level; i++) coeff_bit_vec.push_back(m.logp);
+    for (int i = 0; i < m.boot_level; i++) coeff_bit_vec.push_back(m.logq);
+    coeff_bit_vec.push_back(m.log_special_prime);
+    const std::size_t poly_modulus_degree = (std::size_t)1 << m.logN;
+    m.parms.set_poly_modulus_degree(poly_modulus_degree);
+    m.parms.set_coeff_modulus(CoeffModulus::Create(poly_modulus_degree, coeff_bit_vec));
+    m.parms.set_secret_key_hamming_weight(192);
+    const double scale = std::pow(2.0, m.logp);
+    m.context = std::make_unique<SEALContext>(m.parms);
+    m.keygen = std::make_unique<KeyGenerator>(*m.context);
+    m.keygen->create_public_key(m.public_key);
+    m.secret_key = m.keygen->secret_key();
+    m.keygen->create_relin_keys(m.relin_keys);
+    m.encoder = std::make_unique<CKKSEncoder>(*m.context);
+    m.encryptor = std::make_unique<Encryptor>(*m.context, m.public_key);
+    m.evaluator = std::make_unique<Evaluator>(*m.context, *m.encoder);
+    m.decryptor = std::make_unique<Decryptor>(*m.context, m.secret_key);
+    const long logns[3] = { m.logn_1, m.logn_2, m.logn_3 };
+    for (int i = 0; i < 3; i++)
+        m.boot[i] = std::make_unique<Bootstrapper>(m.loge, logns[i], m.logN - 1, m.total_level, scale, m.boundary_K,
+                                                   m.boot_deg, m.scale_factor, m.inverse_deg, *m.context, *m.keygen,
+                                                   *m.encoder, *m.encryptor, *m.decryptor, *m.evaluator, m.relin_keys,
+                                                   m.gal_keys);
+    for (auto &b : m.boot) b->prepare_mod_polynomial();
+    // every rotation step (materialised lazily) plus the bootstrappers' steps
+    std::vector<int> gal_steps_vector{ 0 };
+    for (long i = 1; i < (1L << (m.logN - 1)); i++) gal_steps_vector.push_back((int)i);
+    m.keygen->create_galois_keys(gal_steps_vector, m.gal_keys);
+    for (int i = 0; i < 3; i++)
+    {
+        m.boot[i]->slot_vec.push_back(logns[i]);
+        m.boot[i]->generate_LT_coefficient_3();
+    }
+    setup_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+ResNetRunner::~ResNetRunner() = default;
+
+double ResNetRunner::galois_key_gb() const
+{
+    return impl_->gal_keys.device_bytes() / 1e9;
+}
+
+ResNetResult ResNetRunner::infer(const std::vector<double> &img)
+{
+    // infer_seal.cpp:404-577 (one image)
+    Impl &m = *impl_;
+    Evaluator &evaluator = *m.evaluator;
+    CKKSEncoder &encoder = *m.encoder;
+    Encryptor &encryptor = *m.encryptor;
+    Decryptor &decryptor = *m.decryptor;
+    ResNetResult res;
+    using clk = std::chrono::steady_clock;
+    auto sync = [&] { mhe_stream_sync(m.context->engine(), m.context->stream()); };
+    std::vector<Ciphertext> cipher_pool(14);
+    TensorCipher cnn, temp;
+    int co = 0, st = 0;
+    const int fh = 3, fw = 3;
+    const long init_p = 8, n = 1L << m.logn;
+    int stage = 0;
+    const double epsilon = 0.00001;
+    const auto &prm = m.prm;
+
+    std::vector<double> image(n, 0.0);
+    for (long i = 0; i < 32 * 32 * 3 && i < (long)img.size(); i++) image[i] = img[i];
+    for (long i = n / init_p; i < n; i++) image[i] = image[i % (n / init_p)];
+    for (long i = 0; i < n; i++) image[i] /= m.B; // for boundary [-1,1]
+
+    cnn = TensorCipher((int)m.logn, 1, 32, 32, 3, 3, (int)init_p, image, encryptor, encoder, m.logq);
+    sync();
+    const auto total_start = clk::now();
+    double t_boot = 0, t_relu = 0;
+
+    Ciphertext ctxt = cnn.cipher();
+    for (int i = 0; i < m.boot_level - 3; i++) evaluator.mod_switch_to_next_inplace(ctxt);
+    cnn.set_ciphertext(ctxt);
+
+    // layer 0
+    multiplexed_parallel_convolution_seal(cnn, cnn, 16, 1, fh, fw, prm.conv_weight[stage], prm.bn_running_var[stage],
+                                          prm.bn_weight[stage], epsilon, encoder, encryptor, evaluator, m.gal_keys,
+                                          cipher_pool);
+    // scaling factor ~2^51 -> 2^46
+    {
+        const auto &modulus = m.context->first_context_data()->parms().coeff_modulus();
+        ctxt = cnn.cipher();
+        const std::size_t cur_level = ctxt.coeff_modulus_size();
+        Plaintext scaler;
+        const double scale_change = std::pow(2.0, 46) * ((double)modulus[cur_level - 1].value()) / ctxt.scale();
+        encoder.encode(1, scale_change, scaler);
+        evaluator.mod_switch_to_inplace(scaler, ctxt.parms_id());
+        evaluator.multiply_plain_inplace(ctxt, scaler);
+        evaluator.rescale_to_next_inplace(ctxt);
+        ctxt.scale() = std::pow(2.0, 46);
+        cnn.set_ciphertext(ctxt);
+    }
+    multiplexed_parallel_batch_norm_seal(cnn, cnn, prm.bn_bias[stage], prm.bn_running_mean[stage],
+                                         prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder, encryptor,
+                                         evaluator, m.B);
+    auto relu = [&] {
+        sync();
+        const auto a = clk::now();
+        ReLU_seal(cnn, cnn, m.comp_no, m.deg, m.alpha, m.tree, m.scaled_val, m.logp, encryptor, evaluator, decryptor,
+                  encoder, m.public_key, m.secret_key, m.relin_keys, m.B);
+        sync();
+        t_relu += std::chrono::duration<double>(clk::now() - a).count();
+    };
+    auto bootstrap = [&](int j) {
+        sync();
+        const auto a = clk::now();
+        Ciphertext c = cnn.cipher(), rtn;
+        m.boot[j]->bootstrap_real_3(rtn, c);
+        cnn.set_ciphertext(rtn);
+        sync();
+        t_boot += std::chrono::duration<double>(clk::now() - a).count();
+        res.bootstraps++;
+    };
+    relu();
+
+    for (int j = 0; j < 3; j++) // layer 1_x, 2_x, 3_x
+    {
+        co = j == 0 ? 16 : j == 1 ? 32 : 64;
+        for (std::size_t k = 0; k <= m.end_num; k++)
+        {
+            stage = (int)(2 * ((m.end_num + 1) * j + k) + 1);
+            temp = cnn;
+            st = (j >= 1 && k == 0) ? 2 : 1;
+            multiplexed_parallel_convolution_seal(cnn, cnn, co, st, fh, fw, prm.conv_weight[stage],
+                                                  prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
+                                                  encryptor, evaluator, m.gal_keys, cipher_pool);
+            multiplexed_parallel_batch_norm_seal(cnn, cnn, prm.bn_bias[stage], prm.bn_running_mean[stage],
+                                                 prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
+                                                 encryptor, evaluator, m.B);
+            bootstrap(j);
+            relu();
+
+            stage = (int)(2 * ((m.end_num + 1) * j + k) + 2);
+            st = 1;
+            multiplexed_parallel_convolution_seal(cnn, cnn, co, st, fh, fw, prm.conv_weight[stage],
+                                                  prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
+                                                  encryptor, evaluator, m.gal_keys, cipher_pool);
+            multiplexed_parallel_batch_norm_seal(cnn, cnn, prm.bn_bias[stage], prm.bn_running_mean[stage],
+                                                 prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
+                                                 encryptor, evaluator, m.B);
+            if (j >= 1 && k == 0) multiplexed_parallel_downsampling_seal(temp, temp, evaluator, m.gal_keys);
+            cnn_add_seal(temp, cnn, cnn, evaluator);
+            bootstrap(j);
+            relu();
+        }
+    }
+    std::ofstream devnull;
+    averagepooling_seal_scale(cnn, cnn, evaluator, m.gal_keys, m.B, encoder, decryptor, devnull);
+    matrix_multiplication_seal(cnn, cnn, prm.linear_weight, prm.linear_bias, 10, 64, evaluator, m.gal_keys);
+    sync();
+    res.seconds = std::chrono::duration<double>(clk::now() - total_start).count();
+    res.boot_seconds = t_boot;
+    res.relu_seconds = t_relu;
+    res.linear_seconds = res.seconds - t_boot - t_relu;
+
+    Plaintext plain;
+    decryptor.decrypt(cnn.cipher(), plain);
+    std::vector<std::complex<double>> rtn_vec;
+    encoder.decode(plain, rtn_vec);
+    double max_score = -100.0;
+    for (std::size_t i = 0; i < 10; i++)
+    {
+        res.logits.push_back(rtn_vec[i].real());
+        if (max_score < rtn_vec[i].real())
+        {
+            res.label = i;
+            max_score = rtn_vec[i].real();
+        }
+    }
+    return res;
+}
+
+void ResNet_cifar10_seal_sparse(std::size_t layer_num, std::size_t start_image_id, std::size_t end_image_id)
+{
+    ResNetParams prm;
+    if (const char *bin = std::getenv("MHE_RESNET_PARAMS"))
+        prm = load_resnet_params_bin(bin, layer_num);
+    else
+        import_parameters_cifar10(prm.linear_weight, prm.linear_bias, prm.conv_weight, prm.bn_bias,
+                                  prm.bn_running_mean, prm.bn_running_var, prm.bn_weight, layer_num,
+                                  end_num_of(layer_num));
+    const char *cd = std::getenv("MHE_COMP_DIR");
+    ResNetRunner runner(layer_num, prm, cd ? cd : "../result");
+    std::ifstream values("../../../testFile/test_values.txt"), labels("../../../testFile/test_label.txt");
+    const bool have_images = values.is_open();
+    double all = 0;
+    for (std::size_t image_id = start_image_id; image_id <= end_image_id; image_id++)
+    {
+        std::vector<double> img(32 * 32 * 3);
+        int image_label = -1;
+        if (have_images)
+        {
+            double v;
+            values.clear();
+            values.seekg(0);
+            for (std::size_t i = 0; i < 32 * 32 * 3 * image_id; i++) values >> v;
+            for (auto &x : img) values >> x;
+            labels.clear();
+            labels.seekg(0);
+            for (std::size_t i = 0; i <= image_id; i++) labels >> image_label;
+        }
+        else
+        {
+            std::mt19937_64 g(image_id);
+            std::uniform_real_distribution<double> U(-2.5, 2.5);
+            for (auto &x : img) x = U(g);
+        }
+        ResNetResult r = runner.infer(img);
+        all += r.seconds;
+        std::cout << "( ";
+        for (std::size_t i = 0; i < 9; i++) std::cout << r.logits[i] << ", ";
+        std::cout << r.logits[9] << ")" << std::endl;
+        std::cout << "total time : " << (long)(r.seconds * 1000) << " ms" << std::endl;
+        std::cout << "image label: " << image_label << std::endl;
+        std::cout << "inferred label: " << r.label << std::endl;
+    }
+    std::cout << "all threads time : " << (long)(all * 1000) << " ms" << std::endl;
+}

@@ -1,0 +1,147 @@
+// GPU end-to-end test of encrypted ResNet CIFAR-10 inference (include/mhe_resnet.h; the reference's
+// cnn/infer_seal.cpp ResNet_cifar10_seal_sparse) with the reference's pretrained ResNet-20
+// parameters (tests/golden/resnet/resnet20_params.bin) on seeded synthetic images (the reference's
+// testFile/test_values.txt is not in the repository).  The decrypted logits are compared with the
+// same network evaluated in plain doubles with the exact ReLU; prints the time per image.
+//   resnet_test <params.bin> <comp_dir> [images] [layers]
+#include "mhe_resnet.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+
+static std::vector<double> conv(const std::vector<double> &in, const std::vector<double> &wt, int h, int w, int ci,
+                                int co, int st)
+{
+    const int ho = h / st, wo = w / st;
+    std::vector<double> out((size_t)co * ho * wo, 0.0);
+    for (int b = 0; b < co; b++)
+        for (int y = 0; y < ho; y++)
+            for (int x = 0; x < wo; x++)
+            {
+                double s = 0;
+                for (int a = 0; a < ci; a++)
+                    for (int i1 = 0; i1 < 3; i1++)
+                        for (int i2 = 0; i2 < 3; i2++)
+                        {
+                            const int yy = st * y + i1 - 1, xx = st * x + i2 - 1;
+                            if (yy < 0 || yy >= h || xx < 0 || xx >= w) continue;
+                            s += wt[((size_t)(b * ci + a) * 3 + i1) * 3 + i2] * in[(size_t)a * h * w + yy * w + xx];
+                        }
+                out[(size_t)b * ho * wo + y * wo + x] = s;
+            }
+    return out;
+}
+
+static void bn(std::vector<double> &v, const ResNetParams &p, int s, int c, int hw)
+{
+    for (int b = 0; b < c; b++)
+    {
+        const double g = p.bn_weight[s][b] / std::sqrt(p.bn_running_var[s][b] + 1e-5);
+        for (int i = 0; i < hw; i++)
+            v[(size_t)b * hw + i] = (v[(size_t)b * hw + i] - p.bn_running_mean[s][b]) * g + p.bn_bias[s][b];
+    }
+}
+
+static void relu(std::vector<double> &v)
+{
+    for (auto &x : v) x = std::max(x, 0.0);
+}
+
+static std::vector<double> plain_resnet(const ResNetParams &p, const std::vector<double> &img, int end_num)
+{
+    std::vector<double> x = conv(img, p.conv_weight[0], 32, 32, 3, 16, 1);
+    int h = 32, c = 16;
+    bn(x, p, 0, c, h * h);
+    relu(x);
+    for (int j = 0; j < 3; j++)
+        for (int k = 0; k <= end_num; k++)
+        {
+            const int s1 = 2 * ((end_num + 1) * j + k) + 1, s2 = s1 + 1;
+            const int co = j == 0 ? 16 : j == 1 ? 32 : 64, st = (j >= 1 && k == 0) ? 2 : 1;
+            std::vector<double> temp = x;
+            std::vector<double> y = conv(x, p.conv_weight[s1], h, h, c, co, st);
+            const int ho = h / st;
+            bn(y, p, s1, co, ho * ho);
+            relu(y);
+            y = conv(y, p.conv_weight[s2], ho, ho, co, co, 1);
+            bn(y, p, s2, co, ho * ho);
+            if (st == 2)
+            {
+                // option-A shortcut: stride-2 subsample, input channel a -> output channel a + c/2
+                std::vector<double> ds((size_t)co * ho * ho, 0.0);
+                for (int a = 0; a < c; a++)
+                    for (int yy = 0; yy < ho; yy++)
+                        for (int xx = 0; xx < ho; xx++)
+                            ds[(size_t)(a + c / 2) * ho * ho + yy * ho + xx] = temp[(size_t)a * h * h + 2 * yy * h + 2 * xx];
+                temp = ds;
+            }
+            for (size_t i = 0; i < y.size(); i++) y[i] += temp[i];
+            relu(y);
+            x = y;
+            h = ho;
+            c = co;
+        }
+    std::vector<double> f(64, 0.0), logits(10, 0.0);
+    for (int b = 0; b < 64; b++)
+    {
+        for (int i = 0; i < h * h; i++) f[b] += x[(size_t)b * h * h + i];
+        f[b] /= h * h;
+    }
+    for (int i = 0; i < 10; i++)
+    {
+        logits[i] = p.linear_bias[i];
+        for (int b = 0; b < 64; b++) logits[i] += p.linear_weight[(size_t)i * 64 + b] * f[b];
+    }
+    return logits;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 3)
+    {
+        std::fprintf(stderr, "usage: resnet_test <params.bin> <comp_dir> [images] [layers]\n");
+        return 2;
+    }
+    const int images = argc > 3 ? std::atoi(argv[3]) : 1;
+    const std::size_t layers = argc > 4 ? std::atoi(argv[4]) : 20;
+    const ResNetParams prm = load_resnet_params_bin(argv[1], layers);
+    ResNetRunner runner(layers, prm, argv[2]);
+    std::printf("setup: %.2f s\n", runner.setup_seconds());
+    int fail = 0;
+    double total = 0;
+    for (int id = 0; id < images; id++)
+    {
+        std::mt19937_64 g(id);
+        std::uniform_real_distribution<double> U(-2.5, 2.5);
+        std::vector<double> img(3072);
+        for (auto &x : img) x = U(g);
+        const ResNetResult r = runner.infer(img);
+        const std::vector<double> want = plain_resnet(prm, img, 2);
+        double err = 0, mag = 0;
+        std::size_t wl = 0;
+        for (int i = 0; i < 10; i++)
+        {
+            err = std::max(err, std::fabs(r.logits[i] - want[i]));
+            mag = std::max(mag, std::fabs(want[i]));
+            if (want[i] > want[wl]) wl = i;
+        }
+        std::printf("image %d: %.3f s (bootstrap %.3f s x%d, ReLU %.3f s, linear %.3f s); label %zu (plain %zu); "
+                    "max |logit error| %.3g of max |logit| %.3g\n",
+                    id, r.seconds, r.boot_seconds, r.bootstraps, r.relu_seconds, r.linear_seconds, r.label, wl, err,
+                    mag);
+        std::printf("  logits:");
+        for (double v : r.logits) std::printf(" %.4f", v);
+        std::printf("\n  plain: ");
+        for (double v : want) std::printf(" %.4f", v);
+        std::printf("\n");
+        if (id > 0 || images == 1) total += r.seconds;
+        if (!(err < 0.05 * std::max(1.0, mag))) fail++;
+    }
+    std::printf("galois key memory %.1f GB; mean %.3f s/image\n", runner.galois_key_gb(),
+                total / std::max(1, images > 1 ? images - 1 : 1));
+    std::printf("%s\n", fail ? "FAILED" : "ok");
+    return fail ? 1 : 0;
+}

@@ -77,6 +77,42 @@ def test_bootstrapping_end_to_end():
 
 
 @pytest.mark.gpu
+def test_resnet20_end_to_end():
+    """Encrypted ResNet-20 CIFAR-10 (include/mhe_resnet.h, cnn/infer_seal.cpp semantics: multiplexed
+    conv/BN, approximate ReLU, 18 sparse-slot bootstraps, average pooling, FC) with the reference's
+    pretrained parameters on a seeded synthetic image; decrypted logits vs the plain network with the
+    exact ReLU within 5% of the largest logit, same label (tests/cpp/resnet_test.cpp)."""
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "resnet_test"),
+                        os.path.join(ROOT, "tests", "golden", "resnet", "resnet20_params.bin"),
+                        os.path.join(ROOT, "tests", "golden", "comp"), "1"],
+                       capture_output=True, text=True, timeout=900)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_resnet_params_fixture():
+    """The packed parameter fixture has ResNet-20's 271098 values in import_parameters_cifar10
+    order (cnn/infer_seal.cpp:3-100): 19 conv weight tensors, 19 x 4 batch-norm vectors, FC."""
+    import numpy as np
+
+    v = np.fromfile(os.path.join(ROOT, "tests", "golden", "resnet", "resnet20_params.bin"), dtype="<f8")
+    conv = 9 * 3 * 16 + 3 * 2 * 9 * 16 * 16 + 9 * 16 * 32 + 9 * 32 * 32 + 2 * 2 * 9 * 32 * 32 + 9 * 32 * 64 \
+        + 9 * 64 * 64 + 2 * 2 * 9 * 64 * 64
+    bnv = 4 * (16 + 6 * 16 + 6 * 32 + 6 * 64)
+    assert v.size == conv + bnv + 640 + 10
+    assert np.isfinite(v).all()
+    # running variances are positive
+    off = conv
+    sizes = [16] + [16] * 6 + [32] * 6 + [64] * 6
+    for c in sizes:
+        var = v[off + 2 * c: off + 3 * c]
+        assert (var > 0).all()
+        off += 4 * c
+
+
+@pytest.mark.gpu
 def test_seal_api_end_to_end():
     _build()
     r = subprocess.run([DRIVER], capture_output=True, text=True, timeout=600)
