@@ -51,6 +51,9 @@ public:
     ~ResNetRunner();
     // one image: 3 x 32 x 32 values (channel-major, the test_values.txt order), before /B
     ResNetResult infer(const std::vector<double> &image);
+    // images on `threads` host threads at once, each on its own HIP stream (the reference runs one
+    // image per OpenMP thread, infer_seal.cpp:404); results in image order
+    std::vector<ResNetResult> infer_batch(const std::vector<std::vector<double>> &images, int threads);
     double setup_seconds() const { return setup_s_; }
     double galois_key_gb() const;
 

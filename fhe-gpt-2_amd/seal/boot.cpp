@@ -928,6 +928,9 @@ bool Bootstrapper::PtKey::operator<(const PtKey &o) const
 namespace
 {
 std::mutex g_pt_mu;
+// the input scale of the bootstrap running on this thread (Bootstrapper objects are shared by the
+// threads of an image batch, like the reference's OpenMP team shares bootstrapper_1..3)
+thread_local double tl_initial_scale = 0;
 bool pt_cache_on()
 {
     const char *e = std::getenv("MHE_BOOT_PT_CACHE");
@@ -1142,8 +1145,8 @@ void Bootstrapper::sfl_half_3(Ciphertext &rtncipher, Ciphertext &cipher)
     const double mod_zero = (double)modulus[0].value();
     const double curr_mod = (double)modulus[curr_level].value();
     // fftcoeff3_scale = fftcoeff3 * curr_mod * q0 * final_scale / (2 s^2 initial_scale)
-    const double coeff_scale =
-        curr_mod * mod_zero * final_scale / (2 * tmpct2.scale() * tmpct2.scale() * initial_scale);
+    const double init = tl_initial_scale != 0 ? tl_initial_scale : initial_scale;
+    const double coeff_scale = curr_mod * mod_zero * final_scale / (2 * tmpct2.scale() * tmpct2.scale() * init);
     bsgs_linear_transform(rtncipher, tmpct2, totlen3, basicstep3, (int)logn + 1, fftcoeff3[slot_index],
                           coeff_scale);
     evaluator.rescale_to_next_inplace(rtncipher);
@@ -1242,7 +1245,8 @@ void Bootstrapper::bootstrap_sparse_real_3(Ciphertext &rtncipher, Ciphertext &ci
     {
         const auto curr_level = context.get_context_data(modrtn.parms_id())->chain_index();
         const double mod_zero = (double)modulus[0].value(), curr_mod = (double)modulus[curr_level].value();
-        const double scale_adj = curr_mod * mod_zero * final_scale / (modrtn.scale() * modrtn.scale() * initial_scale);
+        const double init = tl_initial_scale != 0 ? tl_initial_scale : initial_scale;
+        const double scale_adj = curr_mod * mod_zero * final_scale / (modrtn.scale() * modrtn.scale() * init);
         std::vector<cd> stc_vec(Nh, 0.0);
         for (long i = 0; i < Nh; i++) stc_vec[i] = i % 2 == 0 ? cd(scale_adj) : cd(0, 1.0) * scale_adj;
         evaluator.multiply_vector_reduced_error(modrtn, stc_vec, rtncipher);
@@ -1263,8 +1267,8 @@ void Bootstrapper::bootstrap_sparse_real_3(Ciphertext &rtncipher, Ciphertext &ci
 
 void Bootstrapper::bootstrap_real_3(Ciphertext &rtncipher, Ciphertext &cipher)
 {
-    // Bootstrapper.cpp:3421-3425
-    initial_scale = cipher.scale();
+    // Bootstrapper.cpp:3421-3425 (initial_scale kept per thread)
+    tl_initial_scale = cipher.scale();
     if (logn == logNh) throw std::logic_error("full-slot bootstrapping (logn == logNh) is not supported");
     bootstrap_sparse_real_3(rtncipher, cipher);
 }

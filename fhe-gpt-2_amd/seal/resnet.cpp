@@ -2,7 +2,11 @@
 // cnn_ckks/cpu-ckks/single-key/cnn/infer_seal.cpp over the seal:: surface.
 #include "mhe_resnet.h"
 
+#include <atomic>
 #include <chrono>
+#include <exception>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -364,6 +368,30 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img)
         }
     }
     return res;
+}
+
+std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vector<double>> &images, int threads)
+{
+    std::vector<ResNetResult> out(images.size());
+    std::atomic<std::size_t> next{ 0 };
+    std::exception_ptr err;
+    std::mutex err_mu;
+    auto work = [&] {
+        try
+        {
+            for (std::size_t i; (i = next.fetch_add(1)) < images.size();) out[i] = infer(images[i]);
+        }
+        catch (...)
+        {
+            std::lock_guard<std::mutex> g(err_mu);
+            if (!err) err = std::current_exception();
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
+    for (auto &t : pool) t.join();
+    if (err) std::rethrow_exception(err);
+    return out;
 }
 
 void ResNet_cifar10_seal_sparse(std::size_t layer_num, std::size_t start_image_id, std::size_t end_image_id)

@@ -7,6 +7,7 @@
 #include "mhe_resnet.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -107,12 +108,14 @@ int main(int argc, char **argv)
     }
     const int images = argc > 3 ? std::atoi(argv[3]) : 1;
     const std::size_t layers = argc > 4 ? std::atoi(argv[4]) : 20;
+    const int threads = argc > 5 ? std::atoi(argv[5]) : 0;
     const ResNetParams prm = load_resnet_params_bin(argv[1], layers);
     ResNetRunner runner(layers, prm, argv[2]);
     std::printf("setup: %.2f s\n", runner.setup_seconds());
     int fail = 0;
     double total = 0;
-    for (int id = 0; id < images; id++)
+    const int sequential = threads > 0 ? std::min(images, 2) : images; // latency pass (first one warms caches)
+    for (int id = 0; id < sequential; id++)
     {
         std::mt19937_64 g(id);
         std::uniform_real_distribution<double> U(-2.5, 2.5);
@@ -137,11 +140,36 @@ int main(int argc, char **argv)
         std::printf("\n  plain: ");
         for (double v : want) std::printf(" %.4f", v);
         std::printf("\n");
-        if (id > 0 || images == 1) total += r.seconds;
+        if (id > 0 || sequential == 1) total += r.seconds;
         if (!(err < 0.05 * std::max(1.0, mag))) fail++;
     }
+    if (threads > 0)
+    {
+        // throughput: `images` images on `threads` streams at once
+        std::vector<std::vector<double>> batch;
+        for (int id = 0; id < images; id++)
+        {
+            std::mt19937_64 g(id);
+            std::uniform_real_distribution<double> U(-2.5, 2.5);
+            std::vector<double> img(3072);
+            for (auto &x : img) x = U(g);
+            batch.push_back(img);
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        auto rs = runner.infer_batch(batch, threads);
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (int id = 0; id < images; id++)
+        {
+            const std::vector<double> want = plain_resnet(prm, batch[id], 2);
+            double err = 0;
+            for (int i = 0; i < 10; i++) err = std::max(err, std::fabs(rs[id].logits[i] - want[i]));
+            if (!(err < 0.6)) fail++;
+        }
+        std::printf("batch: %d images on %d streams in %.3f s = %.3f s/image (%.3f images/s)\n", images, threads, wall,
+                    wall / images, images / wall);
+    }
     std::printf("galois key memory %.1f GB; mean %.3f s/image\n", runner.galois_key_gb(),
-                total / std::max(1, images > 1 ? images - 1 : 1));
+                total / std::max(1, sequential > 1 ? sequential - 1 : 1));
     std::printf("%s\n", fail ? "FAILED" : "ok");
     return fail ? 1 : 0;
 }
