@@ -1927,6 +1927,29 @@ MHE_EXPORT int mhe_apply_galois(mhe_ctx *c, uint64_t *ct, uint32_t elt, const ui
     return run_switch_key(c, ct, w->tmp, key, key_limbs, limbs, st);
 }
 
+MHE_EXPORT int mhe_apply_galois_to(mhe_ctx *c, const uint64_t *in, uint64_t *out, uint32_t elt, const uint64_t *key,
+                                   int key_limbs, int limbs, void *s)
+{
+    TR("out", out, (size_t)2 * limbs * ((size_t)1 << c->log_n)); TR("in", in, (size_t)2 * limbs * ((size_t)1 << c->log_n));
+    TRC(0, 0, 0, 0);
+    int r = check_limbs(c, limbs, 1);
+    if (r) return r;
+    if (!in || !out || !key) return fail(MHE_ERR_ARG, "Galois key not present");
+    if (in == out) return fail(MHE_ERR_ARG, "result cannot point to the same value as operand");
+    hipStream_t st = S(s);
+    Workspace *w;
+    r = get_ws(c, st, c->K - 1, &w);
+    if (r) return r;
+    const size_t ps = (size_t)limbs << c->log_n;
+    // evaluator.cpp:2193-2214: out0 <- perm(c0), tmp <- perm(c1), out1 <- 0, then out += KS(tmp)
+    r = launch_galois(c, in, elt, out, 1, limbs, st);
+    if (r) return r;
+    r = launch_galois(c, in + ps, elt, w->tmp, 1, limbs, st);
+    if (r) return r;
+    HIP_TRY(hipMemsetAsync(out + ps, 0, ps * sizeof(u64), st));
+    return run_switch_key(c, out, w->tmp, key, key_limbs, limbs, st);
+}
+
 MHE_EXPORT int mhe_rescale_to_next(mhe_ctx *c, const uint64_t *in, uint64_t *out, int size, int limbs, void *s)
 {
     TR("out", out, (size_t)size * (limbs - 1) * ((size_t)1 << c->log_n)); TR("in", in, (size_t)size * limbs * ((size_t)1 << c->log_n));

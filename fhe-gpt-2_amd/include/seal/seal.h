@@ -510,6 +510,9 @@ public:
                               MemoryPoolHandle = {}) const;
     void rotate_vector_inplace(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                                MemoryPoolHandle = {}) const;
+    // (not SEAL API) apply_galois reading encrypted, writing destination (no copy)
+    void apply_galois_to(const Ciphertext &encrypted, std::uint32_t galois_elt, const GaloisKeys &galois_keys,
+                         Ciphertext &destination) const;
     void rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                        Ciphertext &destination, MemoryPoolHandle = {}) const;
     void complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKeys &galois_keys, MemoryPoolHandle = {}) const;

@@ -54,6 +54,7 @@ SIGNATURES = {
     "mhe_switch_key": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_relinearize": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_apply_galois": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_apply_galois_to": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_permute_galois": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_rescale_to_next": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_mod_switch_drop": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
@@ -273,6 +274,12 @@ class Engine:
         _check(lib().mhe_apply_galois(self._h, _ptr(ct), elt, _ptr(key), self._key_limbs(key), ct.shape[1],
                                       self.stream()))
         return ct
+
+    def apply_galois_to(self, ct, elt, key, out=None):
+        out = self.empty(*ct.shape) if out is None else out
+        _check(lib().mhe_apply_galois_to(self._h, _ptr(ct), _ptr(out), elt, _ptr(key), self._key_limbs(key),
+                                         ct.shape[1], self.stream()))
+        return out
 
     def permute_galois(self, a, elt, out=None):
         out = self.empty(*a.shape) if out is None else out

@@ -388,7 +388,9 @@ void PolyStore::resize_words(std::size_t words, bool preserve)
     writer_ = s;
     writer_done_ = false;
     dev_valid_ = true;
-    if (preserve && host_valid_)
+    // the device copy is authoritative from here on; a host mirror is only kept when it already
+    // held data (a fresh store would otherwise zero-fill a host vector of the full size)
+    if (preserve && host_valid_ && !host_.empty())
         host_.resize(words, 0);
     else
     {
@@ -1181,6 +1183,18 @@ std::size_t Evaluator::limbs_of(const parms_id_type &id) const
     return level_of(context_, id, "parms_id").L;
 }
 
+namespace
+{
+// destination takes src's level, size, scale and form; its previous contents are not kept (no copy)
+void fresh_dest(const SEALContext &ctx, const Ciphertext &src, Ciphertext &dst, std::size_t size)
+{
+    dst.resize(ctx, src.parms_id(), 0);
+    dst.resize(size);
+    dst.scale() = src.scale();
+    dst.is_ntt_form() = src.is_ntt_form();
+}
+} // namespace
+
 void Evaluator::negate_inplace(Ciphertext &encrypted) const
 {
     // evaluator.cpp:78-101
@@ -1192,8 +1206,12 @@ void Evaluator::negate_inplace(Ciphertext &encrypted) const
 
 void Evaluator::negate(const Ciphertext &encrypted, Ciphertext &destination) const
 {
-    destination = encrypted;
-    negate_inplace(destination);
+    if (&encrypted == &destination) return negate_inplace(destination);
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    void *s = context_.stream();
+    fresh_dest(context_, encrypted, destination, encrypted.size());
+    chk(mhe_negate(context_.engine(), encrypted.store().dev_read(s), destination.store().dev_write(s, true),
+                   (int)encrypted.size(), (int)lv.L, s));
 }
 
 namespace
@@ -1312,6 +1330,26 @@ void Evaluator::multiply_inplace(Ciphertext &encrypted1, const Ciphertext &encry
 void Evaluator::multiply(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
                          MemoryPoolHandle) const
 {
+    if (&encrypted1 != &destination && &encrypted2 != &destination && encrypted1.size() == 2 &&
+        encrypted2.size() == 2)
+    {
+        // ckks_multiply into a fresh destination (SEAL copies encrypted1 first)
+        check_ct(context_, encrypted1, "encrypted1");
+        check_ct(context_, encrypted2, "encrypted2");
+        if (encrypted1.parms_id() != encrypted2.parms_id())
+            throw std::invalid_argument("encrypted1 and encrypted2 parameter mismatch");
+        if (!encrypted1.is_ntt_form() || !encrypted2.is_ntt_form())
+            throw std::invalid_argument("encrypted1 or encrypted2 must be in NTT form");
+        Level lv = level_of(context_, encrypted1.parms_id(), "encrypted1");
+        const double new_scale = encrypted1.scale() * encrypted2.scale();
+        check_scale(new_scale, lv);
+        void *s = context_.stream();
+        fresh_dest(context_, encrypted1, destination, 3);
+        const std::uint64_t *a = encrypted1.store().dev_read(s), *b = encrypted2.store().dev_read(s);
+        chk(mhe_ct_multiply(context_.engine(), a, b, destination.store().dev_write(s, true), (int)lv.L, s));
+        destination.scale() = new_scale;
+        return;
+    }
     if (&encrypted2 == &destination)
         multiply_inplace(destination, encrypted1);
     else
@@ -1364,8 +1402,17 @@ void Evaluator::square_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
 
 void Evaluator::square(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle) const
 {
-    destination = encrypted;
-    square_inplace(destination);
+    if (&encrypted == &destination) return square_inplace(destination);
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+    if (encrypted.size() != 2) throw std::logic_error("only size-2 ciphertexts are squared (relinearize first)");
+    const double new_scale = encrypted.scale() * encrypted.scale();
+    check_scale(new_scale, lv);
+    void *s = context_.stream();
+    fresh_dest(context_, encrypted, destination, 3);
+    chk(mhe_ct_square(context_.engine(), encrypted.store().dev_read(s), destination.store().dev_write(s, true),
+                      (int)lv.L, s));
+    destination.scale() = new_scale;
 }
 
 void Evaluator::switch_key(Ciphertext &encrypted, const std::uint64_t *target, const KSwitchKeys &keys,
@@ -1546,7 +1593,13 @@ void Evaluator::rescale_to_inplace(Ciphertext &encrypted, parms_id_type parms_id
 
 void Evaluator::multiply_plain_inplace(Ciphertext &encrypted, const Plaintext &plain, MemoryPoolHandle) const
 {
-    // evaluator.cpp:1726-1761, multiply_plain_ntt :1891-1930
+    multiply_plain(encrypted, plain, encrypted);
+}
+
+void Evaluator::multiply_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination,
+                               MemoryPoolHandle) const
+{
+    // evaluator.cpp:1726-1761, multiply_plain_ntt :1891-1930 (out of place: no copy of encrypted)
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (plain.is_ntt_form()) level_of(context_, plain.parms_id(), "plain");
     if (encrypted.is_ntt_form() != plain.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
@@ -1557,16 +1610,19 @@ void Evaluator::multiply_plain_inplace(Ciphertext &encrypted, const Plaintext &p
     check_scale(new_scale, lv);
     void *s = context_.stream();
     const std::uint64_t *b = plain.store().dev_read(s);
-    std::uint64_t *a = encrypted.store().dev_write(s);
-    chk(mhe_multiply_plain(context_.engine(), a, b, a, (int)encrypted.size(), (int)lv.L, s));
-    encrypted.scale() = new_scale;
-}
-
-void Evaluator::multiply_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination,
-                               MemoryPoolHandle) const
-{
-    destination = encrypted;
-    multiply_plain_inplace(destination, plain);
+    if (&encrypted == &destination)
+    {
+        std::uint64_t *a = destination.store().dev_write(s);
+        chk(mhe_multiply_plain(context_.engine(), a, b, a, (int)destination.size(), (int)lv.L, s));
+    }
+    else
+    {
+        fresh_dest(context_, encrypted, destination, encrypted.size());
+        const std::uint64_t *a = encrypted.store().dev_read(s);
+        chk(mhe_multiply_plain(context_.engine(), a, b, destination.store().dev_write(s, true),
+                               (int)encrypted.size(), (int)lv.L, s));
+    }
+    destination.scale() = new_scale;
 }
 
 namespace
@@ -1686,9 +1742,37 @@ void Evaluator::rotate_vector_inplace(Ciphertext &encrypted, int steps, const Ga
     rotate_internal(encrypted, steps, galois_keys);
 }
 
+void Evaluator::apply_galois_to(const Ciphertext &encrypted, std::uint32_t galois_elt, const GaloisKeys &galois_keys,
+                                Ciphertext &destination) const
+{
+    // apply_galois_inplace (evaluator.cpp:2120-2222) reading encrypted and writing destination
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    if (galois_keys.parms_id() != context_.key_parms_id())
+        throw std::invalid_argument("galois_keys is not valid for encryption parameters");
+    if (!(galois_elt & 1) || galois_elt >= 2 * lv.n) throw std::invalid_argument("Galois element is not valid");
+    if (encrypted.size() > 2) throw std::invalid_argument("encrypted size must be 2");
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+    if (!galois_keys.has_key(galois_elt)) throw std::invalid_argument("Galois key not present");
+    void *s = context_.stream();
+    std::size_t kl = 0;
+    const std::uint64_t *key = galois_keys.key_for(GaloisKeys::get_index(galois_elt), lv.L, s, kl);
+    fresh_dest(context_, encrypted, destination, 2);
+    chk(mhe_apply_galois_to(context_.engine(), encrypted.store().dev_read(s), destination.store().dev_write(s, true),
+                            galois_elt, key, (int)kl, (int)lv.L, s));
+}
+
 void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                               Ciphertext &destination, MemoryPoolHandle) const
 {
+    if (&encrypted != &destination && steps != 0)
+    {
+        Level lv = level_of(context_, encrypted.parms_id(), "encrypted");
+        if (galois_keys.parms_id() != context_.key_parms_id())
+            throw std::invalid_argument("galois_keys is not valid for encryption parameters");
+        const std::uint32_t elt = mhe_galois_elt_from_step(__builtin_ctzll(lv.n), steps);
+        if (!elt) throw std::invalid_argument("step count too large");
+        if (galois_keys.has_key(elt)) return apply_galois_to(encrypted, elt, galois_keys, destination);
+    }
     destination = encrypted;
     rotate_vector_inplace(destination, steps, galois_keys);
 }
@@ -1702,8 +1786,9 @@ void Evaluator::complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKey
 void Evaluator::complex_conjugate(const Ciphertext &encrypted, const GaloisKeys &galois_keys, Ciphertext &destination,
                                   MemoryPoolHandle) const
 {
-    destination = encrypted;
-    complex_conjugate_inplace(destination, galois_keys);
+    if (&encrypted == &destination) return complex_conjugate_inplace(destination, galois_keys);
+    const std::size_t n = level_of(context_, encrypted.parms_id(), "encrypted").n;
+    apply_galois_to(encrypted, (std::uint32_t)(2 * n - 1), galois_keys, destination);
 }
 
 // ---- modified SEAL entry points (evaluator.cpp:287-486) ------------------------------------
@@ -1724,8 +1809,20 @@ void Evaluator::add_const_inplace(Ciphertext &encrypted, double value) const
 
 void Evaluator::add_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const
 {
-    destination = encrypted;
-    add_const_inplace(destination, value);
+    if (&encrypted == &destination) return add_const_inplace(destination, value);
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
+    std::vector<std::uint64_t> r(lv.L);
+    chk(mhe_ckks_encode_scalar_at(context_.engine(), value, encrypted.scale(), (int)L1, (int)lv.L, r.data()));
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+    void *s = context_.stream();
+    const std::size_t pw = lv.L * lv.n;
+    fresh_dest(context_, encrypted, destination, encrypted.size());
+    const std::uint64_t *a = encrypted.store().dev_read(s);
+    std::uint64_t *d = destination.store().dev_write(s, true);
+    chk(mhe_add_scalar(context_.engine(), a, r.data(), d, 1, (int)lv.L, s));
+    if (encrypted.size() > 1)
+        chk(mhe_memcpy_d2d(context_.engine(), d + pw, a + pw, (encrypted.size() - 1) * pw * 8, s));
 }
 
 void Evaluator::multiply_const_inplace(Ciphertext &encrypted, double value) const
@@ -1745,8 +1842,19 @@ void Evaluator::multiply_const_inplace(Ciphertext &encrypted, double value) cons
 
 void Evaluator::multiply_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const
 {
-    destination = encrypted;
-    multiply_const_inplace(destination, value);
+    if (&encrypted == &destination) return multiply_const_inplace(destination, value);
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
+    std::vector<std::uint64_t> r(lv.L);
+    chk(mhe_ckks_encode_scalar_at(context_.engine(), value, encrypted.scale(), (int)L1, (int)lv.L, r.data()));
+    if (!encrypted.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+    const double new_scale = encrypted.scale() * encrypted.scale();
+    check_scale(new_scale, lv);
+    void *s = context_.stream();
+    fresh_dest(context_, encrypted, destination, encrypted.size());
+    chk(mhe_multiply_scalar(context_.engine(), encrypted.store().dev_read(s), r.data(),
+                            destination.store().dev_write(s, true), (int)encrypted.size(), (int)lv.L, s));
+    destination.scale() = new_scale;
 }
 
 namespace

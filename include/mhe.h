@@ -132,6 +132,9 @@ int mhe_relinearize(mhe_ctx *ctx, uint64_t *ct3, const uint64_t *key, int key_li
  * (util/galois.cpp:192-218): ct[2][L][n] in place. */
 int mhe_apply_galois(mhe_ctx *ctx, uint64_t *ct, uint32_t galois_elt, const uint64_t *key, int key_limbs,
                      int limbs, void *stream);
+/* The same with the input left untouched: out[2][L][n] = KS-rotated in (out must not alias in). */
+int mhe_apply_galois_to(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, uint32_t galois_elt, const uint64_t *key,
+                        int key_limbs, int limbs, void *stream);
 /* GaloisTool::apply_galois_ntt alone on [polys][limbs][n] (out must not alias in). */
 int mhe_permute_galois(mhe_ctx *ctx, const uint64_t *in, uint32_t galois_elt, uint64_t *out, int polys, int limbs,
                        void *stream);

@@ -216,8 +216,13 @@ def test_rotate_vector(small, step):
     assert elt == O.galois_elt_from_step(ch.n, step)
     key = ch.rand_key()
     ct = ch.rand(2, L, ch.n)
-    got = ch.down(ch.eng.apply_galois(ch.up(ct), elt, ch.up(key)))
-    assert np.array_equal(got, ch.oc.apply_galois(ct, elt, key))
+    want = ch.oc.apply_galois(ct, elt, key)
+    src = ch.up(ct)
+    got_to = ch.down(ch.eng.apply_galois_to(src, elt, ch.up(key)))  # out of place: input untouched
+    assert np.array_equal(got_to, want)
+    assert np.array_equal(ch.down(src), ct)
+    got = ch.down(ch.eng.apply_galois(src, elt, ch.up(key)))
+    assert np.array_equal(got, want)
 
 
 def test_apply_galois_ntt_permutation(small):
@@ -334,8 +339,13 @@ def test_rotate_c2_full_bit_exact(c2):
     key = ch.rand_key()
     ct = ch.rand(2, L, ch.n)
     elt = mhe.galois_elt_from_step(16, 5)
-    got = ch.down(ch.eng.apply_galois(ch.up(ct), elt, ch.up(key)))
-    assert np.array_equal(got, ch.oc.apply_galois(ct, elt, key))
+    want = ch.oc.apply_galois(ct, elt, key)
+    src = ch.up(ct)
+    got_to = ch.down(ch.eng.apply_galois_to(src, elt, ch.up(key)))  # out of place: input untouched
+    assert np.array_equal(got_to, want)
+    assert np.array_equal(ch.down(src), ct)
+    got = ch.down(ch.eng.apply_galois(src, elt, ch.up(key)))
+    assert np.array_equal(got, want)
 
 
 @pytest.mark.slow
