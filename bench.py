@@ -83,7 +83,7 @@ def cpu_baseline(moduli, L, threads, seconds_hint):
 RESNET20_CPU_S = 2188.8  # reference CPU SEAL, s/image, 1 thread per image (BASELINE.md / SURVEY.md §6)
 
 
-def resnet_leg(device, images, streams):
+def resnet_leg(device, images, streams, layers=20):
     """Second half of BASELINE.json's metric: seconds per image of encrypted ResNet-20 CIFAR-10
     (config C3: multiplexed conv + approximate ReLU + 18 bootstraps at N=2^16) on this GPU, run by
     build/resnet_test (include/mhe_resnet.h) with the reference's pretrained parameters on seeded
@@ -96,8 +96,9 @@ def resnet_leg(device, images, streams):
     if not os.path.exists(exe):
         return None
     env = dict(os.environ, MHE_DEVICE=str(device))
-    cmd = [exe, os.path.join(ROOT, "tests", "golden", "resnet", "resnet20_params.bin"),
-           os.path.join(ROOT, "tests", "golden", "comp"), str(images), "20", str(streams)]
+    params = "resnet20_params.bin" if layers == 20 else f"resnet{layers}_params.d7"
+    cmd = [exe, os.path.join(ROOT, "tests", "golden", "resnet", params),
+           os.path.join(ROOT, "tests", "golden", "comp"), str(images), str(layers), str(streams)]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900)
     if p.returncode != 0:
         raise RuntimeError("resnet_test failed:\n" + p.stdout[-2000:] + p.stderr[-2000:])
@@ -108,7 +109,8 @@ def resnet_leg(device, images, streams):
     setup = re.search(r"setup: ([0-9.]+) s", p.stdout)
     steady = per[1:] if len(per) > 1 else per
     return {
-        "workload": "C3: ResNet-20 CIFAR-10, N=2^16, 31+1 primes, sparse bootstrapping (logn 14/13/12)",
+        "workload": ("C3" if layers == 20 else "C4" if layers == 110 else "ResNet")
+        + f": ResNet-{layers} CIFAR-10, N=2^16, 31+1 primes, sparse bootstrapping (logn 14/13/12)",
         "data": "reference pretrained parameters (tests/golden/resnet), seeded synthetic images",
         "sec_per_image_1stream": round(sum(steady) / len(steady), 4),
         "bootstrap_s_per_image": round(boot[-1], 4) if boot else None,
@@ -117,7 +119,7 @@ def resnet_leg(device, images, streams):
         "batch_images": int(m.group(1)) if m else None,
         "streams": int(m.group(2)) if m else None,
         "setup_s": float(setup.group(1)) if setup else None,
-        "reference_cpu_sec_per_image": RESNET20_CPU_S,
+        "reference_cpu_sec_per_image": RESNET20_CPU_S if layers == 20 else None,
     }
 
 
@@ -149,6 +151,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--resnet-images", type=int, default=4,
                     help="ResNet-20 CIFAR-10 images per GPU for the sec/image leg (0 = skip)")
+    ap.add_argument("--resnet-layers", type=int, default=20, choices=(20, 110),
+                    help="20: config C3 (ResNet-20); 110: config C4's network (ResNet-110, one image per GPU "
+                         "with --resnet-images 1 --resnet-streams 1)")
     ap.add_argument("--resnet-streams", type=int, default=4, help="images in flight per GPU (one stream each)")
     ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams the batch is spread over (round robin; 4 = the hardware queues per process)")
@@ -321,7 +326,7 @@ def main():
         },
     }
     if args.resnet_images > 0:
-        r = resnet_leg(local, args.resnet_images, args.resnet_streams)
+        r = resnet_leg(local, args.resnet_images, args.resnet_streams, args.resnet_layers)
         if r is not None:
             t = torch.tensor([r["batch_wall_s"], r["sec_per_image_1stream"]], dtype=torch.float64, device=dev)
             if world > 1:
@@ -329,8 +334,9 @@ def main():
             r["batch_wall_s"], r["sec_per_image_1stream"] = float(t[0]), float(t[1])
             r["images_per_s"] = round(world * args.resnet_images / r["batch_wall_s"], 4)
             r["n_gpus"] = world
-            r["vs_reference_cpu"] = round(RESNET20_CPU_S / r["sec_per_image_1stream"], 1)
-            result["resnet20"] = r
+            if args.resnet_layers == 20:
+                r["vs_reference_cpu"] = round(RESNET20_CPU_S / r["sec_per_image_1stream"], 1)
+            result[f"resnet{args.resnet_layers}"] = r
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(moduli, L, args.cpu_threads, 20)
     if rank == 0:

@@ -26,6 +26,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <functional>
+#include <iosfwd>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -56,6 +57,37 @@ enum class sec_level_type : int
 
 using parms_id_type = std::array<std::uint64_t, 4>;
 extern const parms_id_type parms_id_zero;
+
+using seal_byte = std::byte;
+
+// SEAL/serialization.h: only uncompressed streams are produced and accepted (the reference builds
+// SEAL with ZLIB/ZSTD off for its drivers; a compressed stream is rejected as SEAL does).
+enum class compr_mode_type : std::uint8_t
+{
+    none = 0,
+    zlib = 1,
+    zstd = 2
+};
+
+class Serialization
+{
+public:
+    static constexpr std::uint16_t seal_magic = 0xA15E;
+    static constexpr std::uint8_t seal_header_size = 0x10;
+    static constexpr compr_mode_type compr_mode_default = compr_mode_type::none;
+    struct SEALHeader
+    {
+        std::uint16_t magic = seal_magic;
+        std::uint8_t header_size = seal_header_size;
+        std::uint8_t version_major = 3;
+        std::uint8_t version_minor = 6;
+        compr_mode_type compr_mode = compr_mode_type::none;
+        std::uint16_t reserved = 0;
+        std::uint64_t size = 0;
+    };
+    static_assert(sizeof(SEALHeader) == 16, "");
+    static bool IsValidHeader(const SEALHeader &header) noexcept;
+};
 
 class MemoryPoolHandle
 {
@@ -268,6 +300,15 @@ public:
     }
     std::size_t dyn_array_size() const noexcept { return store_.words(); }
 
+    // SEAL/ciphertext.h save/load (byte-compatible with SEAL 3.6, compr_mode_type::none)
+    std::streamoff save_size(compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff save(std::ostream &stream, compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff save(seal_byte *out, std::size_t size,
+                        compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff load(const SEALContext &context, std::istream &stream);
+    std::streamoff load(const SEALContext &context, const seal_byte *in, std::size_t size);
+    std::streamoff unsafe_load(const SEALContext &context, std::istream &stream) { return load(context, stream); }
+
     // engine plumbing
     PolyStore &store() noexcept { return store_; }
     const PolyStore &store() const noexcept { return store_; }
@@ -294,6 +335,14 @@ public:
     const std::uint64_t *data() const { return store_.host(); }
     std::uint64_t &operator[](std::size_t i) { return store_.host()[i]; }
     std::size_t limbs() const noexcept { return limbs_; }
+
+    // SEAL/plaintext.h save/load (byte-compatible with SEAL 3.6, compr_mode_type::none)
+    std::streamoff save_size(compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff save(std::ostream &stream, compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff save(seal_byte *out, std::size_t size,
+                        compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff load(const SEALContext &context, std::istream &stream);
+    std::streamoff load(const SEALContext &context, const seal_byte *in, std::size_t size);
 
     // engine plumbing
     void set_level(const SEALContext &ctx, const parms_id_type &id, std::size_t limbs);

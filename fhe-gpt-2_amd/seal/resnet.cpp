@@ -9,6 +9,7 @@
 #include <thread>
 #include <cmath>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
@@ -129,8 +130,26 @@ ResNetParams load_resnet_params_bin(const std::string &path, std::size_t layer_n
     shapes(layer_num, cs, bs);
     std::ifstream in(path, std::ios::binary);
     if (!in.is_open()) throw std::runtime_error("parameter file is not open: " + path);
+    // ".d7": 4-byte words sign | (exp + 64) << 24 | 7-digit mantissa, the reference's "%e" text
+    // losslessly (tests/golden/make_resnet_params.py); the decimal is re-formed and parsed with
+    // strtod, as the reference's `>>` parses its text
+    const bool d7 = path.size() > 3 && path.compare(path.size() - 3, 3, ".d7") == 0;
     auto take = [&](std::size_t count) {
         std::vector<double> v(count);
+        if (d7)
+        {
+            std::vector<std::uint32_t> w(count);
+            in.read(reinterpret_cast<char *>(w.data()), (std::streamsize)(count * sizeof(std::uint32_t)));
+            if (!in) throw std::runtime_error("parameter file is truncated: " + path);
+            char buf[32];
+            for (std::size_t i = 0; i < count; i++)
+            {
+                std::snprintf(buf, sizeof buf, "%s%ue%d", (w[i] >> 31) ? "-" : "", w[i] & 0xFFFFFFu,
+                              (int)((w[i] >> 24) & 0x7F) - 64 - 6);
+                v[i] = std::strtod(buf, nullptr);
+            }
+            return v;
+        }
         in.read(reinterpret_cast<char *>(v.data()), (std::streamsize)(count * sizeof(double)));
         if (!in) throw std::runtime_error("parameter file is truncated: " + path);
         return v;

@@ -179,15 +179,16 @@ std::uint64_t Blake2xbPRNGFactory::seed() const
     return seeded_ ? seed_ : fresh_seed(nullptr);
 }
 
+parms_id_type blake2b_parms_id(const std::uint64_t *words, std::size_t count); // serialize.cpp
+
 parms_id_type EncryptionParameters::parms_id() const
 {
-    // Opaque 256-bit identifier of (scheme, n, coeff_modulus) (SEAL hashes the same fields).
-    parms_id_type id{};
-    std::uint64_t st = 0x243f6a8885a308d3ULL ^ (std::uint64_t)scheme_;
-    st ^= splitmix(st) ^ n_;
-    for (auto &m : coeff_modulus_) st = splitmix(st) ^ m.value();
-    for (auto &w : id) w = splitmix(st);
-    return id;
+    // SEAL's parms_id (encryptionparams.cpp:124-158): BLAKE2b-256 of [scheme, n, coeff moduli...,
+    // plain modulus] as u64 words; the CKKS plain modulus is the zero Modulus (one word)
+    std::vector<std::uint64_t> w{ (std::uint64_t)scheme_, (std::uint64_t)n_ };
+    for (auto &m : coeff_modulus_) w.push_back(m.value());
+    w.push_back(0);
+    return blake2b_parms_id(w.data(), w.size());
 }
 
 // ------------------------------------------------------------------------------ SEALContext

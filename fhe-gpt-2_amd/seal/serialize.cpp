@@ -1,0 +1,295 @@
+// serialize.cpp -- SEAL 3.6 byte format for Ciphertext / Plaintext and SEAL's parms_id hash.
+//
+// Formats (SEAL/serialization.h:60-120, SEAL/ciphertext.cpp:183-345, SEAL/plaintext.cpp:204-300,
+// SEAL/dynarray.h:652-720):
+//   object    = SEALHeader(16 B: magic 0xA15E, header size 0x10, version 3.6, compr mode, 0, total
+//               size in bytes incl. the header) + members
+//   Ciphertext members = parms_id (4 x u64) | is_ntt_form (1 byte) | size u64 | poly_modulus_degree
+//               u64 | coeff_modulus_size u64 | scale f64 | DynArray
+//   Plaintext members  = parms_id | coeff_count u64 | scale f64 | DynArray
+//   DynArray  = SEALHeader + element count u64 + elements (u64, [poly][limb][n])
+// Only compr_mode_type::none is written or accepted.  Seeded (half-size) ciphertexts are not
+// produced by this library's Encryptor, so they are rejected on load.
+//
+// parms_id (SEAL/encryptionparams.cpp:124-158, util/hash.h:30-37) is BLAKE2b with a 32-byte digest
+// over the u64 words [scheme, poly_modulus_degree, coeff moduli..., plain modulus (0 for CKKS)].
+// BLAKE2b itself follows RFC 7693 (12 rounds, SHA-512 IV, no key).
+#include "seal/seal.h"
+
+#include <cstring>
+#include <istream>
+#include <ostream>
+#include <sstream>
+
+namespace seal
+{
+namespace
+{
+// ----------------------------------------------------------------------- BLAKE2b (RFC 7693)
+constexpr std::uint64_t kIV[8] = { 0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                                   0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                   0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL };
+constexpr std::uint8_t kSigma[12][16] = {
+    { 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15 }, { 14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3 },
+    { 11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4 }, { 7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8 },
+    { 9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13 }, { 2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9 },
+    { 12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11 }, { 13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10 },
+    { 6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5 }, { 10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0 },
+    { 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15 }, { 14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3 },
+};
+
+inline std::uint64_t rotr(std::uint64_t x, int r) { return (x >> r) | (x << (64 - r)); }
+
+void blake2b_compress(std::uint64_t h[8], const std::uint8_t block[128], std::uint64_t t, bool last)
+{
+    std::uint64_t m[16], v[16];
+    std::memcpy(m, block, 128); // little-endian host (x86-64 / gfx950 hosts)
+    for (int i = 0; i < 8; i++)
+    {
+        v[i] = h[i];
+        v[i + 8] = kIV[i];
+    }
+    v[12] ^= t; // the byte counter never exceeds 2^64 here
+    if (last) v[14] = ~v[14];
+    auto G = [&](int a, int b, int c, int d, std::uint64_t x, std::uint64_t y) {
+        v[a] = v[a] + v[b] + x;
+        v[d] = rotr(v[d] ^ v[a], 32);
+        v[c] = v[c] + v[d];
+        v[b] = rotr(v[b] ^ v[c], 24);
+        v[a] = v[a] + v[b] + y;
+        v[d] = rotr(v[d] ^ v[a], 16);
+        v[c] = v[c] + v[d];
+        v[b] = rotr(v[b] ^ v[c], 63);
+    };
+    for (int r = 0; r < 12; r++)
+    {
+        const std::uint8_t *s = kSigma[r];
+        G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+        G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+        G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+        G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+        G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+        G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+        G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+        G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+    }
+    for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[i + 8];
+}
+
+template <class T>
+void put(std::ostream &s, const T &v)
+{
+    s.write(reinterpret_cast<const char *>(&v), sizeof(T));
+}
+template <class T>
+T get(std::istream &s)
+{
+    T v{};
+    s.read(reinterpret_cast<char *>(&v), sizeof(T));
+    if (!s) throw std::runtime_error("I/O error");
+    return v;
+}
+
+Serialization::SEALHeader read_header(std::istream &s)
+{
+    auto h = get<Serialization::SEALHeader>(s);
+    if (!Serialization::IsValidHeader(h)) throw std::logic_error("loaded SEALHeader is invalid");
+    if (h.compr_mode != compr_mode_type::none) throw std::logic_error("unsupported compression mode");
+    return h;
+}
+
+void write_header(std::ostream &s, std::uint64_t total, compr_mode_type mode)
+{
+    if (mode != compr_mode_type::none) throw std::invalid_argument("unsupported compression mode");
+    Serialization::SEALHeader h;
+    h.size = total;
+    put(s, h);
+}
+
+constexpr std::streamoff kHeader = sizeof(Serialization::SEALHeader);
+
+// DynArray<u64>: header + count + words
+std::streamoff dynarray_size(std::size_t words) { return kHeader + 8 + (std::streamoff)(8 * words); }
+void write_dynarray(std::ostream &s, const std::uint64_t *p, std::size_t words)
+{
+    write_header(s, (std::uint64_t)dynarray_size(words), compr_mode_type::none);
+    put<std::uint64_t>(s, words);
+    if (words) s.write(reinterpret_cast<const char *>(p), (std::streamsize)(8 * words));
+}
+// reads the count (bounded by `max_words`, SEAL's in_size check) into `out`
+void read_dynarray(std::istream &s, std::vector<std::uint64_t> &out, std::size_t max_words)
+{
+    const auto h = read_header(s);
+    const auto words = get<std::uint64_t>(s);
+    if (words > max_words || h.size != (std::uint64_t)dynarray_size(words))
+        throw std::logic_error("ciphertext data is invalid");
+    out.resize(words);
+    if (words) s.read(reinterpret_cast<char *>(out.data()), (std::streamsize)(8 * words));
+    if (!s) throw std::runtime_error("I/O error");
+}
+
+template <class Obj>
+std::streamoff save_to_buffer(const Obj &o, seal_byte *out, std::size_t size, compr_mode_type mode)
+{
+    const std::streamoff need = o.save_size(mode);
+    if (!out || (std::streamoff)size < need) throw std::invalid_argument("insufficient size");
+    std::ostringstream ss(std::ios::binary);
+    o.save(ss, mode);
+    const std::string b = ss.str();
+    std::memcpy(out, b.data(), b.size());
+    return (std::streamoff)b.size();
+}
+
+template <class Obj>
+std::streamoff load_from_buffer(Obj &o, const SEALContext &ctx, const seal_byte *in, std::size_t size)
+{
+    if (!in) throw std::invalid_argument("in cannot be null");
+    std::istringstream ss(std::string(reinterpret_cast<const char *>(in), size), std::ios::binary);
+    return o.load(ctx, ss);
+}
+
+// residues of a [polys][limbs][n] block must be canonical (SEAL: is_data_valid_for)
+bool residues_valid(const std::vector<std::uint64_t> &w, const std::vector<Modulus> &cm, std::size_t n)
+{
+    const std::size_t L = cm.size();
+    for (std::size_t i = 0; i < w.size(); i++)
+        if (w[i] >= cm[(i / n) % L].value()) return false;
+    return true;
+}
+} // namespace
+
+parms_id_type blake2b_parms_id(const std::uint64_t *words, std::size_t count)
+{
+    std::uint64_t h[8];
+    for (int i = 0; i < 8; i++) h[i] = kIV[i];
+    h[0] ^= 0x01010000ULL ^ 32; // no key, 32-byte digest
+    const std::size_t bytes = count * 8;
+    const auto *p = reinterpret_cast<const std::uint8_t *>(words);
+    std::uint8_t block[128];
+    std::size_t off = 0;
+    while (bytes - off > 128)
+    {
+        std::memcpy(block, p + off, 128);
+        off += 128;
+        blake2b_compress(h, block, off, false);
+    }
+    std::memset(block, 0, 128);
+    std::memcpy(block, p + off, bytes - off);
+    blake2b_compress(h, block, bytes, true);
+    parms_id_type id;
+    for (int i = 0; i < 4; i++) id[i] = h[i];
+    return id;
+}
+
+bool Serialization::IsValidHeader(const SEALHeader &h) noexcept
+{
+    return h.magic == seal_magic && h.header_size == seal_header_size && h.version_major == 3 &&
+           (h.version_minor == 6 || h.version_minor == 5 || h.version_minor == 4) &&
+           (std::uint8_t)h.compr_mode <= 2 && h.size >= seal_header_size;
+}
+
+// ------------------------------------------------------------------------------ Ciphertext
+std::streamoff Ciphertext::save_size(compr_mode_type) const
+{
+    return kHeader + 32 + 1 + 8 * 3 + 8 + dynarray_size(store_.words());
+}
+
+std::streamoff Ciphertext::save(std::ostream &stream, compr_mode_type mode) const
+{
+    const std::streamoff total = save_size(mode);
+    write_header(stream, (std::uint64_t)total, mode);
+    put(stream, parms_id_);
+    put<std::uint8_t>(stream, is_ntt_form_ ? 1 : 0);
+    put<std::uint64_t>(stream, size_);
+    put<std::uint64_t>(stream, poly_modulus_degree_);
+    put<std::uint64_t>(stream, coeff_modulus_size_);
+    put<double>(stream, scale_);
+    write_dynarray(stream, store_.words() ? data() : nullptr, store_.words());
+    if (!stream) throw std::runtime_error("I/O error");
+    return total;
+}
+
+std::streamoff Ciphertext::save(seal_byte *out, std::size_t size, compr_mode_type mode) const
+{
+    return save_to_buffer(*this, out, size, mode);
+}
+
+std::streamoff Ciphertext::load(const SEALContext &context, std::istream &stream)
+{
+    const auto h = read_header(stream);
+    const auto id = get<parms_id_type>(stream);
+    const auto ntt = get<std::uint8_t>(stream);
+    const auto size = get<std::uint64_t>(stream);
+    const auto n = get<std::uint64_t>(stream);
+    const auto L = get<std::uint64_t>(stream);
+    const auto scale = get<double>(stream);
+    // metadata validity (SEAL: is_metadata_valid_for, pure key levels allowed)
+    auto cd = context.get_context_data(id);
+    if (!cd || ntt > 1 || cd->parms().poly_modulus_degree() != n || cd->parms().coeff_modulus().size() != L ||
+        (size != 0 && (size < 2 || size > 16)))
+        throw std::logic_error("ciphertext data is invalid");
+    std::vector<std::uint64_t> w;
+    read_dynarray(stream, w, (std::size_t)(size * n * L));
+    if (w.size() != size * n * L || !residues_valid(w, cd->parms().coeff_modulus(), n) ||
+        h.size != (std::uint64_t)(kHeader + 32 + 1 + 24 + 8 + dynarray_size(w.size())))
+        throw std::logic_error("ciphertext data is invalid");
+    resize(context, id, (std::size_t)size);
+    is_ntt_form_ = ntt != 0;
+    scale_ = scale;
+    if (!w.empty()) std::memcpy(data(), w.data(), 8 * w.size());
+    return (std::streamoff)h.size;
+}
+
+std::streamoff Ciphertext::load(const SEALContext &context, const seal_byte *in, std::size_t size)
+{
+    return load_from_buffer(*this, context, in, size);
+}
+
+// ------------------------------------------------------------------------------ Plaintext
+std::streamoff Plaintext::save_size(compr_mode_type) const { return kHeader + 32 + 8 + 8 + dynarray_size(store_.words()); }
+
+std::streamoff Plaintext::save(std::ostream &stream, compr_mode_type mode) const
+{
+    const std::streamoff total = save_size(mode);
+    write_header(stream, (std::uint64_t)total, mode);
+    put(stream, parms_id_);
+    put<std::uint64_t>(stream, store_.words());
+    put<double>(stream, scale_);
+    write_dynarray(stream, store_.words() ? data() : nullptr, store_.words());
+    if (!stream) throw std::runtime_error("I/O error");
+    return total;
+}
+
+std::streamoff Plaintext::save(seal_byte *out, std::size_t size, compr_mode_type mode) const
+{
+    return save_to_buffer(*this, out, size, mode);
+}
+
+std::streamoff Plaintext::load(const SEALContext &context, std::istream &stream)
+{
+    const auto h = read_header(stream);
+    const auto id = get<parms_id_type>(stream);
+    const auto count = get<std::uint64_t>(stream);
+    const auto scale = get<double>(stream);
+    // CKKS plaintexts are in NTT form at a chain level (parms_id_zero marks BFV-style coefficient
+    // plaintexts, which the CKKS-only surface does not carry)
+    auto cd = context.get_context_data(id);
+    if (!cd) throw std::logic_error("plaintext data is invalid");
+    const std::size_t n = cd->parms().poly_modulus_degree(), L = cd->parms().coeff_modulus().size();
+    if (count != n * L) throw std::logic_error("plaintext data is invalid");
+    std::vector<std::uint64_t> w;
+    read_dynarray(stream, w, (std::size_t)count);
+    if (w.size() != count || !residues_valid(w, cd->parms().coeff_modulus(), n) ||
+        h.size != (std::uint64_t)(kHeader + 32 + 8 + 8 + dynarray_size(w.size())))
+        throw std::logic_error("plaintext data is invalid");
+    set_level(context, id, L);
+    scale_ = scale;
+    std::memcpy(data(), w.data(), 8 * w.size());
+    return (std::streamoff)h.size;
+}
+
+std::streamoff Plaintext::load(const SEALContext &context, const seal_byte *in, std::size_t size)
+{
+    return load_from_buffer(*this, context, in, size);
+}
+} // namespace seal

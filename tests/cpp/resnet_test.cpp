@@ -103,17 +103,43 @@ int main(int argc, char **argv)
 {
     if (argc < 3)
     {
-        std::fprintf(stderr, "usage: resnet_test <params.bin> <comp_dir> [images] [layers]\n");
+        std::fprintf(stderr, "usage: resnet_test <params.bin|.d7> <comp_dir> [images (-1: load only)] [layers] [threads]\n");
         return 2;
     }
     const int images = argc > 3 ? std::atoi(argv[3]) : 1;
     const std::size_t layers = argc > 4 ? std::atoi(argv[4]) : 20;
     const int threads = argc > 5 ? std::atoi(argv[5]) : 0;
+    const int end_num = (int)(layers - 2) / 6 - 1; // infer_seal.cpp: 20 -> 2, 110 -> 17
     const ResNetParams prm = load_resnet_params_bin(argv[1], layers);
+    if (images < 0)
+    {
+        // host-only fixture check (no GPU): value count and sum in load order
+        double sum = 0;
+        std::size_t count = 0;
+        auto acc = [&](const std::vector<double> &v) {
+            for (double x : v) sum += x;
+            count += v.size();
+        };
+        for (auto &v : prm.conv_weight) acc(v);
+        for (std::size_t i = 0; i < prm.bn_bias.size(); i++)
+        {
+            acc(prm.bn_bias[i]);
+            acc(prm.bn_running_mean[i]);
+            acc(prm.bn_running_var[i]);
+            acc(prm.bn_weight[i]);
+        }
+        acc(prm.linear_weight);
+        acc(prm.linear_bias);
+        std::printf("params: %zu values, sum %.17g\n", count, sum);
+        return 0;
+    }
     ResNetRunner runner(layers, prm, argv[2]);
     std::printf("setup: %.2f s\n", runner.setup_seconds());
     int fail = 0;
     double total = 0;
+    // decrypted logits vs the plain network with the exact ReLU: the approximate ReLU's error
+    // (alpha 13) compounds with depth, so the deeper networks get a wider band
+    const double tol = layers <= 20 ? 0.05 : 0.08;
     const int sequential = threads > 0 ? std::min(images, 2) : images; // latency pass (first one warms caches)
     for (int id = 0; id < sequential; id++)
     {
@@ -122,7 +148,7 @@ int main(int argc, char **argv)
         std::vector<double> img(3072);
         for (auto &x : img) x = U(g);
         const ResNetResult r = runner.infer(img);
-        const std::vector<double> want = plain_resnet(prm, img, 2);
+        const std::vector<double> want = plain_resnet(prm, img, end_num);
         double err = 0, mag = 0;
         std::size_t wl = 0;
         for (int i = 0; i < 10; i++)
@@ -141,7 +167,7 @@ int main(int argc, char **argv)
         for (double v : want) std::printf(" %.4f", v);
         std::printf("\n");
         if (id > 0 || sequential == 1) total += r.seconds;
-        if (!(err < 0.05 * std::max(1.0, mag))) fail++;
+        if (!(err < tol * std::max(1.0, mag))) fail++;
     }
     if (threads > 0)
     {
@@ -160,10 +186,15 @@ int main(int argc, char **argv)
         const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int id = 0; id < images; id++)
         {
-            const std::vector<double> want = plain_resnet(prm, batch[id], 2);
-            double err = 0;
-            for (int i = 0; i < 10; i++) err = std::max(err, std::fabs(rs[id].logits[i] - want[i]));
-            if (!(err < 0.6)) fail++;
+            const std::vector<double> want = plain_resnet(prm, batch[id], end_num);
+            double err = 0, mag = 0;
+            for (int i = 0; i < 10; i++)
+            {
+                err = std::max(err, std::fabs(rs[id].logits[i] - want[i]));
+                mag = std::max(mag, std::fabs(want[i]));
+            }
+            std::printf("  batch image %d: max |logit error| %.3g of max |logit| %.3g\n", id, err, mag);
+            if (!(err < tol * std::max(1.0, mag))) fail++;
         }
         std::printf("batch: %d images on %d streams in %.3f s = %.3f s/image (%.3f images/s)\n", images, threads, wall,
                     wall / images, images / wall);

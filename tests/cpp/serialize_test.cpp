@@ -1,0 +1,182 @@
+// Serialization of the SEAL surface (fhe-gpt-2_amd/seal/serialize.cpp): SEAL 3.6's byte format for
+// Ciphertext / Plaintext and SEAL's BLAKE2b parms_id.
+//   serialize_test parms            -- host only: prints the parms_id of the CNN chain (checked
+//                                      against hashlib.blake2b by tests/test_serialize.py)
+//   serialize_test roundtrip <dir>  -- GPU: save/load round trips (stream and buffer), decrypts after
+//                                      load, rejects corrupt streams; writes ct.bin / pt.bin into
+//                                      <dir> for the independent Python parser of the format
+// Follows the reference's SEAL tests CiphertextTest.SaveLoadCiphertext and
+// PlaintextTest.SaveLoadPlaintext (native/tests/seal/ciphertext.cpp, plaintext.cpp).
+#include "seal/seal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+using namespace seal;
+
+static int g_fail = 0;
+#define CHECK(cond)                                                                  \
+    do                                                                               \
+    {                                                                                \
+        if (!(cond))                                                                 \
+        {                                                                            \
+            g_fail++;                                                                \
+            std::fprintf(stderr, "  FAILED %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+        }                                                                            \
+    } while (0)
+
+template <typename F>
+static bool throws(F f)
+{
+    try
+    {
+        f();
+    }
+    catch (const std::exception &)
+    {
+        return true;
+    }
+    return false;
+}
+
+static EncryptionParameters cnn_parms(std::size_t n)
+{
+    // cnn/infer_seal.cpp:306-310 chain: {51} + 30 x {46} + {51 special}
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(n);
+    std::vector<int> bits{ 51 };
+    for (int i = 0; i < 30; i++) bits.push_back(46);
+    bits.push_back(51);
+    parms.set_coeff_modulus(CoeffModulus::Create(n, bits));
+    return parms;
+}
+
+static void print_id(const char *tag, const parms_id_type &id)
+{
+    std::printf("%s", tag);
+    for (auto w : id) std::printf(" %016llx", (unsigned long long)w);
+    std::printf("\n");
+}
+
+int main(int argc, char **argv)
+{
+    const std::string mode = argc > 1 ? argv[1] : "parms";
+    if (mode == "parms")
+    {
+        for (std::size_t n : { 1u << 12, 1u << 16 })
+        {
+            auto p = cnn_parms(n);
+            std::printf("moduli %zu", n);
+            for (auto &m : p.coeff_modulus()) std::printf(" %llu", (unsigned long long)m.value());
+            std::printf("\n");
+            print_id("parms_id", p.parms_id());
+        }
+        return 0;
+    }
+    const std::string dir = argc > 2 ? argv[2] : ".";
+    const std::size_t n = 1 << 13;
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(n);
+    parms.set_coeff_modulus(CoeffModulus::Create(n, { 51, 46, 46, 51 }));
+    SEALContext ctx(parms, true, sec_level_type::none);
+    KeyGenerator keygen(ctx);
+    PublicKey pk;
+    keygen.create_public_key(pk);
+    CKKSEncoder encoder(ctx);
+    Encryptor encryptor(ctx, pk);
+    Decryptor decryptor(ctx, keygen.secret_key());
+    const double scale = std::pow(2.0, 46);
+    std::vector<double> x(encoder.slot_count());
+    for (std::size_t i = 0; i < x.size(); i++) x[i] = 0.5 * std::cos(0.001 * (double)i);
+    Plaintext pt;
+    encoder.encode(x, scale, pt);
+    Ciphertext ct;
+    encryptor.encrypt(pt, ct);
+    print_id("first_parms_id", ctx.first_parms_id());
+    CHECK(ctx.first_parms_id() == parms.parms_id() || ctx.key_parms_id() == parms.parms_id());
+
+    // stream round trip
+    std::stringstream ss;
+    const auto wrote = ct.save(ss);
+    CHECK(wrote == ct.save_size());
+    CHECK((std::streamoff)ss.str().size() == wrote);
+    Ciphertext ct2;
+    const auto read = ct2.load(ctx, ss);
+    CHECK(read == wrote);
+    CHECK(ct2.parms_id() == ct.parms_id());
+    CHECK(ct2.size() == ct.size() && ct2.coeff_modulus_size() == ct.coeff_modulus_size());
+    CHECK(ct2.poly_modulus_degree() == n && ct2.is_ntt_form() && ct2.scale() == ct.scale());
+    CHECK(std::memcmp(ct2.data(), ct.data(), 8 * ct.dyn_array_size()) == 0);
+    Plaintext back;
+    decryptor.decrypt(ct2, back);
+    std::vector<double> y;
+    encoder.decode(back, y);
+    double err = 0;
+    for (std::size_t i = 0; i < x.size(); i++) err = std::max(err, std::fabs(y[i] - x[i]));
+    std::printf("decrypt after load: max error %.3g\n", err);
+    CHECK(err < 1e-6);
+
+    // buffer round trip, lower level
+    Evaluator evaluator(ctx, encoder);
+    Ciphertext low;
+    evaluator.mod_switch_to_next(ct, low);
+    std::vector<seal_byte> buf((std::size_t)low.save_size());
+    CHECK(low.save(buf.data(), buf.size()) == (std::streamoff)buf.size());
+    CHECK(throws([&] { low.save(buf.data(), buf.size() - 1); }));
+    Ciphertext low2;
+    low2.load(ctx, buf.data(), buf.size());
+    CHECK(low2.parms_id() == low.parms_id() && low2.coeff_modulus_size() == low.coeff_modulus_size());
+    CHECK(std::memcmp(low2.data(), low.data(), 8 * low.dyn_array_size()) == 0);
+
+    // plaintext round trip
+    std::stringstream ps;
+    CHECK(pt.save(ps) == pt.save_size());
+    Plaintext pt2;
+    pt2.load(ctx, ps);
+    CHECK(pt2.parms_id() == pt.parms_id() && pt2.scale() == pt.scale() && pt2.coeff_count() == pt.coeff_count());
+    CHECK(std::memcmp(pt2.data(), pt.data(), 8 * pt.coeff_count()) == 0);
+
+    // corrupt streams are rejected
+    std::string good = [&] {
+        std::stringstream t;
+        ct.save(t);
+        return t.str();
+    }();
+    auto load_str = [&](const std::string &s) {
+        std::stringstream t(s);
+        Ciphertext c;
+        c.load(ctx, t);
+    };
+    CHECK(!throws([&] { load_str(good); }));
+    std::string bad = good;
+    bad[0] ^= 1; // magic
+    CHECK(throws([&] { load_str(bad); }));
+    bad = good;
+    bad[5] = 2; // zstd
+    CHECK(throws([&] { load_str(bad); }));
+    bad = good;
+    bad[16] ^= 0x40; // parms_id
+    CHECK(throws([&] { load_str(bad); }));
+    bad = good;
+    std::uint64_t q0 = ctx.first_context_data()->parms().coeff_modulus()[0].value();
+    std::memcpy(&bad[16 + 32 + 1 + 32 + 16 + 8], &q0, 8); // first residue = q_0: not canonical
+    CHECK(throws([&] { load_str(bad); }));
+    CHECK(throws([&] { load_str(good.substr(0, good.size() - 8)); })); // truncated
+
+    // files for the Python-side format check
+    {
+        std::ofstream f(dir + "/ct.bin", std::ios::binary);
+        ct.save(f);
+        std::ofstream g(dir + "/pt.bin", std::ios::binary);
+        pt.save(g);
+        std::ofstream m(dir + "/moduli.txt");
+        for (auto &q : ctx.first_context_data()->parms().coeff_modulus()) m << q.value() << "\n";
+    }
+    std::printf("%s\n", g_fail ? "FAILED" : "ok");
+    return g_fail ? 1 : 0;
+}

@@ -3,6 +3,7 @@ the CPU side checks that it loads; the GPU side runs tests/cpp/seal_api_test.cpp
 reference's CKKS GoogleTest scenarios written against the same API -- end to end."""
 import ctypes
 import os
+import sys
 import subprocess
 
 import pytest
@@ -110,6 +111,50 @@ def test_resnet_params_fixture():
         var = v[off + 2 * c: off + 3 * c]
         assert (var > 0).all()
         off += 4 * c
+
+
+@pytest.mark.gpu
+def test_resnet110_end_to_end():
+    """Config C4's network: encrypted ResNet-110 CIFAR-10 (end_num 17: 54 residual blocks, 108
+    sparse-slot bootstraps) with the reference's pretrained ResNet-110 parameters
+    (tests/golden/resnet/resnet110_params.d7) on one seeded synthetic image; decrypted logits vs the
+    plain network within 8% of the largest logit (tests/cpp/resnet_test.cpp)."""
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "resnet_test"),
+                        os.path.join(ROOT, "tests", "golden", "resnet", "resnet110_params.d7"),
+                        os.path.join(ROOT, "tests", "golden", "comp"), "1", "110"],
+                       capture_output=True, text=True, timeout=900)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_resnet110_params_fixture():
+    """The lossless 4-byte ".d7" packing of ResNet-110's parameters: the C++ loader
+    (load_resnet_params_bin) and the Python decoder of make_resnet_params.py agree value for value
+    (count and left-to-right sum printed by `resnet_test ... -1 110`, no GPU); where the reference
+    is mounted, the decoded values equal the reference's text parsed as doubles."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_resnet_params as m
+
+    path = os.path.join(ROOT, "tests", "golden", "resnet", "resnet110_params.d7")
+    v = m.unpack_d7(open(path, "rb").read())
+    conv = 9 * 3 * 16 + 18 * 2 * 9 * 16 * 16 + 9 * 16 * 32 + 9 * 32 * 32 + 17 * 2 * 9 * 32 * 32 \
+        + 9 * 32 * 64 + 9 * 64 * 64 + 17 * 2 * 9 * 64 * 64
+    assert v.size == conv + 4 * (16 + 36 * (16 + 32 + 64)) + 640 + 10
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "resnet_test"), path, "unused", "-1", "110"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"params: {v.size} values, sum {sum(v.tolist())!r}" in r.stdout, r.stdout
+    src = "/root/reference/pretrained_parameters/resnet110_new"
+    if os.path.isdir(src):
+        w = np.array([float(t) for t in open(os.path.join(src, "conv1_weight.txt")).read().split()[:432]])
+        assert np.array_equal(v[:432], w)
+        b = np.array([float(t) for t in open(os.path.join(src, "linear_bias.txt")).read().split()[:10]])
+        assert np.array_equal(v[-10:], b)
 
 
 @pytest.mark.gpu
