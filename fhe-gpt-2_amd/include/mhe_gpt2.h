@@ -1,0 +1,110 @@
+// mhe_gpt2.h -- the GPT-2 approximation and packed-matmul layer of the reference
+// (gpt2_ckks/gpt2-ckks/single-key/gpt2/: PolyApprox.cpp, IterApprox.cpp, Fold.cpp, MatrixMul.cpp,
+// util.cpp, pack.cpp) over the MI355X seal:: surface.  Same names, argument order and operation
+// sequence as the reference, so its callers and its doctest cases (gpt2_ckks/run/
+// run_approx_test.cpp) read unchanged; every ciphertext operation runs on the GPU.
+//
+// Deviations, by design:
+//  * sign_function / compute_gelu take and return Ciphertext instead of the GPT-2 TensorCipher
+//    wrapper (gpt2/tensor.h; the wrapper only carries the ciphertext on this path) and drop the
+//    Bootstrapper argument, which the reference accepts but never uses on this path
+//    (PolyApprox.cpp:308-334, 443-504);
+//  * the debugging printf()s of the reference are not reproduced;
+//  * compute_gelu_q rescales its last product before the final add (PolyApprox.cpp:429-431 adds it
+//    unrescaled, which loses half the polynomial; see gpt2.cpp).
+#pragma once
+
+#include <vector>
+
+#include "seal/seal.h"
+
+namespace gpt2
+{
+using seal::CKKSEncoder;
+using seal::Ciphertext;
+using seal::Decryptor;
+using seal::Encryptor;
+using seal::Evaluator;
+using seal::GaloisKeys;
+using seal::RelinKeys;
+
+constexpr int LOGP = 46, LOGQ = 49, BOOT_LEVEL = 14; // gpt2/util.h:22-25
+double encode_scale();                               // ENCODE_SCALE, 2^LOGP by default
+// The reference hard-codes ENCODE_SCALE = 2^46, but its *_reduced_error ops overwrite scales and so
+// assume the scale tracks the primes being rescaled away; on its own chain ({49} + 21 x {46} +
+// 14 x {49}) the top levels rescale by 49-bit primes and a 2^46 scale collapses to ~2^1 within one
+// Chebyshev evaluation.  Callers working at scale 2^49 set the plaintexts' scale to match.
+void set_encode_scale(double scale);
+
+// util.cpp:258-261: next power of two
+int round_to_2(double x);
+
+// PolyApprox.cpp:14-101: [T0, T1, T2, T3, T4, T8, ...] -- T0 an encryption of ones, T2 = 2x^2 - 1,
+// T3 = 2x T2 - x, then n-2 doublings T_{2k} = 2 T_k^2 - 1
+void build_cheby_basis(Ciphertext &input, std::vector<Ciphertext> &chebyBasis, int n, CKKSEncoder &encoder,
+                       Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                       RelinKeys &relin_keys);
+
+// PolyApprox.cpp:103-305: the two composite-sign polynomials f and g in the Chebyshev basis
+void compute_sign_f(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void compute_sign_g(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// PolyApprox.cpp:308-334: sign(x) ~ f^(df) o g^(dg) (x), applied in pairs
+void sign_function(const Ciphertext &input, Ciphertext &output, int df, int dg, CKKSEncoder &encoder,
+                   Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                   RelinKeys &relin_keys);
+
+// PolyApprox.cpp:336-433: the two GELU pieces
+void compute_gelu_p(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void compute_gelu_q(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// PolyApprox.cpp:443-504: piecewise GELU = b1 p(x) + b2 q(x) + b3 x with b from three signs
+void compute_gelu(Ciphertext &inputs, Ciphertext &outputs, CKKSEncoder &encoder, Encryptor &encryptor,
+                  Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// PolyApprox.cpp:511-531: exp(x) ~ (1 + x/2^r)^(2^r)
+void compute_exp(Ciphertext &input, Ciphertext &output, int r, CKKSEncoder &encoder, Encryptor &encryptor,
+                 Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// IterApprox.cpp:15-68: Goldschmidt 1/x (inputs normalised by 0.001)
+void compute_inverse(Ciphertext &input, Ciphertext &output, int iters, CKKSEncoder &encoder, Encryptor &encryptor,
+                     Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// Fold.cpp:20-45: out = sum of input rotated by 0, 1, 2, ..., n/2 (log2(n) rotate+add steps)
+void quickSum(Ciphertext &input, Ciphertext &output, int n, CKKSEncoder &encoder, Encryptor &encryptor,
+              Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// util.cpp:292-301: keep slots [start, start+length), rescaled
+void mask_out(Ciphertext &cipher, Ciphertext &out, int start, int length, CKKSEncoder &encoder, Evaluator &evaluator,
+              RelinKeys &relin_keys);
+
+// util.cpp:303-316: row i of v at slot i * 2 * round_to_2(row_size) (32768-slot ciphertexts)
+void pack_plain_row(std::vector<std::vector<double>> &v, int rows, int row_size,
+                    std::vector<std::vector<double>> &out);
+
+// pack.cpp:153-178: pack_plain_row + encode at ENCODE_SCALE + encrypt
+void pack_from_row(std::vector<std::vector<double>> &input, std::vector<Ciphertext> &output, CKKSEncoder &encoder,
+                   Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                   RelinKeys &relin_keys);
+
+// util.cpp:277-290: num_ciphers encryptions of zero at ENCODE_SCALE
+void init_output(int num_ciphers, std::vector<Ciphertext> &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                 Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// MatrixMul.cpp:118-188: A x W^T for row-packed A (A_rows x A_cols) and W (W_rows x W_cols), both
+// encrypted; per (input, weight, chunk rotation): rotate, multiply, fold, quickSum, then every chunk
+// is masked and rotated into its output position; bias added at the end
+void row_matrix_multiplication_seal(std::vector<Ciphertext> &left_inputs, std::vector<Ciphertext> &weights,
+                                    Ciphertext bias, std::vector<Ciphertext> &outputs, int A_rows, int A_cols,
+                                    int W_rows, int W_cols, CKKSEncoder &encoder, Encryptor &encryptor,
+                                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                                    RelinKeys &relin_keys);
+
+// The rotation steps of the reference's INIT() (gpt2/util.h:36-74): powers of two below N/2, the
+// listed rotation_kinds and the multiples of 2048
+std::vector<int> gpt2_rotation_steps(int logN);
+} // namespace gpt2

@@ -1,0 +1,404 @@
+// gpt2.cpp -- GPT-2 approximations, folds and the row-packed matmul of the reference
+// (gpt2_ckks/gpt2-ckks/single-key/gpt2/) over the MI355X seal:: surface; see mhe_gpt2.h.
+// Each function keeps the reference's operation sequence (levels and scales therefore match the
+// reference's), citing the lines it follows.
+#include "mhe_gpt2.h"
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+
+namespace gpt2
+{
+using seal::Plaintext;
+
+namespace
+{
+double g_encode_scale = 70368744177664.0; // 2^LOGP
+}
+double encode_scale() { return g_encode_scale; }
+void set_encode_scale(double scale)
+{
+    if (!(scale > 0)) throw std::invalid_argument("set_encode_scale: scale must be positive");
+    g_encode_scale = scale;
+}
+
+int round_to_2(double x) { return (int)std::pow(2.0, std::ceil(std::log2(x))); } // util.cpp:258-261
+
+void build_cheby_basis(Ciphertext &input, std::vector<Ciphertext> &chebyBasis, int n, CKKSEncoder &encoder,
+                       Encryptor &encryptor, Decryptor &, Evaluator &evaluator, GaloisKeys &, RelinKeys &relin_keys)
+{
+    if (n <= 0) throw std::invalid_argument("build_cheby_basis: n must be positive");
+    // PolyApprox.cpp:29-35: T0 = Enc(1) at the input's scale, T1 = x
+    Plaintext plain;
+    Ciphertext cipher, tmp_cipher, tmp2;
+    std::vector<double> ones(encoder.slot_count(), 1.0);
+    encoder.encode(ones, input.scale(), plain);
+    encryptor.encrypt(plain, cipher);
+    chebyBasis.push_back(cipher);
+    chebyBasis.push_back(input);
+    // :36-52: T2 = 2 x^2 - 1
+    cipher = input;
+    evaluator.square_inplace(cipher);
+    evaluator.relinearize_inplace(cipher, relin_keys);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.add_inplace(cipher, cipher);
+    evaluator.add_const_inplace(cipher, -1.0);
+    chebyBasis.push_back(cipher);
+    // :57-75: T3 = 2x T2 - x
+    evaluator.add(input, input, tmp2);
+    evaluator.multiply_reduced_error(tmp2, cipher, relin_keys, tmp_cipher);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.multiply_const(input, -1.0, tmp2);
+    evaluator.rescale_to_next_inplace(tmp2);
+    evaluator.add_inplace_reduced_error(tmp_cipher, tmp2);
+    chebyBasis.push_back(tmp_cipher);
+    // :80-99: T4, T8, ... = 2 T^2 - 1
+    for (int i = 0; i < n - 2; i++)
+    {
+        evaluator.square_inplace(cipher);
+        evaluator.relinearize_inplace(cipher, relin_keys);
+        evaluator.rescale_to_next_inplace(cipher);
+        evaluator.add_inplace(cipher, cipher);
+        evaluator.add_const_inplace(cipher, -1.0);
+        chebyBasis.push_back(cipher);
+    }
+}
+
+namespace
+{
+// PolyApprox.cpp:103-305: compute_sign_f and compute_sign_g are the same evaluation with
+// different coefficients:
+//   out = (fq1 x) T2 + fr1 x + (frq2_q T3 + frq2_r x) T4 + (fq3 x) T8
+struct SignCoeffs
+{
+    double fq1, fr1, frq2_q, frq2_r, fq3;
+};
+constexpr SignCoeffs kSignF{ -0.6767578125, 1.563049316, -0.02685546875, 0.1384277344, 0.002136230469 };
+constexpr SignCoeffs kSignG{ -1.121704102, 1.978370667, -0.6178588867, 0.403533935, 0.3557052612 };
+
+void sign_poly(const SignCoeffs &c, Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder,
+               Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+               RelinKeys &relin_keys)
+{
+    Ciphertext cipher, tmp_cipher;
+    std::vector<Ciphertext> cheby_basis;
+    build_cheby_basis(input, cheby_basis, 4, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    // first level (:118-139)
+    evaluator.multiply_const(input, c.fq1, output);
+    evaluator.rescale_to_next_inplace(output);
+    evaluator.multiply_inplace_reduced_error(output, cheby_basis[2], relin_keys);
+    evaluator.rescale_to_next_inplace(output);
+    evaluator.multiply_const(input, c.fr1, cipher);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.add_inplace_reduced_error(output, cipher);
+    // second level (:145-175)
+    evaluator.multiply_const(cheby_basis[3], c.frq2_q, cipher);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.multiply_const(input, c.frq2_r, tmp_cipher);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.add_inplace_reduced_error(cipher, tmp_cipher);
+    evaluator.multiply_inplace_reduced_error(cipher, cheby_basis[4], relin_keys);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.add_inplace_reduced_error(output, cipher);
+    // third level (:181-201)
+    evaluator.multiply_const(input, c.fq3, cipher);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.multiply_inplace_reduced_error(cipher, cheby_basis[5], relin_keys);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.add_inplace_reduced_error(output, cipher);
+}
+} // namespace
+
+void compute_sign_f(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    sign_poly(kSignF, input, output, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+}
+
+void compute_sign_g(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    sign_poly(kSignG, input, output, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+}
+
+void sign_function(const Ciphertext &input, Ciphertext &output, int df, int dg, CKKSEncoder &encoder,
+                   Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                   RelinKeys &relin_keys)
+{
+    // PolyApprox.cpp:315-331
+    Ciphertext cipher = input, tmp_cipher;
+    for (int i = 0; i < dg / 2; i++)
+    {
+        compute_sign_g(cipher, tmp_cipher, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        compute_sign_g(tmp_cipher, cipher, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    }
+    for (int i = 0; i < df / 2; i++)
+    {
+        compute_sign_f(cipher, tmp_cipher, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        compute_sign_f(tmp_cipher, cipher, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    }
+    output = cipher;
+}
+
+void compute_gelu_p(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    // PolyApprox.cpp:336-371: p(x) = (q1 x + q0) T2 + (r1 x + r0)
+    Ciphertext tmp_cipher;
+    std::vector<Ciphertext> cheby_basis;
+    build_cheby_basis(input, cheby_basis, 2, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    const double q_0 = -0.05745879353, q_1 = -0.005337069175;
+    const double r_0 = -0.55528939, r_1 = -0.4187418723;
+    evaluator.multiply_const(input, q_1, tmp_cipher);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.add_const_inplace(tmp_cipher, q_0);
+    evaluator.multiply_inplace_reduced_error(tmp_cipher, cheby_basis[2], relin_keys);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.multiply_const(input, r_1, output);
+    evaluator.rescale_to_next_inplace(output);
+    evaluator.add_const_inplace(output, r_0);
+    evaluator.add_inplace_reduced_error(output, tmp_cipher);
+}
+
+void compute_gelu_q(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    // PolyApprox.cpp:372-433:
+    //   q(x) = (qq1_1 x + qq1_0) T2 + (qr1_1 x + qr1_0) + (qq_2 x^2 + qq2_1 x + qq2_0) T4
+    Ciphertext cipher, tmp_cipher;
+    std::vector<Ciphertext> cheby_basis;
+    build_cheby_basis(input, cheby_basis, 4, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    const double qq1_0 = 0.1634058825, qq1_1 = -0.00324699876;
+    const double qr1_0 = 0.1750485092, qr1_1 = 0.5027208006;
+    evaluator.multiply_const(input, qq1_1, tmp_cipher);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.add_const_inplace(tmp_cipher, qq1_0);
+    evaluator.multiply_inplace_reduced_error(tmp_cipher, cheby_basis[2], relin_keys);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.multiply_const(input, qr1_1, output);
+    evaluator.rescale_to_next_inplace(output);
+    evaluator.add_const_inplace(output, qr1_0);
+    evaluator.add_inplace_reduced_error(output, tmp_cipher);
+
+    const double qq2_0 = -0.004401064777, qq2_1 = 0.0002609111473, qq_2 = 0.0001533078376;
+    evaluator.square(input, tmp_cipher);
+    evaluator.relinearize_inplace(tmp_cipher, relin_keys);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.multiply_const_inplace(tmp_cipher, qq_2);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    evaluator.multiply_const(input, qq2_1, cipher);
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.add_inplace_reduced_error(cipher, tmp_cipher);
+    evaluator.add_const_inplace(cipher, qq2_0);
+    evaluator.multiply_inplace_reduced_error(cipher, cheby_basis[4], relin_keys);
+    // deviation: the reference adds this product unrescaled (PolyApprox.cpp:429-431); both terms then
+    // sit at one level and add_inplace_reduced_error overwrites the sum's scale with the product's
+    // squared scale, so the qr/qq1 part is lost.  Rescaling first gives the value the reference's own
+    // GeluQ case expects (run_approx_test.cpp:464-486, the exact polynomial).
+    evaluator.rescale_to_next_inplace(cipher);
+    evaluator.add_inplace_reduced_error(output, cipher);
+}
+
+void compute_gelu(Ciphertext &inputs, Ciphertext &outputs, CKKSEncoder &encoder, Encryptor &encryptor,
+                  Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    // PolyApprox.cpp:443-504
+    Ciphertext s0, s1, s2, b1, b2, b3, p, q, tc;
+    auto half_sign = [&](double shift, Ciphertext &s) {
+        evaluator.add_const(inputs, shift, s);
+        sign_function(s, tc, 2, 2, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        evaluator.multiply_const(tc, 0.5, s);
+        evaluator.rescale_to_next_inplace(s);
+    };
+    half_sign(-3.0, s2);
+    half_sign(1.95, s1);
+    half_sign(4.0, s0);
+    evaluator.sub_reduced_error(s0, s1, b1);
+    evaluator.sub_reduced_error(s1, s2, b2);
+    evaluator.multiply_const(s2, 0.5, b3);
+    evaluator.rescale_to_next_inplace(b3);
+    compute_gelu_p(inputs, p, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    compute_gelu_q(inputs, q, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    evaluator.multiply_reduced_error(b1, p, relin_keys, outputs);
+    evaluator.rescale_to_next_inplace(outputs);
+    evaluator.multiply_inplace_reduced_error(b2, q, relin_keys);
+    evaluator.rescale_to_next_inplace(b2);
+    evaluator.multiply_inplace_reduced_error(b3, inputs, relin_keys);
+    evaluator.rescale_to_next_inplace(b3);
+    evaluator.add_inplace_reduced_error(outputs, b2);
+    evaluator.add_inplace_reduced_error(outputs, b3);
+}
+
+void compute_exp(Ciphertext &input, Ciphertext &output, int r, CKKSEncoder &, Encryptor &, Decryptor &,
+                 Evaluator &evaluator, GaloisKeys &, RelinKeys &relin_keys)
+{
+    // PolyApprox.cpp:511-531
+    const double power = std::pow(2.0, r);
+    evaluator.multiply_const(input, 1 / power, output);
+    evaluator.rescale_to_next_inplace(output);
+    evaluator.add_const_inplace(output, 1);
+    for (int i = 0; i < r; i++)
+    {
+        evaluator.square_inplace(output);
+        evaluator.relinearize_inplace(output, relin_keys);
+        evaluator.rescale_to_next_inplace(output);
+    }
+}
+
+void compute_inverse(Ciphertext &input, Ciphertext &output, int iters, CKKSEncoder &encoder, Encryptor &encryptor,
+                     Decryptor &, Evaluator &evaluator, GaloisKeys &, RelinKeys &relin_keys)
+{
+    // IterApprox.cpp:15-68: n_0 = 0.001, d_0 = 0.001 x; f = 2 - d; n *= f; d *= f
+    Ciphertext two_cipher, d_cipher, f_cipher;
+    Plaintext plain;
+    const double normalize_factor = 0.001;
+    std::vector<double> one_vec(32768, normalize_factor), two_vec(32768, 2.0);
+    encoder.encode(one_vec, encode_scale(), plain);
+    evaluator.mod_switch_to_inplace(plain, input.parms_id());
+    encryptor.encrypt(plain, output);
+    encoder.encode(two_vec, encode_scale(), plain);
+    evaluator.mod_switch_to_inplace(plain, input.parms_id());
+    encryptor.encrypt(plain, two_cipher);
+    evaluator.multiply_const(input, normalize_factor, d_cipher);
+    evaluator.rescale_to_next_inplace(d_cipher);
+    for (int i = 0; i < iters; i++)
+    {
+        evaluator.sub_reduced_error(two_cipher, d_cipher, f_cipher);
+        evaluator.multiply_inplace_reduced_error(output, f_cipher, relin_keys);
+        evaluator.rescale_to_next_inplace(output);
+        evaluator.multiply_inplace_reduced_error(d_cipher, f_cipher, relin_keys);
+        evaluator.rescale_to_next_inplace(d_cipher);
+    }
+}
+
+void quickSum(Ciphertext &input, Ciphertext &output, int n, CKKSEncoder &, Encryptor &, Decryptor &,
+              Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &)
+{
+    // Fold.cpp:20-45
+    Ciphertext cipher;
+    int acc = 1;
+    evaluator.rotate_vector(input, acc, gal_keys, cipher);
+    evaluator.add(input, cipher, output);
+    acc *= 2;
+    for (int i = 0; i < std::log2(n) - 1; i++)
+    {
+        evaluator.rotate_vector(output, acc, gal_keys, cipher);
+        evaluator.add_inplace_reduced_error(output, cipher);
+        acc *= 2;
+    }
+}
+
+void mask_out(Ciphertext &cipher, Ciphertext &out, int start, int length, CKKSEncoder &, Evaluator &evaluator,
+              RelinKeys &)
+{
+    // util.cpp:292-301
+    if (start < 0 || length < 0 || start + length > 32768) throw std::invalid_argument("mask_out: range");
+    std::vector<double> x(32768, 0.0);
+    std::fill(x.begin() + start, x.begin() + start + length, 1.0);
+    evaluator.multiply_vector_reduced_error(cipher, x, out);
+    evaluator.rescale_to_next_inplace(out);
+}
+
+void pack_plain_row(std::vector<std::vector<double>> &v, int rows, int row_size, std::vector<std::vector<double>> &out)
+{
+    // util.cpp:303-316
+    const int rounded_row_size = round_to_2(row_size);
+    for (int i = 0; i < rows; i++)
+        for (int j = 0; j < row_size; j++)
+        {
+            const long pos = (long)i * rounded_row_size * 2 + j;
+            if ((std::size_t)(pos / 32768) >= out.size()) throw std::invalid_argument("pack_plain_row: out too small");
+            out[pos / 32768][pos % 32768] = v[i][j];
+        }
+}
+
+void init_output(int num_ciphers, std::vector<Ciphertext> &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                 Decryptor &, Evaluator &, GaloisKeys &, RelinKeys &)
+{
+    // util.cpp:277-290
+    std::vector<double> x(1, 0.0);
+    Plaintext plain;
+    Ciphertext cipher;
+    for (int i = 0; i < num_ciphers; i++)
+    {
+        encoder.encode(x, encode_scale(), plain);
+        encryptor.encrypt(plain, cipher);
+        output.push_back(cipher);
+    }
+}
+
+void pack_from_row(std::vector<std::vector<double>> &input, std::vector<Ciphertext> &output, CKKSEncoder &encoder,
+                   Encryptor &encryptor, Decryptor &, Evaluator &, GaloisKeys &, RelinKeys &)
+{
+    // pack.cpp:153-178
+    const int rows = (int)input.size(), cols = (int)input[0].size();
+    const int chunk_size = round_to_2(cols) * 2;
+    const int num_ciphers = std::max(1, (rows * chunk_size) / 32768);
+    std::vector<std::vector<double>> plain_out(num_ciphers, std::vector<double>(32768, 0));
+    pack_plain_row(input, rows, cols, plain_out);
+    Plaintext plain;
+    Ciphertext cipher;
+    for (int i = 0; i < num_ciphers; i++)
+    {
+        encoder.encode(plain_out[i], encode_scale(), plain);
+        encryptor.encrypt(plain, cipher);
+        output.push_back(cipher);
+    }
+}
+
+void row_matrix_multiplication_seal(std::vector<Ciphertext> &left_inputs, std::vector<Ciphertext> &weights,
+                                    Ciphertext bias, std::vector<Ciphertext> &outputs, int A_rows, int A_cols,
+                                    int W_rows, int W_cols, CKKSEncoder &encoder, Encryptor &encryptor,
+                                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                                    RelinKeys &relin_keys)
+{
+    // MatrixMul.cpp:118-188
+    const int W_rows_rounded = round_to_2(W_rows), W_cols_rounded = round_to_2(W_cols);
+    const int chunk_size = W_rows_rounded * 2, num_chunks = 32768 / chunk_size, out_chunk_size = W_cols_rounded * 2;
+    Ciphertext rolled, folded, res1, masked_out;
+    for (std::size_t i = 0; i < left_inputs.size(); i++)
+        for (std::size_t j = 0; j < weights.size(); j++)
+            for (int rots = 0; rots < num_chunks; rots++)
+            {
+                // Hadamard products against the rotated weights
+                evaluator.rotate_vector(weights[j], rots * chunk_size, gal_keys, rolled);
+                evaluator.multiply_reduced_error(left_inputs[i], rolled, relin_keys, res1);
+                evaluator.rescale_to_next_inplace(res1);
+                // format for the fold, fold
+                evaluator.rotate_vector(res1, 32768 - W_rows_rounded, gal_keys, rolled);
+                evaluator.add_inplace_reduced_error(res1, rolled);
+                quickSum(res1, folded, W_rows_rounded, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+                for (int pos = 0; pos < num_chunks; ++pos)
+                {
+                    const int row = (int)i * num_chunks + pos;
+                    const int col = (int)j * num_chunks + ((rots + pos) % num_chunks);
+                    mask_out(folded, masked_out, pos * chunk_size, 1, encoder, evaluator, relin_keys);
+                    const int cipher_idx = (row * out_chunk_size) / 32768;
+                    const int cipher_chunk = ((row * out_chunk_size) % 32768) / out_chunk_size;
+                    const int desired_location = cipher_chunk * out_chunk_size + col;
+                    const int shift_amt = desired_location - pos * chunk_size;
+                    if (cipher_idx >= (int)outputs.size())
+                        throw std::invalid_argument("row_matrix_multiplication_seal: outputs too small");
+                    evaluator.rotate_vector_inplace(masked_out, -shift_amt, gal_keys);
+                    evaluator.add_inplace_reduced_error(outputs[cipher_idx], masked_out);
+                }
+            }
+    for (auto &o : outputs) evaluator.add_inplace_reduced_error(o, bias);
+}
+
+std::vector<int> gpt2_rotation_steps(int logN)
+{
+    // gpt2/util.h:58-67
+    std::vector<int> steps;
+    for (int i = 0; i < logN - 1; i++) steps.push_back(1 << i);
+    std::vector<int> kinds = { 0,     1,     2,     3,     4,     5,     6,     7,     8,     9,     10,
+                               32640, 31744, 12288, 16384, 20480, 24576, 28672, 32672, 32704, 32736, 32,
+                               64,    96,    31872, 32096, 32320, 32544, 224,   448,   672,   896,   32765,
+                               32766, 32767, 32740, 32747, 32754, 32761, 14,    21,    28 };
+    for (int i = 0; i < 32768; i += 2048) kinds.push_back(i);
+    for (int r : kinds)
+        if (std::find(steps.begin(), steps.end(), r) == steps.end()) steps.push_back(r);
+    return steps;
+}
+} // namespace gpt2

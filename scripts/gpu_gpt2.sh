@@ -1,0 +1,9 @@
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 ./build/gpt2_test ${GPT2_LOGSCALE:-49} > gpurun_out/gpt2_test.log 2>&1
+rc=$?; echo "rc=$rc" >> gpurun_out/gpt2_test.log
+[ $rc -le 1 ] || exit $rc
+true
+echo "rc=$?" >> gpurun_out/gpt2_test46.log
+exit $rc
