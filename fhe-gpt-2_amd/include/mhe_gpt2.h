@@ -74,6 +74,13 @@ void compute_exp(Ciphertext &input, Ciphertext &output, int r, CKKSEncoder &enco
 void compute_inverse(Ciphertext &input, Ciphertext &output, int iters, CKKSEncoder &encoder, Encryptor &encryptor,
                      Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
 
+// PolyApprox.cpp:595-649: softmax over rows of 128 packed at slot i*256 with a fixed shift gamma in
+// place of the row max (exp, masked fold + quickSum, Goldschmidt inverse); in place on `input`.
+// (compute_softmax / compute_layernorm are not provided: the reference's versions bootstrap inside
+// quickMax and call fakeBootstrap, a decrypt/re-encrypt, IterApprox.cpp:160,306.)
+void compute_smax(Ciphertext &input, int r, int gamma, CKKSEncoder &encoder, Encryptor &encryptor,
+                  Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
 // Fold.cpp:20-45: out = sum of input rotated by 0, 1, 2, ..., n/2 (log2(n) rotate+add steps)
 void quickSum(Ciphertext &input, Ciphertext &output, int n, CKKSEncoder &encoder, Encryptor &encryptor,
               Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);

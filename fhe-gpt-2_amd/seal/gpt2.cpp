@@ -272,6 +272,36 @@ void compute_inverse(Ciphertext &input, Ciphertext &output, int iters, CKKSEncod
     }
 }
 
+void compute_smax(Ciphertext &input, int r, int gamma, CKKSEncoder &encoder, Encryptor &encryptor,
+                  Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    // PolyApprox.cpp:595-649: rows of 128 scores at slot i*256, the next 128 slots padding.  The
+    // padding gets -gamma (a fixed shift in place of the max), exp, padding zeroed, row sums by a
+    // fold + quickSum(128), Goldschmidt 1/sum (4 steps), product.  The result replaces the input.
+    (void)r; // the reference passes r but evaluates compute_exp with r = 6
+    std::vector<double> zeros_mask(32768, 1.0), gamma_mask(32768, 0.0);
+    for (int i = 0; i < 128; i++)
+        for (int j = 0; j < 128; j++)
+        {
+            zeros_mask[i * 256 + 128 + j] = 0.0;
+            gamma_mask[i * 256 + 128 + j] = -gamma;
+        }
+    Plaintext plain_gamma;
+    Ciphertext rolled, exps, summed, inverses;
+    encoder.encode(gamma_mask, input.scale(), plain_gamma);
+    evaluator.mod_switch_to_inplace(plain_gamma, input.parms_id());
+    evaluator.add_plain_inplace(input, plain_gamma);
+    compute_exp(input, exps, 6, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    evaluator.multiply_vector_inplace_reduced_error(exps, zeros_mask);
+    evaluator.rescale_to_next_inplace(exps);
+    evaluator.rotate_vector(exps, 32768 - 128, gal_keys, rolled);
+    evaluator.add_inplace_reduced_error(rolled, exps);
+    quickSum(rolled, summed, 128, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    compute_inverse(summed, inverses, 4, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    evaluator.multiply_reduced_error(exps, inverses, relin_keys, input);
+    evaluator.rescale_to_next_inplace(input);
+}
+
 void quickSum(Ciphertext &input, Ciphertext &output, int n, CKKSEncoder &, Encryptor &, Decryptor &,
               Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &)
 {

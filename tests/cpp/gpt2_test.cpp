@@ -252,6 +252,60 @@ static int run_all(int log_scale)
     plain_case("compute_gelu_p", gelu_p, plain_gelu_p, -1, 1);
     plain_case("compute_gelu_q", gelu_q, plain_gelu_q, -2, 2);
     {
+        // compute_smax (PolyApprox.cpp:595-649) vs the same pipeline restated in doubles:
+        // rotate_vector(x, k)[i] = x[(i + k) mod 32768]; quickSum as Fold.cpp:20-45
+        const int S = 32768, gamma = 2;
+        auto rot = [&](const std::vector<double> &x, int k) {
+            std::vector<double> y(S);
+            for (int i = 0; i < S; i++) y[i] = x[((i + k) % S + S) % S];
+            return y;
+        };
+        auto qsum = [&](const std::vector<double> &x, int nn) {
+            std::vector<double> o(S), r1 = rot(x, 1);
+            for (int i = 0; i < S; i++) o[i] = x[i] + r1[i];
+            for (int acc = 2; acc < nn; acc *= 2)
+            {
+                const auto ro = rot(o, acc);
+                for (int i = 0; i < S; i++) o[i] += ro[i];
+            }
+            return o;
+        };
+        std::uniform_real_distribution<double> U(-1, 1);
+        std::vector<double> v(S, 0.0);
+        for (int i = 0; i < 128; i++)
+            for (int j = 0; j < 128; j++) v[i * 256 + j] = U(rng);
+        std::vector<double> e(S), want(S);
+        for (int i = 0; i < S; i++)
+        {
+            const bool pad = (i % 256) >= 128;
+            e[i] = pad ? 0.0 : std::pow(1 + v[i] / 64.0, 64);
+        }
+        auto rolled = rot(e, S - 128);
+        for (int i = 0; i < S; i++) rolled[i] += e[i];
+        const auto summed = qsum(rolled, 128);
+        for (int i = 0; i < S; i++)
+        {
+            double nn = 0.001, d = 0.001 * summed[i];
+            for (int k = 0; k < 4; k++)
+            {
+                const double f = 2 - d;
+                nn *= f;
+                d *= f;
+            }
+            want[i] = e[i] * nn;
+        }
+        std::printf("-- compute_smax\n");
+        Ciphertext c = enc(v);
+        const auto t = std::chrono::steady_clock::now();
+        compute_smax(c, 6, gamma, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+        const auto got = dec(c);
+        double err = 0;
+        for (int i = 0; i < S; i++) err = std::max(err, std::fabs(got[i] - want[i]));
+        std::printf("  compute_smax: output %zu limbs\n", c.coeff_modulus_size());
+        report("compute_smax(gamma 2) vs plain restatement, 32768 slots", err < 1e-3, err, secs);
+    }
+    {
         // RowMatMul (run_approx_test.cpp:231-297): ones(8 x 2048) x ones(8 x 2048)^T = 2048 everywhere
         std::vector<std::vector<double>> A1(8, std::vector<double>(2048, 1.0)), A1_pre(1, std::vector<double>(32768, 0.0));
         pack_plain_row(A1, 8, 2048, A1_pre);
@@ -272,6 +326,46 @@ static int run_all(int log_scale)
                 ok &= approx(res[i * 16 + j], 2048.0);
             }
         report("RowMatMul 8x2048 . (8x2048)^T (run_approx_test.cpp)", ok, err, secs);
+    }
+    {
+        // C5-style feed-forward slice: random A (8 x 2048) times random W (8 x 2048)^T by the
+        // row-packed encrypted matmul, + bias, then the GELU polynomial p over every slot; checked
+        // against the same pipeline in doubles (the matmul result lands at slot i*16 + j,
+        // MatrixMul.cpp:171-180; every other slot holds the bias only)
+        std::uniform_real_distribution<double> U(-0.05, 0.05), B(-0.5, 0.5);
+        std::vector<std::vector<double>> A(8, std::vector<double>(2048)), W(8, std::vector<double>(2048));
+        for (auto &r : A)
+            for (auto &x : r) x = U(rng);
+        for (auto &r : W)
+            for (auto &x : r) x = U(rng);
+        std::vector<double> bias(32768);
+        for (auto &x : bias) x = B(rng);
+        std::vector<std::vector<double>> Ap(1, std::vector<double>(32768, 0.0)), Wp(1, std::vector<double>(32768, 0.0));
+        pack_plain_row(A, 8, 2048, Ap);
+        pack_plain_row(W, 8, 2048, Wp);
+        std::vector<double> want(bias);
+        for (int i = 0; i < 8; i++)
+            for (int j = 0; j < 8; j++)
+            {
+                double acc = 0;
+                for (int k = 0; k < 2048; k++) acc += A[i][k] * W[j][k];
+                want[i * 16 + j] += acc;
+            }
+        for (auto &x : want) x = plain_gelu_p(x);
+        std::printf("-- ffn slice\n");
+        std::vector<Ciphertext> a{ enc(Ap[0]) }, w{ enc(Wp[0]) }, output;
+        init_output(1, output, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        Ciphertext bc = enc(bias), g;
+        const auto t = std::chrono::steady_clock::now();
+        row_matrix_multiplication_seal(a, w, bc, output, 8, 2048, 2048, 8, encoder, encryptor, decryptor, evaluator,
+                                       gal_keys, relin_keys);
+        compute_gelu_p(output[0], g, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        const auto got = dec(g);
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+        double err = 0;
+        for (int i = 0; i < 32768; i++) err = std::max(err, std::fabs(got[i] - want[i]));
+        std::printf("  ffn slice: output %zu limbs\n", g.coeff_modulus_size());
+        report("FFN slice: row matmul 8x2048 . (8x2048)^T + bias -> GELU p vs plain, 32768 slots", err < 1e-3, err, secs);
     }
     std::printf("%s\n", g_fail ? "FAILED" : "ok");
     return g_fail ? 1 : 0;
