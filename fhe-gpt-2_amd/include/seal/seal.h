@@ -373,6 +373,12 @@ public:
     const Ciphertext &data() const noexcept { return pk_; }
     Ciphertext &data() noexcept { return pk_; }
     const parms_id_type &parms_id() const noexcept { return pk_.parms_id(); }
+    // SEAL/publickey.h: the key's ciphertext in SEAL's format
+    std::streamoff save(std::ostream &stream, compr_mode_type m = Serialization::compr_mode_default) const
+    {
+        return pk_.save(stream, m);
+    }
+    std::streamoff load(const SEALContext &context, std::istream &stream) { return pk_.load(context, stream); }
 
 private:
     Ciphertext pk_;
@@ -407,6 +413,13 @@ public:
     const std::shared_ptr<KeyMaker> &maker() const noexcept { return maker_; }
     // bytes of device memory held by materialised keys
     std::size_t device_bytes() const;
+
+    // SEAL/kswitchkeys.cpp:42-140 byte format: parms_id | u64 dim1 | per index: u64 dim2 | dim2
+    // PublicKey (Ciphertext) objects at the key level.  Deferred (lazily materialised, level-truncated)
+    // Galois keys are not serialisable: set MHE_EAGER_GALOIS=1 to build SEAL's full keys and save them.
+    std::streamoff save_size(compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff save(std::ostream &stream, compr_mode_type compr_mode = Serialization::compr_mode_default) const;
+    std::streamoff load(const SEALContext &context, std::istream &stream);
 
 private:
     mutable std::map<std::size_t, PolyStore> keys_;

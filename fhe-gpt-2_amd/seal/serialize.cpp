@@ -245,6 +245,103 @@ std::streamoff Ciphertext::load(const SEALContext &context, const seal_byte *in,
     return load_from_buffer(*this, context, in, size);
 }
 
+// ------------------------------------------------------------------------------ KSwitchKeys
+// Every key index holds `digits` PublicKeys: a size-2 NTT-form ciphertext over the key level, which
+// is exactly the [digit][2][K][n] slice of the device buffer (keygenerator.cpp:384-414).
+namespace
+{
+std::streamoff pk_size(std::size_t K, std::size_t n) { return kHeader + 32 + 1 + 24 + 8 + dynarray_size(2 * K * n); }
+} // namespace
+
+std::streamoff KSwitchKeys::save_size(compr_mode_type) const
+{
+    if (maker_) throw std::logic_error("deferred Galois keys cannot be serialized");
+    const std::size_t dim1 = keys_.empty() ? 0 : keys_.rbegin()->first + 1;
+    std::streamoff total = kHeader + 32 + 8 + (std::streamoff)(8 * dim1);
+    for (const auto &kv : keys_)
+    {
+        const std::size_t K = key_limbs_, words = kv.second.words();
+        // full keys hold one digit per data prime (decomp_mod_count = K - 1)
+        const std::size_t n = K > 1 ? words / (2 * K * (K - 1)) : 0;
+        if (!n || words != (K - 1) * 2 * K * n) throw std::logic_error("key data is invalid");
+        total += (std::streamoff)(K - 1) * pk_size(K, n);
+    }
+    return total;
+}
+
+std::streamoff KSwitchKeys::save(std::ostream &stream, compr_mode_type mode) const
+{
+    const std::streamoff total = save_size(mode);
+    write_header(stream, (std::uint64_t)total, mode);
+    put(stream, parms_id_);
+    const std::size_t dim1 = keys_.empty() ? 0 : keys_.rbegin()->first + 1;
+    put<std::uint64_t>(stream, dim1);
+    for (std::size_t i = 0; i < dim1; i++)
+    {
+        auto it = keys_.find(i);
+        if (it == keys_.end())
+        {
+            put<std::uint64_t>(stream, 0);
+            continue;
+        }
+        const std::size_t K = key_limbs_, digits = K - 1, n = it->second.words() / (2 * K * digits);
+        put<std::uint64_t>(stream, digits);
+        const std::uint64_t *p = it->second.host();
+        for (std::size_t d = 0; d < digits; d++)
+        {
+            write_header(stream, (std::uint64_t)pk_size(K, n), compr_mode_type::none);
+            put(stream, parms_id_);
+            put<std::uint8_t>(stream, 1);
+            put<std::uint64_t>(stream, 2);
+            put<std::uint64_t>(stream, n);
+            put<std::uint64_t>(stream, K);
+            put<double>(stream, 1.0);
+            write_dynarray(stream, p + d * 2 * K * n, 2 * K * n);
+        }
+    }
+    if (!stream) throw std::runtime_error("I/O error");
+    return total;
+}
+
+std::streamoff KSwitchKeys::load(const SEALContext &context, std::istream &stream)
+{
+    const auto h = read_header(stream);
+    const auto id = get<parms_id_type>(stream);
+    if (id != context.key_parms_id()) throw std::logic_error("KSwitchKeys data is invalid");
+    const auto cd = context.key_context_data();
+    const std::size_t K = cd->parms().coeff_modulus().size(), n = cd->parms().poly_modulus_degree();
+    const auto dim1 = get<std::uint64_t>(stream);
+    if (dim1 > 4 * n) throw std::logic_error("KSwitchKeys data is invalid");
+    std::map<std::size_t, PolyStore> keys;
+    std::streamoff total = kHeader + 32 + 8;
+    for (std::size_t i = 0; i < dim1; i++)
+    {
+        const auto digits = get<std::uint64_t>(stream);
+        total += 8;
+        if (!digits) continue;
+        if (digits != K - 1) throw std::logic_error("KSwitchKeys data is invalid");
+        PolyStore &ps = keys[i];
+        ps.bind(context);
+        ps.resize_words(digits * 2 * K * n, false);
+        std::uint64_t *dst = ps.host();
+        for (std::size_t d = 0; d < digits; d++)
+        {
+            Ciphertext pk;
+            total += pk.load(context, stream);
+            if (pk.parms_id() != id || pk.size() != 2 || !pk.is_ntt_form())
+                throw std::logic_error("KSwitchKeys data is invalid");
+            std::memcpy(dst + d * 2 * K * n, pk.data(), 8 * 2 * K * n);
+        }
+    }
+    if ((std::uint64_t)total != h.size) throw std::logic_error("KSwitchKeys data is invalid");
+    keys_ = std::move(keys);
+    limbs_of_.clear();
+    parms_id_ = id;
+    key_limbs_ = K;
+    maker_.reset();
+    return total;
+}
+
 // ------------------------------------------------------------------------------ Plaintext
 std::streamoff Plaintext::save_size(compr_mode_type) const { return kHeader + 32 + 8 + 8 + dynarray_size(store_.words()); }
 

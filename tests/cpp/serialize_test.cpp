@@ -168,6 +168,55 @@ int main(int argc, char **argv)
     CHECK(throws([&] { load_str(bad); }));
     CHECK(throws([&] { load_str(good.substr(0, good.size() - 8)); })); // truncated
 
+    // keys: RelinKeys / PublicKey round trips (kswitchkeys.cpp:42-140, publickey.h); relinearizing
+    // with the loaded key is bit-identical, encrypting with the loaded public key decrypts
+    RelinKeys rlk;
+    keygen.create_relin_keys(rlk);
+    std::stringstream ks;
+    const auto kbytes = rlk.save(ks);
+    CHECK(kbytes == rlk.save_size() && (std::streamoff)ks.str().size() == kbytes);
+    const std::string kstr = ks.str();
+    RelinKeys rlk2;
+    CHECK(rlk2.load(ctx, ks) == kbytes);
+    CHECK(rlk2.parms_id() == ctx.key_parms_id() && rlk2.has_key(2));
+    Ciphertext sq1, sq2;
+    evaluator.square(ct, sq1);
+    sq2 = sq1;
+    evaluator.relinearize_inplace(sq1, rlk);
+    evaluator.relinearize_inplace(sq2, rlk2);
+    CHECK(std::memcmp(sq1.data(), sq2.data(), 8 * sq1.dyn_array_size()) == 0);
+    std::stringstream pks;
+    pk.save(pks);
+    PublicKey pk2;
+    pk2.load(ctx, pks);
+    Encryptor enc2(ctx, pk2);
+    Ciphertext ct3;
+    enc2.encrypt(pt, ct3);
+    Plaintext back3;
+    decryptor.decrypt(ct3, back3);
+    std::vector<double> y3;
+    encoder.decode(back3, y3);
+    double err3 = 0;
+    for (std::size_t i = 0; i < x.size(); i++) err3 = std::max(err3, std::fabs(y3[i] - x[i]));
+    CHECK(err3 < 1e-6);
+    GaloisKeys glk;
+    keygen.create_galois_keys(std::vector<int>{ 1 }, glk); // deferred by default
+    CHECK(throws([&] {
+        std::stringstream t;
+        glk.save(t);
+    }));
+    {
+        std::string badk = kstr;
+        badk[16] ^= 1; // parms_id
+        std::stringstream t(badk);
+        RelinKeys r;
+        CHECK(throws([&] { r.load(ctx, t); }));
+    }
+    {
+        std::ofstream kf(dir + "/relin.bin", std::ios::binary);
+        kf << kstr;
+    }
+
     // files for the Python-side format check
     {
         std::ofstream f(dir + "/ct.bin", std::ios::binary);

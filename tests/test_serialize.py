@@ -85,3 +85,18 @@ def test_save_load_roundtrip(tmp_path):
     assert cc == L * n and pscale == 2.0**46
     assert _header(p, 64) == len(p) - 64
     assert struct.unpack_from("<Q", p, 80)[0] == cc
+    # relin keys: header | key parms_id | dim1 = 1 | dim2 = K - 1 | K - 1 PublicKeys (size 2, key level)
+    k = open(tmp_path / "relin.bin", "rb").read()
+    assert _header(k) == len(k)
+    K = len(moduli) + 1
+    key_id = list(struct.unpack_from("<4Q", k, 16))
+    dim1, dim2 = struct.unpack_from("<QQ", k, 48)
+    assert dim1 == 1 and dim2 == K - 1
+    off = 64
+    for _ in range(dim2):
+        size = _header(k, off)
+        assert list(struct.unpack_from("<4Q", k, off + 16)) == key_id
+        ntt, sz, nn, kl = struct.unpack_from("<BQQQ", k, off + 48)
+        assert (ntt, sz, nn, kl) == (1, 2, n, K)
+        off += size
+    assert off == len(k)
