@@ -74,10 +74,23 @@ void compute_exp(Ciphertext &input, Ciphertext &output, int r, CKKSEncoder &enco
 void compute_inverse(Ciphertext &input, Ciphertext &output, int iters, CKKSEncoder &encoder, Encryptor &encryptor,
                      Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
 
+// util.cpp:266-275 (decrypt + re-encrypt at the top level; the reference's bootstrapping stand-in)
+void fakeBootstrap(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                   Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+// IterApprox.cpp:69-120 / :128-166 / :168-246
+void taylor_expand(Ciphertext &input, Ciphertext &output, int iters, double guess, CKKSEncoder &encoder,
+                   Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                   RelinKeys &relin_keys);
+void compute_inv_sqrt(Ciphertext &input, Ciphertext &output, int iters, double guess, CKKSEncoder &encoder,
+                      Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                      RelinKeys &relin_keys);
+void compute_layernorm(Ciphertext &input, Ciphertext &output, std::vector<double> gamma, std::vector<double> beta,
+                       int row_size, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                       Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
 // PolyApprox.cpp:595-649: softmax over rows of 128 packed at slot i*256 with a fixed shift gamma in
 // place of the row max (exp, masked fold + quickSum, Goldschmidt inverse); in place on `input`.
-// (compute_softmax / compute_layernorm are not provided: the reference's versions bootstrap inside
-// quickMax and call fakeBootstrap, a decrypt/re-encrypt, IterApprox.cpp:160,306.)
+// (compute_softmax is not provided: the reference's version bootstraps inside quickMax.)
 void compute_smax(Ciphertext &input, int r, int gamma, CKKSEncoder &encoder, Encryptor &encryptor,
                   Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
 

@@ -272,6 +272,130 @@ void compute_inverse(Ciphertext &input, Ciphertext &output, int iters, CKKSEncod
     }
 }
 
+void fakeBootstrap(Ciphertext &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                   Decryptor &decryptor, Evaluator &, GaloisKeys &, RelinKeys &)
+{
+    // util.cpp:266-275: the reference's stand-in for bootstrapping -- decrypt, decode, re-encode at
+    // ENCODE_SCALE and re-encrypt at the top data level
+    Plaintext plain;
+    std::vector<double> res;
+    decryptor.decrypt(input, plain);
+    encoder.decode(plain, res);
+    encoder.encode(res, encode_scale(), plain);
+    encryptor.encrypt(plain, output);
+}
+
+void taylor_expand(Ciphertext &input, Ciphertext &output, int iters, double guess, CKKSEncoder &, Encryptor &,
+                   Decryptor &, Evaluator &evaluator, GaloisKeys &, RelinKeys &relin_keys)
+{
+    // IterApprox.cpp:69-120, as written: sum_{i<3} c_i / (i+1)! * (x * guess^(p_i/(i+1)))^(i+1)
+    // with c = {-0.5, 0.75, -1.875}, p = {-1.5, -2.5, -3.5}.  The reference builds an a+1 plaintext
+    // but never uses it (no constant term, no x - a shift), and ignores `iters`.
+    (void)iters;
+    const double coeffs[3] = { -0.5, -0.5 * -1.5, -2.5 * -1.5 * -0.5 };
+    const double powers[3] = { -1.5, -2.5, -3.5 };
+    Ciphertext cipher, tmp_cipher, tmp2;
+    int fact_acc = 1;
+    for (int i = 0; i < 3; i++)
+    {
+        const double coefficient = coeffs[i] * 1 / fact_acc;
+        evaluator.multiply_const(input, std::pow(guess, powers[i] / (i + 1)), tmp2);
+        evaluator.rescale_to_next_inplace(tmp2);
+        tmp_cipher = tmp2;
+        for (int j = 0; j < i; j++)
+        {
+            evaluator.multiply_inplace_reduced_error(tmp_cipher, tmp2, relin_keys);
+            evaluator.rescale_to_next_inplace(tmp_cipher);
+        }
+        evaluator.multiply_const_inplace(tmp_cipher, coefficient);
+        evaluator.rescale_to_next_inplace(tmp_cipher);
+        if (i == 0)
+            cipher = tmp_cipher;
+        else
+            evaluator.add_inplace_reduced_error(cipher, tmp_cipher);
+        fact_acc *= (i + 2);
+    }
+    output = cipher;
+}
+
+void compute_inv_sqrt(Ciphertext &input, Ciphertext &output, int iters, double guess, CKKSEncoder &encoder,
+                      Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                      RelinKeys &relin_keys)
+{
+    // IterApprox.cpp:128-166: Taylor start, then Newton x <- x (1.5 - 0.5 a x^2), each step
+    // followed by fakeBootstrap
+    taylor_expand(input, output, 3, guess, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    Ciphertext cipher, tmp_cipher;
+    evaluator.multiply_const(input, -0.5, tmp_cipher);
+    evaluator.rescale_to_next_inplace(tmp_cipher);
+    for (int i = 0; i < iters; i++)
+    {
+        evaluator.square(output, cipher);
+        evaluator.relinearize_inplace(cipher, relin_keys);
+        evaluator.rescale_to_next_inplace(cipher);
+        evaluator.multiply_inplace_reduced_error(cipher, tmp_cipher, relin_keys);
+        evaluator.rescale_to_next_inplace(cipher);
+        evaluator.add_const_inplace(cipher, 1.5);
+        evaluator.multiply_inplace_reduced_error(output, cipher, relin_keys);
+        evaluator.rescale_to_next_inplace(output);
+        fakeBootstrap(output, output, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    }
+}
+
+void compute_layernorm(Ciphertext &input, Ciphertext &output, std::vector<double> gamma, std::vector<double> beta,
+                       int row_size, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                       Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    // IterApprox.cpp:168-246, operation for operation.  Rows of row_size values start every
+    // 2 * R slots (R = round_to_2(row_size), 16 rows).  Defects kept as written:
+    // the inverse square root is computed and fakeBootstrapped but the product that follows is
+    // y * z (the masked squares times the centred values), not inv_sqrt * z; the result is left
+    // in y (the reference never writes `output`; here `output` = y); beta (not the tiled
+    // beta_factor) is added, so only the first row gets it.  R = 1024 for GPT-2's 768.
+    const int R = round_to_2(row_size);
+    if (16 * 2 * R > 32768) throw std::invalid_argument("compute_layernorm: 16 rows of 2 * round_to_2(row_size) exceed 32768 slots");
+    if ((int)gamma.size() > 2 * R || (int)beta.size() > 32768)
+        throw std::invalid_argument("compute_layernorm: gamma longer than a row stride");
+    for (auto &g : gamma) g *= std::sqrt((double)row_size);
+    std::vector<double> mask(32768, 0.0), mul_factor(32768, 0.0);
+    for (int i = 0; i < 16; i++)
+    {
+        std::fill(mask.begin() + i * 2 * R, mask.begin() + i * 2 * R + R, 1.0);
+        std::copy(gamma.begin(), gamma.end(), mul_factor.begin() + i * 2 * R);
+    }
+    Plaintext plain_beta;
+    Ciphertext rolled, folded, y, z, inv_sqrt;
+    // :193-197 row sums
+    evaluator.rotate_vector(input, -R, gal_keys, rolled);
+    evaluator.add_inplace_reduced_error(rolled, input);
+    quickSum(rolled, folded, R, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    // :200-207 z = row_size * x - sum
+    evaluator.multiply_const(input, row_size, z);
+    evaluator.rescale_to_next_inplace(z);
+    evaluator.sub_inplace_reduced_error(z, folded);
+    // :211-217 y = z^2, masked to the row slots
+    evaluator.square(z, y);
+    evaluator.relinearize_inplace(y, relin_keys);
+    evaluator.rescale_to_next_inplace(y);
+    evaluator.multiply_vector_inplace_reduced_error(y, mask);
+    evaluator.rescale_to_next_inplace(y);
+    // :225-233 fold again, inverse square root (4 Newton steps from 323251)
+    evaluator.rotate_vector(y, 32768 - R, gal_keys, rolled);
+    evaluator.add_inplace_reduced_error(rolled, y);
+    quickSum(rolled, folded, R, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    compute_inv_sqrt(folded, inv_sqrt, 4, 323251, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    fakeBootstrap(inv_sqrt, inv_sqrt, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    // :235-245
+    evaluator.multiply_inplace_reduced_error(y, z, relin_keys);
+    evaluator.rescale_to_next_inplace(y);
+    evaluator.multiply_vector_inplace_reduced_error(y, mul_factor);
+    evaluator.rescale_to_next_inplace(y);
+    encoder.encode(beta, y.scale(), plain_beta);
+    evaluator.mod_switch_to_inplace(plain_beta, y.parms_id());
+    evaluator.add_plain_inplace(y, plain_beta);
+    output = y;
+}
+
 void compute_smax(Ciphertext &input, int r, int gamma, CKKSEncoder &encoder, Encryptor &encryptor,
                   Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
 {

@@ -306,6 +306,85 @@ static int run_all(int log_scale)
         report("compute_smax(gamma 2) vs plain restatement, 32768 slots", err < 1e-3, err, secs);
     }
     {
+        // compute_inv_sqrt (IterApprox.cpp:128-166) and compute_layernorm (:168-246) vs the same
+        // operation sequences restated in doubles (taylor_expand as written, :69-120; Newton with
+        // fakeBootstrap; layernorm's y * z product and first-row beta as written -- DESIGN.md §8)
+        const int S = 32768, row = 768, R = 1024;
+        const double guess = 323251;
+        auto rot = [&](const std::vector<double> &x, int k) {
+            std::vector<double> y(S);
+            for (int i = 0; i < S; i++) y[i] = x[((i + k) % S + S) % S];
+            return y;
+        };
+        auto qsum = [&](const std::vector<double> &x, int nn) {
+            std::vector<double> o(S), r1 = rot(x, 1);
+            for (int i = 0; i < S; i++) o[i] = x[i] + r1[i];
+            for (int acc = 2; acc < nn; acc *= 2)
+            {
+                const auto ro = rot(o, acc);
+                for (int i = 0; i < S; i++) o[i] += ro[i];
+            }
+            return o;
+        };
+        auto plain_inv_sqrt = [&](double a) {
+            double x = -0.5 * (a * std::pow(guess, -1.5)) + 0.375 * std::pow(a * std::pow(guess, -1.25), 2) -
+                       0.3125 * std::pow(a * std::pow(guess, -3.5 / 3), 3);
+            for (int k = 0; k < 4; k++) x = x * ((x * x) * (-0.5 * a) + 1.5);
+            return x;
+        };
+        {
+            std::uniform_real_distribution<double> A(0.6 * guess, 1.6 * guess);
+            std::vector<double> a(S), want(S);
+            for (int i = 0; i < S; i++) want[i] = plain_inv_sqrt(a[i] = A(rng));
+            std::printf("-- compute_inv_sqrt\n");
+            Ciphertext c = enc(a), o;
+            const auto t = std::chrono::steady_clock::now();
+            compute_inv_sqrt(c, o, 4, guess, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            const auto got = dec(o);
+            double err = 0;
+            for (int i = 0; i < S; i++) err = std::max(err, std::fabs(got[i] - want[i]) / std::fabs(want[i]));
+            report("compute_inv_sqrt(4, 323251) vs plain restatement, 32768 slots (relative)", err < 1e-3, err, secs);
+        }
+        {
+            std::uniform_real_distribution<double> X(-0.05, 0.05), G(0.5, 1.5), B(-0.5, 0.5);
+            std::vector<double> x(S, 0.0), gamma(row), beta(row), mask(S, 0.0), mulf(S, 0.0), betap(S, 0.0);
+            for (auto &g : gamma) g = G(rng);
+            for (auto &b : beta) b = B(rng);
+            for (int i = 0; i < 16; i++)
+                for (int j = 0; j < row; j++) x[i * 2 * R + j] = X(rng);
+            for (int i = 0; i < 16; i++)
+                for (int j = 0; j < R; j++)
+                {
+                    mask[i * 2 * R + j] = 1.0;
+                    if (j < row) mulf[i * 2 * R + j] = gamma[j] * std::sqrt((double)row);
+                }
+            for (int j = 0; j < row; j++) betap[j] = beta[j];
+            auto rolled = rot(x, -R);
+            for (int i = 0; i < S; i++) rolled[i] += x[i];
+            const auto folded = qsum(rolled, R);
+            std::vector<double> want(S);
+            double wmax = 0;
+            for (int i = 0; i < S; i++)
+            {
+                const double z = row * x[i] - folded[i];
+                want[i] = (z * z * mask[i]) * z * mulf[i] + betap[i];
+                wmax = std::max(wmax, std::fabs(want[i]));
+            }
+            std::printf("-- compute_layernorm\n");
+            Ciphertext c = enc(x), o;
+            const auto t = std::chrono::steady_clock::now();
+            compute_layernorm(c, o, gamma, beta, row, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            const auto got = dec(o);
+            double err = 0;
+            for (int i = 0; i < S; i++) err = std::max(err, std::fabs(got[i] - want[i]));
+            std::printf("  compute_layernorm: output %zu limbs, max |want| %.4g\n", o.coeff_modulus_size(), wmax);
+            report("compute_layernorm(768) vs plain restatement, 32768 slots (error / max|want|)", err / wmax < 1e-5,
+                   err / wmax, secs);
+        }
+    }
+    {
         // RowMatMul (run_approx_test.cpp:231-297): ones(8 x 2048) x ones(8 x 2048)^T = 2048 everywhere
         std::vector<std::vector<double>> A1(8, std::vector<double>(2048, 1.0)), A1_pre(1, std::vector<double>(32768, 0.0));
         pack_plain_row(A1, 8, 2048, A1_pre);

@@ -23,7 +23,8 @@ def test_gpt2_symbols_exported():
     for sym in ("gpt2::build_cheby_basis", "gpt2::compute_sign_f", "gpt2::compute_sign_g", "gpt2::sign_function",
                 "gpt2::compute_gelu_p", "gpt2::compute_gelu_q", "gpt2::compute_gelu", "gpt2::compute_exp",
                 "gpt2::compute_inverse", "gpt2::quickSum", "gpt2::mask_out", "gpt2::pack_from_row",
-                "gpt2::row_matrix_multiplication_seal", "gpt2::compute_smax"):
+                "gpt2::row_matrix_multiplication_seal", "gpt2::compute_smax",
+                "gpt2::fakeBootstrap", "gpt2::taylor_expand", "gpt2::compute_inv_sqrt", "gpt2::compute_layernorm"):
         assert sym in out, sym
 
 
