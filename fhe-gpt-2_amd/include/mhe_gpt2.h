@@ -126,5 +126,19 @@ void row_matrix_multiplication_seal(std::vector<Ciphertext> &left_inputs, std::v
 
 // The rotation steps of the reference's INIT() (gpt2/util.h:36-74): powers of two below N/2, the
 // listed rotation_kinds and the multiples of 2048
+// util.cpp:344-356: rotate right by shift_amt with a Galois key generated for that one step
+void surefire_rotate(Ciphertext &cipher, int shift_amt, seal::KeyGenerator &keygen, Evaluator &evaluator);
+
+// MatrixMul.cpp:244-358 / :360-478: attention projections into 12 heads (outputs[0..11]), as
+// written in the reference (weights-only working ciphertexts, placement rotations by 0 steps)
+void attn_proj_row_seal(std::vector<Ciphertext> &left_inputs, std::vector<Ciphertext> &weights, Ciphertext bias,
+                        std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                        seal::KeyGenerator &keygen, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                        Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void attn_proj_col_seal(std::vector<Ciphertext> &left_inputs, std::vector<Ciphertext> &weights, Ciphertext bias,
+                        std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                        seal::KeyGenerator &keygen, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                        Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
 std::vector<int> gpt2_rotation_steps(int logN);
 } // namespace gpt2

@@ -541,6 +541,81 @@ void row_matrix_multiplication_seal(std::vector<Ciphertext> &left_inputs, std::v
     for (auto &o : outputs) evaluator.add_inplace_reduced_error(o, bias);
 }
 
+void surefire_rotate(Ciphertext &cipher, int shift_amt, seal::KeyGenerator &keygen, Evaluator &evaluator)
+{
+    // util.cpp:344-356: a one-step Galois key made on the spot (GPU keygen here), then a right
+    // rotation by shift_amt
+    GaloisKeys tmp_keys;
+    keygen.create_galois_keys(std::vector<int>{ -shift_amt }, tmp_keys);
+    evaluator.rotate_vector_inplace(cipher, -shift_amt, tmp_keys);
+}
+
+namespace
+{
+// MatrixMul.cpp:244-358 (row) and :360-478 (col) share one operation sequence and differ only in
+// the head an element is accumulated into.  As written in the reference (its "temporary memory
+// saving" state): the working ciphertexts are weights[j] masked to slot 0, rotated by -1024 and
+// quickSum'd over 1024 -- left_inputs only sets the loop count -- and the placement rotation is
+// by 0 steps.  The reference's OpenMP loop runs the (i, j) pairs in any order; the sum into each
+// head is order-independent up to CKKS rounding.
+template <class HeadOf>
+void attn_proj_seal(std::vector<Ciphertext> &left_inputs, std::vector<Ciphertext> &weights, Ciphertext bias,
+                    std::vector<Ciphertext> &outputs, CKKSEncoder &encoder, Encryptor &encryptor,
+                    Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys,
+                    HeadOf head_of)
+{
+    if (outputs.size() < 12) throw std::invalid_argument("attn_proj: outputs must hold 12 heads");
+    std::vector<std::vector<double>> masks(16, std::vector<double>(32768, 0.0));
+    for (int k = 0; k < 16; k++) masks[k][k * 2048] = 1.0;
+    Ciphertext working, placed;
+    for (std::size_t i = 0; i < left_inputs.size(); i++)
+        for (std::size_t j = 0; j < weights.size(); j++)
+        {
+            // the 16 working ciphertexts of the reference are identical: build one
+            evaluator.multiply_vector_reduced_error(weights[j], masks[0], working);
+            evaluator.rescale_to_next_inplace(working);
+            evaluator.rotate_vector_inplace(working, -1024, gal_keys);
+            quickSum(working, working, 1024, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            for (int rots = 0; rots < 16; rots++)
+                for (int pos = 0; pos < 16; pos++)
+                {
+                    const int head = head_of((int)i, (int)j, rots, pos);
+                    evaluator.multiply_vector_reduced_error(working, masks[pos], placed);
+                    evaluator.rescale_to_next_inplace(placed);
+                    evaluator.rotate_vector_inplace(placed, 0, gal_keys);
+                    evaluator.add_inplace_reduced_error(outputs[head], placed);
+                }
+        }
+    for (auto &o : outputs) evaluator.add_inplace_reduced_error(o, bias);
+}
+} // namespace
+
+void attn_proj_row_seal(std::vector<Ciphertext> &left_inputs, std::vector<Ciphertext> &weights, Ciphertext bias,
+                        std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                        seal::KeyGenerator &, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                        Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    (void)A_rows, (void)A_cols, (void)W_rows;
+    attn_proj_seal(left_inputs, weights, bias, outputs, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys,
+                   [W_cols](int i, int j, int rots, int pos) {
+                       const int abs_pos = (i * 16 + pos) * W_cols + (j * 16 + ((rots + pos) % 16));
+                       return (abs_pos / 64) % 12;
+                   });
+}
+
+void attn_proj_col_seal(std::vector<Ciphertext> &left_inputs, std::vector<Ciphertext> &weights, Ciphertext bias,
+                        std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                        seal::KeyGenerator &, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                        Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    (void)A_rows, (void)A_cols, (void)W_rows, (void)W_cols;
+    attn_proj_seal(left_inputs, weights, bias, outputs, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys,
+                   [](int i, int j, int rots, int pos) {
+                       const int abs_pos = (i * 16 + pos) * 768 + (j * 16 + ((rots + pos) % 16));
+                       return (abs_pos / 64) % 12;
+                   });
+}
+
 std::vector<int> gpt2_rotation_steps(int logN)
 {
     // gpt2/util.h:58-67

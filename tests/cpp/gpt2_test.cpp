@@ -385,6 +385,84 @@ static int run_all(int log_scale)
         }
     }
     {
+        // surefire_rotate (util.cpp:344-356): a key made on the spot, rotation right by the shift
+        const int S = 32768;
+        std::uniform_real_distribution<double> U(-1, 1);
+        std::vector<double> x(S);
+        for (auto &v : x) v = U(rng);
+        Ciphertext c = enc(x);
+        const auto t = std::chrono::steady_clock::now();
+        surefire_rotate(c, 100, keygen, evaluator);
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+        const auto got = dec(c);
+        double err = 0;
+        for (int i = 0; i < S; i++) err = std::max(err, std::fabs(got[i] - x[((i - 100) % S + S) % S]));
+        report("surefire_rotate(100): on-the-spot Galois key, right rotation", err < 1e-6, err, secs);
+    }
+    for (int col = 0; col < 2; col++)
+    {
+        // attn_proj_row_seal / attn_proj_col_seal (MatrixMul.cpp:244-478), as written, vs the same
+        // sequence restated in doubles: working_j = quickSum(rot(w_j * e_0, -1024), 1024); every
+        // (rots, pos) adds working_j * e_{pos*2048} into head (abs_pos / 64) % 12; then + bias
+        const int S = 32768;
+        auto rot = [&](const std::vector<double> &x, int k) {
+            std::vector<double> y(S);
+            for (int i = 0; i < S; i++) y[i] = x[((i + k) % S + S) % S];
+            return y;
+        };
+        auto qsum = [&](const std::vector<double> &x, int nn) {
+            std::vector<double> o(S), r1 = rot(x, 1);
+            for (int i = 0; i < S; i++) o[i] = x[i] + r1[i];
+            for (int acc = 2; acc < nn; acc *= 2)
+            {
+                const auto ro = rot(o, acc);
+                for (int i = 0; i < S; i++) o[i] += ro[i];
+            }
+            return o;
+        };
+        std::uniform_real_distribution<double> U(-1, 1);
+        const int n_left = 1, n_w = 2, W_cols = 768;
+        std::vector<std::vector<double>> w(n_w, std::vector<double>(S));
+        std::vector<double> bias(S);
+        for (auto &r : w)
+            for (auto &v : r) v = U(rng);
+        for (auto &v : bias) v = U(rng);
+        std::vector<std::vector<double>> want(12, bias);
+        for (int i = 0; i < n_left; i++)
+            for (int j = 0; j < n_w; j++)
+            {
+                std::vector<double> m(S, 0.0);
+                m[0] = w[j][0];
+                const auto working = qsum(rot(m, -1024), 1024);
+                for (int rots = 0; rots < 16; rots++)
+                    for (int pos = 0; pos < 16; pos++)
+                    {
+                        const int abs_pos = (i * 16 + pos) * (col ? 768 : W_cols) + (j * 16 + ((rots + pos) % 16));
+                        want[(abs_pos / 64) % 12][pos * 2048] += working[pos * 2048];
+                    }
+            }
+        std::vector<Ciphertext> left{ enc(std::vector<double>(S, 0.5)) }, wc, out;
+        for (auto &r : w) wc.push_back(enc(r));
+        init_output(12, out, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        const auto t = std::chrono::steady_clock::now();
+        if (col)
+            attn_proj_col_seal(left, wc, enc(bias), out, 128, 768, 768, W_cols, keygen, encoder, encryptor, decryptor,
+                               evaluator, gal_keys, relin_keys);
+        else
+            attn_proj_row_seal(left, wc, enc(bias), out, 128, 768, 768, W_cols, keygen, encoder, encryptor, decryptor,
+                               evaluator, gal_keys, relin_keys);
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+        double err = 0;
+        for (int h = 0; h < 12; h++)
+        {
+            const auto got = dec(out[h]);
+            for (int s = 0; s < S; s++) err = std::max(err, std::fabs(got[s] - want[h][s]));
+        }
+        report(col ? "attn_proj_col_seal (1 x 2 ciphers, 12 heads) vs plain restatement"
+                   : "attn_proj_row_seal (1 x 2 ciphers, 12 heads) vs plain restatement",
+               err < 1e-3, err, secs);
+    }
+    {
         // RowMatMul (run_approx_test.cpp:231-297): ones(8 x 2048) x ones(8 x 2048)^T = 2048 everywhere
         std::vector<std::vector<double>> A1(8, std::vector<double>(2048, 1.0)), A1_pre(1, std::vector<double>(32768, 0.0));
         pack_plain_row(A1, 8, 2048, A1_pre);

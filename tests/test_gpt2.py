@@ -24,7 +24,8 @@ def test_gpt2_symbols_exported():
                 "gpt2::compute_gelu_p", "gpt2::compute_gelu_q", "gpt2::compute_gelu", "gpt2::compute_exp",
                 "gpt2::compute_inverse", "gpt2::quickSum", "gpt2::mask_out", "gpt2::pack_from_row",
                 "gpt2::row_matrix_multiplication_seal", "gpt2::compute_smax",
-                "gpt2::fakeBootstrap", "gpt2::taylor_expand", "gpt2::compute_inv_sqrt", "gpt2::compute_layernorm"):
+                "gpt2::fakeBootstrap", "gpt2::taylor_expand", "gpt2::compute_inv_sqrt", "gpt2::compute_layernorm",
+                "gpt2::surefire_rotate", "gpt2::attn_proj_row_seal", "gpt2::attn_proj_col_seal"):
         assert sym in out, sym
 
 
