@@ -140,5 +140,16 @@ void attn_proj_col_seal(std::vector<Ciphertext> &left_inputs, std::vector<Cipher
                         seal::KeyGenerator &keygen, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
                         Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
 
+// MatrixMul.cpp:480-533 / :535-584: Q.K^T scores into rows of 256 slots, and S.V back into the
+// 2048-slot row layout (outputs[0..127]); every placement uses surefire_rotate
+void qk_matmul(std::vector<Ciphertext> &Q, std::vector<Ciphertext> &K, std::vector<Ciphertext> &outputs, int A_rows,
+               int A_cols, int W_rows, int W_cols, seal::KeyGenerator &keygen, CKKSEncoder &encoder,
+               Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+               RelinKeys &relin_keys);
+void sv_matmul(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vector<Ciphertext> &outputs, int A_rows,
+               int A_cols, int W_rows, int W_cols, seal::KeyGenerator &keygen, CKKSEncoder &encoder,
+               Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+               RelinKeys &relin_keys);
+
 std::vector<int> gpt2_rotation_steps(int logN);
 } // namespace gpt2

@@ -616,6 +616,73 @@ void attn_proj_col_seal(std::vector<Ciphertext> &left_inputs, std::vector<Cipher
                    });
 }
 
+void qk_matmul(std::vector<Ciphertext> &Q, std::vector<Ciphertext> &K, std::vector<Ciphertext> &outputs, int A_rows,
+               int A_cols, int W_rows, int W_cols, seal::KeyGenerator &keygen, CKKSEncoder &encoder,
+               Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+               RelinKeys &relin_keys)
+{
+    // MatrixMul.cpp:480-533: K[i] is doubled in place (K + rot(K, 16384)); the Q.K product is
+    // folded over 64 slots, and each of the 128 x 128 (rots, pos) entries is masked to slot
+    // pos*128 and moved by surefire_rotate to row*256 + head_col of outputs[i]
+    (void)A_rows, (void)A_cols, (void)W_rows, (void)W_cols;
+    if (K.size() < Q.size() || outputs.size() < Q.size())
+        throw std::invalid_argument("qk_matmul: K and outputs need one ciphertext per Q ciphertext");
+    Ciphertext rolled, cipher, folded, masked_out;
+    for (std::size_t i = 0; i < Q.size(); i++)
+    {
+        evaluator.rotate_vector(K[i], 16384, gal_keys, rolled);
+        evaluator.add_inplace_reduced_error(K[i], rolled);
+        for (int rots = 0; rots < 128; rots++)
+        {
+            evaluator.multiply_reduced_error(Q[i], K[i], relin_keys, cipher);
+            evaluator.rescale_to_next_inplace(cipher);
+            evaluator.rotate_vector(cipher, 32768 - 64, gal_keys, rolled);
+            quickSum(rolled, folded, 64, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            for (int pos = 0; pos < 128; pos++)
+            {
+                const int row = (int)i * 128 + pos, col = (int)i * 128 + ((rots + pos) % 128);
+                const int head_col = (row * 128 + col) % 128;
+                mask_out(folded, masked_out, pos * 128, 1, encoder, evaluator, relin_keys);
+                const int shift_amt = row * 256 + head_col - pos * 128;
+                surefire_rotate(masked_out, shift_amt, keygen, evaluator);
+                evaluator.add_inplace_reduced_error(outputs[i], masked_out);
+            }
+        }
+    }
+}
+
+void sv_matmul(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vector<Ciphertext> &outputs, int A_rows,
+               int A_cols, int W_rows, int W_cols, seal::KeyGenerator &keygen, CKKSEncoder &encoder,
+               Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+               RelinKeys &relin_keys)
+{
+    // MatrixMul.cpp:535-584: V[i] rotated by 16384 + rots*256, times S[i], folded over 128; each
+    // (rots, pos) entry masked to slot pos*256 and moved by surefire_rotate to
+    // (pos % 16)*2048 + i*64 + (rots + pos) % 64 of outputs[pos]
+    (void)A_rows, (void)A_cols, (void)W_rows, (void)W_cols;
+    if (V.size() < S.size() || outputs.size() < 128)
+        throw std::invalid_argument("sv_matmul: V needs one ciphertext per S ciphertext, outputs 128");
+    Ciphertext cipher, rolled, folded, masked_out;
+    for (std::size_t i = 0; i < S.size(); i++)
+        for (int rots = 0; rots < 64; rots++)
+        {
+            evaluator.rotate_vector(V[i], 32768 - 16384, gal_keys, cipher);
+            evaluator.rotate_vector_inplace(cipher, rots * 256, gal_keys);
+            evaluator.multiply_inplace_reduced_error(cipher, S[i], relin_keys);
+            evaluator.rescale_to_next_inplace(cipher);
+            evaluator.rotate_vector(cipher, 32768 - 128, gal_keys, rolled);
+            quickSum(rolled, folded, 128, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            for (int pos = 0; pos < 128; pos++)
+            {
+                const int col = (rots + pos) % 64;
+                const int desired_location = (pos % 16) * 2048 + (int)i * 64 + col;
+                mask_out(folded, masked_out, pos * 256, 1, encoder, evaluator, relin_keys);
+                surefire_rotate(masked_out, desired_location - pos * 256, keygen, evaluator);
+                evaluator.add_inplace_reduced_error(outputs[pos], masked_out);
+            }
+        }
+}
+
 std::vector<int> gpt2_rotation_steps(int logN)
 {
     // gpt2/util.h:58-67

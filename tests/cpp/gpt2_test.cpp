@@ -96,6 +96,12 @@ static int run_all(int log_scale)
     std::vector<int> steps = gpt2_rotation_steps((int)logN);
     for (int k = 1; k <= 16; k++)
         if (std::find(steps.begin(), steps.end(), 32768 - k) == steps.end()) steps.push_back(32768 - k);
+    // GPT2_QKV=1 adds the qk/sv attention matmul cases, and with them sv_matmul's rotations by
+    // rots*256 (MatrixMul.cpp:551), which INIT()'s list also lacks
+    const bool qkv = std::getenv("GPT2_QKV") != nullptr;
+    if (qkv)
+        for (int r = 1; r < 64; r++)
+            if (std::find(steps.begin(), steps.end(), r * 256) == steps.end()) steps.push_back(r * 256);
     keygen.create_galois_keys(steps, gal_keys);
     set_encode_scale(std::pow(2.0, log_scale));
     CKKSEncoder encoder(context);
@@ -461,6 +467,74 @@ static int run_all(int log_scale)
         report(col ? "attn_proj_col_seal (1 x 2 ciphers, 12 heads) vs plain restatement"
                    : "attn_proj_row_seal (1 x 2 ciphers, 12 heads) vs plain restatement",
                err < 1e-3, err, secs);
+    }
+    if (qkv)
+    {
+        // qk_matmul (MatrixMul.cpp:480-533) and sv_matmul (:535-584) on one ciphertext each, vs the
+        // same sequences restated in doubles; 16384 + 8192 surefire_rotate keys made on the spot
+        const int S = 32768;
+        auto rot = [&](const std::vector<double> &x, int k) {
+            std::vector<double> y(S);
+            for (int i = 0; i < S; i++) y[i] = x[((i + k) % S + S) % S];
+            return y;
+        };
+        auto qsum = [&](const std::vector<double> &x, int nn) {
+            std::vector<double> o(S), r1 = rot(x, 1);
+            for (int i = 0; i < S; i++) o[i] = x[i] + r1[i];
+            for (int acc = 2; acc < nn; acc *= 2)
+            {
+                const auto ro = rot(o, acc);
+                for (int i = 0; i < S; i++) o[i] += ro[i];
+            }
+            return o;
+        };
+        std::uniform_real_distribution<double> U(-1, 1);
+        std::vector<double> q(S), k(S), sm(S), v(S);
+        for (auto *p : { &q, &k, &sm, &v })
+            for (auto &x : *p) x = U(rng);
+        {
+            auto k2 = rot(k, 16384), prod = q;
+            for (int s = 0; s < S; s++) prod[s] *= k[s] + k2[s];
+            const auto folded = qsum(rot(prod, S - 64), 64);
+            std::vector<double> want(S, 0.0);
+            for (int rots = 0; rots < 128; rots++)
+                for (int pos = 0; pos < 128; pos++) want[pos * 256 + (rots + pos) % 128] += folded[pos * 128];
+            std::vector<Ciphertext> Q{ enc(q) }, K{ enc(k) }, out;
+            init_output(1, out, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            std::printf("-- qk_matmul (16384 on-the-spot keys)\n");
+            const auto t = std::chrono::steady_clock::now();
+            qk_matmul(Q, K, out, 128, 64, 128, 64, keygen, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            const auto got = dec(out[0]);
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            double err = 0;
+            for (int s = 0; s < S; s++) err = std::max(err, std::fabs(got[s] - want[s]));
+            report("qk_matmul (1 ciphertext, 128 x 128 placements) vs plain restatement", err < 1e-3, err, secs);
+        }
+        {
+            std::vector<std::vector<double>> want(128, std::vector<double>(S, 0.0));
+            for (int rots = 0; rots < 64; rots++)
+            {
+                auto c = rot(v, 16384 + rots * 256);
+                for (int s = 0; s < S; s++) c[s] *= sm[s];
+                const auto folded = qsum(rot(c, S - 128), 128);
+                for (int pos = 0; pos < 128; pos++)
+                    want[pos][(pos % 16) * 2048 + (rots + pos) % 64] += folded[pos * 256];
+            }
+            std::vector<Ciphertext> Sc{ enc(sm) }, V{ enc(v) }, out;
+            init_output(128, out, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            std::printf("-- sv_matmul (8192 on-the-spot keys)\n");
+            const auto t = std::chrono::steady_clock::now();
+            sv_matmul(Sc, V, out, 128, 128, 128, 64, keygen, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            double err = 0;
+            for (int p = 0; p < 128; p++)
+            {
+                const auto got = dec(out[p]);
+                for (int s = 0; s < S; s++) err = std::max(err, std::fabs(got[s] - want[p][s]));
+            }
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            report("sv_matmul (1 ciphertext, 64 x 128 placements into 128 outputs) vs plain restatement", err < 1e-3, err,
+                   secs);
+        }
     }
     {
         // RowMatMul (run_approx_test.cpp:231-297): ones(8 x 2048) x ones(8 x 2048)^T = 2048 everywhere

@@ -25,7 +25,8 @@ def test_gpt2_symbols_exported():
                 "gpt2::compute_inverse", "gpt2::quickSum", "gpt2::mask_out", "gpt2::pack_from_row",
                 "gpt2::row_matrix_multiplication_seal", "gpt2::compute_smax",
                 "gpt2::fakeBootstrap", "gpt2::taylor_expand", "gpt2::compute_inv_sqrt", "gpt2::compute_layernorm",
-                "gpt2::surefire_rotate", "gpt2::attn_proj_row_seal", "gpt2::attn_proj_col_seal"):
+                "gpt2::surefire_rotate", "gpt2::attn_proj_row_seal", "gpt2::attn_proj_col_seal",
+                "gpt2::qk_matmul", "gpt2::sv_matmul"):
         assert sym in out, sym
 
 
@@ -33,6 +34,18 @@ def test_gpt2_symbols_exported():
 def test_gpt2_approximations_end_to_end():
     _build()
     r = subprocess.run([os.path.join(ROOT, "build", "gpt2_test")], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.environ.get("MHE_LONG"), reason="about 3 minutes of on-the-spot keygen; set MHE_LONG=1")
+def test_gpt2_attention_matmuls():
+    """qk_matmul / sv_matmul (MatrixMul.cpp:480-584): 16384 + 8192 surefire_rotate keys."""
+    _build()
+    env = dict(os.environ, GPT2_QKV="1")
+    r = subprocess.run([os.path.join(ROOT, "build", "gpt2_test")], capture_output=True, text=True, timeout=900, env=env)
     print(r.stdout)
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
