@@ -14,6 +14,8 @@
 //    unrescaled, which loses half the polynomial; see gpt2.cpp).
 #pragma once
 
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "seal/seal.h"
@@ -150,6 +152,22 @@ void sv_matmul(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vect
                int A_cols, int W_rows, int W_cols, seal::KeyGenerator &keygen, CKKSEncoder &encoder,
                Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
                RelinKeys &relin_keys);
+
+// MatrixMul.cpp:586-628 / :630-649 / :651-725: the reference's benchmark-shaped kernels over
+// weights["test"] (cipher_plain_128_128 writes no output, as in the reference)
+void cipher_plain_128_128(Ciphertext &left_input, std::unordered_map<std::string, std::vector<double>> &weights,
+                          Ciphertext bias, std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows,
+                          int W_cols, seal::KeyGenerator &keygen, CKKSEncoder &encoder, Encryptor &encryptor,
+                          Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void batch_matmul(std::vector<Ciphertext> &left_inputs, std::unordered_map<std::string, std::vector<double>> &weights,
+                  Ciphertext bias, std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                  seal::KeyGenerator &keygen, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                  Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void qk_matmul_col(std::vector<Ciphertext> &left_input, std::vector<Ciphertext> &right_input,
+                   std::unordered_map<std::string, std::vector<double>> &weights, Ciphertext bias,
+                   std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                   seal::KeyGenerator &keygen, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                   Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
 
 std::vector<int> gpt2_rotation_steps(int logN);
 } // namespace gpt2

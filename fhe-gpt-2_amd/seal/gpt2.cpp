@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <cmath>
 #include <stdexcept>
+#include <string>
+#include <unordered_map>
 
 namespace gpt2
 {
@@ -681,6 +683,92 @@ void sv_matmul(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vect
                 evaluator.add_inplace_reduced_error(outputs[pos], masked_out);
             }
         }
+}
+
+namespace
+{
+const std::vector<double> &test_weights(const std::unordered_map<std::string, std::vector<double>> &weights,
+                                        const char *who)
+{
+    const auto it = weights.find("test");
+    if (it == weights.end()) throw std::invalid_argument(std::string(who) + ": weights[\"test\"] missing");
+    return it->second;
+}
+} // namespace
+
+void cipher_plain_128_128(Ciphertext &left_input, std::unordered_map<std::string, std::vector<double>> &weights,
+                          Ciphertext bias, std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows,
+                          int W_cols, seal::KeyGenerator &, CKKSEncoder &encoder, Encryptor &encryptor,
+                          Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    // MatrixMul.cpp:586-628, as written: 128 rounds of four plain products, two quickSums(128) and
+    // a second plain product pair summed; the results stay in locals (outputs is not written)
+    (void)bias, (void)outputs, (void)A_rows, (void)A_cols, (void)W_rows, (void)W_cols;
+    const auto &w = test_weights(weights, "cipher_plain_128_128");
+    Ciphertext p0l, p0r, p1l, p1r, lt, rt, out0;
+    for (int rots = 0; rots < 128; rots++)
+    {
+        evaluator.multiply_vector_reduced_error(left_input, w, p0l);
+        evaluator.rescale_to_next_inplace(p0l);
+        evaluator.multiply_vector_reduced_error(left_input, w, p0r);
+        evaluator.rescale_to_next_inplace(p0r);
+        evaluator.multiply_vector_reduced_error(left_input, w, p1l);
+        evaluator.rescale_to_next_inplace(p1l);
+        evaluator.multiply_vector_reduced_error(left_input, w, p1r);
+        evaluator.rescale_to_next_inplace(p1r);
+        quickSum(p0l, p0l, 128, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        quickSum(p0r, p0r, 128, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        evaluator.multiply_vector_reduced_error(p0l, w, lt);
+        evaluator.multiply_vector_reduced_error(p0r, w, rt);
+        evaluator.add(lt, rt, out0);
+        evaluator.rescale_to_next_inplace(out0);
+    }
+}
+
+void batch_matmul(std::vector<Ciphertext> &left_inputs, std::unordered_map<std::string, std::vector<double>> &weights,
+                  Ciphertext bias, std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                  seal::KeyGenerator &, CKKSEncoder &, Encryptor &, Decryptor &, Evaluator &evaluator, GaloisKeys &,
+                  RelinKeys &)
+{
+    // MatrixMul.cpp:630-649: outputs[i] = sum_{j<128} left_inputs[j] * weights["test"], i < 64
+    (void)bias, (void)A_rows, (void)A_cols, (void)W_rows, (void)W_cols;
+    const auto &w = test_weights(weights, "batch_matmul");
+    if (left_inputs.size() < 128 || outputs.size() < 64)
+        throw std::invalid_argument("batch_matmul: needs 128 left inputs and 64 outputs");
+    std::vector<Ciphertext> cipher(128);
+    for (int i = 0; i < 64; i++)
+    {
+        for (int j = 0; j < 128; j++)
+        {
+            evaluator.multiply_vector_reduced_error(left_inputs[j], w, cipher[j]);
+            evaluator.rescale_to_next_inplace(cipher[j]);
+        }
+        evaluator.add_many(cipher, outputs[i]);
+    }
+}
+
+void qk_matmul_col(std::vector<Ciphertext> &left_input, std::vector<Ciphertext> &right_input,
+                   std::unordered_map<std::string, std::vector<double>> &weights, Ciphertext bias,
+                   std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_rows, int W_cols,
+                   seal::KeyGenerator &, CKKSEncoder &, Encryptor &, Decryptor &, Evaluator &evaluator,
+                   GaloisKeys &gal_keys, RelinKeys &relin_keys)
+{
+    // MatrixMul.cpp:651-725: outputs[i] = sum_{j<64} left[j] * rot(right[j], i); right_input is
+    // rotated by one slot in place after each of the 128 rounds
+    (void)weights, (void)bias, (void)A_rows, (void)A_cols, (void)W_rows, (void)W_cols;
+    if (left_input.size() < 64 || right_input.size() < 64 || outputs.size() < 128)
+        throw std::invalid_argument("qk_matmul_col: needs 64 left and right inputs and 128 outputs");
+    std::vector<Ciphertext> cipher(64);
+    for (int i = 0; i < 128; i++)
+    {
+        for (int j = 0; j < 64; j++)
+        {
+            evaluator.multiply_reduced_error(left_input[j], right_input[j], relin_keys, cipher[j]);
+            evaluator.rescale_to_next_inplace(cipher[j]);
+        }
+        evaluator.add_many(cipher, outputs[i]);
+        for (int j = 0; j < 64; j++) evaluator.rotate_vector_inplace(right_input[j], 1, gal_keys);
+    }
 }
 
 std::vector<int> gpt2_rotation_steps(int logN)

@@ -18,6 +18,7 @@
 #include <functional>
 #include <random>
 #include <string>
+#include <unordered_map>
 
 using namespace seal;
 using namespace gpt2;
@@ -534,6 +535,77 @@ static int run_all(int log_scale)
             const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
             report("sv_matmul (1 ciphertext, 64 x 128 placements into 128 outputs) vs plain restatement", err < 1e-3, err,
                    secs);
+        }
+    }
+    if (qkv)
+    {
+        // batch_matmul (MatrixMul.cpp:630-649), qk_matmul_col (:651-725), cipher_plain_128_128
+        // (:586-628) vs plain restatements
+        const int S = 32768;
+        std::uniform_real_distribution<double> U(-1, 1);
+        std::unordered_map<std::string, std::vector<double>> weights{ { "test", std::vector<double>(S) } };
+        for (auto &x : weights["test"]) x = U(rng);
+        const auto &w = weights["test"];
+        std::vector<std::vector<double>> L(128, std::vector<double>(S)), R(64, std::vector<double>(S));
+        for (auto &r : L)
+            for (auto &x : r) x = U(rng);
+        for (auto &r : R)
+            for (auto &x : r) x = U(rng);
+        std::vector<Ciphertext> Lc, Rc, out;
+        for (auto &r : L) Lc.push_back(enc(r));
+        for (auto &r : R) Rc.push_back(enc(r));
+        Ciphertext bias = enc(std::vector<double>(S, 0.0));
+        {
+            std::vector<double> want(S, 0.0);
+            for (int j = 0; j < 128; j++)
+                for (int s = 0; s < S; s++) want[s] += L[j][s] * w[s];
+            init_output(64, out, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            std::printf("-- batch_matmul\n");
+            const auto t = std::chrono::steady_clock::now();
+            batch_matmul(Lc, weights, bias, out, 128, 128, 128, 128, keygen, encoder, encryptor, decryptor, evaluator,
+                         gal_keys, relin_keys);
+            double err = 0;
+            for (int i : { 0, 31, 63 })
+            {
+                const auto got = dec(out[i]);
+                for (int s = 0; s < S; s++) err = std::max(err, std::fabs(got[s] - want[s]));
+            }
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            report("batch_matmul (128 x weights[\"test\"] into 64 outputs) vs plain", err < 1e-3, err, secs);
+        }
+        {
+            out.clear();
+            init_output(128, out, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            std::printf("-- qk_matmul_col\n");
+            std::vector<Ciphertext> Lh(Lc.begin(), Lc.begin() + 64);
+            const auto t = std::chrono::steady_clock::now();
+            qk_matmul_col(Lh, Rc, weights, bias, out, 128, 64, 128, 64, keygen, encoder, encryptor, decryptor,
+                          evaluator, gal_keys, relin_keys);
+            double err = 0;
+            for (int i : { 0, 1, 77, 127 })
+            {
+                const auto got = dec(out[i]);
+                for (int s = 0; s < S; s++)
+                {
+                    double want = 0;
+                    for (int j = 0; j < 64; j++) want += L[j][s] * R[j][(s + i) % S];
+                    err = std::max(err, std::fabs(got[s] - want));
+                }
+            }
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            report("qk_matmul_col (64 pairs, 128 rotation rounds) vs plain", err < 1e-3, err, secs);
+        }
+        {
+            std::printf("-- cipher_plain_128_128\n");
+            const auto before = dec(out[0]);
+            const auto t = std::chrono::steady_clock::now();
+            cipher_plain_128_128(Lc[0], weights, bias, out, 128, 128, 128, 128, keygen, encoder, encryptor, decryptor,
+                                 evaluator, gal_keys, relin_keys);
+            const auto after = dec(out[0]);
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            double err = 0;
+            for (int s = 0; s < S; s++) err = std::max(err, std::fabs(after[s] - before[s]));
+            report("cipher_plain_128_128 runs its 128 rounds and leaves outputs untouched", err == 0, err, secs);
         }
     }
     {

@@ -26,7 +26,8 @@ def test_gpt2_symbols_exported():
                 "gpt2::row_matrix_multiplication_seal", "gpt2::compute_smax",
                 "gpt2::fakeBootstrap", "gpt2::taylor_expand", "gpt2::compute_inv_sqrt", "gpt2::compute_layernorm",
                 "gpt2::surefire_rotate", "gpt2::attn_proj_row_seal", "gpt2::attn_proj_col_seal",
-                "gpt2::qk_matmul", "gpt2::sv_matmul"):
+                "gpt2::qk_matmul", "gpt2::sv_matmul",
+                "gpt2::batch_matmul", "gpt2::qk_matmul_col", "gpt2::cipher_plain_128_128"):
         assert sym in out, sym
 
 
