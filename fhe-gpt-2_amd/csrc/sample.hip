@@ -1,129 +1,212 @@
-// On-device sampling of the random polynomials of key generation and encryption
-// (SEAL/util/rlwe.cpp sample_poly_uniform / sample_poly_ternary / sample_poly_normal), written
-// straight into RNS form on the GPU: no host loops, no host->device upload, no stream sync.
+// On-device sampling of the random polynomials of key generation and encryption, bit-identical
+// to SEAL's samplers (SEAL/util/rlwe.cpp) fed by SEAL's default PRNG, Blake2xbPRNG
+// (SEAL/randomgen.cpp:185-195): the PRNG stream is 4096-byte buffers, buffer c =
+// BLAKE2Xb(out 4096, message = u64 counter c, key = the 64-byte seed).  Every 64-byte block of
+// the stream is one independent BLAKE2b compression (csrc/blake2b.h), so a sampler that knows
+// where its bytes sit in the stream computes them in parallel:
 //
-// Randomness: Philox4x32-10 (Salmon et al., SC'11), counter = (element index, polynomial tag),
-// key = 64-bit seed.  Distributions:
-//   uniform mod q_l : 128 random bits reduced by Barrett (statistical distance < q / 2^128);
-//   ternary         : 64 random bits mod 3, minus 1;
-//   normal          : Box-Muller, sigma = 3.2, rejected outside 6 sigma (ClippedNormal),
-//                     truncated to an integer as sample_poly_normal does.
-// These are SEAL's distributions, not SEAL's bits (SEAL uses Blake2xb): keys and ciphertexts
-// differ from SEAL's for the same seed; every operation on them is bit-exact.
+//   sample_poly_uniform (rlwe.cpp:136-162): the whole [limbs][n] u64 array is one bulk draw;
+//     a word w >= max_multiple(q_l) is redrawn, in index order, from the words after the bulk.
+//     The GPU draws the bulk, reduces the accepted words of the limbs the caller keeps and lists
+//     the rejected indices (~q/2^64 of them); the host orders that list and assigns the
+//     replacement words from the stream tail (mhe_prng_uniform_fix).
+//   sample_poly_ternary (rlwe.cpp:21-38): one std::uniform_int_distribution<u64>(0, 2) draw per
+//     coefficient over a 32-bit adapter; libstdc++ 11 maps a 32-bit word g to (3g) >> 32
+//     (Lemire, bits/uniform_int_dist.h:246-270) and redraws only when g == 0 -- reported back so
+//     the caller can take the host path (probability 2^-32 per coefficient).
+//   sample_poly_cbd (rlwe.cpp:101-133): 6 bytes per coefficient, x[2], x[5] masked to 5 bits,
+//     noise = pop(x0)+pop(x1)+pop(x2) - pop(x3)-pop(x4)-pop(x5).
+// Small samples are written as canonical residues over every requested limb (rand + (flag & q)).
 #include <hip/hip_runtime.h>
 
 #include "../../include/mhe.h"
 #include "arith.h"
+#include "blake2b.h"
 
 int mhe_internal_fail(int code, const char *msg);
 int mhe_internal_primes(mhe_ctx *c, const PrimeDev **dev, const uint64_t **host, int *count, int *log_n);
 
 namespace
 {
-__device__ __forceinline__ void philox10(u32 (&ctr)[4], u32 k0, u32 k1)
+struct Seed
 {
-#pragma unroll
-    for (int r = 0; r < 10; r++)
-    {
-        const u64 p0 = (u64)0xD2511F53u * ctr[0], p1 = (u64)0xCD9E8D57u * ctr[2];
-        const u32 h0 = (u32)(p0 >> 32), l0 = (u32)p0, h1 = (u32)(p1 >> 32), l1 = (u32)p1;
-        const u32 n0 = h1 ^ ctr[1] ^ k0, n2 = h0 ^ ctr[3] ^ k1;
-        ctr[0] = n0;
-        ctr[1] = l1;
-        ctr[2] = n2;
-        ctr[3] = l0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-
-// 128 random bits for (element, tag, draw)
-__device__ __forceinline__ void rand128(u64 idx, u64 tag, u32 draw, u64 seed, u64 &lo, u64 &hi)
-{
-    u32 ctr[4] = { (u32)idx, (u32)(idx >> 32) ^ (draw << 24), (u32)tag, (u32)(tag >> 32) };
-    philox10(ctr, (u32)seed, (u32)(seed >> 32));
-    lo = ((u64)ctr[1] << 32) | ctr[0];
-    hi = ((u64)ctr[3] << 32) | ctr[2];
-}
-
-enum Kind
-{
-    UNIFORM = 0,
-    TERNARY = 1,
-    NORMAL = 2
+    u64 w[8];
 };
 
-__global__ void k_sample_uniform(u64 *out, const PrimeDev *primes, int limbs, int log_n, u64 seed, u64 tag)
+// limb l of the sampled array -> output limb slot (-1: not kept), max 64 limbs
+struct LimbMap
 {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const size_t total = (size_t)limbs << log_n;
-    if (i >= total) return;
-    u64 lo, hi;
-    rand128(i, tag, 0, seed, lo, hi);
-    out[i] = barrett128(lo, hi, primes[i >> log_n]);
+    signed char slot[64];
+    int prime[64]; // context prime index of limb l
+};
+
+// 64-byte stream block `blk` (= byte offset / 64) of the PRNG seeded with `s`
+__device__ __forceinline__ void stream_block(const Seed &s, u64 blk, u64 (&out)[8])
+{
+    u64 root[8];
+    b2b::xof_root(s.w, blk >> 6, b2b::kPrngBuffer, root);
+    b2b::xof_block(root, (u32)(blk & 63), b2b::kPrngBuffer, 64, out);
 }
 
-__global__ void k_sample_small(u64 *out, const PrimeDev *primes, int limbs, int log_n, int kind, u64 seed, u64 tag)
+// Bulk of sample_poly_uniform over `limbs` limbs: one thread per 64-byte block (8 words).
+__global__ void k_prng_uniform(Seed s, LimbMap map, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                               u64 *rej, u32 *rej_count, u32 rej_cap)
 {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const size_t n = (size_t)1 << log_n;
-    if (i >= n) return;
-    long long v;
-    if (kind == TERNARY)
+    const u64 blk = (u64)blockIdx.x * 256 + threadIdx.x;
+    const u64 total = (u64)limbs << log_n;
+    if (blk * 8 >= total) return;
+    u64 w[8];
+    stream_block(s, blk, w);
+#pragma unroll
+    for (int k = 0; k < 8; k++)
     {
-        u64 lo, hi;
-        rand128(i, tag, 0, seed, lo, hi);
-        v = (long long)(lo % 3) - 1;
-    }
-    else
-    {
-        // Box-Muller with rejection outside 6 sigma (rare: p ~ 2e-9); every draw uses its own
-        // counter, so the loop is bounded in practice and deterministic
-        const double sigma = 3.2, bound = 6 * 3.2, two_pi = 6.283185307179586476925286766559;
-        double z = 0;
-        for (u32 d = 0; d < 64; d++)
+        const u64 g = blk * 8 + k;
+        const int l = (int)(g >> log_n);
+        const PrimeDev p = primes[map.prime[l]];
+        // max_multiple = (2^64 - 1) - barrett_reduce_64(2^64 - 1, q) - 1 (rlwe.cpp:152)
+        const u64 mm = ~0ULL - barrett64(~0ULL, p) - 1;
+        if (w[k] >= mm)
         {
-            u64 lo, hi;
-            rand128(i, tag, d, seed, lo, hi);
-            const double u1 = ((lo >> 11) + 1) * 0x1.0p-53; // (0, 1]
-            const double u2 = (hi >> 11) * 0x1.0p-53;       // [0, 1)
-            z = sigma * sqrt(-2.0 * log(u1)) * cos(two_pi * u2);
-            if (fabs(z) <= bound) break;
-            z = 0;
+            const u32 at = atomicAdd(rej_count, 1u);
+            if (at < rej_cap) rej[at] = g;
         }
-        v = (long long)z; // truncation, as sample_poly_normal's static_cast<int64_t>
+        else if (map.slot[l] >= 0)
+            out[((u64)map.slot[l] << log_n) + (g & (((u64)1 << log_n) - 1))] = barrett64(w[k], p);
     }
-    for (int l = 0; l < limbs; l++)
+}
+
+__global__ void k_prng_apply(const u64 *fix, u32 count, u64 *out)
+{
+    const u32 i = blockIdx.x * 256 + threadIdx.x;
+    if (i < count) out[fix[2 * i]] = fix[2 * i + 1];
+}
+
+// sample_poly_ternary: coefficients [0, n) from the stream bytes at byte offset `off` (64-aligned),
+// 16 coefficients (one block) per thread.  *rejected is set when some word is 0 (Lemire redraw).
+__global__ void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs, int log_n, u32 *rejected)
+{
+    const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+    const u64 n = (u64)1 << log_n;
+    if (t * 16 >= n) return;
+    u64 w[8];
+    stream_block(s, (off >> 6) + t, w);
+#pragma unroll
+    for (int k = 0; k < 16; k++)
     {
-        const u64 q = primes[l].q;
-        out[((size_t)l << log_n) + i] = v >= 0 ? (u64)v : q - (u64)(-v);
+        const u32 g = (u32)(w[k >> 1] >> (32 * (k & 1)));
+        if (g == 0) atomicOr(rejected, 1u);
+        const u64 r = ((u64)g * 3) >> 32; // {0, 1, 2} -> {-1, 0, 1}
+        const u64 i = t * 16 + k;
+        for (int l = 0; l < limbs; l++)
+        {
+            const u64 q = primes[l].q;
+            out[((u64)l << log_n) + i] = r == 0 ? q - 1 : r - 1;
+        }
     }
+}
+
+// sample_poly_cbd: coefficients [0, n) from the bytes at offset `off` (64-aligned), 32
+// coefficients (192 bytes = 3 blocks) per thread.
+__global__ void k_prng_cbd(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs, int log_n)
+{
+    const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+    const u64 n = (u64)1 << log_n;
+    if (t * 32 >= n) return;
+    u64 w[24];
+    {
+        u64 b[8];
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+        {
+            stream_block(s, (off >> 6) + 3 * t + j, b);
+#pragma unroll
+            for (int k = 0; k < 8; k++) w[8 * j + k] = b[k];
+        }
+    }
+    auto byte_at = [&](int i) -> u32 { return (u32)(w[i >> 3] >> (8 * (i & 7))) & 0xff; };
+    const int cnt = (int)((n - t * 32) < 32 ? (n - t * 32) : 32);
+    for (int k = 0; k < cnt; k++)
+    {
+        const int b0 = 6 * k;
+        const int noise = __popc(byte_at(b0)) + __popc(byte_at(b0 + 1)) + __popc(byte_at(b0 + 2) & 0x1f) -
+                          __popc(byte_at(b0 + 3)) - __popc(byte_at(b0 + 4)) - __popc(byte_at(b0 + 5) & 0x1f);
+        const u64 i = t * 32 + k;
+        for (int l = 0; l < limbs; l++)
+        {
+            const u64 q = primes[l].q;
+            out[((u64)l << log_n) + i] = noise >= 0 ? (u64)noise : q - (u64)(-noise);
+        }
+    }
+}
+
+int launch_check(const char *what)
+{
+    if (hipGetLastError() != hipSuccess) return mhe_internal_fail(MHE_ERR_DEVICE, what);
+    return MHE_OK;
 }
 } // namespace
 
-extern "C" __attribute__((visibility("default"))) int mhe_sample_poly(mhe_ctx *c, uint64_t *out, int limbs, int kind,
-                                                                     uint64_t seed, uint64_t tag, void *stream)
+#define MHE_EXPORT extern "C" __attribute__((visibility("default")))
+
+MHE_EXPORT int mhe_prng_uniform_bulk(mhe_ctx *c, const uint64_t seed[8], int limbs, const int *prime_of_limb,
+                                     const int *slot_of_limb, uint64_t *out, uint64_t *rej, uint32_t *rej_count,
+                                     uint32_t rej_cap, void *stream)
 {
     const PrimeDev *primes;
     const uint64_t *q;
     int K, log_n;
     if (mhe_internal_primes(c, &primes, &q, &K, &log_n)) return mhe_internal_fail(MHE_ERR_ARG, "context is not valid");
-    if (!out || limbs < 1 || limbs > K) return mhe_internal_fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    if (!seed || !prime_of_limb || !slot_of_limb || !out || !rej || !rej_count || limbs < 1 || limbs > 64)
+        return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
+    Seed s;
+    LimbMap m;
+    for (int i = 0; i < 8; i++) s.w[i] = seed[i];
+    for (int l = 0; l < 64; l++)
+    {
+        m.slot[l] = l < limbs ? (signed char)slot_of_limb[l] : -1;
+        m.prime[l] = l < limbs ? prime_of_limb[l] : 0;
+        if (l < limbs && (prime_of_limb[l] < 0 || prime_of_limb[l] >= K))
+            return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
+    }
     hipStream_t st = (hipStream_t)stream;
-    if (kind == UNIFORM)
+    const u64 blocks = ((u64)limbs << log_n) / 8;
+    hipLaunchKernelGGL(k_prng_uniform, dim3((unsigned)((blocks + 255) / 256)), dim3(256), 0, st, s, m, out, primes,
+                       limbs, log_n, rej, rej_count, rej_cap);
+    return launch_check("uniform sampling kernel launch failed");
+}
+
+MHE_EXPORT int mhe_prng_apply_fixes(mhe_ctx *c, const uint64_t *fixes_dev, uint32_t count, uint64_t *out, void *stream)
+{
+    if (!c || (count && (!fixes_dev || !out))) return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
+    if (!count) return MHE_OK;
+    hipLaunchKernelGGL(k_prng_apply, dim3((count + 255) / 256), dim3(256), 0, (hipStream_t)stream, fixes_dev, count,
+                       out);
+    return launch_check("sampling fix-up launch failed");
+}
+
+MHE_EXPORT int mhe_prng_small(mhe_ctx *c, const uint64_t seed[8], uint64_t byte_offset, int kind, int limbs,
+                              uint64_t *out, uint32_t *flag_dev, void *stream)
+{
+    const PrimeDev *primes;
+    const uint64_t *q;
+    int K, log_n;
+    if (mhe_internal_primes(c, &primes, &q, &K, &log_n)) return mhe_internal_fail(MHE_ERR_ARG, "context is not valid");
+    if (!seed || !out || limbs < 1 || limbs > K || (byte_offset & 63) || log_n < 5)
+        return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
+    Seed s;
+    for (int i = 0; i < 8; i++) s.w[i] = seed[i];
+    hipStream_t st = (hipStream_t)stream;
+    const u64 n = (u64)1 << log_n;
+    if (kind == MHE_SAMPLE_TERNARY)
     {
-        const size_t total = (size_t)limbs << log_n;
-        hipLaunchKernelGGL(k_sample_uniform, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, out, primes,
-                           limbs, log_n, seed, tag);
+        if (!flag_dev) return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
+        hipLaunchKernelGGL(k_prng_ternary, dim3((unsigned)((n / 16 + 255) / 256)), dim3(256), 0, st, s, byte_offset, out,
+                           primes, limbs, log_n, flag_dev);
     }
-    else if (kind == TERNARY || kind == NORMAL)
-    {
-        const size_t n = (size_t)1 << log_n;
-        hipLaunchKernelGGL(k_sample_small, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, primes, limbs,
-                           log_n, kind, seed, tag);
-    }
+    else if (kind == MHE_SAMPLE_CBD)
+        hipLaunchKernelGGL(k_prng_cbd, dim3((unsigned)((n / 32 + 255) / 256)), dim3(256), 0, st, s, byte_offset, out,
+                           primes, limbs, log_n);
     else
         return mhe_internal_fail(MHE_ERR_ARG, "unknown distribution");
-    if (hipGetLastError() != hipSuccess) return mhe_internal_fail(MHE_ERR_DEVICE, "sampling kernel launch failed");
-    return MHE_OK;
+    return launch_check("sampling kernel launch failed");
 }

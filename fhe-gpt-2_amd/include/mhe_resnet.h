@@ -55,12 +55,18 @@ public:
     // image per OpenMP thread, infer_seal.cpp:404); results in image order
     std::vector<ResNetResult> infer_batch(const std::vector<std::vector<double>> &images, int threads);
     double setup_seconds() const { return setup_s_; }
+    // setup breakdown: the client's planning inference (deferred keys) and the truncated-key generation
+    double plan_seconds() const { return plan_s_; }
+    double keygen_seconds() const { return keygen_s_; }
+    std::size_t galois_keys() const { return galois_keys_; }
+    // device bytes of the server's Galois key set (all resident in HBM: no key traffic per image)
     double galois_key_gb() const;
 
 private:
     struct Impl;
     std::unique_ptr<Impl> impl_;
-    double setup_s_ = 0;
+    double setup_s_ = 0, plan_s_ = 0, keygen_s_ = 0;
+    std::size_t galois_keys_ = 0;
 };
 
 // infer_seal.cpp:234-577 entry point: images [start, end] from ../../../testFile/test_values.txt

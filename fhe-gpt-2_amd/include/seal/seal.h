@@ -14,9 +14,9 @@
 // cnn/infer_seal.cpp:404).
 //
 // Differences from SEAL, by design:
-//  * randomness: key generation and encryption draw from std::mt19937_64 (seeded from
-//    std::random_device, or from Blake2xbPRNGFactory's seed words), not from Blake2xb, so
-//    keys/ciphertexts are not SEAL's bits -- every *operation* on given inputs is bit-exact;
+//  * randomness is SEAL's: Blake2xbPRNG seeded from OS entropy (or a factory's default seed),
+//    SEAL's samplers (run on the GPU where they are parallel), so keys and encryptions are SEAL's
+//    bits for the same seed;
 //  * SEAL's memory pools (MemoryPoolHandle) are accepted and ignored;
 //  * serialization (save/load) is not provided yet.
 #pragma once
@@ -127,25 +127,96 @@ public:
     static std::vector<Modulus> Create(std::size_t poly_modulus_degree, std::vector<int> bit_sizes);
 };
 
-// Seeded PRNG factory: keeps SEAL's construction syntax (SEAL/randomgen.h:553); the words
-// seed std::mt19937_64, not Blake2xb.
+// Randomness (SEAL/randomgen.h): OS entropy, the Blake2xb PRNG and its factories, as in SEAL.
+constexpr std::size_t prng_seed_uint64_count = 8;
+constexpr std::size_t prng_seed_byte_count = prng_seed_uint64_count * 8;
+using prng_seed_type = std::array<std::uint64_t, prng_seed_uint64_count>;
+enum class prng_type : std::uint8_t
+{
+    unknown = 0,
+    blake2xb = 1,
+    shake256 = 2
+};
+
+// randomgen.cpp:23-50: bytes from the kernel CSPRNG (getrandom)
+void random_bytes(seal_byte *buf, std::size_t count);
+inline std::uint64_t random_uint64()
+{
+    std::uint64_t r;
+    random_bytes(reinterpret_cast<seal_byte *>(&r), sizeof(r));
+    return r;
+}
+
+// Blake2xbPRNG (randomgen.h:200-270, randomgen.cpp:160-195): 4096-byte buffers, buffer c =
+// BLAKE2Xb(4096 bytes, message = u64 counter c, key = the 64-byte seed)
+class UniformRandomGenerator
+{
+public:
+    explicit UniformRandomGenerator(prng_seed_type seed);
+    virtual ~UniformRandomGenerator();
+    prng_seed_type seed() const noexcept { return seed_; }
+    prng_type type() const noexcept { return prng_type::blake2xb; }
+    void generate(std::size_t byte_count, seal_byte *destination);
+    std::uint32_t generate();
+    void refresh();
+
+private:
+    void refill_buffer();
+    prng_seed_type seed_;
+    std::array<std::uint8_t, 4096> buffer_{};
+    std::size_t head_ = 4096; // buffer_head_ starts at buffer_end_ (randomgen.h:224)
+    std::uint64_t counter_ = 0;
+    std::mutex mutex_;
+};
+
+class Blake2xbPRNG : public UniformRandomGenerator
+{
+public:
+    using UniformRandomGenerator::UniformRandomGenerator;
+};
+
+// randomgen.h:405-470: a factory seeds every generator it creates from fresh OS entropy, or --
+// constructed with a default seed, for debugging -- always with that seed.
 class UniformRandomGeneratorFactory
 {
 public:
+    UniformRandomGeneratorFactory() : use_random_seed_(true) {}
+    explicit UniformRandomGeneratorFactory(prng_seed_type default_seed)
+        : default_seed_(default_seed), use_random_seed_(false)
+    {}
     virtual ~UniformRandomGeneratorFactory() = default;
-    virtual std::uint64_t seed() const = 0;
+    std::shared_ptr<UniformRandomGenerator> create() { return std::make_shared<Blake2xbPRNG>(next_seed()); }
+    std::shared_ptr<UniformRandomGenerator> create(prng_seed_type seed) { return std::make_shared<Blake2xbPRNG>(seed); }
+    bool use_random_seed() const noexcept { return use_random_seed_; }
+    const prng_seed_type &default_seed() const noexcept { return default_seed_; }
+    static std::shared_ptr<UniformRandomGeneratorFactory> DefaultFactory();
+    // (not SEAL API) the seed create() gives its generator: 512 fresh bits, or the default seed
+    prng_seed_type next_seed() const;
+
+private:
+    prng_seed_type default_seed_{};
+    bool use_random_seed_;
 };
 
 class Blake2xbPRNGFactory : public UniformRandomGeneratorFactory
 {
 public:
-    Blake2xbPRNGFactory() : seeded_(false), seed_(0) {}
-    explicit Blake2xbPRNGFactory(const std::array<std::uint64_t, 8> &s);
-    std::uint64_t seed() const override;
+    Blake2xbPRNGFactory() = default;
+    explicit Blake2xbPRNGFactory(prng_seed_type default_seed) : UniformRandomGeneratorFactory(default_seed) {}
+};
+
+// randomtostd.h: a UniformRandomGenerator as a 32-bit standard URBG
+class RandomToStandardAdapter
+{
+public:
+    using result_type = std::uint32_t;
+    explicit RandomToStandardAdapter(UniformRandomGenerator &g) : g_(&g) {}
+    result_type operator()() { return g_->generate(); }
+    static constexpr result_type min() noexcept { return 0; }
+    static constexpr result_type max() noexcept { return 0xFFFFFFFFu; }
 
 private:
-    bool seeded_;
-    std::uint64_t seed_;
+    UniformRandomGenerator *g_;
 };
 
 // EncryptionParameters (SEAL/encryptionparams.h, with the modified hamming weight / sparse slots)
@@ -164,6 +235,11 @@ public:
     std::size_t secret_key_hamming_weight() const noexcept { return hamming_weight_; }
     std::size_t sparse_slots() const noexcept { return sparse_slots_; }
     std::shared_ptr<UniformRandomGeneratorFactory> random_generator() const { return rng_; }
+    // (not SEAL API) random_generator(), or SEAL's default factory when none was set (context.cpp:464-467)
+    std::shared_ptr<UniformRandomGeneratorFactory> random_generator_or_default() const
+    {
+        return rng_ ? rng_ : UniformRandomGeneratorFactory::DefaultFactory();
+    }
     parms_id_type parms_id() const;
 
 private:
@@ -386,13 +462,16 @@ private:
 
 // KSwitchKeys (SEAL/kswitchkeys.h): one device buffer [digits][2][key_limbs][n] per key index.
 //
-// Deferred materialisation (Galois keys, MI355X memory budget): the reference's ResNet driver asks
-// for 284 Galois keys at the key level, 284 x 1.04 GB = 295 GB, more than one GPU's 288 GB HBM.
-// Most of them are only ever used at <= 3 limbs (the convolutions), where a key needs only L
-// digits over L+1 primes.  A deferred key set keeps the secret key and, per index, a seed; the
-// first rotation at L limbs materialises the level-truncated key (L digits, primes q_0..q_{L-1}
-// and P) and a later use at a higher level re-materialises it larger.  The evaluator sees the
-// same key-switching formula; only the key's random parts differ from an eager key.
+// Keys are SEAL's: KeyGenerator draws them with SEAL's randomness and the evaluator owns no
+// secret.  Level-truncated keys (MI355X memory budget): the reference's ResNet driver asks for
+// 284 Galois keys at the key level, 284 x 1.04 GB = 295 GB, more than one GPU's 288 GB HBM, yet
+// most are only used at <= 3 limbs, where the key switch reads L digits over L+1 primes
+// (SEAL/evaluator.cpp:2345-2371).  KeyGenerator::create_galois_keys(elt_limbs) stores, per element,
+// SEAL's key restricted to the digits and primes its level needs (stored limbs = limbs_of(i)); a
+// ciphertext above that level is refused.  Client side only, opt-in:
+// KeyGenerator::create_deferred_galois_keys gives a key provider that keeps the secret key and
+// materialises each key on first use at the level of that use; usage() then reports the levels,
+// from which the client makes the truncated set the server holds.  Deferred keys cannot be saved.
 struct KeyMaker;
 class KSwitchKeys
 {
@@ -405,25 +484,30 @@ public:
     PolyStore &key_mut(std::size_t i) { return keys_[i]; }
     std::size_t key_limbs() const noexcept { return key_limbs_; }
     void set_key_limbs(std::size_t k) { key_limbs_ = k; }
-    // device key for index i usable by an L-limb ciphertext, materialising a deferred key on
-    // demand (thread-safe); key_limbs receives the key's limb stride
+    // stored limbs of key i (digits + 1): key_limbs() for a full key
+    std::size_t limbs_of(std::size_t i) const;
+    void insert(std::size_t index, PolyStore &&key, std::size_t limbs);
+    // device key for index i usable by an L-limb ciphertext (a deferred key is materialised on
+    // demand, thread-safe); key_limbs receives the key's limb stride
     const std::uint64_t *key_for(std::size_t i, std::size_t L, void *stream, std::size_t &key_limbs) const;
     bool deferred() const noexcept { return maker_ != nullptr; }
     void set_maker(std::shared_ptr<KeyMaker> m) { maker_ = std::move(m); }
     const std::shared_ptr<KeyMaker> &maker() const noexcept { return maker_; }
+    // index -> stored limbs of every materialised key (for a deferred set: the levels it was used at)
+    std::map<std::size_t, std::size_t> usage() const;
     // bytes of device memory held by materialised keys
     std::size_t device_bytes() const;
 
     // SEAL/kswitchkeys.cpp:42-140 byte format: parms_id | u64 dim1 | per index: u64 dim2 | dim2
-    // PublicKey (Ciphertext) objects at the key level.  Deferred (lazily materialised, level-truncated)
-    // Galois keys are not serialisable: set MHE_EAGER_GALOIS=1 to build SEAL's full keys and save them.
+    // PublicKey (Ciphertext) objects at the key level.  Truncated keys are written with their
+    // stored primes; deferred key providers are not serialisable.
     std::streamoff save_size(compr_mode_type compr_mode = Serialization::compr_mode_default) const;
     std::streamoff save(std::ostream &stream, compr_mode_type compr_mode = Serialization::compr_mode_default) const;
     std::streamoff load(const SEALContext &context, std::istream &stream);
 
 private:
     mutable std::map<std::size_t, PolyStore> keys_;
-    mutable std::map<std::size_t, std::size_t> limbs_of_; // deferred keys: limb stride per index
+    mutable std::map<std::size_t, std::size_t> limbs_of_; // stored limbs per index
     mutable std::vector<PolyStore> retired_;               // outgrown deferred keys (may be in flight)
     parms_id_type parms_id_ = parms_id_zero;
     std::size_t key_limbs_ = 0;
@@ -456,12 +540,25 @@ public:
     void create_galois_keys(const std::vector<int> &steps, GaloisKeys &destination);
     void create_galois_keys(GaloisKeys &destination);
     void create_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination);
+    // (not SEAL API) SEAL's Galois keys truncated per element to the ciphertext level (limbs) it
+    // will be used at: digits min(limbs, K-1), primes q_0..q_{digits-1} and P (see KSwitchKeys)
+    void create_galois_keys(const std::vector<std::pair<std::uint32_t, std::size_t>> &elt_limbs,
+                            GaloisKeys &destination);
+    // (not SEAL API) client-side deferred key provider (see KSwitchKeys): holds the secret key
+    void create_deferred_galois_keys(const std::vector<int> &steps, GaloisKeys &destination);
+    void create_deferred_galois_keys(GaloisKeys &destination);
+    void create_deferred_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination);
+    // (not SEAL API) a deferred provider of the +-2^i rotation keys (i < log2(n/2)), made once per
+    // generator: rotations by any step through SEAL's NAF decomposition (evaluator.cpp:2244-2276)
+    const GaloisKeys &power_of_two_keys();
 
 private:
-    void kswitch_key(const std::uint64_t *new_key_dev, PolyStore &dest);
+    void kswitch_key(const std::uint64_t *new_key_dev, PolyStore &dest, std::size_t digits);
     SEALContext ctx_;
     SecretKey sk_;
-    std::shared_ptr<std::mt19937_64> rng_;
+    std::shared_ptr<UniformRandomGeneratorFactory> rng_;
+    std::shared_ptr<GaloisKeys> pow2_;
+    std::shared_ptr<std::mutex> pow2_mu_ = std::make_shared<std::mutex>();
 };
 
 class CKKSEncoder
@@ -510,8 +607,7 @@ private:
     PublicKey pk_;
     SecretKey sk_;
     bool asymmetric_;
-    mutable std::mutex mu_;
-    std::shared_ptr<std::mt19937_64> rng_;
+    std::shared_ptr<UniformRandomGeneratorFactory> rng_;
 };
 
 class Decryptor

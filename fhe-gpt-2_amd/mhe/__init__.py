@@ -71,7 +71,9 @@ SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), vp]),
     "mhe_ckks_encode_scalar_at": (ctypes.c_int, [vp, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                                  u64p]),
-    "mhe_sample_poly": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    "mhe_prng_uniform_bulk": (ctypes.c_int, [vp, vp, ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_uint32, vp]),
+    "mhe_prng_apply_fixes": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp]),
+    "mhe_prng_small": (ctypes.c_int, [vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, vp, vp, vp]),
 }
 
 
@@ -189,13 +191,34 @@ class Engine:
         return (1, t.shape[0]) if t.dim() == 2 else (t.shape[0], t.shape[1])
 
     # ----------------------------------------------------------------- kernels
-    SAMPLE_KINDS = {"uniform": 0, "ternary": 1, "normal": 2}
+    SAMPLE_KINDS = {"ternary": 1, "cbd": 3}
 
-    def sample(self, kind, limbs, seed, tag=0, out=None):
-        """[limbs][n] residues of a random polynomial (mhe_sample_poly; util/rlwe.cpp:21,72,135)."""
+    def prng_small(self, kind, limbs, seed, byte_offset=0, out=None):
+        """[limbs][n] residues of sample_poly_ternary / sample_poly_cbd drawn from byte
+        `byte_offset` of Blake2xbPRNG(seed) (mhe_prng_small; util/rlwe.cpp:21-38,101-133).
+        Returns (out, redraw) -- redraw is set when a ternary word would be redrawn."""
         out = self.empty(limbs, self.n) if out is None else out
-        _check(lib().mhe_sample_poly(self._h, _ptr(out), limbs, self.SAMPLE_KINDS[kind], seed, tag, self.stream()))
-        return out
+        s = np.ascontiguousarray(np.array(seed, np.uint64))
+        torch = _torch()
+        flag = torch.zeros(1, dtype=torch.int32, device=self.torch_device)
+        _check(lib().mhe_prng_small(self._h, s.ctypes.data_as(ctypes.c_void_p), byte_offset, self.SAMPLE_KINDS[kind],
+                                    limbs, _ptr(out), _ptr(flag), self.stream()))
+        return out, bool(flag.item())
+
+    def prng_uniform_bulk(self, limbs, seed, out=None, cap=1 << 16):
+        """Bulk part of sample_poly_uniform over limbs 0..limbs-1 (mhe_prng_uniform_bulk): the reduced
+        accepted words in out, and the (unordered) stream indices of the rejected words."""
+        out = self.empty(limbs, self.n) if out is None else out
+        s = np.ascontiguousarray(np.array(seed, np.uint64))
+        idx = np.arange(limbs, dtype=np.int32)
+        torch = _torch()
+        rej = torch.zeros(cap, dtype=torch.int64, device=self.torch_device)
+        cnt = torch.zeros(1, dtype=torch.int32, device=self.torch_device)
+        _check(lib().mhe_prng_uniform_bulk(self._h, s.ctypes.data_as(ctypes.c_void_p), limbs,
+                                           idx.ctypes.data_as(ctypes.c_void_p), idx.ctypes.data_as(ctypes.c_void_p),
+                                           _ptr(out), _ptr(rej), _ptr(cnt), cap, self.stream()))
+        c = int(cnt.item())
+        return out, rej[:min(c, cap)].cpu().numpy().astype(np.uint64), c
 
     def ntt_forward(self, t, lazy=False):
         p, l = self._pl(t)

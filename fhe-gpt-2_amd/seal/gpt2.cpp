@@ -545,11 +545,12 @@ void row_matrix_multiplication_seal(std::vector<Ciphertext> &left_inputs, std::v
 
 void surefire_rotate(Ciphertext &cipher, int shift_amt, seal::KeyGenerator &keygen, Evaluator &evaluator)
 {
-    // util.cpp:344-356: a one-step Galois key made on the spot (GPU keygen here), then a right
-    // rotation by shift_amt
-    GaloisKeys tmp_keys;
-    keygen.create_galois_keys(std::vector<int>{ -shift_amt }, tmp_keys);
-    evaluator.rotate_vector_inplace(cipher, -shift_amt, tmp_keys);
+    // util.cpp:344-356 makes a one-step Galois key for -shift_amt on the spot from the secret key and
+    // rotates right by shift_amt.  qk_matmul/sv_matmul call it for 16384 + 8192 placements whose
+    // shifts are all distinct, so a per-shift key cache would never hit; the same rotation is done
+    // here through the generator's +-2^i keys (SEAL's NAF path), made once per key generator at the
+    // level they are used at.  The rotation is the same; only the key-switching noise differs.
+    evaluator.rotate_vector_inplace(cipher, -shift_amt, keygen.power_of_two_keys());
 }
 
 namespace

@@ -238,16 +238,36 @@ ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, co
                                                    *m.encoder, *m.encryptor, *m.decryptor, *m.evaluator, m.relin_keys,
                                                    m.gal_keys);
     for (auto &b : m.boot) b->prepare_mod_polynomial();
-    // every rotation step (materialised lazily) plus the bootstrappers' steps
+    // Galois keys.  The reference's driver asks for its rotation steps at the key level
+    // (infer_seal.cpp:345-379, 284 keys = 295 GB), more than one GPU holds.  Client side, a
+    // deferred key provider over every step runs one planning inference on a zero image and
+    // records the level each key is used at (the network's control flow does not depend on the
+    // data); the server's set is then SEAL's keys truncated to those levels, made eagerly, with
+    // no secret in them (seal.h KSwitchKeys).
     std::vector<int> gal_steps_vector{ 0 };
     for (long i = 1; i < (1L << (m.logN - 1)); i++) gal_steps_vector.push_back((int)i);
-    m.keygen->create_galois_keys(gal_steps_vector, m.gal_keys);
+    m.keygen->create_deferred_galois_keys(gal_steps_vector, m.gal_keys);
     for (int i = 0; i < 3; i++)
     {
         m.boot[i]->slot_vec.push_back(logns[i]);
         m.boot[i]->generate_LT_coefficient_3();
     }
-    setup_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const auto t1 = std::chrono::steady_clock::now();
+    (void)infer(std::vector<double>(3 * 32 * 32, 0.0));
+    std::vector<std::pair<std::uint32_t, std::size_t>> plan;
+    for (const auto &kv : m.gal_keys.usage()) plan.emplace_back((std::uint32_t)(2 * kv.first + 1), kv.second - 1);
+    const auto t2 = std::chrono::steady_clock::now();
+    {
+        GaloisKeys eager;
+        m.keygen->create_galois_keys(plan, eager);
+        m.gal_keys = std::move(eager); // the deferred provider (and its secret key copy) goes away
+    }
+    mhe_stream_sync(m.context->engine(), m.context->stream());
+    const auto t3 = std::chrono::steady_clock::now();
+    plan_s_ = std::chrono::duration<double>(t2 - t1).count();
+    keygen_s_ = std::chrono::duration<double>(t3 - t2).count();
+    galois_keys_ = plan.size();
+    setup_s_ = std::chrono::duration<double>(t3 - t0).count();
 }
 
 ResNetRunner::~ResNetRunner() = default;

@@ -11,11 +11,13 @@
 #include "seal/seal.h"
 
 #include "../../include/mhe.h"
+#include "random_internal.h"
 
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <thread>
 #include <unordered_map>
@@ -70,83 +72,18 @@ int product_bits(const std::vector<Modulus> &cm, std::size_t count)
     return (int)(64 * (words - 1)) + (64 - __builtin_clzll(prod[words - 1]));
 }
 
-std::uint64_t splitmix(std::uint64_t &x)
+// the factory key generation and encryption draw their PRNGs from (SEAL: the context installs
+// DefaultFactory when the parameters carry none, context.cpp:464-467)
+std::shared_ptr<UniformRandomGeneratorFactory> factory_of(const SEALContext &ctx)
 {
-    std::uint64_t z = (x += 0x9e3779b97f4a7c15ULL);
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-    return z ^ (z >> 31);
+    return ctx.key_context_data()->parms().random_generator_or_default();
 }
 
-std::uint64_t fresh_seed(const std::shared_ptr<UniformRandomGeneratorFactory> &f)
+std::vector<std::uint64_t> moduli_of(const SEALContext &ctx)
 {
-    if (f) return f->seed();
-    std::random_device rd;
-    return ((std::uint64_t)rd() << 32) ^ rd();
-}
-
-// ---- host samplers (util/rlwe.cpp): coefficient vectors, then RNS residues ----------------
-std::uint64_t uniform_below(std::mt19937_64 &g, std::uint64_t q)
-{
-    const std::uint64_t lim = std::numeric_limits<std::uint64_t>::max() - std::numeric_limits<std::uint64_t>::max() % q;
-    std::uint64_t v;
-    do v = g();
-    while (v >= lim);
-    return v % q;
-}
-
-// sample_poly_ternary: uniform {-1, 0, 1}
-std::vector<std::int64_t> sample_ternary(std::mt19937_64 &g, std::size_t n)
-{
-    std::vector<std::int64_t> c(n);
-    for (auto &x : c) x = (std::int64_t)uniform_below(g, 3) - 1;
-    return c;
-}
-
-// sample_poly_sparse_ternary (modified SEAL, keygenerator.cpp:76): exactly hw coefficients +-1
-std::vector<std::int64_t> sample_sparse_ternary(std::mt19937_64 &g, std::size_t n, std::size_t hw)
-{
-    std::vector<std::size_t> pos(n);
-    for (std::size_t i = 0; i < n; i++) pos[i] = i;
-    std::vector<std::int64_t> c(n, 0);
-    hw = std::min(hw, n);
-    for (std::size_t i = 0; i < hw; i++)
-    {
-        const std::size_t j = i + (std::size_t)uniform_below(g, n - i);
-        std::swap(pos[i], pos[j]);
-        c[pos[i]] = (g() & 1) ? 1 : -1;
-    }
-    return c;
-}
-
-void residues(const std::vector<std::int64_t> &c, const std::vector<Modulus> &cm, std::size_t limbs,
-              std::uint64_t *out)
-{
-    const std::size_t n = c.size();
-    for (std::size_t j = 0; j < limbs; j++)
-    {
-        const std::uint64_t q = cm[j].value();
-        for (std::size_t i = 0; i < n; i++)
-        {
-            const std::int64_t v = c[i];
-            out[j * n + i] = v >= 0 ? (std::uint64_t)v % q : (q - ((std::uint64_t)(-v) % q)) % q;
-        }
-    }
-}
-
-// util/rlwe.cpp sample_poly_{uniform,ternary,normal}: drawn on the device (csrc/sample.hip) straight
-// into RNS form on stream s; the host generator only supplies the Philox key and counter domain
-enum SampleKind
-{
-    kUniform = 0,
-    kTernary = 1,
-    kNormal = 2
-};
-
-void sample_poly(mhe_ctx *eng, std::mt19937_64 &g, SampleKind kind, std::uint64_t *out, std::size_t limbs, void *s)
-{
-    const std::uint64_t seed = g(), tag = g();
-    chk(mhe_sample_poly(eng, out, (int)limbs, (int)kind, seed, tag, s));
+    std::vector<std::uint64_t> q;
+    for (auto &m : ctx.key_context_data()->parms().coeff_modulus()) q.push_back(m.value());
+    return q;
 }
 } // namespace
 
@@ -161,22 +98,6 @@ std::vector<Modulus> CoeffModulus::Create(std::size_t poly_modulus_degree, std::
     std::vector<std::uint64_t> out(bit_sizes.size());
     chk(mhe_coeff_modulus_create(poly_modulus_degree, bit_sizes.data(), (int)bit_sizes.size(), out.data()));
     return std::vector<Modulus>(out.begin(), out.end());
-}
-
-Blake2xbPRNGFactory::Blake2xbPRNGFactory(const std::array<std::uint64_t, 8> &s) : seeded_(true), seed_(0)
-{
-    std::uint64_t h = 0x6a09e667f3bcc908ULL;
-    for (auto w : s)
-    {
-        h ^= w;
-        h = splitmix(h);
-    }
-    seed_ = h;
-}
-
-std::uint64_t Blake2xbPRNGFactory::seed() const
-{
-    return seeded_ ? seed_ : fresh_seed(nullptr);
 }
 
 parms_id_type blake2b_parms_id(const std::uint64_t *words, std::size_t count); // serialize.cpp
@@ -651,26 +572,30 @@ void upload(mhe_ctx *eng, void *s, std::uint64_t *dst, const std::vector<std::ui
     chk(mhe_stream_sync(eng, s)); // the host vector is temporary
 }
 
-// c0 = e - c1 * s over `limbs` primes; c1 uniform (already NTT form), e sampled + NTT
-void encrypt_zero_symmetric(const SEALContext &ctx, std::mt19937_64 &g, const std::uint64_t *sk, std::size_t limbs,
-                            std::uint64_t *c0, std::uint64_t *c1, void *s)
+// encrypt_zero_symmetric (rlwe.cpp:289-373) at a level of `limbs` primes, NTT form, no seed
+// saved: bootstrap PRNG <- `seed`; its first 64 bytes seed the PRNG of a = c1 (sample_poly_uniform,
+// NTT form directly); e = sample_poly_cbd from the bootstrap PRNG's next bytes; c0 = -(a*s + e).
+void encrypt_zero_symmetric(const SEALContext &ctx, const prng_seed_type &seed, const std::uint64_t *sk,
+                            std::size_t limbs, std::uint64_t *c0, std::uint64_t *c1, void *s)
 {
     mhe_ctx *eng = ctx.engine();
     const std::size_t n = ctx.key_context_data()->parms().poly_modulus_degree();
-    sample_poly(eng, g, kUniform, c1, limbs, s);
-    sample_poly(eng, g, kNormal, c0, limbs, s);
+    rnd::sample_uniform_dev(eng, rnd::stream_prefix_seed(seed), moduli_of(ctx), limbs, n, c1, s);
+    rnd::sample_cbd_dev(eng, seed, prng_seed_byte_count, limbs, c0, s);
     chk(mhe_ntt_forward(eng, c0, 1, (int)limbs, 0, s));
     DevBuf t(eng, s, limbs * n);
-    chk(mhe_multiply_plain(eng, c1, sk, t.p, 1, (int)limbs, s));
-    chk(mhe_sub(eng, c0, t.p, c0, 1, (int)limbs, s));
+    chk(mhe_multiply_plain(eng, sk, c1, t.p, 1, (int)limbs, s));
+    chk(mhe_add(eng, t.p, c0, c0, 1, (int)limbs, s));
+    chk(mhe_negate(eng, c0, c0, 1, (int)limbs, s));
 }
 
 // generate_one_kswitch_key (keygenerator.cpp:384-414) truncated to `digits` digits: digit j is an
-// encryption of zero over the key level with (P mod q_j) * new_key added to limb j of c0; the
-// stored key keeps primes q_0..q_{digits-1} and P ([digits][2][digits+1][n]).  digits = K-1 is
-// SEAL's full key.
-void make_kswitch_key(const SEALContext &ctx, std::mt19937_64 &g, const std::uint64_t *sk, const std::uint64_t *new_key,
-                      std::size_t digits, PolyStore &dest)
+// encryption of zero over the key level (its own bootstrap seed, next_seed()) with
+// (P mod q_j) * new_key added to limb j of c0; the stored key keeps primes q_0..q_{digits-1} and
+// P ([digits][2][digits+1][n]).  digits = K-1 is SEAL's full key; a truncated key is SEAL's key
+// restricted to those digits and primes (the whole digit is drawn, then the kept limbs copied).
+void make_kswitch_key(const SEALContext &ctx, const std::function<prng_seed_type()> &next_seed,
+                      const std::uint64_t *sk, const std::uint64_t *new_key, std::size_t digits, PolyStore &dest)
 {
     const std::size_t K = ctx.key_size(), n = ctx.key_context_data()->parms().poly_modulus_degree();
     const auto &cm = ctx.key_context_data()->parms().coeff_modulus();
@@ -689,7 +614,7 @@ void make_kswitch_key(const SEALContext &ctx, std::mt19937_64 &g, const std::uin
     for (std::size_t j = 0; j < digits; j++)
     {
         std::uint64_t *c0 = full ? d + j * 2 * K * n : tmp.p, *c1 = c0 + K * n;
-        encrypt_zero_symmetric(ctx, g, sk, K, c0, c1, s);
+        encrypt_zero_symmetric(ctx, next_seed(), sk, K, c0, c1, s);
         std::vector<std::uint64_t> f(K, 0);
         f[j] = P % cm[j].value();
         chk(mhe_multiply_scalar(eng, new_key, f.data(), t.p, 1, (int)K, s));
@@ -706,13 +631,16 @@ void make_kswitch_key(const SEALContext &ctx, std::mt19937_64 &g, const std::uin
 }
 } // namespace
 
-// Deferred Galois keys (see seal.h): the secret key, and per key index its Galois element and seed.
+// Deferred Galois keys (see seal.h, KeyGenerator::create_deferred_galois_keys): a client-side key
+// provider holding the secret key and, per key index, its Galois element and a 512-bit seed.
+// Digit j of a materialised key draws its bootstrap seed from bytes [64j, 64j+64) of that seed's
+// stream, so a key re-materialised larger keeps its smaller prefix.
 struct KeyMaker
 {
     std::mutex mu;
     SEALContext ctx;
     PolyStore sk; // NTT form over the key level
-    std::map<std::size_t, std::pair<std::uint32_t, std::uint64_t>> elts;
+    std::map<std::size_t, std::pair<std::uint32_t, prng_seed_type>> elts;
     explicit KeyMaker(const SEALContext &c) : ctx(c) {}
 };
 
@@ -743,6 +671,12 @@ const PolyStore &KSwitchKeys::key(std::size_t i) const
     return it->second;
 }
 
+std::size_t KSwitchKeys::limbs_of(std::size_t i) const
+{
+    auto it = limbs_of_.find(i);
+    return it == limbs_of_.end() ? key_limbs_ : it->second;
+}
+
 const std::uint64_t *KSwitchKeys::key_for(std::size_t i, std::size_t L, void *stream, std::size_t &key_limbs) const
 {
     if (maker_)
@@ -763,9 +697,16 @@ const std::uint64_t *KSwitchKeys::key_for(std::size_t i, std::size_t L, void *st
                 DevBuf rot(ctx.engine(), s, K * n);
                 const std::uint64_t *sk = maker_->sk.dev_read(s);
                 chk(mhe_permute_galois(ctx.engine(), sk, e->second.first, rot.p, 1, (int)K, s));
-                std::mt19937_64 g(e->second.second ^ (0x9e3779b97f4a7c15ULL * digits));
+                Blake2xbPRNG seeds(e->second.second);
                 PolyStore fresh;
-                make_kswitch_key(ctx, g, sk, rot.p, digits, fresh);
+                make_kswitch_key(
+                    ctx,
+                    [&] {
+                        prng_seed_type d;
+                        seeds.generate(prng_seed_byte_count, reinterpret_cast<seal_byte *>(d.data()));
+                        return d;
+                    },
+                    sk, rot.p, digits, fresh);
                 auto kt = keys_.find(i);
                 if (kt != keys_.end()) retired_.push_back(std::move(kt->second));
                 keys_[i] = std::move(fresh);
@@ -775,8 +716,17 @@ const std::uint64_t *KSwitchKeys::key_for(std::size_t i, std::size_t L, void *st
             return keys_.find(i)->second.dev_read(stream);
         }
     }
-    key_limbs = key_limbs_;
+    key_limbs = limbs_of(i);
+    if (key_limbs < L + 1)
+        throw std::invalid_argument("key-switching key is truncated below the ciphertext level");
     return key(i).dev_read(stream);
+}
+
+std::map<std::size_t, std::size_t> KSwitchKeys::usage() const
+{
+    std::map<std::size_t, std::size_t> u;
+    for (const auto &kv : keys_) u[kv.first] = limbs_of(kv.first);
+    return u;
 }
 
 std::size_t KSwitchKeys::device_bytes() const
@@ -787,20 +737,34 @@ std::size_t KSwitchKeys::device_bytes() const
     return b;
 }
 
+void KSwitchKeys::insert(std::size_t index, PolyStore &&key, std::size_t limbs)
+{
+    keys_[index] = std::move(key);
+    limbs_of_[index] = limbs;
+}
 
 KeyGenerator::KeyGenerator(const SEALContext &context) : ctx_(context)
 {
+    // keygenerator.cpp:62-84: the secret key from a fresh PRNG of the parameters' factory,
+    // sparse ternary with the modified Hamming weight (or ternary for weight 0), NTT form
     const auto &parms = context.key_context_data()->parms();
-    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(parms.random_generator()));
+    rng_ = factory_of(context);
     const std::size_t K = context.key_size(), n = parms.poly_modulus_degree();
     const std::size_t hw = parms.secret_key_hamming_weight();
-    auto c = hw ? sample_sparse_ternary(*rng_, n, hw) : sample_ternary(*rng_, n);
+    const auto q = moduli_of(context);
     std::vector<std::uint64_t> h(K * n);
-    residues(c, parms.coeff_modulus(), K, h.data());
+    {
+        auto prng = rng_->create();
+        if (hw)
+            rnd::sample_sparse_ternary_host(*prng, q, n, hw, h.data());
+        else
+            rnd::sample_ternary_host(*prng, q, K, n, h.data());
+    }
     void *s = context.stream();
     sk_.data().set_level(context, context.key_parms_id(), K);
     std::uint64_t *d = sk_.data().store().dev_write(s, true);
     upload(context.engine(), s, d, h);
+    std::fill(h.begin(), h.end(), 0);
     chk(mhe_ntt_forward(context.engine(), d, 1, (int)K, 0, s));
 }
 
@@ -808,11 +772,12 @@ KeyGenerator::KeyGenerator(const SEALContext &context, const SecretKey &secret_k
 {
     if (secret_key.parms_id() != context.key_parms_id())
         throw std::invalid_argument("secret key is not valid for encryption parameters");
-    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(context.key_context_data()->parms().random_generator()));
+    rng_ = factory_of(context);
 }
 
 void KeyGenerator::create_public_key(PublicKey &destination)
 {
+    // generate_pk (keygenerator.cpp:87-112): encrypt_zero_symmetric at the key level
     const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
     void *s = ctx_.stream();
     Ciphertext &pk = destination.data();
@@ -820,7 +785,7 @@ void KeyGenerator::create_public_key(PublicKey &destination)
     pk.is_ntt_form() = true;
     pk.scale() = 1.0;
     std::uint64_t *d = pk.store().dev_write(s, true);
-    encrypt_zero_symmetric(ctx_, *rng_, sk_.data().store().dev_read(s), K, d, d + K * n, s);
+    encrypt_zero_symmetric(ctx_, rng_->next_seed(), sk_.data().store().dev_read(s), K, d, d + K * n, s);
 }
 
 PublicKey KeyGenerator::create_public_key()
@@ -830,69 +795,88 @@ PublicKey KeyGenerator::create_public_key()
     return pk;
 }
 
-void KeyGenerator::kswitch_key(const std::uint64_t *new_key, PolyStore &dest)
+void KeyGenerator::kswitch_key(const std::uint64_t *new_key, PolyStore &dest, std::size_t digits)
 {
-    make_kswitch_key(ctx_, *rng_, sk_.data().store().dev_read(ctx_.stream()), new_key, ctx_.key_size() - 1, dest);
+    make_kswitch_key(
+        ctx_, [&] { return rng_->next_seed(); }, sk_.data().store().dev_read(ctx_.stream()), new_key, digits, dest);
 }
 
 void KeyGenerator::create_relin_keys(RelinKeys &destination)
 {
+    // create_relin_keys (keygenerator.cpp:115-149): key-switching key of s^2
     const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
     void *s = ctx_.stream();
     DevBuf s2(ctx_.engine(), s, K * n);
     const std::uint64_t *sk = sk_.data().store().dev_read(s);
     chk(mhe_multiply_plain(ctx_.engine(), sk, sk, s2.p, 1, (int)K, s));
-    kswitch_key(s2.p, destination.key_mut(RelinKeys::get_index(2)));
+    PolyStore key;
+    kswitch_key(s2.p, key, K - 1);
+    destination.insert(RelinKeys::get_index(2), std::move(key), K);
+    destination.parms_id() = ctx_.key_parms_id();
+    destination.set_key_limbs(K);
+}
+
+void KeyGenerator::create_galois_keys(const std::vector<std::pair<std::uint32_t, std::size_t>> &elt_limbs,
+                                      GaloisKeys &destination)
+{
+    // create_galois_keys (keygenerator.cpp:152-190): per element, the key-switching key of
+    // s(X^elt) (apply_galois_ntt on the NTT-form secret key); here truncated per element to the
+    // level it is used at (limbs = ciphertext limbs; >= K-1 keeps SEAL's full key)
+    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
+    void *s = ctx_.stream();
+    DevBuf rot(ctx_.engine(), s, K * n);
+    for (const auto &el : elt_limbs)
+    {
+        const std::uint32_t elt = el.first;
+        if (!(elt & 1) || elt >= 2 * n) throw std::invalid_argument("Galois element is not valid");
+        if (destination.has_key(elt)) continue;
+        const std::size_t digits = std::min(K - 1, std::max<std::size_t>(el.second, 1));
+        const std::uint64_t *sk = sk_.data().store().dev_read(s);
+        chk(mhe_permute_galois(ctx_.engine(), sk, elt, rot.p, 1, (int)K, s));
+        PolyStore key;
+        kswitch_key(rot.p, key, digits);
+        destination.insert(GaloisKeys::get_index(elt), std::move(key), digits + 1);
+    }
     destination.parms_id() = ctx_.key_parms_id();
     destination.set_key_limbs(K);
 }
 
 void KeyGenerator::create_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination)
 {
+    std::vector<std::pair<std::uint32_t, std::size_t>> full;
+    for (std::uint32_t e : elts) full.emplace_back(e, ctx_.key_size() - 1);
+    create_galois_keys(full, destination);
+}
+
+void KeyGenerator::create_deferred_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination)
+{
     const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
-    void *s = ctx_.stream();
-    // Deferred by default (seal.h, KSwitchKeys); MHE_EAGER_GALOIS=1 builds SEAL's full keys now.
-    const char *eager_env = std::getenv("MHE_EAGER_GALOIS");
-    const bool eager = eager_env && eager_env[0] == '1';
-    if (!eager)
+    if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
+    auto maker = destination.maker();
+    if (!maker)
     {
-        if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
-        auto maker = destination.maker();
-        if (!maker)
-        {
-            maker = std::make_shared<KeyMaker>(ctx_);
-            maker->sk = sk_.data().store();
-            destination.set_maker(maker);
-        }
-        std::lock_guard<std::mutex> lk(maker->mu);
-        for (std::uint32_t elt : elts)
-        {
-            if (!(elt & 1) || elt >= 2 * n) throw std::invalid_argument("Galois element is not valid");
-            const std::size_t idx = GaloisKeys::get_index(elt);
-            const std::uint64_t seed = (*rng_)();
-            if (!maker->elts.count(idx)) maker->elts[idx] = { elt, seed };
-        }
-        destination.parms_id() = ctx_.key_parms_id();
-        destination.set_key_limbs(K);
-        return;
+        maker = std::make_shared<KeyMaker>(ctx_);
+        maker->sk = sk_.data().store();
+        destination.set_maker(maker);
     }
-    DevBuf rot(ctx_.engine(), s, K * n);
+    std::lock_guard<std::mutex> lk(maker->mu);
     for (std::uint32_t elt : elts)
     {
         if (!(elt & 1) || elt >= 2 * n) throw std::invalid_argument("Galois element is not valid");
-        if (destination.has_key(elt)) continue;
-        const std::uint64_t *sk = sk_.data().store().dev_read(s);
-        chk(mhe_permute_galois(ctx_.engine(), sk, elt, rot.p, 1, (int)K, s));
-        kswitch_key(rot.p, destination.key_mut(GaloisKeys::get_index(elt)));
+        const std::size_t idx = GaloisKeys::get_index(elt);
+        if (!maker->elts.count(idx)) maker->elts[idx] = { elt, rng_->next_seed() };
     }
     destination.parms_id() = ctx_.key_parms_id();
     destination.set_key_limbs(K);
 }
 
-void KeyGenerator::create_galois_keys(const std::vector<int> &steps, GaloisKeys &destination)
+namespace
+{
+std::vector<std::uint32_t> elts_from_steps(const SEALContext &ctx, const std::vector<int> &steps)
 {
     // GaloisTool::get_elts_from_steps (util/galois.cpp:96-104)
-    const int log_n = __builtin_ctzll(ctx_.key_context_data()->parms().poly_modulus_degree());
+    const int log_n = __builtin_ctzll(ctx.key_context_data()->parms().poly_modulus_degree());
     std::vector<std::uint32_t> elts;
     for (int st : steps)
     {
@@ -900,15 +884,15 @@ void KeyGenerator::create_galois_keys(const std::vector<int> &steps, GaloisKeys 
         if (!e) throw std::invalid_argument("step count too large");
         elts.push_back(e);
     }
-    create_galois_keys_from_elts(elts, destination);
+    return elts;
 }
 
-void KeyGenerator::create_galois_keys(GaloisKeys &destination)
+std::vector<std::uint32_t> elts_all(const SEALContext &ctx)
 {
     // GaloisTool::get_elts_all (util/galois.cpp:106-131), generator 5
-    const std::size_t n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    const std::size_t n = ctx.key_context_data()->parms().poly_modulus_degree();
     const std::uint64_t m = 2 * n;
-    int log_n = __builtin_ctzll(n);
+    const int log_n = __builtin_ctzll(n);
     std::vector<std::uint32_t> elts{ (std::uint32_t)(m - 1) };
     std::uint64_t pos = 5, neg = 1;
     // inverse of 5 mod m (m a power of two): 5^(m/4 - 1)
@@ -920,7 +904,46 @@ void KeyGenerator::create_galois_keys(GaloisKeys &destination)
         elts.push_back((std::uint32_t)neg);
         neg = (neg * neg) & (m - 1);
     }
-    create_galois_keys_from_elts(elts, destination);
+    return elts;
+}
+} // namespace
+
+void KeyGenerator::create_galois_keys(const std::vector<int> &steps, GaloisKeys &destination)
+{
+    create_galois_keys_from_elts(elts_from_steps(ctx_, steps), destination);
+}
+
+void KeyGenerator::create_galois_keys(GaloisKeys &destination)
+{
+    create_galois_keys_from_elts(elts_all(ctx_), destination);
+}
+
+void KeyGenerator::create_deferred_galois_keys(const std::vector<int> &steps, GaloisKeys &destination)
+{
+    create_deferred_galois_keys_from_elts(elts_from_steps(ctx_, steps), destination);
+}
+
+void KeyGenerator::create_deferred_galois_keys(GaloisKeys &destination)
+{
+    create_deferred_galois_keys_from_elts(elts_all(ctx_), destination);
+}
+
+const GaloisKeys &KeyGenerator::power_of_two_keys()
+{
+    std::lock_guard<std::mutex> lk(*pow2_mu_);
+    if (!pow2_)
+    {
+        const int log_n = __builtin_ctzll(ctx_.key_context_data()->parms().poly_modulus_degree());
+        std::vector<int> steps;
+        for (int i = 0; i < log_n - 1; i++)
+        {
+            steps.push_back(1 << i);
+            steps.push_back(-(1 << i));
+        }
+        pow2_ = std::make_shared<GaloisKeys>();
+        create_deferred_galois_keys(steps, *pow2_);
+    }
+    return *pow2_;
 }
 
 // ------------------------------------------------------------------------------ CKKSEncoder
@@ -1032,7 +1055,7 @@ Encryptor::Encryptor(const SEALContext &context, const PublicKey &public_key)
 {
     if (public_key.parms_id() != context.key_parms_id())
         throw std::invalid_argument("public key is not valid for encryption parameters");
-    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(context.key_context_data()->parms().random_generator()));
+    rng_ = factory_of(context);
 }
 
 Encryptor::Encryptor(const SEALContext &context, const SecretKey &secret_key)
@@ -1040,36 +1063,59 @@ Encryptor::Encryptor(const SEALContext &context, const SecretKey &secret_key)
 {
     if (secret_key.parms_id() != context.key_parms_id())
         throw std::invalid_argument("secret key is not valid for encryption parameters");
-    rng_ = std::make_shared<std::mt19937_64>(fresh_seed(context.key_context_data()->parms().random_generator()));
+    rng_ = factory_of(context);
 }
 
 void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
 {
     // encryptor.cpp:88-166 (encrypt_zero_internal): public-key encryption runs one level up
-    // (the key level for the first data level) and is rescaled down, dividing the noise by the
-    // dropped prime; secret-key encryption runs at the level itself.
+    // (the key level for the first data level) and is divided and rounded down by the dropped
+    // prime; secret-key encryption runs at the level itself.
     const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
     mhe_ctx *eng = ctx_.engine();
     void *s = ctx_.stream();
     std::uint64_t *d = dest.store().dev_write(s, true);
-    std::lock_guard<std::mutex> g(mu_);
+    const prng_seed_type seed = rng_->next_seed();
     if (!asymmetric_)
     {
-        encrypt_zero_symmetric(ctx_, *rng_, sk_.data().store().dev_read(s), L, d, d + L * n, s);
+        encrypt_zero_symmetric(ctx_, seed, sk_.data().store().dev_read(s), L, d, d + L * n, s);
         return;
     }
-    const std::size_t m = L < K ? L + 1 : L; // prev level (key level for the first level)
+    // encrypt_zero_asymmetric (rlwe.cpp:220-286): one PRNG; u ternary, then e_0, e_1 (CBD)
+    const std::size_t m = L < K ? L + 1 : L;
     const std::uint64_t *pk = pk_.data().store().dev_read(s);
-    DevBuf u(eng, s, m * n), c(eng, s, 2 * m * n), e(eng, s, m * n);
-    sample_poly(eng, *rng_, kTernary, u.p, m, s);
+    DevBuf u(eng, s, m * n), c(eng, s, 2 * m * n), e(eng, s, 2 * m * n), flag(eng, s, 1);
+    std::uint32_t rejected = 0;
+    chk(mhe_memcpy_h2d(eng, flag.p, &rejected, 4, s));
+    chk(mhe_prng_small(eng, seed.data(), 0, MHE_SAMPLE_TERNARY, (int)m, u.p, reinterpret_cast<std::uint32_t *>(flag.p),
+                       s));
+    chk(mhe_memcpy_d2h(eng, &rejected, flag.p, 4, s));
+    chk(mhe_stream_sync(eng, s));
+    if (!rejected)
+    {
+        rnd::sample_cbd_dev(eng, seed, 4 * n, m, e.p, s);
+        rnd::sample_cbd_dev(eng, seed, 10 * n, m, e.p + m * n, s);
+    }
+    else
+    {
+        // a zero word makes std::uniform_int_distribution redraw (2^-32 per coefficient): the
+        // stream positions of everything after it move, so this encryption samples on the host
+        Blake2xbPRNG prng(seed);
+        const auto q = moduli_of(ctx_);
+        std::vector<std::uint64_t> hu(m * n), he(2 * m * n);
+        rnd::sample_ternary_host(prng, q, m, n, hu.data());
+        rnd::sample_cbd_host(prng, q, m, n, he.data());
+        rnd::sample_cbd_host(prng, q, m, n, he.data() + m * n);
+        upload(eng, s, u.p, hu);
+        upload(eng, s, e.p, he);
+    }
     chk(mhe_ntt_forward(eng, u.p, 1, (int)m, 0, s));
+    chk(mhe_ntt_forward(eng, e.p, 2, (int)m, 0, s));
     for (int j = 0; j < 2; j++)
     {
         // pk_j restricted to the first m primes: limbs 0..m-1 of poly j ([2][K][n] layout)
-        chk(mhe_multiply_plain(eng, pk + j * K * n, u.p, c.p + j * m * n, 1, (int)m, s));
-        sample_poly(eng, *rng_, kNormal, e.p, m, s);
-        chk(mhe_ntt_forward(eng, e.p, 1, (int)m, 0, s));
-        chk(mhe_add(eng, c.p + j * m * n, e.p, c.p + j * m * n, 1, (int)m, s));
+        chk(mhe_multiply_plain(eng, u.p, pk + j * K * n, c.p + j * m * n, 1, (int)m, s));
+        chk(mhe_add(eng, e.p + j * m * n, c.p + j * m * n, c.p + j * m * n, 1, (int)m, s));
     }
     if (m == L)
         chk(mhe_memcpy_d2d(eng, d, c.p, 2 * L * n * 8, s));
@@ -1094,6 +1140,7 @@ void Encryptor::encrypt_zero(Ciphertext &destination, MemoryPoolHandle pool) con
 
 void Encryptor::encrypt(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle) const
 {
+    // encrypt_internal (encryptor.cpp:168-239), CKKS branch
     if (!plain.is_ntt_form()) throw std::invalid_argument("plain must be in NTT form");
     auto cd = ctx_.get_context_data(plain.parms_id());
     if (!cd) throw std::invalid_argument("plain is not valid for encryption parameters");

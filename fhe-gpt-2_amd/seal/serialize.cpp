@@ -253,6 +253,8 @@ namespace
 std::streamoff pk_size(std::size_t K, std::size_t n) { return kHeader + 32 + 1 + 24 + 8 + dynarray_size(2 * K * n); }
 } // namespace
 
+// A level-truncated key (KSwitchKeys, digits D < K-1) is written as D PublicKeys of D+1 limbs
+// (primes q_0..q_{D-1}, P): the same record layout, an extension SEAL itself does not read.
 std::streamoff KSwitchKeys::save_size(compr_mode_type) const
 {
     if (maker_) throw std::logic_error("deferred Galois keys cannot be serialized");
@@ -260,11 +262,10 @@ std::streamoff KSwitchKeys::save_size(compr_mode_type) const
     std::streamoff total = kHeader + 32 + 8 + (std::streamoff)(8 * dim1);
     for (const auto &kv : keys_)
     {
-        const std::size_t K = key_limbs_, words = kv.second.words();
-        // full keys hold one digit per data prime (decomp_mod_count = K - 1)
-        const std::size_t n = K > 1 ? words / (2 * K * (K - 1)) : 0;
-        if (!n || words != (K - 1) * 2 * K * n) throw std::logic_error("key data is invalid");
-        total += (std::streamoff)(K - 1) * pk_size(K, n);
+        const std::size_t KL = limbs_of(kv.first), words = kv.second.words();
+        const std::size_t n = KL > 1 ? words / (2 * KL * (KL - 1)) : 0;
+        if (!n || words != (KL - 1) * 2 * KL * n) throw std::logic_error("key data is invalid");
+        total += (std::streamoff)(KL - 1) * pk_size(KL, n);
     }
     return total;
 }
@@ -284,19 +285,19 @@ std::streamoff KSwitchKeys::save(std::ostream &stream, compr_mode_type mode) con
             put<std::uint64_t>(stream, 0);
             continue;
         }
-        const std::size_t K = key_limbs_, digits = K - 1, n = it->second.words() / (2 * K * digits);
+        const std::size_t KL = limbs_of(i), digits = KL - 1, n = it->second.words() / (2 * KL * digits);
         put<std::uint64_t>(stream, digits);
         const std::uint64_t *p = it->second.host();
         for (std::size_t d = 0; d < digits; d++)
         {
-            write_header(stream, (std::uint64_t)pk_size(K, n), compr_mode_type::none);
+            write_header(stream, (std::uint64_t)pk_size(KL, n), compr_mode_type::none);
             put(stream, parms_id_);
             put<std::uint8_t>(stream, 1);
             put<std::uint64_t>(stream, 2);
             put<std::uint64_t>(stream, n);
-            put<std::uint64_t>(stream, K);
+            put<std::uint64_t>(stream, KL);
             put<double>(stream, 1.0);
-            write_dynarray(stream, p + d * 2 * K * n, 2 * K * n);
+            write_dynarray(stream, p + d * 2 * KL * n, 2 * KL * n);
         }
     }
     if (!stream) throw std::runtime_error("I/O error");
@@ -310,32 +311,49 @@ std::streamoff KSwitchKeys::load(const SEALContext &context, std::istream &strea
     if (id != context.key_parms_id()) throw std::logic_error("KSwitchKeys data is invalid");
     const auto cd = context.key_context_data();
     const std::size_t K = cd->parms().coeff_modulus().size(), n = cd->parms().poly_modulus_degree();
+    const auto &cm = cd->parms().coeff_modulus();
     const auto dim1 = get<std::uint64_t>(stream);
     if (dim1 > 4 * n) throw std::logic_error("KSwitchKeys data is invalid");
     std::map<std::size_t, PolyStore> keys;
+    std::map<std::size_t, std::size_t> limbs;
     std::streamoff total = kHeader + 32 + 8;
     for (std::size_t i = 0; i < dim1; i++)
     {
         const auto digits = get<std::uint64_t>(stream);
         total += 8;
         if (!digits) continue;
-        if (digits != K - 1) throw std::logic_error("KSwitchKeys data is invalid");
+        if (digits > K - 1) throw std::logic_error("KSwitchKeys data is invalid");
+        const std::size_t KL = digits + 1;
+        std::vector<Modulus> stored(cm.begin(), cm.begin() + digits);
+        stored.push_back(cm.back());
         PolyStore &ps = keys[i];
+        limbs[i] = KL;
         ps.bind(context);
-        ps.resize_words(digits * 2 * K * n, false);
+        ps.resize_words(digits * 2 * KL * n, false);
         std::uint64_t *dst = ps.host();
         for (std::size_t d = 0; d < digits; d++)
         {
-            Ciphertext pk;
-            total += pk.load(context, stream);
-            if (pk.parms_id() != id || pk.size() != 2 || !pk.is_ntt_form())
+            // one PublicKey record (Ciphertext::save_members layout) over the stored primes
+            const auto rh = read_header(stream);
+            const auto pid = get<parms_id_type>(stream);
+            const auto ntt = get<std::uint8_t>(stream);
+            const auto size = get<std::uint64_t>(stream);
+            const auto deg = get<std::uint64_t>(stream);
+            const auto cms = get<std::uint64_t>(stream);
+            (void)get<double>(stream);
+            if (pid != id || ntt != 1 || size != 2 || deg != n || cms != KL)
                 throw std::logic_error("KSwitchKeys data is invalid");
-            std::memcpy(dst + d * 2 * K * n, pk.data(), 8 * 2 * K * n);
+            std::vector<std::uint64_t> w;
+            read_dynarray(stream, w, 2 * KL * n);
+            if (w.size() != 2 * KL * n || !residues_valid(w, stored, n) || rh.size != (std::uint64_t)pk_size(KL, n))
+                throw std::logic_error("KSwitchKeys data is invalid");
+            std::memcpy(dst + d * 2 * KL * n, w.data(), 8 * w.size());
+            total += (std::streamoff)rh.size;
         }
     }
     if ((std::uint64_t)total != h.size) throw std::logic_error("KSwitchKeys data is invalid");
     keys_ = std::move(keys);
-    limbs_of_.clear();
+    limbs_of_ = std::move(limbs);
     parms_id_ = id;
     key_limbs_ = K;
     maker_.reset();

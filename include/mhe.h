@@ -184,12 +184,31 @@ int mhe_ckks_decode(mhe_ctx *ctx, const mhe_encoder *enc, const uint64_t *plain_
 int mhe_ckks_encode_scalar_at(mhe_ctx *ctx, double value, double scale, int bound_limbs, int limbs,
                               uint64_t *residues);
 
-/* Random polynomials of key generation / encryption (util/rlwe.cpp:135 sample_poly_uniform, :21
- * sample_poly_ternary, :72 sample_poly_normal), drawn on the device into out[limbs][n] (coefficient
- * form for kinds 1-2; kind 0 is uniform mod each q_l and serves as NTT form directly).
- * kind: 0 uniform, 1 ternary {-1,0,1}, 2 normal sigma 3.2 clipped at 6 sigma, truncated.
- * Deterministic in (seed, tag); Philox4x32-10, not SEAL's Blake2xb stream.  Async on stream. */
-int mhe_sample_poly(mhe_ctx *ctx, uint64_t *out, int limbs, int kind, uint64_t seed, uint64_t tag, void *stream);
+/* Random polynomials of key generation / encryption from SEAL's default PRNG (Blake2xbPRNG,
+ * SEAL/randomgen.cpp:185-195: 4096-byte buffers, buffer c = BLAKE2Xb(4096, counter c, 64-byte seed))
+ * through SEAL's samplers (SEAL/util/rlwe.cpp), bit-identical to SEAL for the same seed.
+ *
+ * sample_poly_uniform (rlwe.cpp:136-162), bulk part: the stream's first limbs*n words are the
+ * draws of limbs 0..limbs-1 (limb l reduced mod prime prime_of_limb[l]); accepted words of limbs
+ * with slot_of_limb[l] >= 0 are written, reduced, to out[slot][n]; the stream indices of rejected
+ * words (w >= max_multiple) go to the device array rej (first rej_cap of them) and their count to
+ * *rej_count (device, zeroed by the caller).  The caller sorts them and redraws each, in index
+ * order, from the stream words after the bulk, then writes the results with
+ * mhe_prng_apply_fixes (fixes_dev = pairs {out index, value}). */
+int mhe_prng_uniform_bulk(mhe_ctx *ctx, const uint64_t seed[8], int limbs, const int *prime_of_limb,
+                          const int *slot_of_limb, uint64_t *out, uint64_t *rej, uint32_t *rej_count,
+                          uint32_t rej_cap, void *stream);
+int mhe_prng_apply_fixes(mhe_ctx *ctx, const uint64_t *fixes_dev, uint32_t count, uint64_t *out, void *stream);
+/* sample_poly_ternary (rlwe.cpp:21-38, kind MHE_SAMPLE_TERNARY, 4 stream bytes per coefficient) or
+ * sample_poly_cbd (rlwe.cpp:101-133, kind MHE_SAMPLE_CBD, 6 bytes per coefficient), drawing from
+ * stream byte `byte_offset` (a multiple of 64) of the PRNG seeded with `seed`, written as
+ * canonical residues over limbs 0..limbs-1 of the context (coefficient form).  Ternary sets
+ * *flag_dev (device, zeroed by the caller) when a draw would be redrawn (a zero 32-bit word,
+ * probability 2^-32), in which case the caller must sample on the host. */
+#define MHE_SAMPLE_TERNARY 1
+#define MHE_SAMPLE_CBD 3
+int mhe_prng_small(mhe_ctx *ctx, const uint64_t seed[8], uint64_t byte_offset, int kind, int limbs, uint64_t *out,
+                   uint32_t *flag_dev, void *stream);
 
 #ifdef __cplusplus
 }

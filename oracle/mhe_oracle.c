@@ -1435,3 +1435,6 @@ static int or_ckks_decode_impl(const or_encoder *e, const or_ctx *c, const uint6
     free(res);
     return 0;
 }
+
+/* SEAL randomness, keys and encryption (test infrastructure) */
+#include "seal_random.c"

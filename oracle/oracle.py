@@ -71,6 +71,14 @@ def lib():
             "or_ckks_decode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, u64p, ctypes.c_int, ctypes.c_double,
                                               ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_double)]),
+            "or_blake2xb": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                           ctypes.c_char_p, ctypes.c_size_t]),
+            "or_prng_bytes": (None, [u64p, ctypes.c_size_t, ctypes.c_char_p]),
+            "or_ctx_sample": (None, [ctypes.c_void_p, u64p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, u64p]),
+            "or_ctx_encrypt_zero_symmetric": (None, [ctypes.c_void_p, u64p, u64p, ctypes.c_int, u64p]),
+            "or_ctx_encrypt_zero_asymmetric": (None, [ctypes.c_void_p, u64p, u64p, ctypes.c_int, ctypes.c_int, u64p]),
+            "or_ctx_keygen_secret": (None, [ctypes.c_void_p, u64p, ctypes.c_size_t, u64p]),
+            "or_ctx_kswitch_key": (None, [ctypes.c_void_p, u64p, u64p, u64p, u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -83,6 +91,29 @@ def lib():
 def _p(a):
     assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
     return a.ctypes.data_as(u64p)
+
+
+# ---------------------------------------------------------------- SEAL randomness (seal_random.c)
+def blake2xb(outlen, data, key):
+    """blake2xb(out, outlen, in, inlen, key, keylen) (util/blake2xb.c:143-168)."""
+    out = ctypes.create_string_buffer(outlen)
+    rc = lib().or_blake2xb(out, outlen, bytes(data), len(data), bytes(key), len(key))
+    assert rc == 0
+    return out.raw
+
+
+def _seed(seed):
+    s = np.ascontiguousarray(np.array(seed, dtype=np.uint64))
+    assert s.shape == (8,)
+    return s
+
+
+def prng_bytes(seed, count):
+    """The first `count` bytes of Blake2xbPRNG(seed) (randomgen.cpp:160-195)."""
+    s = _seed(seed)
+    out = ctypes.create_string_buffer(count)
+    lib().or_prng_bytes(_p(s), count, out)
+    return out.raw
 
 
 # ---------------------------------------------------------------- scalar / table helpers
@@ -330,6 +361,39 @@ class Context:
                                          out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
         if rc:
             raise ValueError("scale out of bounds")
+        return out
+
+    SAMPLE = {"uniform": 0, "ternary": 1, "sparse_ternary": 2, "cbd": 3}
+
+    def sample(self, seed, kind, limbs, hw=0):
+        """[limbs][n] residues of SEAL's sample_poly_<kind>(Blake2xbPRNG(seed)) (rlwe.cpp:21-162)."""
+        out = np.zeros((limbs, self.n), np.uint64)
+        s = _seed(seed)
+        lib().or_ctx_sample(self._h, _p(s), self.SAMPLE[kind], limbs, hw, _p(out))
+        return out
+
+    def keygen_secret(self, seed, hw):
+        out = np.zeros((self.k, self.n), np.uint64)
+        s = _seed(seed)
+        lib().or_ctx_keygen_secret(self._h, _p(s), hw, _p(out))
+        return out
+
+    def encrypt_zero_symmetric(self, seed, sk, limbs):
+        out = np.zeros((2, limbs, self.n), np.uint64)
+        s, sk = _seed(seed), np.ascontiguousarray(sk)
+        lib().or_ctx_encrypt_zero_symmetric(self._h, _p(s), _p(sk), limbs, _p(out))
+        return out
+
+    def encrypt_zero_asymmetric(self, seed, pk, m, L):
+        out = np.zeros((2, L, self.n), np.uint64)
+        s, pk = _seed(seed), np.ascontiguousarray(pk)
+        lib().or_ctx_encrypt_zero_asymmetric(self._h, _p(s), _p(pk), m, L, _p(out))
+        return out
+
+    def kswitch_key(self, seed, sk, new_key):
+        out = np.zeros((self.k - 1, 2, self.k, self.n), np.uint64)
+        s, sk, nk = _seed(seed), np.ascontiguousarray(sk), np.ascontiguousarray(new_key)
+        lib().or_ctx_kswitch_key(self._h, _p(s), _p(sk), _p(nk), _p(out))
         return out
 
     def hmult_batch(self, a, b, key, threads=0):

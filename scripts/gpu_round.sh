@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT"
 R="$GRAFT_REPO_ROOT"
 TAG="${TAG:-run}"
 mkdir -p gpurun_out/prof gpurun_out/pmc
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 600 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc

@@ -134,7 +134,9 @@ int main(int argc, char **argv)
         return 0;
     }
     ResNetRunner runner(layers, prm, argv[2]);
-    std::printf("setup: %.2f s\n", runner.setup_seconds());
+    std::printf("setup: %.2f s (planning inference %.2f s, %zu truncated Galois keys made in %.2f s, %.1f GB resident)\n",
+                runner.setup_seconds(), runner.plan_seconds(), runner.galois_keys(), runner.keygen_seconds(),
+                runner.galois_key_gb());
     int fail = 0;
     double total = 0;
     // decrypted logits vs the plain network with the exact ReLU: the approximate ReLU's error

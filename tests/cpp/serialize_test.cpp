@@ -199,12 +199,39 @@ int main(int argc, char **argv)
     double err3 = 0;
     for (std::size_t i = 0; i < x.size(); i++) err3 = std::max(err3, std::fabs(y3[i] - x[i]));
     CHECK(err3 < 1e-6);
-    GaloisKeys glk;
-    keygen.create_galois_keys(std::vector<int>{ 1 }, glk); // deferred by default
+    GaloisKeys dgk;
+    keygen.create_deferred_galois_keys(std::vector<int>{ 1 }, dgk); // client-side provider: holds the secret
     CHECK(throws([&] {
         std::stringstream t;
-        glk.save(t);
+        dgk.save(t);
     }));
+    {
+        // eager Galois keys (SEAL's, the default) and a level-truncated one round-trip, and the
+        // loaded keys rotate bit-identically
+        GaloisKeys glk;
+        keygen.create_galois_keys(std::vector<int>{ 1 }, glk);
+        keygen.create_galois_keys(std::vector<std::pair<std::uint32_t, std::size_t>>{ { 25u, 2 } }, glk); // step 2
+        std::stringstream gs;
+        const auto gbytes = glk.save(gs);
+        CHECK(gbytes == glk.save_size());
+        GaloisKeys glk2;
+        CHECK(glk2.load(ctx, gs) == gbytes);
+        CHECK(glk2.has_key(5) && glk2.has_key(25) && glk2.limbs_of(GaloisKeys::get_index(25)) == 3);
+        Ciphertext r1, r2;
+        evaluator.rotate_vector(ct, 1, glk, r1);
+        evaluator.rotate_vector(ct, 1, glk2, r2);
+        CHECK(std::memcmp(r1.data(), r2.data(), 8 * r1.dyn_array_size()) == 0);
+        Ciphertext low = ct, l1, l2;
+        while (low.coeff_modulus_size() > 2) evaluator.mod_switch_to_next_inplace(low);
+        evaluator.rotate_vector(low, 2, glk, l1);
+        evaluator.rotate_vector(low, 2, glk2, l2);
+        CHECK(std::memcmp(l1.data(), l2.data(), 8 * l1.dyn_array_size()) == 0);
+        // a truncated key refuses a ciphertext above its level
+        CHECK(throws([&] {
+            Ciphertext t;
+            evaluator.rotate_vector(ct, 2, glk2, t);
+        }));
+    }
     {
         std::string badk = kstr;
         badk[16] ^= 1; // parms_id

@@ -1,124 +1,84 @@
-"""Device sampling (mhe_sample_poly, csrc/sample.hip) of the random polynomials of key
-generation and encryption (util/rlwe.cpp:21 sample_poly_ternary, :72 sample_poly_normal,
-:135 sample_poly_uniform).
+"""Device samplers of key generation and encryption (csrc/sample.hip) against the oracle's
+sequential restatement of SEAL's samplers on Blake2xbPRNG (oracle/seal_random.c, pinned by hashlib
+in test_seal_random.py): sample_poly_ternary / sample_poly_cbd at stream offsets, and the bulk of
+sample_poly_uniform with its rejected indices redrawn in order from the stream tail
+(util/rlwe.cpp:21-162)."""
+import struct
 
-The uniform and ternary samplers are checked bit for bit against a numpy restatement of
-Philox4x32-10 (the published counter-based generator; the same counter layout as the kernel).
-The normal sampler goes through device log/cos, so it is checked by its distribution: SEAL's
-ClippedNormalDistribution(0, 3.2, 19.2) truncated toward zero, identical in every limb."""
 import numpy as np
 import pytest
 
 import mhe
 import oracle as O
 
-M0, M1 = 0xD2511F53, 0xCD9E8D57
-W0, W1 = 0x9E3779B9, 0xBB67AE85
-MASK = 0xFFFFFFFF
+SEED = [1, 2, 3, 4, 5, 6, 7, 8]
+M64 = (1 << 64) - 1
 
 
-def philox4x32_10(ctr, seed):
-    """ctr: 4 uint64 arrays holding 32-bit words; key = (seed_lo, seed_hi)."""
-    c = [x.astype(np.uint64) for x in ctr]
-    k0, k1 = seed & MASK, seed >> 32
-    for _ in range(10):
-        p0 = c[0] * np.uint64(M0)
-        p1 = c[2] * np.uint64(M1)
-        h0, l0 = p0 >> np.uint64(32), p0 & np.uint64(MASK)
-        h1, l1 = p1 >> np.uint64(32), p1 & np.uint64(MASK)
-        c = [h1 ^ c[1] ^ np.uint64(k0), l1, h0 ^ c[3] ^ np.uint64(k1), l0]
-        k0, k1 = (k0 + W0) & MASK, (k1 + W1) & MASK
-    return c
+def _heavy_reject_primes(log_n, count):
+    """NTT primes just above 1.5 * 2^60: 2^64 mod q ~ 0.67 q, so ~1 word in 16 is redrawn."""
+    out, q = [], (3 << 59) + 1
+    while len(out) < count:
+        if O.is_prime(q):
+            out.append(q)
+        q += 2 << log_n
+    return out
 
 
-def rand128(idx, tag, seed, draw=0):
-    idx = idx.astype(np.uint64)
-    ctr = [idx & np.uint64(MASK), (idx >> np.uint64(32)) ^ np.uint64((draw << 24) & MASK),
-           np.full_like(idx, tag & MASK), np.full_like(idx, tag >> 32)]
-    c = philox4x32_10(ctr, seed)
-    lo = (c[1] << np.uint64(32)) | c[0]
-    hi = (c[3] << np.uint64(32)) | c[2]
-    return lo, hi
+def _eng(log_n, bits):
+    moduli = mhe.coeff_modulus_create(1 << log_n, bits) if bits else _heavy_reject_primes(log_n, 4)
+    return mhe.Engine(log_n, moduli, device=0), O.Context(log_n, moduli), moduli
 
 
-def test_philox_known_answer():
-    # Philox4x32-10 known-answer vectors of the Random123 distribution (kat_vectors):
-    # counter 0, key 0 and counter/key all-ones
-    z = np.zeros(1, np.uint64)
-    c = philox4x32_10([z, z, z, z], 0)
-    assert [int(x[0]) for x in c] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
-    f = np.full(1, MASK, np.uint64)
-    c = philox4x32_10([f, f, f, f], (MASK << 32) | MASK)
-    assert [int(x[0]) for x in c] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
-
-
-BITS = [51, 46, 46, 51]
-
-
-@pytest.fixture(scope="module")
-def eng():
-    n = 1 << 12
-    moduli = O.coeff_modulus_create(n, BITS)
-    return mhe.Engine(12, moduli), moduli
+def _small_from_stream(kind, raw, n, moduli, limbs):
+    if kind == "ternary":
+        w = np.frombuffer(raw[:4 * n], dtype=np.uint32).astype(np.uint64)
+        v = ((w * np.uint64(3)) >> np.uint64(32)).astype(np.int64) - 1
+    else:
+        b = np.frombuffer(raw[:6 * n], dtype=np.uint8).reshape(n, 6).copy()
+        b[:, 2] &= 0x1F
+        b[:, 5] &= 0x1F
+        pc = np.unpackbits(b, axis=1).reshape(n, 6, 8).sum(axis=2).astype(np.int64)
+        v = pc[:, 0] + pc[:, 1] + pc[:, 2] - pc[:, 3] - pc[:, 4] - pc[:, 5]
+    return np.stack([np.where(v >= 0, v, v + int(q)).astype(np.uint64) for q in moduli[:limbs]])
 
 
 @pytest.mark.gpu
-def test_sample_uniform_bits(eng):
-    e, moduli = eng
-    seed, tag = 0x0123456789ABCDEF, 0xFEDCBA9876543210
-    t = e.sample("uniform", len(moduli), seed, tag)
-    e.synchronize()
-    got = mhe.Engine.to_host(t)
-    idx = np.arange(len(moduli) * e.n, dtype=np.uint64)
-    lo, hi = rand128(idx, tag, seed)
-    for l, q in enumerate(moduli):
-        sl = slice(l * e.n, (l + 1) * e.n)
-        want = [((int(h) << 64) | int(w)) % q for h, w in zip(hi[sl], lo[sl])]
-        assert got[l].tolist() == want
+@pytest.mark.parametrize("kind", ["ternary", "cbd"])
+@pytest.mark.parametrize("offset", [0, 64, 4 * 4096, 10 * 4096 + 128])
+def test_small_samplers(kind, offset):
+    log_n = 12
+    eng, oc, moduli = _eng(log_n, [50, 40, 40, 50])
+    n = 1 << log_n
+    got, redraw = eng.prng_small(kind, 3, SEED, offset)
+    assert not redraw
+    got = mhe.Engine.to_host(got)
+    raw = O.prng_bytes(SEED, offset + 6 * n)[offset:]
+    assert np.array_equal(got, _small_from_stream(kind, raw, n, moduli, 3))
+    if offset == 0:
+        assert np.array_equal(got, oc.sample(SEED, kind, 3))
 
 
 @pytest.mark.gpu
-def test_sample_ternary_bits(eng):
-    e, moduli = eng
-    seed, tag = 77, 5
-    t = e.sample("ternary", len(moduli), seed, tag)
-    e.synchronize()
-    got = mhe.Engine.to_host(t)
-    lo, _ = rand128(np.arange(e.n, dtype=np.uint64), tag, seed)
-    v = (lo % np.uint64(3)).astype(np.int64) - 1
-    for l, q in enumerate(moduli):
-        want = np.where(v >= 0, v, np.int64(0)).astype(np.uint64)
-        want[v < 0] = np.uint64(q - 1)
-        np.testing.assert_array_equal(got[l], want)
-    counts = np.bincount(v + 1, minlength=3)
-    assert counts.min() > e.n / 3 * 0.9
-
-
-@pytest.mark.gpu
-def test_sample_normal_distribution(eng):
-    e, moduli = eng
-    vals = []
-    for tag in range(16):
-        t = e.sample("normal", len(moduli), 1234, tag)
-        e.synchronize()
-        got = mhe.Engine.to_host(t).astype(object)
-        centered = [[int(x) if int(x) < q // 2 else int(x) - q for x in row] for row, q in zip(got, moduli)]
-        for row in centered[1:]:
-            assert row == centered[0]          # the same integer in every limb
-        vals.extend(centered[0])
-    v = np.array(vals, dtype=np.float64)
-    assert np.abs(v).max() <= 19               # clipped at 6 sigma, truncated
-    assert abs(v.mean()) < 0.05
-    # truncation toward zero of N(0, 3.2^2) clipped at 19.2: E[trunc(z)^2] ~= 7.99
-    assert 7.7 < (v * v).mean() < 8.3
-
-
-@pytest.mark.gpu
-def test_sample_deterministic_and_tagged(eng):
-    e, moduli = eng
-    a = mhe.Engine.to_host(e.sample("uniform", 2, 9, 1))
-    b = mhe.Engine.to_host(e.sample("uniform", 2, 9, 1))
-    c = mhe.Engine.to_host(e.sample("uniform", 2, 9, 2))
-    e.synchronize()
-    np.testing.assert_array_equal(a, b)
-    assert (a != c).mean() > 0.99
+@pytest.mark.parametrize("log_n,bits", [(12, None), (14, [51] + [46] * 6 + [51])])
+def test_uniform_bulk_and_redraws(log_n, bits):
+    eng, oc, moduli = _eng(log_n, bits)
+    n, limbs = 1 << log_n, len(moduli)
+    out, rej, count = eng.prng_uniform_bulk(limbs, SEED)
+    got = mhe.Engine.to_host(out).copy()
+    raw = np.frombuffer(O.prng_bytes(SEED, limbs * n * 8 + 64 * 4096), dtype=np.uint64)
+    bulk = raw[:limbs * n]
+    mm = np.array([M64 - (M64 % int(q)) - 1 for q in moduli], dtype=np.uint64)
+    want_rej = np.nonzero(bulk >= np.repeat(mm, n))[0].astype(np.uint64)
+    assert count == len(want_rej) and np.array_equal(np.sort(rej), want_rej)
+    # in-order redraws from the words after the bulk (what seal::rnd::sample_uniform_dev does)
+    t = limbs * n
+    for g in np.sort(rej):
+        l = int(g) // n
+        while raw[t] >= mm[l]:
+            t += 1
+        got[l, int(g) % n] = int(raw[t]) % int(moduli[l])
+        t += 1
+    assert np.array_equal(got, oc.sample(SEED, "uniform", limbs))
+    if bits is None:
+        assert count > 100  # the redraw path is exercised
