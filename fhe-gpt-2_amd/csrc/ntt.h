@@ -638,9 +638,10 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     T *x0 = &xch[0][sl * R], *x1 = &xch[1][sl * R];
 
     auto run = [&](const auto &ar) {
-        // FP: the key inner products run in FP64 as well (fp_mulmod_gen); with q < 2^47 (LZ)
-        // the digits stay unreduced and 44 products (|.| <= 1.1q each) sum exactly below 2^53,
-        // otherwise digits are reduced and the sums every second digit.  Integer: 128-bit
+        // FP: the key inner products run in FP64 as well (fp_mulmod_gen); with q < 2^47 and
+        // 1.25 (j1 - j0) q < 2^53 (LZ, chosen below) the digits stay unreduced and the products
+        // (|.| < 1.25q each) sum exactly, otherwise digits are reduced and the sums every second
+        // digit.  Integer: 128-bit
         // accumulation, one Barrett reduction at the end (evaluator.cpp:2412-2462).
         constexpr bool LZ = std::is_same<typename std::decay<decltype(ar)>::type, NttArithF<true>>::value;
         using AccT = typename std::conditional<FP, double, Acc128>::type;
@@ -793,7 +794,9 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     };
     if constexpr (FP)
     {
-        if (p.q < (1ull << 47))
+        // lazy digits and sums only while this group's j1 - j0 products (|.| < 1.25q each) sum
+        // exactly: 1.25 (j1 - j0) q < 2^53 (q < 2^47 allows up to 51 digits per group)
+        if (p.q < (1ull << 47) && (double)(j1 - j0) * 1.25 * (double)p.q < 9007199254740992.0)
             run(NttArithF<true>(p, tw_all + ((size_t)pi << log_n), twd));
         else
             run(ar0);

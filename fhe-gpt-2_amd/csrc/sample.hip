@@ -9,11 +9,13 @@
 //     a word w >= max_multiple(q_l) is redrawn, in index order, from the words after the bulk.
 //     The GPU draws the bulk, reduces the accepted words of the limbs the caller keeps and lists
 //     the rejected indices (~q/2^64 of them); the host orders that list and assigns the
-//     replacement words from the stream tail (mhe_prng_uniform_fix).
+//     replacement words from the stream tail (mhe_prng_apply_fixes writes them).
 //   sample_poly_ternary (rlwe.cpp:21-38): one std::uniform_int_distribution<u64>(0, 2) draw per
 //     coefficient over a 32-bit adapter; libstdc++ 11 maps a 32-bit word g to (3g) >> 32
-//     (Lemire, bits/uniform_int_dist.h:246-270) and redraws only when g == 0 -- reported back so
-//     the caller can take the host path (probability 2^-32 per coefficient).
+//     (Lemire, bits/uniform_int_dist.h:246-270) and redraws only when g == 0 (probability 2^-32
+//     per coefficient): then one thread redoes the poly sequentially and records how many bytes the
+//     redraws used, so the samples drawn after it (the CBD errors) start at the right byte -- all
+//     on the stream, no host round trip.
 //   sample_poly_cbd (rlwe.cpp:101-133): 6 bytes per coefficient, x[2], x[5] masked to 5 bits,
 //     noise = pop(x0)+pop(x1)+pop(x2) - pop(x3)-pop(x4)-pop(x5).
 // Small samples are written as canonical residues over every requested limb (rand + (flag & q)).
@@ -82,8 +84,9 @@ __global__ void k_prng_apply(const u64 *fix, u32 count, u64 *out)
 }
 
 // sample_poly_ternary: coefficients [0, n) from the stream bytes at byte offset `off` (64-aligned),
-// 16 coefficients (one block) per thread.  *rejected is set when some word is 0 (Lemire redraw).
-__global__ void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs, int log_n, u32 *rejected)
+// 16 coefficients (one block) per thread.  A zero word would be redrawn (Lemire); those are
+// counted in state[1] and k_prng_ternary_fix redoes the poly sequentially.
+__global__ void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs, int log_n, u32 *state)
 {
     const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
     const u64 n = (u64)1 << log_n;
@@ -94,7 +97,7 @@ __global__ void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes
     for (int k = 0; k < 16; k++)
     {
         const u32 g = (u32)(w[k >> 1] >> (32 * (k & 1)));
-        if (g == 0) atomicOr(rejected, 1u);
+        if (g == 0) atomicAdd(&state[1], 1u);
         const u64 r = ((u64)g * 3) >> 32; // {0, 1, 2} -> {-1, 0, 1}
         const u64 i = t * 16 + k;
         for (int l = 0; l < limbs; l++)
@@ -105,31 +108,75 @@ __global__ void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes
     }
 }
 
-// sample_poly_cbd: coefficients [0, n) from the bytes at offset `off` (64-aligned), 32
-// coefficients (192 bytes = 3 blocks) per thread.
-__global__ void k_prng_cbd(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs, int log_n)
+// The rare redraw path of sample_poly_ternary (probability ~ n 2^-32 per poly): one thread walks
+// the stream 4 bytes at a time, skipping zero words as libstdc++ 11's uniform_int_distribution
+// does for a 32-bit URBG (threshold 2^32 mod 3 = 1), and records in state[0] how many bytes the
+// redraws consumed, which moves the offsets of the samples drawn after it.
+__global__ void k_prng_ternary_fix(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                                   u32 *state)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (state[1] == 0)
+    {
+        state[0] = 0;
+        return;
+    }
+    const u64 n = (u64)1 << log_n;
+    u64 pos = off, cached = ~0ULL, w[8];
+    for (u64 i = 0; i < n; i++)
+    {
+        u32 g;
+        do
+        {
+            const u64 blk = pos >> 6;
+            if (blk != cached)
+            {
+                stream_block(s, blk, w);
+                cached = blk;
+            }
+            g = (u32)(w[(pos & 63) >> 3] >> (32 * ((pos >> 2) & 1)));
+            pos += 4;
+        } while (g == 0);
+        const u64 r = ((u64)g * 3) >> 32;
+        for (int l = 0; l < limbs; l++)
+        {
+            const u64 q = primes[l].q;
+            out[((u64)l << log_n) + i] = r == 0 ? q - 1 : r - 1;
+        }
+    }
+    state[0] = (u32)(pos - off - 4 * n);
+}
+
+// sample_poly_cbd: coefficients [0, n) from the bytes at offset off + (*extra when given), a
+// multiple of 4; 32 coefficients (192 bytes, 3-4 blocks) per thread.
+__global__ void k_prng_cbd(Seed s, u64 off, const u32 *extra, u64 *out, const PrimeDev *primes, int limbs, int log_n)
 {
     const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
     const u64 n = (u64)1 << log_n;
     if (t * 32 >= n) return;
-    u64 w[24];
+    const int cnt = (int)((n - t * 32) < 32 ? (n - t * 32) : 32);
+    const u64 start = off + (extra ? extra[0] : 0) + 192 * t;
+    const u64 b0 = start >> 6, b1 = (start + 6 * cnt - 1) >> 6;
+    u64 w[32];
     {
         u64 b[8];
-#pragma unroll
-        for (int j = 0; j < 3; j++)
+        for (u64 j = 0; j <= b1 - b0; j++)
         {
-            stream_block(s, (off >> 6) + 3 * t + j, b);
+            stream_block(s, b0 + j, b);
 #pragma unroll
             for (int k = 0; k < 8; k++) w[8 * j + k] = b[k];
         }
     }
-    auto byte_at = [&](int i) -> u32 { return (u32)(w[i >> 3] >> (8 * (i & 7))) & 0xff; };
-    const int cnt = (int)((n - t * 32) < 32 ? (n - t * 32) : 32);
+    const u32 skip = (u32)(start - 64 * b0);
+    auto byte_at = [&](u32 i) -> u32 {
+        i += skip;
+        return (u32)(w[i >> 3] >> (8 * (i & 7))) & 0xff;
+    };
     for (int k = 0; k < cnt; k++)
     {
-        const int b0 = 6 * k;
-        const int noise = __popc(byte_at(b0)) + __popc(byte_at(b0 + 1)) + __popc(byte_at(b0 + 2) & 0x1f) -
-                          __popc(byte_at(b0 + 3)) - __popc(byte_at(b0 + 4)) - __popc(byte_at(b0 + 5) & 0x1f);
+        const u32 c0 = 6 * k;
+        const int noise = __popc(byte_at(c0)) + __popc(byte_at(c0 + 1)) + __popc(byte_at(c0 + 2) & 0x1f) -
+                          __popc(byte_at(c0 + 3)) - __popc(byte_at(c0 + 4)) - __popc(byte_at(c0 + 5) & 0x1f);
         const u64 i = t * 32 + k;
         for (int l = 0; l < limbs; l++)
         {
@@ -185,7 +232,7 @@ MHE_EXPORT int mhe_prng_apply_fixes(mhe_ctx *c, const uint64_t *fixes_dev, uint3
 }
 
 MHE_EXPORT int mhe_prng_small(mhe_ctx *c, const uint64_t seed[8], uint64_t byte_offset, int kind, int limbs,
-                              uint64_t *out, uint32_t *flag_dev, void *stream)
+                              uint64_t *out, uint32_t *state_dev, void *stream)
 {
     const PrimeDev *primes;
     const uint64_t *q;
@@ -199,13 +246,17 @@ MHE_EXPORT int mhe_prng_small(mhe_ctx *c, const uint64_t seed[8], uint64_t byte_
     const u64 n = (u64)1 << log_n;
     if (kind == MHE_SAMPLE_TERNARY)
     {
-        if (!flag_dev) return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
+        if (!state_dev) return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
+        if (hipMemsetAsync(state_dev, 0, 8, st) != hipSuccess)
+            return mhe_internal_fail(MHE_ERR_DEVICE, "sampling state reset failed");
         hipLaunchKernelGGL(k_prng_ternary, dim3((unsigned)((n / 16 + 255) / 256)), dim3(256), 0, st, s, byte_offset, out,
-                           primes, limbs, log_n, flag_dev);
+                           primes, limbs, log_n, state_dev);
+        hipLaunchKernelGGL(k_prng_ternary_fix, dim3(1), dim3(64), 0, st, s, byte_offset, out, primes, limbs, log_n,
+                           state_dev);
     }
     else if (kind == MHE_SAMPLE_CBD)
-        hipLaunchKernelGGL(k_prng_cbd, dim3((unsigned)((n / 32 + 255) / 256)), dim3(256), 0, st, s, byte_offset, out,
-                           primes, limbs, log_n);
+        hipLaunchKernelGGL(k_prng_cbd, dim3((unsigned)((n / 32 + 255) / 256)), dim3(256), 0, st, s, byte_offset,
+                           (const u32 *)state_dev, out, primes, limbs, log_n);
     else
         return mhe_internal_fail(MHE_ERR_ARG, "unknown distribution");
     return launch_check("sampling kernel launch failed");

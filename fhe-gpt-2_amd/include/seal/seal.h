@@ -125,6 +125,7 @@ class CoeffModulus
 {
 public:
     static std::vector<Modulus> Create(std::size_t poly_modulus_degree, std::vector<int> bit_sizes);
+    static int MaxBitCount(std::size_t poly_modulus_degree, sec_level_type sec_level = sec_level_type::tc128) noexcept;
 };
 
 // Randomness (SEAL/randomgen.h): OS entropy, the Blake2xb PRNG and its factories, as in SEAL.
@@ -286,7 +287,10 @@ public:
     const parms_id_type &key_parms_id() const;
     const parms_id_type &first_parms_id() const;
     const parms_id_type &last_parms_id() const;
+    // false when the coefficient modulus exceeds CoeffModulus::MaxBitCount for the requested
+    // security level (context.cpp:207-220); keys, encoders, encryptors then refuse the context
     bool parameters_set() const noexcept;
+    sec_level_type sec_level() const noexcept;
     bool using_keyswitching() const noexcept;
 
     // engine plumbing (not SEAL API)

@@ -193,17 +193,19 @@ class Engine:
     # ----------------------------------------------------------------- kernels
     SAMPLE_KINDS = {"ternary": 1, "cbd": 3}
 
-    def prng_small(self, kind, limbs, seed, byte_offset=0, out=None):
+    def prng_small(self, kind, limbs, seed, byte_offset=0, out=None, state=None):
         """[limbs][n] residues of sample_poly_ternary / sample_poly_cbd drawn from byte
         `byte_offset` of Blake2xbPRNG(seed) (mhe_prng_small; util/rlwe.cpp:21-38,101-133).
-        Returns (out, redraw) -- redraw is set when a ternary word would be redrawn."""
+        `state` (int32 device tensor of 2): ternary writes the bytes its redraws used into
+        state[0]; cbd given a state reads from byte_offset + state[0].  Returns (out, state)."""
+        torch = _torch()
         out = self.empty(limbs, self.n) if out is None else out
         s = np.ascontiguousarray(np.array(seed, np.uint64))
-        torch = _torch()
-        flag = torch.zeros(1, dtype=torch.int32, device=self.torch_device)
+        if state is None and kind == "ternary":
+            state = torch.zeros(2, dtype=torch.int32, device=self.torch_device)
         _check(lib().mhe_prng_small(self._h, s.ctypes.data_as(ctypes.c_void_p), byte_offset, self.SAMPLE_KINDS[kind],
-                                    limbs, _ptr(out), _ptr(flag), self.stream()))
-        return out, bool(flag.item())
+                                    limbs, _ptr(out), _ptr(state) if state is not None else None, self.stream()))
+        return out, state
 
     def prng_uniform_bulk(self, limbs, seed, out=None, cap=1 << 16):
         """Bulk part of sample_poly_uniform over limbs 0..limbs-1 (mhe_prng_uniform_bulk): the reduced

@@ -121,6 +121,8 @@ struct SEALContext::Impl
     std::shared_ptr<const ContextData> key, first, last;
     mhe_ctx *eng = nullptr;
     std::size_t K = 0;
+    sec_level_type sec_level = sec_level_type::tc128;
+    bool insecure = false;
     std::mutex mu;
     std::unordered_map<std::thread::id, void *> streams;
 
@@ -146,7 +148,35 @@ struct SEALContext::Impl
     }
 };
 
-SEALContext::SEALContext(const EncryptionParameters &parms, bool expand_mod_chain, sec_level_type)
+namespace
+{
+// CoeffModulus::MaxBitCount (modulus.cpp:112-116, util/hestdparms.h: HomomorphicEncryption.org
+// classical tables; the modified SEAL adds 65536 -> 1792 for tc128)
+int max_bit_count(std::size_t n, sec_level_type sec)
+{
+    static const std::map<std::size_t, int> tc128{ { 1024, 27 },   { 2048, 54 },   { 4096, 109 },  { 8192, 218 },
+                                                   { 16384, 438 }, { 32768, 881 }, { 65536, 1792 } };
+    static const std::map<std::size_t, int> tc192{ { 1024, 19 }, { 2048, 37 }, { 4096, 75 },
+                                                   { 8192, 152 }, { 16384, 305 }, { 32768, 611 } };
+    static const std::map<std::size_t, int> tc256{ { 1024, 14 }, { 2048, 29 }, { 4096, 58 },
+                                                   { 8192, 118 }, { 16384, 237 }, { 32768, 476 } };
+    const std::map<std::size_t, int> *t = sec == sec_level_type::tc128   ? &tc128
+                                          : sec == sec_level_type::tc192 ? &tc192
+                                          : sec == sec_level_type::tc256 ? &tc256
+                                                                         : nullptr;
+    if (!t) return std::numeric_limits<int>::max();
+    auto it = t->find(n);
+    return it == t->end() ? 0 : it->second;
+}
+} // namespace
+
+int CoeffModulus::MaxBitCount(std::size_t poly_modulus_degree, sec_level_type sec_level) noexcept
+{
+    const int m = max_bit_count(poly_modulus_degree, sec_level);
+    return m == std::numeric_limits<int>::max() ? 0 : m;
+}
+
+SEALContext::SEALContext(const EncryptionParameters &parms, bool expand_mod_chain, sec_level_type sec_level)
 {
     if (parms.scheme() != scheme_type::ckks) throw std::invalid_argument("unsupported scheme");
     const auto &cm = parms.coeff_modulus();
@@ -159,6 +189,10 @@ SEALContext::SEALContext(const EncryptionParameters &parms, bool expand_mod_chai
     auto impl = std::make_shared<Impl>();
     impl->parms = parms;
     impl->K = cm.size();
+    // context.cpp:207-220: parameters above the HomomorphicEncryption.org bound for the requested
+    // security level are kept but flagged; key generators, encryptors, ... then refuse them
+    impl->sec_level = sec_level;
+    if (product_bits(cm, cm.size()) > max_bit_count(n, sec_level)) impl->insecure = true;
     std::vector<std::uint64_t> q;
     for (auto &m : cm) q.push_back(m.value());
     int device = 0;
@@ -216,7 +250,19 @@ std::shared_ptr<const SEALContext::ContextData> SEALContext::last_context_data()
 const parms_id_type &SEALContext::key_parms_id() const { return impl_->key->parms_id(); }
 const parms_id_type &SEALContext::first_parms_id() const { return impl_->first->parms_id(); }
 const parms_id_type &SEALContext::last_parms_id() const { return impl_->last->parms_id(); }
-bool SEALContext::parameters_set() const noexcept { return impl_ && impl_->eng; }
+bool SEALContext::parameters_set() const noexcept { return impl_ && impl_->eng && !impl_->insecure; }
+sec_level_type SEALContext::sec_level() const noexcept
+{
+    return impl_ && !impl_->insecure ? impl_->sec_level : sec_level_type::none;
+}
+
+namespace
+{
+void require_set(const SEALContext &ctx)
+{
+    if (!ctx.parameters_set()) throw std::invalid_argument("encryption parameters are not set correctly");
+}
+} // namespace
 bool SEALContext::using_keyswitching() const noexcept { return impl_ && impl_->K > 1; }
 mhe_ctx *SEALContext::engine() const { return impl_->eng; }
 void *SEALContext::stream() const { return impl_->stream(); }
@@ -745,6 +791,7 @@ void KSwitchKeys::insert(std::size_t index, PolyStore &&key, std::size_t limbs)
 
 KeyGenerator::KeyGenerator(const SEALContext &context) : ctx_(context)
 {
+    require_set(context);
     // keygenerator.cpp:62-84: the secret key from a fresh PRNG of the parameters' factory,
     // sparse ternary with the modified Hamming weight (or ternary for weight 0), NTT form
     const auto &parms = context.key_context_data()->parms();
@@ -770,6 +817,7 @@ KeyGenerator::KeyGenerator(const SEALContext &context) : ctx_(context)
 
 KeyGenerator::KeyGenerator(const SEALContext &context, const SecretKey &secret_key) : ctx_(context), sk_(secret_key)
 {
+    require_set(context);
     if (secret_key.parms_id() != context.key_parms_id())
         throw std::invalid_argument("secret key is not valid for encryption parameters");
     rng_ = factory_of(context);
@@ -949,6 +997,7 @@ const GaloisKeys &KeyGenerator::power_of_two_keys()
 // ------------------------------------------------------------------------------ CKKSEncoder
 CKKSEncoder::CKKSEncoder(const SEALContext &context) : ctx_(context)
 {
+    require_set(context);
     const auto &parms = context.first_context_data()->parms();
     const std::size_t n = parms.poly_modulus_degree();
     slots_ = n >> 1;
@@ -1053,6 +1102,7 @@ void CKKSEncoder::decode(const Plaintext &plain, std::vector<double> &destinatio
 Encryptor::Encryptor(const SEALContext &context, const PublicKey &public_key)
     : ctx_(context), pk_(public_key), asymmetric_(true)
 {
+    require_set(context);
     if (public_key.parms_id() != context.key_parms_id())
         throw std::invalid_argument("public key is not valid for encryption parameters");
     rng_ = factory_of(context);
@@ -1061,6 +1111,7 @@ Encryptor::Encryptor(const SEALContext &context, const PublicKey &public_key)
 Encryptor::Encryptor(const SEALContext &context, const SecretKey &secret_key)
     : ctx_(context), sk_(secret_key), asymmetric_(false)
 {
+    require_set(context);
     if (secret_key.parms_id() != context.key_parms_id())
         throw std::invalid_argument("secret key is not valid for encryption parameters");
     rng_ = factory_of(context);
@@ -1084,31 +1135,11 @@ void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
     // encrypt_zero_asymmetric (rlwe.cpp:220-286): one PRNG; u ternary, then e_0, e_1 (CBD)
     const std::size_t m = L < K ? L + 1 : L;
     const std::uint64_t *pk = pk_.data().store().dev_read(s);
-    DevBuf u(eng, s, m * n), c(eng, s, 2 * m * n), e(eng, s, 2 * m * n), flag(eng, s, 1);
-    std::uint32_t rejected = 0;
-    chk(mhe_memcpy_h2d(eng, flag.p, &rejected, 4, s));
-    chk(mhe_prng_small(eng, seed.data(), 0, MHE_SAMPLE_TERNARY, (int)m, u.p, reinterpret_cast<std::uint32_t *>(flag.p),
-                       s));
-    chk(mhe_memcpy_d2h(eng, &rejected, flag.p, 4, s));
-    chk(mhe_stream_sync(eng, s));
-    if (!rejected)
-    {
-        rnd::sample_cbd_dev(eng, seed, 4 * n, m, e.p, s);
-        rnd::sample_cbd_dev(eng, seed, 10 * n, m, e.p + m * n, s);
-    }
-    else
-    {
-        // a zero word makes std::uniform_int_distribution redraw (2^-32 per coefficient): the
-        // stream positions of everything after it move, so this encryption samples on the host
-        Blake2xbPRNG prng(seed);
-        const auto q = moduli_of(ctx_);
-        std::vector<std::uint64_t> hu(m * n), he(2 * m * n);
-        rnd::sample_ternary_host(prng, q, m, n, hu.data());
-        rnd::sample_cbd_host(prng, q, m, n, he.data());
-        rnd::sample_cbd_host(prng, q, m, n, he.data() + m * n);
-        upload(eng, s, u.p, hu);
-        upload(eng, s, e.p, he);
-    }
+    DevBuf u(eng, s, m * n), c(eng, s, 2 * m * n), e(eng, s, 2 * m * n), state(eng, s, 1);
+    auto *st = reinterpret_cast<std::uint32_t *>(state.p);
+    chk(mhe_prng_small(eng, seed.data(), 0, MHE_SAMPLE_TERNARY, (int)m, u.p, st, s));
+    chk(mhe_prng_small(eng, seed.data(), 4 * n, MHE_SAMPLE_CBD, (int)m, e.p, st, s));
+    chk(mhe_prng_small(eng, seed.data(), 10 * n, MHE_SAMPLE_CBD, (int)m, e.p + m * n, st, s));
     chk(mhe_ntt_forward(eng, u.p, 1, (int)m, 0, s));
     chk(mhe_ntt_forward(eng, e.p, 2, (int)m, 0, s));
     for (int j = 0; j < 2; j++)
@@ -1155,6 +1186,7 @@ void Encryptor::encrypt(const Plaintext &plain, Ciphertext &destination, MemoryP
 // ------------------------------------------------------------------------------ Decryptor
 Decryptor::Decryptor(const SEALContext &context, const SecretKey &secret_key) : ctx_(context), sk_(secret_key)
 {
+    require_set(context);
     if (secret_key.parms_id() != context.key_parms_id())
         throw std::invalid_argument("secret key is not valid for encryption parameters");
 }

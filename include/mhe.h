@@ -202,13 +202,15 @@ int mhe_prng_apply_fixes(mhe_ctx *ctx, const uint64_t *fixes_dev, uint32_t count
 /* sample_poly_ternary (rlwe.cpp:21-38, kind MHE_SAMPLE_TERNARY, 4 stream bytes per coefficient) or
  * sample_poly_cbd (rlwe.cpp:101-133, kind MHE_SAMPLE_CBD, 6 bytes per coefficient), drawing from
  * stream byte `byte_offset` (a multiple of 64) of the PRNG seeded with `seed`, written as
- * canonical residues over limbs 0..limbs-1 of the context (coefficient form).  Ternary sets
- * *flag_dev (device, zeroed by the caller) when a draw would be redrawn (a zero 32-bit word,
- * probability 2^-32), in which case the caller must sample on the host. */
+ * canonical residues over limbs 0..limbs-1 of the context (coefficient form).  state_dev is a
+ * device word pair: ternary sets state_dev[0] to the bytes its redraws consumed (a zero word is
+ * redrawn, as libstdc++'s uniform_int_distribution does; usually 0) and CBD, given state_dev, reads
+ * from byte_offset + state_dev[0] -- so the samples after a ternary one follow SEAL's stream with
+ * no host synchronisation.  Async on stream. */
 #define MHE_SAMPLE_TERNARY 1
 #define MHE_SAMPLE_CBD 3
 int mhe_prng_small(mhe_ctx *ctx, const uint64_t seed[8], uint64_t byte_offset, int kind, int limbs, uint64_t *out,
-                   uint32_t *flag_dev, void *stream);
+                   uint32_t *state_dev, void *stream);
 
 #ifdef __cplusplus
 }

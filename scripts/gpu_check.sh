@@ -1,7 +1,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf --durations=15 > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --durations=25 --timeout 600 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

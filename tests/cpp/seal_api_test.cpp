@@ -415,6 +415,25 @@ static void test_reduced_error_ops()
     CHECK(max_err(e.dec(vr), ex) < 1e-5);
 }
 
+static void test_security_level()
+{
+    // context.cpp:207-220: a chain above CoeffModulus::MaxBitCount for the requested level is
+    // flagged and refused by key generation; sec_level_type::none accepts it
+    CHECK(CoeffModulus::MaxBitCount(4096) == 109 && CoeffModulus::MaxBitCount(65536) == 1792);
+    CHECK(CoeffModulus::MaxBitCount(4096, sec_level_type::tc256) == 58);
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(4096);
+    parms.set_coeff_modulus(CoeffModulus::Create(4096, BITS)); // 280 bits > 109
+    SEALContext strict(parms);
+    CHECK(!strict.parameters_set() && strict.sec_level() == sec_level_type::none);
+    CHECK(throws<std::invalid_argument>([&] { KeyGenerator k(strict); }));
+    SEALContext lax(parms, true, sec_level_type::none);
+    CHECK(lax.parameters_set());
+    parms.set_coeff_modulus(CoeffModulus::Create(4096, { 36, 36, 36 })); // 108 bits
+    SEALContext ok(parms);
+    CHECK(ok.parameters_set() && ok.sec_level() == sec_level_type::tc128);
+}
+
 static void test_sparse_secret_and_slots()
 {
     EncryptionParameters parms(scheme_type::ckks);
@@ -488,6 +507,7 @@ int main()
                   { "rotate", test_rotate },
                   { "reduced_error_ops", test_reduced_error_ops },
                   { "sparse_secret_and_slots", test_sparse_secret_and_slots },
+                  { "security_level", test_security_level },
                   { "threads", test_threads } };
     for (auto &t : tests)
     {

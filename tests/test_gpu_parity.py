@@ -196,6 +196,21 @@ def test_switch_key_truncated_key(small):
     assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
 
 
+@pytest.mark.parametrize("L", [51, 53])
+def test_switch_key_many_47bit_digits(L):
+    """More digits than the lazy FP64 key MAC can sum exactly (1.25 L q >= 2^53 for q ~ 2^46.9,
+    L >= 52): the kernel must fall back to reducing sums (csrc/ntt.h k_ks_row_mac)."""
+    ch = Chain(12, [47] * (L + 1), seed=L)
+    assert all(q < (1 << 47) and q > (1 << 46) * 1.8 for q in ch.moduli)
+    key = ch.rand_key()
+    ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+    got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
+    assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
+    assert np.array_equal(got, ch.oc.hmult(a, b, key))
+
+
 def test_relinearize(small):
     ch = small
     L = 6

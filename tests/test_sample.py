@@ -50,8 +50,9 @@ def test_small_samplers(kind, offset):
     log_n = 12
     eng, oc, moduli = _eng(log_n, [50, 40, 40, 50])
     n = 1 << log_n
-    got, redraw = eng.prng_small(kind, 3, SEED, offset)
-    assert not redraw
+    got, state = eng.prng_small(kind, 3, SEED, offset)
+    if state is not None:
+        assert state.cpu().tolist() == [0, 0]  # no zero word: no redraw
     got = mhe.Engine.to_host(got)
     raw = O.prng_bytes(SEED, offset + 6 * n)[offset:]
     assert np.array_equal(got, _small_from_stream(kind, raw, n, moduli, 3))
@@ -82,3 +83,40 @@ def test_uniform_bulk_and_redraws(log_n, bits):
     assert np.array_equal(got, oc.sample(SEED, "uniform", limbs))
     if bits is None:
         assert count > 100  # the redraw path is exercised
+
+
+@pytest.mark.gpu
+def test_cbd_after_shifted_ternary():
+    """CBD reads from byte_offset + state[0]: the offset a ternary redraw leaves behind (4-byte
+    aligned, not 64) -- the 3-4 block path of k_prng_cbd."""
+    log_n = 12
+    eng, oc, moduli = _eng(log_n, [50, 40, 40, 50])
+    n = 1 << log_n
+    torch = pytest.importorskip("torch")
+    for extra in (4, 60, 68):
+        state = torch.tensor([extra, 0], dtype=torch.int32, device=eng.torch_device)
+        got, _ = eng.prng_small("cbd", 2, SEED, 4 * n, state=state)
+        raw = O.prng_bytes(SEED, 4 * n + extra + 6 * n)[4 * n + extra:]
+        assert np.array_equal(mhe.Engine.to_host(got), _small_from_stream("cbd", raw, n, moduli, 2))
+
+
+@pytest.mark.gpu
+def test_ternary_redraw_path():
+    """A seed whose ternary draws hit a zero word (tests/golden/ternary_redraw_seed.json, found by
+    find_ternary_redraw_seed.c): the redraw moves every later draw; the GPU's sequential fix and the
+    CBD offsets after it follow SEAL's stream (oracle sample_poly_ternary / cbd on one PRNG)."""
+    import json
+    import os
+
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ternary_redraw_seed.json")))
+    seed = [fx["seed0"], 2, 3, 4, 5, 6, 7, 8]
+    log_n = fx["log_n"]
+    eng, oc, moduli = _eng(log_n, [50, 40, 40, 50])
+    n = 1 << log_n
+    u, state = eng.prng_small("ternary", 3, seed, 0)
+    assert np.array_equal(mhe.Engine.to_host(u), oc.sample(seed, "ternary", 3))
+    extra = int(state[0].item())
+    assert extra >= 4 and extra % 4 == 0
+    e0, _ = eng.prng_small("cbd", 3, seed, 4 * n, state=state)
+    raw = O.prng_bytes(seed, 4 * n + extra + 6 * n)[4 * n + extra:]
+    assert np.array_equal(mhe.Engine.to_host(e0), _small_from_stream("cbd", raw, n, moduli, 3))
