@@ -12,6 +12,8 @@
 
 #include <memory>
 #include <string>
+#include <complex>
+#include <iosfwd>
 #include <vector>
 
 #include "mhe_boot.h"
@@ -37,6 +39,7 @@ ResNetParams load_resnet_params_bin(const std::string &path, std::size_t layer_n
 struct ResNetResult
 {
     std::vector<double> logits; // 10 scores (real parts of the first 10 slots)
+    std::vector<std::complex<double>> slots; // the first 10 decoded slots as the reference prints them
     std::size_t label = 0;      // argmax
     double seconds = 0;         // total_time of the reference: encryption excluded, decryption excluded
     double boot_seconds = 0, relu_seconds = 0, linear_seconds = 0;
@@ -51,6 +54,8 @@ public:
     ~ResNetRunner();
     // one image: 3 x 32 x 32 values (channel-major, the test_values.txt order), before /B
     ResNetResult infer(const std::vector<double> &image);
+    // the same, writing the reference's per-stage log (op, time, remaining level, scale) to *log
+    ResNetResult infer(const std::vector<double> &image, std::ostream *log);
     // images on `threads` host threads at once, each on its own HIP stream (the reference runs one
     // image per OpenMP thread, infer_seal.cpp:404); results in image order
     std::vector<ResNetResult> infer_batch(const std::vector<std::vector<double>> &images, int threads);

@@ -279,7 +279,15 @@ double ResNetRunner::galois_key_gb() const
 
 ResNetResult ResNetRunner::infer(const std::vector<double> &img)
 {
-    // infer_seal.cpp:404-577 (one image)
+    return infer(img, nullptr);
+}
+
+ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *log)
+{
+    // infer_seal.cpp:404-577 (one image).  With `log`, every stage is written as the reference's
+    // *_print wrappers write it to result/resnet{L}_cifar10_image{id}.txt (cnn_seal.cpp:106-123,
+    // infer_seal.cpp:408-577): "<op>...", "time : <ms> ms", "remaining level : <chain index>",
+    // "scale: <scale>", then a blank line; ReLU outputs are followed by a few decrypted values.
     Impl &m = *impl_;
     Evaluator &evaluator = *m.evaluator;
     CKKSEncoder &encoder = *m.encoder;
@@ -296,6 +304,34 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img)
     int stage = 0;
     const double epsilon = 0.00001;
     const auto &prm = m.prm;
+    auto t_op = clk::now();
+    auto op_begin = [&] {
+        if (!log) return;
+        sync();
+        t_op = clk::now();
+    };
+    auto op_end = [&](const char *what, const Ciphertext &c, bool timed = true, const char *extra = nullptr) {
+        if (!log) return;
+        sync();
+        *log << what << "..." << std::endl;
+        if (timed)
+            *log << "time : " << (long)(std::chrono::duration<double>(clk::now() - t_op).count() * 1000) << " ms"
+                 << std::endl;
+        if (extra) *log << extra << std::endl;
+        *log << "remaining level : " << m.context->get_context_data(c.parms_id())->chain_index() << std::endl;
+        *log << "scale: " << c.scale() << std::endl << std::endl;
+    };
+    auto print_values = [&] {
+        if (!log) return;
+        // decrypt_and_print_part (func.cpp:262-333): four leading slots and the last
+        Plaintext pt;
+        decryptor.decrypt(cnn.cipher(), pt);
+        std::vector<std::complex<double>> v;
+        encoder.decode(pt, v);
+        *log << "intermediate decrypted values: " << std::endl << "( ";
+        for (int i = 0; i < 4; i++) *log << v[i] << ", ";
+        *log << "... " << v.back() << ")" << std::endl << std::endl;
+    };
 
     std::vector<double> image(n, 0.0);
     for (long i = 0; i < 32 * 32 * 3 && i < (long)img.size(); i++) image[i] = img[i];
@@ -312,10 +348,14 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img)
     cnn.set_ciphertext(ctxt);
 
     // layer 0
+    if (log) *log << "layer 0" << std::endl;
+    op_begin();
     multiplexed_parallel_convolution_seal(cnn, cnn, 16, 1, fh, fw, prm.conv_weight[stage], prm.bn_running_var[stage],
                                           prm.bn_weight[stage], epsilon, encoder, encryptor, evaluator, m.gal_keys,
                                           cipher_pool);
+    op_end("multiplexed parallel convolution", cnn.cipher());
     // scaling factor ~2^51 -> 2^46
+    op_begin();
     {
         const auto &modulus = m.context->first_context_data()->parms().coeff_modulus();
         ctxt = cnn.cipher();
@@ -332,60 +372,89 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img)
     multiplexed_parallel_batch_norm_seal(cnn, cnn, prm.bn_bias[stage], prm.bn_running_mean[stage],
                                          prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder, encryptor,
                                          evaluator, m.B);
+    op_end("multiplexed parallel batch normalization", cnn.cipher());
     auto relu = [&] {
         sync();
         const auto a = clk::now();
+        op_begin();
         ReLU_seal(cnn, cnn, m.comp_no, m.deg, m.alpha, m.tree, m.scaled_val, m.logp, encryptor, evaluator, decryptor,
                   encoder, m.public_key, m.secret_key, m.relin_keys, m.B);
         sync();
         t_relu += std::chrono::duration<double>(clk::now() - a).count();
+        op_end("approximate ReLU", cnn.cipher());
+        print_values();
     };
     auto bootstrap = [&](int j) {
         sync();
         const auto a = clk::now();
+        op_begin();
         Ciphertext c = cnn.cipher(), rtn;
         m.boot[j]->bootstrap_real_3(rtn, c);
         cnn.set_ciphertext(rtn);
         sync();
         t_boot += std::chrono::duration<double>(clk::now() - a).count();
         res.bootstraps++;
+        const std::string tag = "bootstrapping " + std::to_string(res.bootstraps) + " result";
+        op_end("bootstrapping", cnn.cipher(), true, tag.c_str());
     };
     relu();
 
+    int layer = 1;
     for (int j = 0; j < 3; j++) // layer 1_x, 2_x, 3_x
     {
         co = j == 0 ? 16 : j == 1 ? 32 : 64;
         for (std::size_t k = 0; k <= m.end_num; k++)
         {
             stage = (int)(2 * ((m.end_num + 1) * j + k) + 1);
+            if (log) *log << "layer " << layer++ << std::endl;
             temp = cnn;
             st = (j >= 1 && k == 0) ? 2 : 1;
+            op_begin();
             multiplexed_parallel_convolution_seal(cnn, cnn, co, st, fh, fw, prm.conv_weight[stage],
                                                   prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
                                                   encryptor, evaluator, m.gal_keys, cipher_pool);
+            op_end("multiplexed parallel convolution", cnn.cipher());
+            op_begin();
             multiplexed_parallel_batch_norm_seal(cnn, cnn, prm.bn_bias[stage], prm.bn_running_mean[stage],
                                                  prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
                                                  encryptor, evaluator, m.B);
+            op_end("multiplexed parallel batch normalization", cnn.cipher());
             bootstrap(j);
             relu();
 
             stage = (int)(2 * ((m.end_num + 1) * j + k) + 2);
+            if (log) *log << "layer " << layer++ << std::endl;
             st = 1;
+            op_begin();
             multiplexed_parallel_convolution_seal(cnn, cnn, co, st, fh, fw, prm.conv_weight[stage],
                                                   prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
                                                   encryptor, evaluator, m.gal_keys, cipher_pool);
+            op_end("multiplexed parallel convolution", cnn.cipher());
+            op_begin();
             multiplexed_parallel_batch_norm_seal(cnn, cnn, prm.bn_bias[stage], prm.bn_running_mean[stage],
                                                  prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder,
                                                  encryptor, evaluator, m.B);
-            if (j >= 1 && k == 0) multiplexed_parallel_downsampling_seal(temp, temp, evaluator, m.gal_keys);
+            op_end("multiplexed parallel batch normalization", cnn.cipher());
+            if (j >= 1 && k == 0)
+            {
+                op_begin();
+                multiplexed_parallel_downsampling_seal(temp, temp, evaluator, m.gal_keys);
+                op_end("multiplexed parallel downsampling", temp.cipher());
+            }
             cnn_add_seal(temp, cnn, cnn, evaluator);
+            op_end("cipher add", cnn.cipher(), false);
             bootstrap(j);
             relu();
         }
     }
+    if (log) *log << "layer " << layer << std::endl;
     std::ofstream devnull;
+    op_begin();
     averagepooling_seal_scale(cnn, cnn, evaluator, m.gal_keys, m.B, encoder, decryptor, devnull);
+    op_end("average pooling", cnn.cipher());
+    op_begin();
     matrix_multiplication_seal(cnn, cnn, prm.linear_weight, prm.linear_bias, 10, 64, evaluator, m.gal_keys);
+    op_end("fully connected layer", cnn.cipher());
     sync();
     res.seconds = std::chrono::duration<double>(clk::now() - total_start).count();
     res.boot_seconds = t_boot;
@@ -400,6 +469,7 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img)
     for (std::size_t i = 0; i < 10; i++)
     {
         res.logits.push_back(rtn_vec[i].real());
+        res.slots.push_back(rtn_vec[i]);
         if (max_score < rtn_vec[i].real())
         {
             res.label = i;
@@ -435,6 +505,10 @@ std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vecto
 
 void ResNet_cifar10_seal_sparse(std::size_t layer_num, std::size_t start_image_id, std::size_t end_image_id)
 {
+    // infer_seal.cpp:234-582: parameters, the shared label file ../../result/resnet{L}_cifar10_label_{s}_{e}
+    // and per image ../../result/resnet{L}_cifar10_image{id}.txt with the per-stage log
+    if (layer_num != 20 && layer_num != 32 && layer_num != 44 && layer_num != 56 && layer_num != 110)
+        throw std::invalid_argument("layer_num is not correct");
     ResNetParams prm;
     if (const char *bin = std::getenv("MHE_RESNET_PARAMS"))
         prm = load_resnet_params_bin(bin, layer_num);
@@ -442,11 +516,14 @@ void ResNet_cifar10_seal_sparse(std::size_t layer_num, std::size_t start_image_i
         import_parameters_cifar10(prm.linear_weight, prm.linear_bias, prm.conv_weight, prm.bn_bias,
                                   prm.bn_running_mean, prm.bn_running_var, prm.bn_weight, layer_num,
                                   end_num_of(layer_num));
+    const std::string net = "resnet" + std::to_string(layer_num) + "_cifar10_";
+    std::ofstream out_share("../../result/" + net + "label_" + std::to_string(start_image_id) + "_" +
+                            std::to_string(end_image_id));
     const char *cd = std::getenv("MHE_COMP_DIR");
-    ResNetRunner runner(layer_num, prm, cd ? cd : "../result");
+    ResNetRunner runner(layer_num, prm, cd ? cd : "../../result");
     std::ifstream values("../../../testFile/test_values.txt"), labels("../../../testFile/test_label.txt");
     const bool have_images = values.is_open();
-    double all = 0;
+    const auto all_start = std::chrono::steady_clock::now();
     for (std::size_t image_id = start_image_id; image_id <= end_image_id; image_id++)
     {
         std::vector<double> img(32 * 32 * 3);
@@ -464,18 +541,27 @@ void ResNet_cifar10_seal_sparse(std::size_t layer_num, std::size_t start_image_i
         }
         else
         {
+            // test_values.txt is not in the reference tree: seeded synthetic pixels
             std::mt19937_64 g(image_id);
             std::uniform_real_distribution<double> U(-2.5, 2.5);
             for (auto &x : img) x = U(g);
         }
-        ResNetResult r = runner.infer(img);
-        all += r.seconds;
-        std::cout << "( ";
-        for (std::size_t i = 0; i < 9; i++) std::cout << r.logits[i] << ", ";
-        std::cout << r.logits[9] << ")" << std::endl;
-        std::cout << "total time : " << (long)(r.seconds * 1000) << " ms" << std::endl;
-        std::cout << "image label: " << image_label << std::endl;
-        std::cout << "inferred label: " << r.label << std::endl;
+        std::ofstream output("../../result/" + net + "image" + std::to_string(image_id) + ".txt");
+        ResNetResult r = runner.infer(img, &output);
+        for (std::ostream *o : { (std::ostream *)&std::cout, (std::ostream *)&output })
+        {
+            *o << "( ";
+            for (std::size_t i = 0; i < 9; i++) *o << r.slots[i] << ", ";
+            *o << r.slots[9] << ")" << std::endl;
+            *o << "total time : " << (long)(r.seconds * 1000) << " ms" << std::endl;
+            *o << "image label: " << image_label << std::endl;
+            *o << "inferred label: " << r.label << std::endl;
+            *o << "max score: " << r.logits[r.label] << std::endl;
+        }
+        out_share << "image_id: " << image_id << ", "
+                  << "image label: " << image_label << ", inferred label: " << r.label << std::endl;
     }
-    std::cout << "all threads time : " << (long)(all * 1000) << " ms" << std::endl;
+    const long all_ms = (long)(std::chrono::duration<double>(std::chrono::steady_clock::now() - all_start).count() * 1000);
+    std::cout << "all threads time : " << all_ms << " ms" << std::endl;
+    out_share << std::endl << "all threads time : " << all_ms << " ms" << std::endl;
 }

@@ -189,3 +189,36 @@ def test_cmake_package_consumer_runs(tmp_path):
     exe = _consumer(str(tmp_path))
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_cnn_cli_stage_levels_match_reference(tmp_path):
+    """Config C1 plumbing: `cnn 20 10 0 0` (cnn_ckks/run/run_cnn.cpp) writes
+    ../../result/resnet20_cifar10_image0.txt and resnet20_cifar10_label_0_0 in the reference's format
+    (cnn/infer_seal.cpp:408-582).  Its stage sequence -- every logged op with its remaining level and
+    printed scale -- must equal the reference's own run on image 0 (tests/golden/resnet/
+    resnet20_image0_stages.json, extracted by make_resnet_stage_fixture.py).  Values differ: the
+    reference's input pixels are not in its tree, so the image is synthetic."""
+    import json
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_resnet_stage_fixture import parse
+
+    _build()
+    run_dir = tmp_path / "cnn_ckks" / "build"
+    run_dir.mkdir(parents=True)
+    (tmp_path / "result").mkdir()
+    env = dict(os.environ, MHE_RESNET_PARAMS=os.path.join(ROOT, "tests", "golden", "resnet", "resnet20_params.bin"),
+               MHE_COMP_DIR=os.path.join(ROOT, "tests", "golden", "comp"))
+    r = subprocess.run([os.path.join(ROOT, "build", "cnn"), "20", "10", "0", "0"], cwd=run_dir, env=env,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "model: ResNet-20" in r.stdout and "inferred label:" in r.stdout
+    log = (tmp_path / "result" / "resnet20_cifar10_image0.txt").read_text()
+    got = parse(log)
+    want = json.load(open(os.path.join(ROOT, "tests", "golden", "resnet", "resnet20_image0_stages.json")))["stages"]
+    assert [(s["layer"], s["op"]) for s in got] == [(s["layer"], s["op"]) for s in want]
+    for g, w in zip(got, want):
+        assert (g["level"], g["scale"]) == (w["level"], w["scale"]), (g, w)
+    share = (tmp_path / "result" / "resnet20_cifar10_label_0_0").read_text()
+    assert share.startswith("image_id: 0, image label: -1, inferred label: ") and "all threads time :" in share
