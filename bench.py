@@ -54,29 +54,69 @@ def rand_residues(shape, moduli_t, gen):
     return torch.remainder(hi, moduli_t.view(*([1] * (len(shape) - 2)), -1, 1))
 
 
-def cpu_baseline(moduli, L, threads, seconds_hint):
-    """Time the oracle (CPU restatement, port of the reference algorithm) on `threads`
-    independent HMults run concurrently on the host cores."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(moduli, L_main, threads):
+    """SURVEY.md §8(d) CPU baseline: the repo's CPU restatement of the reference algorithm (oracle/,
+    "port", bit-exact with the GPU path), compiled on this host with -O3 -march=native, timed in
+    this run on `threads` host cores (the box's CPU share for one GPU): single-thread HMult/s, and
+    B in {1, 8, 32} independent HMults (one per OpenMP thread) for L in {44, 31, 17, 3}."""
+    import tempfile
+
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # test infrastructure: only the baseline leg uses it
 
+    tmp = tempfile.mkdtemp(prefix="mhe_oracle_")
+    O.build_native(tmp)
     n = 1 << LOG_N
     oc = O.Context(LOG_N, moduli)
     rng = np.random.default_rng(20261015)
+    K = len(moduli)
     qs = np.array(moduli, np.uint64)
-    key = rng.integers(0, 2**62, size=(L, 2, len(moduli), n), dtype=np.uint64) % qs[None, None, :, None]
-    a = rng.integers(0, 2**62, size=(threads, 2, L, n), dtype=np.uint64) % qs[None, None, :L, None]
-    b = rng.integers(0, 2**62, size=(threads, 2, L, n), dtype=np.uint64) % qs[None, None, :L, None]
+    Lmax = max(L_main, 44)
+    key = rng.integers(0, 2**62, size=(Lmax, 2, K, n), dtype=np.uint64) % qs[None, None, :, None]
+    a_all = rng.integers(0, 2**62, size=(32, 2, Lmax, n), dtype=np.uint64) % qs[None, None, :Lmax, None]
+    b_all = rng.integers(0, 2**62, size=(32, 2, Lmax, n), dtype=np.uint64) % qs[None, None, :Lmax, None]
+    table, walls = {}, {}
+    for L in (44, 31, 17, 3):
+        kL = np.ascontiguousarray(key[:L])
+        row = {}
+        for B in (1, 8, 32):
+            a = np.ascontiguousarray(a_all[:B, :, :L])
+            b = np.ascontiguousarray(b_all[:B, :, :L])
+            t0 = time.perf_counter()
+            _, used = oc.hmult_batch(a, b, kL, threads=min(B, threads))
+            dt = time.perf_counter() - t0
+            row[str(B)] = round(B / dt, 4)
+            walls[(L, B)] = (dt, used)
+        table[str(L)] = row
+    a1 = np.ascontiguousarray(a_all[:1, :, :L_main])
+    b1 = np.ascontiguousarray(b_all[:1, :, :L_main])
     t0 = time.perf_counter()
-    _, used = oc.hmult_batch(a, b, key, threads=threads)
-    dt = time.perf_counter() - t0
+    oc.hmult_batch(a1, b1, np.ascontiguousarray(key[:L_main]), threads=1)
+    single = 1.0 / (time.perf_counter() - t0)
+    dt, used = walls[(L_main, 32)] if (L_main, 32) in walls else (None, threads)
     return {
-        "value": round(threads / dt, 4),
+        "value": table.get(str(L_main), {}).get("32", round(single, 4)),
         "unit": "HMult/s",
         "cores": int(used),
         "kind": "port",
-        "sample": f"{threads} independent HMults (N=2^16, L={L}, 45-prime C2 chain), one per OpenMP thread, "
-                  f"oracle/mhe_oracle.c -O3; {dt:.1f} s wall",
+        "nproc": os.cpu_count(),
+        "model": cpu_model(),
+        "build": "gcc -O3 -march=native -fopenmp (built on this host in this run)",
+        "single_thread": round(single, 4),
+        "per_L": {"limbs": table, "batch_key": "independent HMults, one per OpenMP thread, min(B, cores) threads"},
+        "sample": f"32 independent HMults (N=2^16, L={L_main}, 45-prime C2 chain) on {used} threads, "
+                  f"oracle/mhe_oracle.c (restatement of SEAL's evaluator); {dt:.1f} s wall"
+                  if dt else f"single HMult at L={L_main}",
     }
 
 
@@ -147,7 +187,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=8, help="independent HMults per GPU per step")
     ap.add_argument("--limbs", type=int, default=44)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host cores for the CPU baseline (16 = one GPU's share of the box's CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--resnet-images", type=int, default=4,
                     help="ResNet-20 CIFAR-10 images per GPU for the sec/image leg (0 = skip)")
@@ -338,7 +379,7 @@ def main():
                 r["vs_reference_cpu"] = round(RESNET20_CPU_S / r["sec_per_image_1stream"], 1)
             result[f"resnet{args.resnet_layers}"] = r
     if rank == 0 and world == 1 and not args.no_cpu:
-        result["cpu_baseline"] = cpu_baseline(moduli, L, args.cpu_threads, 20)
+        result["cpu_baseline"] = cpu_baseline(moduli, L, args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -22,6 +22,18 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+def build_native(dst_dir):
+    """Compile the restatement for the host it runs on (-O3 -march=native; the committed build is
+    portable because the .so travels between machines) into dst_dir and load that build instead.
+    Used by bench.py's cpu_baseline leg on the GPU box.  Returns the library path."""
+    global _LIB_PATH, _lib
+    out = os.path.join(dst_dir, "liboracle_native.so")
+    subprocess.check_call(["gcc", "-O3", "-march=native", "-fPIC", "-fopenmp", "-ffp-contract=off", "-shared",
+                           "-o", out, os.path.join(_HERE, "mhe_oracle.c"), "-lm"])
+    _LIB_PATH, _lib = out, None
+    return out
+
+
 def lib():
     global _lib
     if _lib is None:

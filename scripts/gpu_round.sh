@@ -13,6 +13,6 @@ timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 ||
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o $TAG --output-format csv -- python3 "$R/bench.py" --no-cpu --streams 1 --steps 3 --warmup 1 > gpurun_out/prof.log 2>&1 || exit $?
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "^(k_|void k_)" -d "$R/gpurun_out/pmc/$c" -o pmc --output-format csv -- python3 "$R/bench.py" --no-cpu --streams 1 --steps 1 --warmup 0 --batch 2 > "gpurun_out/pmc/$c.log" 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "^(k_|void k_)" -d "$R/gpurun_out/pmc/$c" -o pmc --output-format csv -- python3 "$R/bench.py" --no-cpu --resnet-images 0 --streams 1 --steps 1 --warmup 0 --batch 2 > "gpurun_out/pmc/$c.log" 2>&1 || exit $?
 done
 exit $rc
