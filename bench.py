@@ -125,40 +125,56 @@ RESNET20_CPU_S = 2188.8  # reference CPU SEAL, s/image, 1 thread per image (BASE
 
 def resnet_leg(device, images, streams, layers=20):
     """Second half of BASELINE.json's metric: seconds per image of encrypted ResNet-20 CIFAR-10
-    (config C3: multiplexed conv + approximate ReLU + 18 bootstraps at N=2^16) on this GPU, run by
-    build/resnet_test (include/mhe_resnet.h) with the reference's pretrained parameters on seeded
-    synthetic images: one image alone (latency), then `images` images on `streams` streams
-    (throughput).  Decrypted logits are checked against the plain network inside the driver."""
-    import re
-    import subprocess
+    (config C3: multiplexed conv + approximate ReLU + 18 bootstraps at N=2^16; config C4's network
+    with layers=110), through the runner's C ABI (include/mhe_resnet_capi.h) in this process, with
+    the reference's pretrained parameters on seeded synthetic images: one image alone (latency), then
+    `images` images on `streams` host threads (one HIP stream each).
+    One key set for the whole job: rank 0 generates it (planning inference + SEAL
+    keys truncated to their levels), every buffer is broadcast over RCCL/xGMI and imported by the
+    other ranks; each rank then runs its own images.  Key traffic per image: none (all resident)."""
+    from mhe import resnet as R
 
-    exe = os.path.join(ROOT, "build", "resnet_test")
-    if not os.path.exists(exe):
-        return None
-    env = dict(os.environ, MHE_DEVICE=str(device))
-    params = "resnet20_params.bin" if layers == 20 else f"resnet{layers}_params.d7"
-    cmd = [exe, os.path.join(ROOT, "tests", "golden", "resnet", params),
-           os.path.join(ROOT, "tests", "golden", "comp"), str(images), str(layers), str(streams)]
-    p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900)
-    if p.returncode != 0:
-        raise RuntimeError("resnet_test failed:\n" + p.stdout[-2000:] + p.stderr[-2000:])
-    per = [float(m) for m in re.findall(r"^image \d+: ([0-9.]+) s", p.stdout, re.M)]
-    boot = [float(m) for m in re.findall(r"bootstrap ([0-9.]+) s x", p.stdout)]
-    relu = [float(m) for m in re.findall(r"ReLU ([0-9.]+) s", p.stdout)]
-    m = re.search(r"batch: (\d+) images on (\d+) streams in ([0-9.]+) s", p.stdout)
-    setup = re.search(r"setup: ([0-9.]+) s", p.stdout)
-    steady = per[1:] if len(per) > 1 else per
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    os.environ["MHE_DEVICE"] = str(device)
+    params = os.path.join(ROOT, "tests", "golden", "resnet",
+                          "resnet20_params.bin" if layers == 20 else f"resnet{layers}_params.d7")
+    comp = os.path.join(ROOT, "tests", "golden", "comp")
+    t0 = time.perf_counter()
+    runner = R.Runner(layers, params, comp, generate_keys=(rank == 0))
+    shared = None
+    if world > 1:
+        t1 = time.perf_counter()
+        nbuf, nbytes = R.share_keys(dist, runner, torch.device("cuda", device), src=0)
+        torch.cuda.synchronize(device)
+        shared = {"buffers": nbuf, "GB": round(nbytes / 1e9, 2), "broadcast_s": round(time.perf_counter() - t1, 2)}
+    setup = time.perf_counter() - t0
+    info = runner.info()
+    rng = np.random.default_rng(1000 + rank)
+    imgs = rng.uniform(-2.5, 2.5, size=(images, 3072))
+    one = runner.infer_batch(imgs[:1], 1)
+    if world > 1:
+        dist.barrier()
+    t2 = time.perf_counter()
+    batch = runner.infer_batch(imgs, streams)
+    batch_wall = time.perf_counter() - t2
+    runner.close()
     return {
         "workload": ("C3" if layers == 20 else "C4" if layers == 110 else "ResNet")
         + f": ResNet-{layers} CIFAR-10, N=2^16, 31+1 primes, sparse bootstrapping (logn 14/13/12)",
         "data": "reference pretrained parameters (tests/golden/resnet), seeded synthetic images",
-        "sec_per_image_1stream": round(sum(steady) / len(steady), 4),
-        "bootstrap_s_per_image": round(boot[-1], 4) if boot else None,
-        "relu_s_per_image": round(relu[-1], 4) if relu else None,
-        "batch_wall_s": float(m.group(3)) if m else None,
-        "batch_images": int(m.group(1)) if m else None,
-        "streams": int(m.group(2)) if m else None,
-        "setup_s": float(setup.group(1)) if setup else None,
+        "sec_per_image_1stream": round(float(one["seconds"][0]), 4),
+        "bootstrap_s_per_image": round(float(one["boot"][0]), 4),
+        "relu_s_per_image": round(float(one["relu"][0]), 4),
+        "batch_wall_s": round(batch_wall, 4),
+        "batch_images": images,
+        "streams": streams,
+        "setup_s": round(setup, 2),
+        "galois_keys": info["galois_keys"],
+        "galois_key_GB_resident": round(info["galois_key_gb"], 2),
+        "key_H2D_GB_per_image": 0.0,
+        "key_sharing": shared if shared else "single GPU: keys generated here",
+        "labels": [int(x) for x in batch["labels"]],
         "reference_cpu_sec_per_image": RESNET20_CPU_S if layers == 20 else None,
     }
 
@@ -368,16 +384,15 @@ def main():
     }
     if args.resnet_images > 0:
         r = resnet_leg(local, args.resnet_images, args.resnet_streams, args.resnet_layers)
-        if r is not None:
-            t = torch.tensor([r["batch_wall_s"], r["sec_per_image_1stream"]], dtype=torch.float64, device=dev)
-            if world > 1:
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            r["batch_wall_s"], r["sec_per_image_1stream"] = float(t[0]), float(t[1])
-            r["images_per_s"] = round(world * args.resnet_images / r["batch_wall_s"], 4)
-            r["n_gpus"] = world
-            if args.resnet_layers == 20:
-                r["vs_reference_cpu"] = round(RESNET20_CPU_S / r["sec_per_image_1stream"], 1)
-            result[f"resnet{args.resnet_layers}"] = r
+        t = torch.tensor([r["batch_wall_s"], r["sec_per_image_1stream"]], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        r["batch_wall_s"], r["sec_per_image_1stream"] = float(t[0]), float(t[1])
+        r["images_per_s"] = round(world * args.resnet_images / r["batch_wall_s"], 4)
+        r["n_gpus"] = world
+        if args.resnet_layers == 20:
+            r["vs_reference_cpu"] = round(RESNET20_CPU_S / r["sec_per_image_1stream"], 1)
+        result[f"resnet{args.resnet_layers}"] = r
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(moduli, L, args.cpu_threads)
     if rank == 0:

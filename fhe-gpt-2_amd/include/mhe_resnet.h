@@ -12,7 +12,9 @@
 
 #include <memory>
 #include <string>
+#include <chrono>
 #include <complex>
+#include <cstdint>
 #include <iosfwd>
 #include <vector>
 
@@ -49,8 +51,18 @@ struct ResNetResult
 class ResNetRunner
 {
 public:
+    // Where the keys come from.  generate: this runner is the client too -- KeyGenerator, public and
+    // relinearization keys, and the level-truncated Galois key set planned by one inference with a
+    // deferred provider.  import: the keys arrive from another runner (export_keys -> broadcast over
+    // RCCL -> import_key on every rank), then finish_import().
+    enum class KeySource
+    {
+        generate,
+        import
+    };
     // comp_dir: directory holding d<alpha>.txt of the approximate ReLU (mhe_comp.h)
-    ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir);
+    ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir,
+                 KeySource keys = KeySource::generate);
     ~ResNetRunner();
     // one image: 3 x 32 x 32 values (channel-major, the test_values.txt order), before /B
     ResNetResult infer(const std::vector<double> &image);
@@ -67,9 +79,25 @@ public:
     // device bytes of the server's Galois key set (all resident in HBM: no key traffic per image)
     double galois_key_gb() const;
 
+    // key buffers as device memory, for sharing one key set across GPUs: kind 0 secret key [K][n],
+    // 1 public key [2][K][n], 2 relinearization key [K-1][2][K][n], 3 Galois key `index` with
+    // `limbs` stored primes ([limbs-1][2][limbs][n]).  dev stays valid while the runner lives.
+    struct KeyBlob
+    {
+        int kind;
+        std::size_t index, limbs, words;
+        const std::uint64_t *dev;
+    };
+    std::vector<KeyBlob> export_keys() const;
+    void import_key(const KeyBlob &blob); // device-to-device copy from blob.dev (this runner's device)
+    void copy_key(const KeyBlob &blob, void *dst_dev) const; // blob -> dst_dev, synchronous
+    void finish_import();                 // after the last import_key (KeySource::import)
+
 private:
+    void finish_setup(bool plan_galois_keys);
     struct Impl;
     std::unique_ptr<Impl> impl_;
+    std::chrono::steady_clock::time_point t0_;
     double setup_s_ = 0, plan_s_ = 0, keygen_s_ = 0;
     std::size_t galois_keys_ = 0;
 };

@@ -198,10 +198,11 @@ struct ResNetRunner::Impl
     std::unique_ptr<Bootstrapper> boot[3];
 };
 
-ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir)
+ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir,
+                           KeySource keys)
     : impl_(std::make_unique<Impl>())
 {
-    const auto t0 = std::chrono::steady_clock::now();
+    t0_ = std::chrono::steady_clock::now();
     Impl &m = *impl_;
     m.layer_num = layer_num;
     m.end_num = end_num_of(layer_num);
@@ -221,16 +222,26 @@ ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, co
     m.parms.set_poly_modulus_degree(poly_modulus_degree);
     m.parms.set_coeff_modulus(CoeffModulus::Create(poly_modulus_degree, coeff_bit_vec));
     m.parms.set_secret_key_hamming_weight(192);
-    const double scale = std::pow(2.0, m.logp);
     m.context = std::make_unique<SEALContext>(m.parms);
-    m.keygen = std::make_unique<KeyGenerator>(*m.context);
-    m.keygen->create_public_key(m.public_key);
-    m.secret_key = m.keygen->secret_key();
-    m.keygen->create_relin_keys(m.relin_keys);
     m.encoder = std::make_unique<CKKSEncoder>(*m.context);
-    m.encryptor = std::make_unique<Encryptor>(*m.context, m.public_key);
     m.evaluator = std::make_unique<Evaluator>(*m.context, *m.encoder);
+    if (keys == KeySource::generate)
+    {
+        m.keygen = std::make_unique<KeyGenerator>(*m.context);
+        m.keygen->create_public_key(m.public_key);
+        m.secret_key = m.keygen->secret_key();
+        m.keygen->create_relin_keys(m.relin_keys);
+        finish_setup(true);
+    }
+}
+
+void ResNetRunner::finish_setup(bool plan_galois_keys)
+{
+    Impl &m = *impl_;
+    if (!m.keygen) m.keygen = std::make_unique<KeyGenerator>(*m.context, m.secret_key);
+    m.encryptor = std::make_unique<Encryptor>(*m.context, m.public_key);
     m.decryptor = std::make_unique<Decryptor>(*m.context, m.secret_key);
+    const double scale = std::pow(2.0, m.logp);
     const long logns[3] = { m.logn_1, m.logn_2, m.logn_3 };
     for (int i = 0; i < 3; i++)
         m.boot[i] = std::make_unique<Bootstrapper>(m.loge, logns[i], m.logN - 1, m.total_level, scale, m.boundary_K,
@@ -238,36 +249,120 @@ ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, co
                                                    *m.encoder, *m.encryptor, *m.decryptor, *m.evaluator, m.relin_keys,
                                                    m.gal_keys);
     for (auto &b : m.boot) b->prepare_mod_polynomial();
-    // Galois keys.  The reference's driver asks for its rotation steps at the key level
-    // (infer_seal.cpp:345-379, 284 keys = 295 GB), more than one GPU holds.  Client side, a
-    // deferred key provider over every step runs one planning inference on a zero image and
-    // records the level each key is used at (the network's control flow does not depend on the
-    // data); the server's set is then SEAL's keys truncated to those levels, made eagerly, with
-    // no secret in them (seal.h KSwitchKeys).
-    std::vector<int> gal_steps_vector{ 0 };
-    for (long i = 1; i < (1L << (m.logN - 1)); i++) gal_steps_vector.push_back((int)i);
-    m.keygen->create_deferred_galois_keys(gal_steps_vector, m.gal_keys);
     for (int i = 0; i < 3; i++)
     {
         m.boot[i]->slot_vec.push_back(logns[i]);
         m.boot[i]->generate_LT_coefficient_3();
     }
-    const auto t1 = std::chrono::steady_clock::now();
-    (void)infer(std::vector<double>(3 * 32 * 32, 0.0));
-    std::vector<std::pair<std::uint32_t, std::size_t>> plan;
-    for (const auto &kv : m.gal_keys.usage()) plan.emplace_back((std::uint32_t)(2 * kv.first + 1), kv.second - 1);
-    const auto t2 = std::chrono::steady_clock::now();
+    if (plan_galois_keys)
     {
-        GaloisKeys eager;
-        m.keygen->create_galois_keys(plan, eager);
-        m.gal_keys = std::move(eager); // the deferred provider (and its secret key copy) goes away
+        // Galois keys.  The reference's driver asks for its rotation steps at the key level
+        // (infer_seal.cpp:345-379, 284 keys = 295 GB), more than one GPU holds.  Client side, a
+        // deferred key provider over every step runs one planning inference on a zero image and
+        // records the level each key is used at (the network's control flow does not depend on
+        // the data); the server's set is then SEAL's keys truncated to those levels, made eagerly,
+        // with no secret in them (seal.h KSwitchKeys).
+        std::vector<int> gal_steps_vector{ 0 };
+        for (long i = 1; i < (1L << (m.logN - 1)); i++) gal_steps_vector.push_back((int)i);
+        m.keygen->create_deferred_galois_keys(gal_steps_vector, m.gal_keys);
+        const auto t1 = std::chrono::steady_clock::now();
+        (void)infer(std::vector<double>(3 * 32 * 32, 0.0));
+        std::vector<std::pair<std::uint32_t, std::size_t>> plan;
+        for (const auto &kv : m.gal_keys.usage()) plan.emplace_back((std::uint32_t)(2 * kv.first + 1), kv.second - 1);
+        const auto t2 = std::chrono::steady_clock::now();
+        {
+            GaloisKeys eager;
+            m.keygen->create_galois_keys(plan, eager);
+            m.gal_keys = std::move(eager); // the deferred provider (and its secret key copy) goes away
+        }
+        mhe_stream_sync(m.context->engine(), m.context->stream());
+        const auto t3 = std::chrono::steady_clock::now();
+        plan_s_ = std::chrono::duration<double>(t2 - t1).count();
+        keygen_s_ = std::chrono::duration<double>(t3 - t2).count();
     }
-    mhe_stream_sync(m.context->engine(), m.context->stream());
-    const auto t3 = std::chrono::steady_clock::now();
-    plan_s_ = std::chrono::duration<double>(t2 - t1).count();
-    keygen_s_ = std::chrono::duration<double>(t3 - t2).count();
-    galois_keys_ = plan.size();
-    setup_s_ = std::chrono::duration<double>(t3 - t0).count();
+    galois_keys_ = m.gal_keys.usage().size();
+    setup_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count();
+}
+
+// ---------------------------------------------------------------- key export / import
+// kind 0 secret key [K][n], 1 public key [2][K][n], 2 relinearization key [K-1][2][K][n],
+// 3 Galois key `index` truncated to `limbs` stored primes ([limbs-1][2][limbs][n])
+std::vector<ResNetRunner::KeyBlob> ResNetRunner::export_keys() const
+{
+    const Impl &m = *impl_;
+    void *s = m.context->stream();
+    const std::size_t K = m.context->key_size();
+    std::vector<KeyBlob> out;
+    out.push_back({ 0, 0, K, m.secret_key.data().store().words(), m.secret_key.data().store().dev_read(s) });
+    out.push_back({ 1, 0, K, m.public_key.data().store().words(), m.public_key.data().store().dev_read(s) });
+    out.push_back({ 2, 0, K, m.relin_keys.key(0).words(), m.relin_keys.key(0).dev_read(s) });
+    for (const auto &kv : m.gal_keys.usage())
+        out.push_back({ 3, kv.first, kv.second, m.gal_keys.key(kv.first).words(), m.gal_keys.key(kv.first).dev_read(s) });
+    mhe_stream_sync(m.context->engine(), s);
+    return out;
+}
+
+void ResNetRunner::import_key(const KeyBlob &b)
+{
+    Impl &m = *impl_;
+    SEALContext &ctx = *m.context;
+    void *s = ctx.stream();
+    const std::size_t K = ctx.key_size(), n = (std::size_t)1 << m.logN;
+    auto copy_in = [&](PolyStore &ps, std::size_t words) {
+        if (words != b.words) throw std::invalid_argument("imported key has the wrong size");
+        ps.bind(ctx);
+        ps.resize_words(words, false);
+        if (mhe_memcpy_d2d(ctx.engine(), ps.dev_write(s, true), b.dev, words * 8, s) != MHE_OK)
+            throw std::runtime_error(mhe_last_error());
+    };
+    switch (b.kind)
+    {
+    case 0:
+        m.secret_key.data().set_level(ctx, ctx.key_parms_id(), K);
+        copy_in(m.secret_key.data().store(), K * n);
+        break;
+    case 1:
+        m.public_key.data().resize(ctx, ctx.key_parms_id(), 2);
+        m.public_key.data().is_ntt_form() = true;
+        m.public_key.data().scale() = 1.0;
+        copy_in(m.public_key.data().store(), 2 * K * n);
+        break;
+    case 2:
+    {
+        PolyStore key;
+        copy_in(key, (K - 1) * 2 * K * n);
+        m.relin_keys.insert(RelinKeys::get_index(2), std::move(key), K);
+        m.relin_keys.parms_id() = ctx.key_parms_id();
+        m.relin_keys.set_key_limbs(K);
+        break;
+    }
+    case 3:
+    {
+        if (b.limbs < 2 || b.limbs > K) throw std::invalid_argument("imported Galois key has invalid limbs");
+        PolyStore key;
+        copy_in(key, (b.limbs - 1) * 2 * b.limbs * n);
+        m.gal_keys.insert(b.index, std::move(key), b.limbs);
+        m.gal_keys.parms_id() = ctx.key_parms_id();
+        m.gal_keys.set_key_limbs(K);
+        break;
+    }
+    default: throw std::invalid_argument("unknown key kind");
+    }
+    mhe_stream_sync(ctx.engine(), s);
+}
+
+void ResNetRunner::copy_key(const KeyBlob &b, void *dst) const
+{
+    const Impl &m = *impl_;
+    void *s = m.context->stream();
+    if (mhe_memcpy_d2d(m.context->engine(), dst, b.dev, b.words * 8, s) != MHE_OK ||
+        mhe_stream_sync(m.context->engine(), s) != MHE_OK)
+        throw std::runtime_error(mhe_last_error());
+}
+
+void ResNetRunner::finish_import()
+{
+    finish_setup(false);
 }
 
 ResNetRunner::~ResNetRunner() = default;

@@ -1,0 +1,48 @@
+/* mhe_resnet_capi.h -- C ABI of the encrypted ResNet CIFAR-10 runner (libmhe_seal.so), for host
+ * processes that are not C++ (one Python process per GPU under torch.distributed).
+ *
+ * It replaces the driver loop of cnn_ckks/cpu-ckks/single-key/cnn/infer_seal.cpp:234-577 (keys made
+ * once, images fanned out over OpenMP threads sharing them, :404) with one runner per GPU: rank 0
+ * generates the key set, every key buffer is exported as device memory, broadcast over RCCL (xGMI)
+ * and imported on the other ranks, which then run their own images with the same keys.
+ * Return values: 0 ok, -1 error (message from mhe_resnet_last_error, the C++ exception text).
+ * Device pointers are on the runner's device (MHE_DEVICE / the calling process's GPU). */
+#ifndef MHE_RESNET_CAPI_H
+#define MHE_RESNET_CAPI_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mhe_resnet mhe_resnet;
+
+/* layers: 20/32/44/56/110; params_bin: tests/golden/resnet/resnet{L}_params.* (make_resnet_params.py
+ * format); comp_dir: holds d13.txt; generate_keys 1 = make the key set here (client + server),
+ * 0 = keys follow through mhe_resnet_key_import + mhe_resnet_finish_import. */
+int mhe_resnet_create(mhe_resnet **runner, int layers, const char *params_bin, const char *comp_dir, int generate_keys);
+int mhe_resnet_destroy(mhe_resnet *runner);
+const char *mhe_resnet_last_error(void);
+
+/* Key buffers (ResNetRunner::KeyBlob): kind 0 secret key [K][n], 1 public key [2][K][n],
+ * 2 relinearization key [K-1][2][K][n], 3 Galois key `index` with `limbs` primes
+ * ([limbs-1][2][limbs][n]); words = u64 count.  Export copies key i into dst_dev (synchronous). */
+int mhe_resnet_key_count(mhe_resnet *runner, int *count);
+int mhe_resnet_key_info(mhe_resnet *runner, int i, int *kind, uint64_t *index, uint64_t *limbs, uint64_t *words);
+int mhe_resnet_key_export(mhe_resnet *runner, int i, void *dst_dev);
+int mhe_resnet_key_import(mhe_resnet *runner, int kind, uint64_t index, uint64_t limbs, uint64_t words,
+                          const void *src_dev);
+int mhe_resnet_finish_import(mhe_resnet *runner);
+
+/* count images (3 x 32 x 32 doubles each, before the /B of infer_seal.cpp:444) on `threads` host
+ * threads (one HIP stream each).  logits: count x 10 (decrypted), labels: count, seconds: count
+ * (per image, as the reference's total_time), boot/relu: count (time in bootstrapping / ReLU),
+ * wall: the whole batch. */
+int mhe_resnet_infer_batch(mhe_resnet *runner, const double *images, int count, int threads, double *logits,
+                           int *labels, double *seconds, double *boot, double *relu, double *wall);
+int mhe_resnet_info(mhe_resnet *runner, double *setup_s, double *galois_key_gb, int *galois_keys);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
