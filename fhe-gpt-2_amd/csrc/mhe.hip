@@ -938,6 +938,7 @@ struct DevAlloc
     std::multimap<size_t, CachedBlock> free_blocks;
     std::vector<hipEvent_t> ev_pool;
     size_t cached = 0, in_use = 0;
+    int contexts = 0; // live engine contexts on this device: the cache is returned when the last goes
 };
 DevAlloc &dev_alloc()
 {
@@ -965,6 +966,21 @@ void release_cached(DevAlloc &a)
     a.cached = 0;
 }
 } // namespace
+
+// context lifetime on the current device (mhe_ctx_create / mhe_ctx_destroy): when the last context
+// of a device goes, its cached blocks go back to the device, so another process (or a later
+// engine) on the same GPU gets that memory
+extern "C" __attribute__((visibility("hidden"))) void mhe_internal_ctx_count(int delta)
+{
+    DevAlloc &a = dev_alloc();
+    std::lock_guard<std::mutex> g(a.mu);
+    a.contexts += delta;
+    if (a.contexts <= 0)
+    {
+        a.contexts = 0;
+        release_cached(a);
+    }
+}
 
 extern "C" __attribute__((visibility("hidden"))) hipError_t mhe_internal_alloc(void **p, size_t bytes, hipStream_t st)
 {
@@ -1455,6 +1471,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
         delete c;
         return fail(MHE_ERR_DEVICE, std::string("mhe_ctx_create: ") + hipGetErrorString(e));
     }
+    mhe_internal_ctx_count(+1);
     *out = c;
     return MHE_OK;
 }
@@ -1479,6 +1496,7 @@ MHE_EXPORT int mhe_ctx_destroy(mhe_ctx *c)
     (void)hipFree(c->invq);
     (void)hipFree(c->twf);
     delete c;
+    mhe_internal_ctx_count(-1);
     return MHE_OK;
 }
 

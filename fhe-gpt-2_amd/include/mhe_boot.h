@@ -188,6 +188,23 @@ public:
     void modraise_inplace(seal::Ciphertext &cipher);
 
     void bootstrap_sparse_real_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
+    // full slots (logn == logNh; the GPT-2 path's bootstrap_3): Bootstrapper.cpp:2499-2760, 3250-3274
+    void sfl_full_half_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
+    void sfl_full_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
+    void slottocoeff_full_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher1, seal::Ciphertext &cipher2);
+    void bootstrap_full_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
+    // Bootstrapper.cpp:3421-3431: complex bootstrapping (full slots)
+    void bootstrap_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
+    void bootstrap_inplace_3(seal::Ciphertext &cipher);
+    void sflinv_full_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
+    void coefftoslot_full_3(seal::Ciphertext &rtncipher1, seal::Ciphertext &rtncipher2, seal::Ciphertext &cipher);
+    void slottocoeff_full_half_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher1, seal::Ciphertext &cipher2);
+    void bootstrap_full_real_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
+
+private:
+    void sfl_full_common(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher, bool half);
+
+public:
     void bootstrap_real_3(seal::Ciphertext &rtncipher, seal::Ciphertext &cipher);
     void bootstrap_inplace_real_3(seal::Ciphertext &cipher);
 

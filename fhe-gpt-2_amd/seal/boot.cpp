@@ -851,8 +851,35 @@ void lt_coefficients_3(int ln, long logNh, long boundary_K, LTDiags &f1, LTDiags
     // genorigcoeff + genfftcoeff_3 + geninvfftcoeff_3 (Bootstrapper.cpp:512-590, 1116-1908), sparse
     // slots: three merged groups each way, with the reference's scalings and 2n-slot extensions.
     const int cn = 1 << ln;
-    if (ln >= logNh) throw std::logic_error("full-slot bootstrapping (logn == logNh) is not supported");
+    if (ln > logNh) throw std::logic_error("slot count above N/2");
     const cd I(0, 1);
+    if (ln == logNh)
+    {
+        // full slots (genfftcoeff_3 / geninvfftcoeff_3, curr_logn == logNh branches,
+        // Bootstrapper.cpp:1131-1249, 1531-1650): no 2n-slot extensions; the last SlotToCoeff
+        // group and the first CoeffToSlot group wrap around the slot period (rotated BSGS); the
+        // CoeffToSlot input is scaled by 1/K and its last group by 1/2 (the real/imaginary split of
+        // coefftoslot_full_3 doubles it back).
+        {
+            const int d3 = (int)std::floor(ln / 3.0), d2 = (int)std::floor((ln - d3) / 2.0), d1 = ln - d3 - d2;
+            const int t1 = (1 << d1) - 1, t2 = (1 << d2) - 1, t3 = (1 << d3) - 1;
+            f1 = layout(merge_stages(false, ln, 0, d1), cn, 1, t1, false);
+            f2 = layout(merge_stages(false, ln, d1, d1 + d2), cn, 1 << d1, t2, false);
+            f3 = layout(merge_stages(false, ln, d1 + d2, ln), cn, 1 << (d1 + d2), t3, true);
+        }
+        {
+            const int d1 = (int)std::floor(ln / 3.0), d2 = (int)std::floor((ln - d1) / 2.0), d3 = ln - d1 - d2;
+            const int t1 = (1 << d1) - 1, t2 = (1 << d2) - 1, t3 = (1 << d3) - 1;
+            i1 = layout(merge_stages(true, ln, 0, d1), cn, 1 << (ln - d1), t1, true);
+            i2 = layout(merge_stages(true, ln, d1, d1 + d2), cn, 1 << (ln - d1 - d2), t2, false);
+            i3 = layout(merge_stages(true, ln, d1 + d2, ln), cn, 1, t3, false);
+            for (auto &v : i1)
+                for (auto &x : v) x *= 1.0 / (double)boundary_K;
+            for (auto &v : i3)
+                for (auto &x : v) x *= 0.5;
+        }
+        return;
+    }
     {
         // SlotToCoeff: stages 0.. in groups of div1 (step 1), div2 (step 2^div1), div3
         const int d3 = (int)std::floor(ln / 3.0), d2 = (int)std::floor((ln - d3) / 2.0), d1 = ln - d3 - d2;
@@ -1172,6 +1199,153 @@ void Bootstrapper::sflinv_3(Ciphertext &rtncipher, Ciphertext &cipher)
     evaluator.rescale_to_next_inplace(rtncipher);
 }
 
+void Bootstrapper::sfl_full_half_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    sfl_full_common(rtncipher, cipher, true);
+}
+
+void Bootstrapper::sfl_full_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    sfl_full_common(rtncipher, cipher, false);
+}
+
+void Bootstrapper::sfl_full_common(Ciphertext &rtncipher, Ciphertext &cipher, bool half)
+{
+    // Bootstrapper.cpp:2422-2458 (sfl_full_3) / 2499-2536 (sfl_full_half_3, the extra 1/2): full
+    // slots, the last group rotated (cyclic) and scaled as in sfl_half_3
+    const int div_part3 = (int)std::floor(logn / 3.0);
+    const int div_part2 = (int)std::floor((logn - div_part3) / 2.0);
+    const int div_part1 = (int)logn - div_part3 - div_part2;
+    const int totlen1 = (1 << div_part1) - 1, totlen2 = (1 << div_part2) - 1, totlen3 = (1 << div_part3) - 1;
+    const int basicstep1 = 1, basicstep2 = 1 << div_part1, basicstep3 = 1 << (div_part1 + div_part2);
+
+    Ciphertext tmpct;
+    bsgs_linear_transform(tmpct, cipher, totlen1, basicstep1, (int)logn, fftcoeff1[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct);
+    Ciphertext tmpct2;
+    bsgs_linear_transform(tmpct2, tmpct, totlen2, basicstep2, (int)logn, fftcoeff2[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct2);
+
+    const auto &modulus = context.first_context_data()->parms().coeff_modulus();
+    const auto curr_level = context.get_context_data(tmpct2.parms_id())->chain_index();
+    const double mod_zero = (double)modulus[0].value();
+    const double curr_mod = (double)modulus[curr_level].value();
+    const double init = tl_initial_scale != 0 ? tl_initial_scale : initial_scale;
+    const double coeff_scale =
+        curr_mod * mod_zero * final_scale / ((half ? 2 : 1) * tmpct2.scale() * tmpct2.scale() * init);
+    rotated_bsgs_linear_transform(rtncipher, tmpct2, totlen3, basicstep3, (int)logn, fftcoeff3[slot_index],
+                                  coeff_scale);
+    evaluator.rescale_to_next_inplace(rtncipher);
+}
+
+void Bootstrapper::sflinv_full_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:2561-2584
+    const int div_part1 = (int)std::floor(logn / 3.0);
+    const int div_part2 = (int)std::floor((logn - div_part1) / 2.0);
+    const int div_part3 = (int)logn - div_part1 - div_part2;
+    const int totlen1 = (1 << div_part1) - 1, totlen2 = (1 << div_part2) - 1, totlen3 = (1 << div_part3) - 1;
+    const int basicstep1 = 1 << (logn - div_part1), basicstep2 = 1 << (logn - div_part1 - div_part2),
+              basicstep3 = 1;
+
+    Ciphertext tmpct;
+    rotated_bsgs_linear_transform(tmpct, cipher, totlen1, basicstep1, (int)logn, invfftcoeff1[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct);
+    Ciphertext tmpct2;
+    bsgs_linear_transform(tmpct2, tmpct, totlen2, basicstep2, (int)logn, invfftcoeff2[slot_index]);
+    evaluator.rescale_to_next_inplace(tmpct2);
+    bsgs_linear_transform(rtncipher, tmpct2, totlen3, basicstep3, (int)logn, invfftcoeff3[slot_index]);
+    evaluator.rescale_to_next_inplace(rtncipher);
+}
+
+void Bootstrapper::coefftoslot_full_3(Ciphertext &rtncipher1, Ciphertext &rtncipher2, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:2705-2724: the slots of the real and the imaginary part of the coefficients
+    // (t + conj t, and (-i t) + conj(-i t)); -i is a scale-1 plaintext, so no rescale
+    Ciphertext tmpct1, tmpct2, tmpct3, tmpct4;
+    sflinv_full_3(tmpct1, cipher);
+    Plaintext minus_i;
+    encoder.encode(std::vector<cd>((std::size_t)Nh, cd(0.0, -1.0)), 1.0, minus_i);
+    evaluator.mod_switch_to_inplace(minus_i, tmpct1.parms_id());
+    evaluator.multiply_plain(tmpct1, minus_i, tmpct2);
+    evaluator.complex_conjugate(tmpct2, gal_keys, tmpct3);
+    evaluator.complex_conjugate(tmpct1, gal_keys, tmpct4);
+    evaluator.add_reduced_error(tmpct1, tmpct4, rtncipher1);
+    evaluator.add_reduced_error(tmpct2, tmpct3, rtncipher2);
+}
+
+void Bootstrapper::slottocoeff_full_half_3(Ciphertext &rtncipher, Ciphertext &cipher1, Ciphertext &cipher2)
+{
+    // Bootstrapper.cpp:2744-2760: recombine real + i * imaginary, then SlotToCoeff
+    Ciphertext tmpct1, tmpct3;
+    Plaintext plus_i;
+    encoder.encode(std::vector<cd>((std::size_t)Nh, cd(0.0, 1.0)), 1.0, plus_i);
+    evaluator.mod_switch_to_inplace(plus_i, cipher2.parms_id());
+    evaluator.multiply_plain(cipher2, plus_i, tmpct1);
+    evaluator.add_reduced_error(cipher1, tmpct1, tmpct3);
+    sfl_full_half_3(rtncipher, tmpct3);
+}
+
+void Bootstrapper::slottocoeff_full_3(Ciphertext &rtncipher, Ciphertext &cipher1, Ciphertext &cipher2)
+{
+    // Bootstrapper.cpp:2726-2742
+    Ciphertext tmpct1, tmpct3;
+    Plaintext plus_i;
+    encoder.encode(std::vector<cd>((std::size_t)Nh, cd(0.0, 1.0)), 1.0, plus_i);
+    evaluator.mod_switch_to_inplace(plus_i, cipher2.parms_id());
+    evaluator.multiply_plain(cipher2, plus_i, tmpct1);
+    evaluator.add_reduced_error(cipher1, tmpct1, tmpct3);
+    sfl_full_3(rtncipher, tmpct3);
+}
+
+void Bootstrapper::bootstrap_full_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:3155-3176: complex slots
+    modraise_inplace(cipher);
+    const auto &modulus = context.first_context_data()->parms().coeff_modulus();
+    cipher.scale() = (double)modulus[0].value();
+    Ciphertext rtn1, rtn2;
+    coefftoslot_full_3(rtn1, rtn2, cipher);
+    Ciphertext modrtn1, modrtn2;
+    mod_reducer->modular_reduction(modrtn1, rtn1);
+    mod_reducer->modular_reduction(modrtn2, rtn2);
+    slottocoeff_full_3(rtncipher, modrtn1, modrtn2);
+    rtncipher.scale() = final_scale;
+}
+
+void Bootstrapper::bootstrap_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:3421-3425
+    tl_initial_scale = cipher.scale();
+    if (logn != logNh) throw std::logic_error("complex sparse-slot bootstrapping is not provided: use bootstrap_real_3");
+    bootstrap_full_3(rtncipher, cipher);
+}
+
+void Bootstrapper::bootstrap_inplace_3(Ciphertext &cipher)
+{
+    Ciphertext rtncipher;
+    bootstrap_3(rtncipher, cipher);
+    cipher = rtncipher;
+}
+
+void Bootstrapper::bootstrap_full_real_3(Ciphertext &rtncipher, Ciphertext &cipher)
+{
+    // Bootstrapper.cpp:3250-3274
+    modraise_inplace(cipher);
+    const auto &modulus = context.first_context_data()->parms().coeff_modulus();
+    cipher.scale() = (double)modulus[0].value();
+    Ciphertext rtn1, rtn2;
+    coefftoslot_full_3(rtn1, rtn2, cipher);
+    Ciphertext modrtn1, modrtn2;
+    mod_reducer->modular_reduction(modrtn1, rtn1);
+    mod_reducer->modular_reduction(modrtn2, rtn2);
+    slottocoeff_full_half_3(rtncipher, modrtn1, modrtn2);
+    rtncipher.scale() = final_scale;
+    Ciphertext conjct;
+    evaluator.complex_conjugate(rtncipher, gal_keys, conjct);
+    evaluator.add_inplace_reduced_error(rtncipher, conjct);
+}
+
 void Bootstrapper::coefftoslot_3(Ciphertext &rtncipher, Ciphertext &cipher)
 {
     // Bootstrapper.cpp:2675-2680
@@ -1269,8 +1443,10 @@ void Bootstrapper::bootstrap_real_3(Ciphertext &rtncipher, Ciphertext &cipher)
 {
     // Bootstrapper.cpp:3421-3425 (initial_scale kept per thread)
     tl_initial_scale = cipher.scale();
-    if (logn == logNh) throw std::logic_error("full-slot bootstrapping (logn == logNh) is not supported");
-    bootstrap_sparse_real_3(rtncipher, cipher);
+    if (logn == logNh)
+        bootstrap_full_real_3(rtncipher, cipher);
+    else
+        bootstrap_sparse_real_3(rtncipher, cipher);
 }
 
 void Bootstrapper::bootstrap_inplace_real_3(Ciphertext &cipher)

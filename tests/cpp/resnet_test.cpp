@@ -4,6 +4,9 @@
 // testFile/test_values.txt is not in the repository).  The decrypted logits are compared with the
 // same network evaluated in plain doubles with the exact ReLU; prints the time per image.
 //   resnet_test <params.bin> <comp_dir> [images] [layers]
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
 #include "mhe_resnet.h"
 
 #include <algorithm>
@@ -99,8 +102,22 @@ static std::vector<double> plain_resnet(const ResNetParams &p, const std::vector
     return logits;
 }
 
+static void on_fault(int sig)
+{
+    // a host fault (seen only under rocprofv3 so far): print the call stack before dying
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "resnet_test: fatal signal, backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    std::signal(sig, SIG_DFL);
+    std::raise(sig);
+}
+
 int main(int argc, char **argv)
 {
+    std::signal(SIGSEGV, on_fault);
+    std::signal(SIGBUS, on_fault);
     if (argc < 3)
     {
         std::fprintf(stderr, "usage: resnet_test <params.bin|.d7> <comp_dir> [images (-1: load only)] [layers] [threads]\n");

@@ -65,12 +65,14 @@ def test_bootstrapping_host_math():
 
 
 @pytest.mark.gpu
-def test_bootstrapping_end_to_end():
+@pytest.mark.parametrize("logn", ["14", "15"], ids=["sparse_logn14", "full_slots_logn15"])
+def test_bootstrapping_end_to_end(logn):
     """CKKS bootstrapping (include/mhe_boot.h, ckks_bootstrapping/Bootstrapper.cpp semantics) in the
-    reference ResNet setting: N=2^16, 31 data limbs, logn 14 sparse slots, 1 limb -> refreshed;
-    decrypted output within 1e-3 of the message (tests/cpp/boot_test.cpp)."""
+    reference ResNet setting: N=2^16, 31 data limbs, 1 limb -> refreshed; logn 14 sparse slots
+    (bootstrap_sparse_real_3) and all 2^15 slots (bootstrap_full_real_3, the GPT-2 path's
+    bootstrap_3); decrypted output within 1e-3 of the message (tests/cpp/boot_test.cpp)."""
     _build()
-    r = subprocess.run([os.path.join(ROOT, "build", "boot_test"), "14", "2"], capture_output=True, text=True,
+    r = subprocess.run([os.path.join(ROOT, "build", "boot_test"), logn, "2"], capture_output=True, text=True,
                        timeout=900)
     print(r.stdout)
     print(r.stderr)
