@@ -18,6 +18,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "mhe_boot.h"
 #include "seal/seal.h"
 
 namespace gpt2
@@ -92,7 +93,7 @@ void compute_layernorm(Ciphertext &input, Ciphertext &output, std::vector<double
 
 // PolyApprox.cpp:595-649: softmax over rows of 128 packed at slot i*256 with a fixed shift gamma in
 // place of the row max (exp, masked fold + quickSum, Goldschmidt inverse); in place on `input`.
-// (compute_softmax is not provided: the reference's version bootstraps inside quickMax.)
+// (compute_softmax, with the bootstrapped row max, is declared below.)
 void compute_smax(Ciphertext &input, int r, int gamma, CKKSEncoder &encoder, Encryptor &encryptor,
                   Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
 
@@ -170,4 +171,22 @@ void qk_matmul_col(std::vector<Ciphertext> &left_input, std::vector<Ciphertext> 
                    Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
 
 std::vector<int> gpt2_rotation_steps(int logN);
+
+// ---- bootstrapped pieces (full-slot Bootstrapper, logn = logN - 1, as the reference's GPT-2 tests)
+// util.cpp:317-326: mod-switch to the last level, then bootstrap_3
+void bootstrap(Ciphertext &ctxt, Ciphertext &rtn, Bootstrapper &bootstrapper, Evaluator &evaluator);
+// util.cpp:328-339
+void init_bootstrap(Bootstrapper &bootstrapper, std::vector<int> &gal_steps_vector, int logn);
+// Fold.cpp:47-88: max(a, b) = 0.5 ((a + b) + (a - b) sign(0.1 (a - b)))
+void computeMax(Ciphertext &input1, Ciphertext &input2, Ciphertext &output, Bootstrapper &bootstrapper,
+                CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                GaloisKeys &gal_keys, RelinKeys &relin_keys);
+// Fold.cpp:91-110: max over n consecutive slots (rotate by 1, 2, 4, ...), bootstrapping below 18 limbs
+void quickMax(Ciphertext &input, Ciphertext &output, int n, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
+              Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+              RelinKeys &relin_keys);
+// PolyApprox.cpp:533-593: softmax over rows of 128 at slot i*256 with the bootstrapped row max
+void compute_softmax(Ciphertext &input, int r, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
+                     Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                     RelinKeys &relin_keys);
 } // namespace gpt2

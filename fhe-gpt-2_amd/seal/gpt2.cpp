@@ -787,3 +787,89 @@ std::vector<int> gpt2_rotation_steps(int logN)
     return steps;
 }
 } // namespace gpt2
+
+// ===================================================================== bootstrapped max / softmax
+namespace gpt2
+{
+void bootstrap(Ciphertext &ctxt, Ciphertext &rtn, Bootstrapper &bootstrapper, Evaluator &evaluator)
+{
+    // util.cpp:317-326: drop to the last level, then the Bootstrapper's bootstrap_3 (full slots)
+    while (ctxt.coeff_modulus_size() > 1) evaluator.mod_switch_to_next_inplace(ctxt);
+    bootstrapper.bootstrap_3(rtn, ctxt);
+}
+
+void init_bootstrap(Bootstrapper &bootstrapper, std::vector<int> &gal_steps_vector, int logn)
+{
+    // util.cpp:328-339
+    bootstrapper.prepare_mod_polynomial();
+    bootstrapper.addLeftRotKeys_Linear_to_vector_3(gal_steps_vector);
+    bootstrapper.slot_vec.push_back(logn);
+    bootstrapper.generate_LT_coefficient_3();
+}
+
+void computeMax(Ciphertext &input1, Ciphertext &input2, Ciphertext &output, Bootstrapper &, CKKSEncoder &encoder,
+                Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                RelinKeys &relin_keys)
+{
+    // Fold.cpp:47-88: max(a, b) = 0.5 ((a + b) + (a - b) sign(0.1 (a - b)))
+    Ciphertext diff_cipher, normalized_diff, sign_cipher;
+    evaluator.sub(input1, input2, diff_cipher);
+    evaluator.multiply_const(diff_cipher, 0.1, normalized_diff);
+    evaluator.rescale_to_next_inplace(normalized_diff);
+    sign_function(normalized_diff, sign_cipher, 2, 2, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    evaluator.multiply_inplace_reduced_error(diff_cipher, sign_cipher, relin_keys);
+    evaluator.rescale_to_next_inplace(diff_cipher);
+    evaluator.add_inplace_reduced_error(diff_cipher, input1);
+    evaluator.add_inplace_reduced_error(diff_cipher, input2);
+    evaluator.multiply_const(diff_cipher, 0.5, output);
+    evaluator.rescale_to_next_inplace(output);
+}
+
+void quickMax(Ciphertext &input, Ciphertext &output, int n, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
+              Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+              RelinKeys &relin_keys)
+{
+    // Fold.cpp:91-110: log2(n) rounds of max(x, rot(x, 2^k)); bootstrapped below 18 limbs
+    Ciphertext cipher = input, rot_cipher, tmp_cipher;
+    int acc = 1;
+    for (int i = 0; i < (int)std::log2((double)n); i++)
+    {
+        tmp_cipher = cipher;
+        evaluator.rotate_vector(tmp_cipher, acc, gal_keys, rot_cipher);
+        computeMax(tmp_cipher, rot_cipher, cipher, bootstrapper, encoder, encryptor, decryptor, evaluator, gal_keys,
+                   relin_keys);
+        if (cipher.coeff_modulus_size() < 18) bootstrap(cipher, cipher, bootstrapper, evaluator);
+        acc *= 2;
+    }
+    output = cipher;
+}
+
+void compute_softmax(Ciphertext &input, int r, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
+                     Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                     RelinKeys &relin_keys)
+{
+    // PolyApprox.cpp:533-593: rows of 128 scores at slot i*256 (the next 128 slots padding): the row
+    // max by quickMax (bootstrapped), x - max, exp, padding zeroed, a bootstrap, the row sums by a
+    // fold + quickSum, Goldschmidt 1/sum, the product; in place on `input`.  The reference's r
+    // argument is accepted; its exp uses r = 6 as written.
+    (void)r;
+    std::vector<double> zeros_mask(32768, 1.0);
+    for (int i = 0; i < 128; i++)
+        for (int j = 0; j < 128; j++) zeros_mask[i * 256 + 128 + j] = 0.0;
+    Ciphertext rolled, maxes, exps, summed, inverses;
+    evaluator.rotate_vector(input, 32640, gal_keys, rolled);
+    evaluator.add_inplace_reduced_error(input, rolled);
+    quickMax(input, maxes, 128, bootstrapper, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    evaluator.sub_inplace_reduced_error(input, maxes);
+    compute_exp(input, exps, 6, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    evaluator.multiply_vector_inplace_reduced_error(exps, zeros_mask);
+    evaluator.rescale_to_next_inplace(exps);
+    bootstrap(exps, rolled, bootstrapper, evaluator);
+    evaluator.rotate_vector_inplace(rolled, -128, gal_keys);
+    evaluator.add_inplace_reduced_error(rolled, exps);
+    quickSum(rolled, summed, 128, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    compute_inverse(summed, inverses, 4, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    evaluator.multiply_reduced_error(exps, inverses, relin_keys, input);
+    evaluator.rescale_to_next_inplace(input);
+}
+} // namespace gpt2

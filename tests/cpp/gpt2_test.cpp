@@ -8,7 +8,10 @@
 //    reference's expected value is the exact function rather than the approximation;
 //  * config C5's bar: the decrypted approximation over all 32768 slots within 1e-3 of the same
 //    polynomial evaluated in plain doubles (the plain restatement below).
+#include "mhe_boot.h"
 #include "mhe_gpt2.h"
+
+#include "../../include/mhe.h"
 
 #include <algorithm>
 #include <chrono>
@@ -311,6 +314,139 @@ static int run_all(int log_scale)
         for (int i = 0; i < S; i++) err = std::max(err, std::fabs(got[i] - want[i]));
         std::printf("  compute_smax: output %zu limbs\n", c.coeff_modulus_size());
         report("compute_smax(gamma 2) vs plain restatement, 32768 slots", err < 1e-3, err, secs);
+    }
+    {
+        // Bootstrapped pieces on a full-slot Bootstrapper (logn = 15, run_approx_test.cpp's constants:
+        // loge 10, K 25, cosine degree 59, 2 double angles, inverse degree 1): computeMax (Fold.cpp:47-88),
+        // quickMax (:91-110) and compute_softmax (PolyApprox.cpp:533-593), each against the same
+        // operation sequence restated in doubles with bootstrapping taken as the identity
+        const int S = 32768;
+        Bootstrapper bt(10, (long)logN - 1, (long)logN - 1, remaining_level + boot_level, encode_scale(), 25, 59, 2, 1,
+                        context, keygen, encoder, encryptor, decryptor, evaluator, relin_keys, gal_keys);
+        std::vector<int> bsteps;
+        for (int i = 0; i < (int)logN - 1; i++) bsteps.push_back(1 << i);
+        const auto tb = std::chrono::steady_clock::now();
+        init_bootstrap(bt, bsteps, (int)logN - 1);
+        std::vector<int> missing;
+        for (int st : bsteps)
+            if (!gal_keys.has_key(seal::GaloisKeys::get_index(mhe_galois_elt_from_step((int)logN, st))))
+                missing.push_back(st);
+        keygen.create_galois_keys(missing, gal_keys);
+        std::printf("full-slot bootstrapper: %zu extra Galois keys, %.2f s\n", missing.size(),
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count());
+        auto rot = [&](const std::vector<double> &x, int k) {
+            std::vector<double> y(S);
+            for (int i = 0; i < S; i++) y[i] = x[((i + k) % S + S) % S];
+            return y;
+        };
+        auto pmax = [&](const std::vector<double> &a, const std::vector<double> &b) {
+            std::vector<double> o(S);
+            for (int i = 0; i < S; i++) o[i] = 0.5 * ((a[i] - b[i]) * plain_sign(0.1 * (a[i] - b[i])) + a[i] + b[i]);
+            return o;
+        };
+        auto maxerr = [&](const std::vector<double> &got, const std::vector<double> &want) {
+            double e = 0;
+            for (int i = 0; i < S; i++) e = std::max(e, std::fabs(got[i] - want[i]));
+            return e;
+        };
+        std::uniform_real_distribution<double> U(-1, 1);
+        {
+            // the reference's ComputeMax doctest inputs, then all slots random
+            std::vector<double> a(S), b(S);
+            const double d1[5] = { 0.1, 0.5, 0.003, 0.4, -0.2 }, d2[5] = { 0.3, 0.1, 0.1, -0.6, 0.0001 };
+            for (int i = 0; i < S; i++)
+            {
+                a[i] = i < 5 ? d1[i] : U(rng);
+                b[i] = i < 5 ? d2[i] : U(rng);
+            }
+            Ciphertext ca = enc(a), cb = enc(b), out;
+            const auto t = std::chrono::steady_clock::now();
+            computeMax(ca, cb, out, bt, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            const auto got = dec(out);
+            std::printf("-- computeMax: doctest slots %.5f %.5f %.5f %.5f %.5f (expected ~0.3 0.5 0.1 0.4 0.0001), "
+                        "%zu limbs\n", got[0], got[1], got[2], got[3], got[4], out.coeff_modulus_size());
+            report("computeMax vs plain restatement, 32768 slots", maxerr(got, pmax(a, b)) < 1e-3, maxerr(got, pmax(a, b)),
+                   secs);
+        }
+        {
+            // QuickMax doctest shape: maxima over 8 consecutive slots of a ciphertext dropped to
+            // TOTAL_LEVEL - BOOT_LEVEL limbs (run_approx_test.cpp:616-648)
+            std::vector<double> v(S);
+            for (int i = 0; i < S; i++) v[i] = i < 16 ? 0.1 * (1 + i % 8) : U(rng);
+            Ciphertext c = enc(v), out;
+            while ((int)c.coeff_modulus_size() > remaining_level) evaluator.mod_switch_to_next_inplace(c);
+            const auto t = std::chrono::steady_clock::now();
+            quickMax(c, out, 8, bt, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            auto want = v;
+            for (int acc = 1; acc < 8; acc *= 2) want = pmax(want, rot(want, acc));
+            const auto got = dec(out);
+            std::printf("-- quickMax(8): first slots %.5f %.5f (doctest expects 0.8), %zu limbs\n", got[0], got[1],
+                        out.coeff_modulus_size());
+            report("quickMax(8) vs plain restatement, 32768 slots", maxerr(got, want) < 1e-3, maxerr(got, want), secs);
+        }
+        {
+            // compute_softmax on rows of 128 scores at slot i*256
+            std::vector<double> v(S, 0.0);
+            for (int i = 0; i < 128; i++)
+                for (int j = 0; j < 128; j++) v[i * 256 + j] = U(rng);
+            auto x = v;
+            {
+                const auto r = rot(v, 32640);
+                for (int i = 0; i < S; i++) x[i] += r[i];
+            }
+            auto mx = x;
+            for (int acc = 1; acc < 128; acc *= 2) mx = pmax(mx, rot(mx, acc));
+            std::vector<double> e(S), want(S);
+            for (int i = 0; i < S; i++)
+            {
+                const bool pad = (i % 256) >= 128;
+                e[i] = pad ? 0.0 : std::pow(1 + (x[i] - mx[i]) / 64.0, 64);
+            }
+            auto rolled = rot(e, -128);
+            for (int i = 0; i < S; i++) rolled[i] += e[i];
+            auto summed = rolled;
+            {
+                auto r1 = rot(summed, 1);
+                for (int i = 0; i < S; i++) summed[i] += r1[i];
+                for (int acc = 2; acc < 128; acc *= 2)
+                {
+                    const auto ro = rot(summed, acc);
+                    for (int i = 0; i < S; i++) summed[i] += ro[i];
+                }
+            }
+            double softmax_err = 0;
+            for (int i = 0; i < S; i++)
+            {
+                double nn = 0.001, d = 0.001 * summed[i];
+                for (int k = 0; k < 4; k++)
+                {
+                    const double f = 2 - d;
+                    nn *= f;
+                    d *= f;
+                }
+                want[i] = e[i] * nn;
+            }
+            for (int r = 0; r < 128; r++)
+            {
+                // against the exact softmax of the row (the approximation's own error, reported)
+                double m = -1e9, z = 0;
+                for (int j = 0; j < 128; j++) m = std::max(m, v[r * 256 + j]);
+                for (int j = 0; j < 128; j++) z += std::exp(v[r * 256 + j] - m);
+                for (int j = 0; j < 128; j++)
+                    softmax_err = std::max(softmax_err, std::fabs(want[r * 256 + j] - std::exp(v[r * 256 + j] - m) / z));
+            }
+            Ciphertext c = enc(v);
+            const auto t = std::chrono::steady_clock::now();
+            compute_softmax(c, 6, bt, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+            const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+            const auto got = dec(c);
+            std::printf("-- compute_softmax: %zu limbs out; the restated pipeline is within %.2g of the exact "
+                        "softmax\n", c.coeff_modulus_size(), softmax_err);
+            report("compute_softmax (bootstrapped quickMax) vs plain restatement, 32768 slots", maxerr(got, want) < 1e-3,
+                   maxerr(got, want), secs);
+        }
     }
     {
         // compute_inv_sqrt (IterApprox.cpp:128-166) and compute_layernorm (:168-246) vs the same

@@ -27,7 +27,9 @@ def test_gpt2_symbols_exported():
                 "gpt2::fakeBootstrap", "gpt2::taylor_expand", "gpt2::compute_inv_sqrt", "gpt2::compute_layernorm",
                 "gpt2::surefire_rotate", "gpt2::attn_proj_row_seal", "gpt2::attn_proj_col_seal",
                 "gpt2::qk_matmul", "gpt2::sv_matmul",
-                "gpt2::batch_matmul", "gpt2::qk_matmul_col", "gpt2::cipher_plain_128_128"):
+                "gpt2::batch_matmul", "gpt2::qk_matmul_col", "gpt2::cipher_plain_128_128",
+                "gpt2::bootstrap", "gpt2::init_bootstrap", "gpt2::computeMax", "gpt2::quickMax",
+                "gpt2::compute_softmax"):
         assert sym in out, sym
 
 
