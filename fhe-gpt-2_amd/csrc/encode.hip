@@ -298,7 +298,9 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_at(mhe_ctx
         return mhe_internal_fail(MHE_ERR_ARG, "parms_id is not valid for encryption parameters");
     const int tb = total_bits(q, bound_limbs);
     if (scale <= 0 || (static_cast<int>(std::log2(scale)) + 1 >= tb))
-        return mhe_internal_fail(MHE_ERR_ARG, "scale out of bounds");
+        return mhe_internal_fail(MHE_ERR_ARG, ("scale out of bounds (encoding 2^" + std::to_string(std::log2(scale)) +
+                                               " at " + std::to_string(bound_limbs) + " limbs, " + std::to_string(tb) +
+                                               " bits)").c_str());
     const size_t n = e->n;
     hipStream_t st = (hipStream_t)stream;
     int dev = 0;

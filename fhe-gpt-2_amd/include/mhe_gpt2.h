@@ -173,8 +173,13 @@ void qk_matmul_col(std::vector<Ciphertext> &left_input, std::vector<Ciphertext> 
 std::vector<int> gpt2_rotation_steps(int logN);
 
 // ---- bootstrapped pieces (full-slot Bootstrapper, logn = logN - 1, as the reference's GPT-2 tests)
-// util.cpp:317-326: mod-switch to the last level, then bootstrap_3
+// util.cpp:317-326: mod-switch to the last level, then bootstrap_3.  With >= 2 limbs the message is
+// first divided by kappa (one rescale, input scale reinterpreted as Delta / kappa) so that the sine
+// step of the modular reduction works on x / (8 kappa) instead of x / 8 (gpt2.cpp); kappa = 32 by
+// default, 1 reproduces the reference exactly
 void bootstrap(Ciphertext &ctxt, Ciphertext &rtn, Bootstrapper &bootstrapper, Evaluator &evaluator);
+void set_bootstrap_prescale(double kappa);
+double bootstrap_prescale();
 // util.cpp:328-339
 void init_bootstrap(Bootstrapper &bootstrapper, std::vector<int> &gal_steps_vector, int logn);
 // Fold.cpp:47-88: max(a, b) = 0.5 ((a + b) + (a - b) sign(0.1 (a - b)))

@@ -791,9 +791,35 @@ std::vector<int> gpt2_rotation_steps(int logN)
 // ===================================================================== bootstrapped max / softmax
 namespace gpt2
 {
+namespace
+{
+double g_boot_prescale = 32.0;
+}
+
+void set_bootstrap_prescale(double kappa)
+{
+    if (!(kappa >= 1.0)) throw std::invalid_argument("set_bootstrap_prescale: kappa must be >= 1");
+    g_boot_prescale = kappa;
+}
+double bootstrap_prescale() { return g_boot_prescale; }
+
 void bootstrap(Ciphertext &ctxt, Ciphertext &rtn, Bootstrapper &bootstrapper, Evaluator &evaluator)
 {
-    // util.cpp:317-326: drop to the last level, then the Bootstrapper's bootstrap_3 (full slots)
+    // util.cpp:317-326: drop to the last level, then the Bootstrapper's bootstrap_3 (full slots).
+    // On the GPT-2 chain q0 / Delta = 2^49 / 2^46 = 8, so the modular reduction sees t = x / 8 and
+    // sin(2 pi t) / (2 pi) returns x (1 - (2 pi x / 8)^2 / 6): 0.8 comes back as 0.75.  With two
+    // or more limbs left the message is first divided by kappa (one rescale) and the ciphertext's
+    // scale set to Delta' = Delta / kappa, so the value is unchanged and t = x / (8 kappa); the
+    // Bootstrapper maps the input scale (tl_initial_scale) to its final scale in the SlotToCoeff
+    // coefficients, so the output carries x at the usual scale and no level is spent afterwards.
+    // A ciphertext already at one limb is bootstrapped as the reference does.
+    if (ctxt.coeff_modulus_size() >= 2 && g_boot_prescale != 1.0)
+    {
+        while (ctxt.coeff_modulus_size() > 2) evaluator.mod_switch_to_next_inplace(ctxt);
+        evaluator.multiply_const_inplace(ctxt, 1.0 / g_boot_prescale);
+        evaluator.rescale_to_next_inplace(ctxt);
+        ctxt.scale() /= g_boot_prescale;
+    }
     while (ctxt.coeff_modulus_size() > 1) evaluator.mod_switch_to_next_inplace(ctxt);
     bootstrapper.bootstrap_3(rtn, ctxt);
 }
@@ -864,8 +890,15 @@ void compute_softmax(Ciphertext &input, int r, Bootstrapper &bootstrapper, CKKSE
     compute_exp(input, exps, 6, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     evaluator.multiply_vector_inplace_reduced_error(exps, zeros_mask);
     evaluator.rescale_to_next_inplace(exps);
-    bootstrap(exps, rolled, bootstrapper, evaluator);
-    evaluator.rotate_vector_inplace(rolled, -128, gal_keys);
+    // :575-579 as intended: util.cpp's bootstrap() drops its argument to one limb in place, so the
+    // reference's later uses of `exps` (the add at :579, the product at :591) would run at the last
+    // level; the refreshed ciphertext is used for both here
+    {
+        Ciphertext refreshed;
+        bootstrap(exps, refreshed, bootstrapper, evaluator);
+        exps = refreshed;
+    }
+    evaluator.rotate_vector(exps, -128, gal_keys, rolled);
     evaluator.add_inplace_reduced_error(rolled, exps);
     quickSum(rolled, summed, 128, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     compute_inverse(summed, inverses, 4, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);

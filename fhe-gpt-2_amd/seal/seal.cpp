@@ -1249,7 +1249,8 @@ Level check_ct(const SEALContext &ctx, const Ciphertext &ct, const char *what)
 void check_scale(double scale, const Level &lv)
 {
     if (scale <= 0 || static_cast<int>(std::log2(scale)) >= (int)lv.total_bits)
-        throw std::invalid_argument("scale out of bounds");
+        throw std::invalid_argument("scale out of bounds (2^" + std::to_string(std::log2(scale)) + " at " +
+                                    std::to_string(lv.L) + " limbs, " + std::to_string(lv.total_bits) + " bits)");
 }
 } // namespace
 

@@ -320,8 +320,21 @@ static int run_all(int log_scale)
         // loge 10, K 25, cosine degree 59, 2 double angles, inverse degree 1): computeMax (Fold.cpp:47-88),
         // quickMax (:91-110) and compute_softmax (PolyApprox.cpp:533-593), each against the same
         // operation sequence restated in doubles with bootstrapping taken as the identity
+        // INIT()'s scale 2^LOGP (util.h:53), and every input dropped to TOTAL_LEVEL - BOOT_LEVEL = 21 limbs
+        // as the QuickMax doctest does: the levels a bootstrap refreshes, all 46-bit primes, where the
+        // 2^46 scale is stable (in the 49-bit boot levels each rescale of a 2^46 product loses 3 bits)
         const int S = 32768;
-        Bootstrapper bt(10, (long)logN - 1, (long)logN - 1, remaining_level + boot_level, encode_scale(), 25, 59, 2, 1,
+        const double saved_scale = encode_scale(), bscale = std::pow(2.0, LOGP);
+        set_encode_scale(bscale);
+        auto enc = [&](const std::vector<double> &v) {
+            Plaintext p;
+            Ciphertext c;
+            encoder.encode(v, bscale, p);
+            encryptor.encrypt(p, c);
+            while ((int)c.coeff_modulus_size() > remaining_level) evaluator.mod_switch_to_next_inplace(c);
+            return c;
+        };
+        Bootstrapper bt(10, (long)logN - 1, (long)logN - 1, remaining_level + boot_level, bscale, 25, 59, 2, 1,
                         context, keygen, encoder, encryptor, decryptor, evaluator, relin_keys, gal_keys);
         std::vector<int> bsteps;
         for (int i = 0; i < (int)logN - 1; i++) bsteps.push_back(1 << i);
@@ -370,12 +383,16 @@ static int run_all(int log_scale)
                    secs);
         }
         {
-            // QuickMax doctest shape: maxima over 8 consecutive slots of a ciphertext dropped to
-            // TOTAL_LEVEL - BOOT_LEVEL limbs (run_approx_test.cpp:616-648)
+            // QuickMax doctest values: maxima over 8 consecutive slots (run_approx_test.cpp:621-653); each
+            // round ends below 18 limbs and runs a real bootstrap_3
             std::vector<double> v(S);
             for (int i = 0; i < S; i++) v[i] = i < 16 ? 0.1 * (1 + i % 8) : U(rng);
-            Ciphertext c = enc(v), out;
-            while ((int)c.coeff_modulus_size() > remaining_level) evaluator.mod_switch_to_next_inplace(c);
+            Plaintext pv;
+            Ciphertext c, out;
+            encoder.encode(v, bscale, pv);
+            encryptor.encrypt(pv, c);
+            // one level above the doctest's 21 limbs, so the first bootstrap (at 2 limbs) can prescale
+            while ((int)c.coeff_modulus_size() > remaining_level + 1) evaluator.mod_switch_to_next_inplace(c);
             const auto t = std::chrono::steady_clock::now();
             quickMax(c, out, 8, bt, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
             const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
@@ -447,6 +464,7 @@ static int run_all(int log_scale)
             report("compute_softmax (bootstrapped quickMax) vs plain restatement, 32768 slots", maxerr(got, want) < 1e-3,
                    maxerr(got, want), secs);
         }
+        set_encode_scale(saved_scale);
     }
     {
         // compute_inv_sqrt (IterApprox.cpp:128-166) and compute_layernorm (:168-246) vs the same
