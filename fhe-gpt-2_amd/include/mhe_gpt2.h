@@ -194,4 +194,126 @@ void quickMax(Ciphertext &input, Ciphertext &output, int n, Bootstrapper &bootst
 void compute_softmax(Ciphertext &input, int r, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
                      Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
                      RelinKeys &relin_keys);
+
+// ============================================================================ gpt2_block.cpp
+// The transformer block (layers.cpp:3-72, which does not compile as written; the plain pipeline
+// plain_approx/full_gpt2.py:94-147) over the packed layouts, for any rows / d_model / heads / d_ff
+// whose heads fit one ciphertext.  Layouts and deviations: gpt2_block.cpp, DESIGN.md.
+struct BlockDims
+{
+    int rows = 128, d_model = 768, heads = 12, d_ff = 3072;
+};
+struct AttentionParams
+{
+    double masked_score = -5.0; // masked scores pinned here before the row max
+    double inv_norm = 0.0;      // Goldschmidt normalisation of the row sums (0: 1 / rows)
+    int inv_iters = 8;          // Goldschmidt steps
+    int newton_iters = 3;       // layer-norm Newton steps
+    double gelu_alpha = 0.1;    // GELU signs taken of alpha (x + shift)
+};
+struct PlainBlockWeights
+{
+    // row-major [in][out] as GPT-2's Conv1D (x W + b)
+    std::vector<double> ln1_g, ln1_b, qw, qb, kw, kb, vw, vb, ow, ob, ln2_g, ln2_b, fc_w, fc_b, pj_w, pj_b;
+};
+struct BlockWeights
+{
+    std::vector<Ciphertext> qw, qb, kw, kb, vw, vb, ow, fc_w, pj_w;
+    Ciphertext ob, fc_b, pj_b;
+    std::vector<double> ln1_g, ln1_b, ln2_g, ln2_b;
+};
+struct BlockTrace
+{
+    std::vector<Ciphertext> ln1, attn, x1, ln2, ffn;
+};
+
+// pack.cpp / pack.py
+std::vector<double> repeat(const std::vector<double> &input, int times);
+void expand_bias(std::vector<double> &input, Ciphertext &output, CKKSEncoder &encoder, Encryptor &encryptor,
+                 Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys,
+                 int rows = -1);
+void expand_bias_head_row(std::vector<double> &input, std::vector<Ciphertext> &output, int heads,
+                          CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                          GaloisKeys &gal_keys, RelinKeys &relin_keys, int rows = -1);
+void expand_bias_head_col(std::vector<double> &input, std::vector<Ciphertext> &output, int heads, int rows, int cols,
+                          CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                          GaloisKeys &gal_keys, RelinKeys &relin_keys);
+std::vector<std::vector<std::vector<double>>> unpack_heads(const std::vector<std::vector<double>> &heads, int num_ciphers,
+                                                           int num_rows, int row_size);
+void pack_heads(std::vector<Ciphertext> &input, std::vector<std::vector<double>> &output, int heads, int num_ciphers,
+                int num_rows, int row_size, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void pack_tight(std::vector<Ciphertext> &input, std::vector<Ciphertext> &output, CKKSEncoder &encoder,
+                Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                RelinKeys &relin_keys);
+void pack_tight(std::vector<Ciphertext> &input, std::vector<Ciphertext> &output, int rows, int row_size, int stride,
+                CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void unpack_tight(std::vector<Ciphertext> &input, std::vector<Ciphertext> &output, CKKSEncoder &encoder,
+                  Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                  RelinKeys &relin_keys);
+void unpack_tight(std::vector<Ciphertext> &input, std::vector<Ciphertext> &output, int rows, int row_size, int stride,
+                  CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                  GaloisKeys &gal_keys, RelinKeys &relin_keys);
+// optimize.cpp:4-40 (KV cache)
+void augment_value_row(std::vector<Ciphertext> &A, std::vector<Ciphertext> &cached_val, int padded_row_size, int idx,
+                       CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                       GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void augment_value_col(std::vector<Ciphertext> &A, std::vector<Ciphertext> &cached_val, int padded_row_size, int idx,
+                       CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                       GaloisKeys &gal_keys, RelinKeys &relin_keys);
+
+// block pieces
+void row_matmul(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, std::vector<Ciphertext> bias,
+                std::vector<Ciphertext> &outputs, int A_rows, int A_cols, int W_cols, CKKSEncoder &encoder,
+                Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                RelinKeys &relin_keys);
+void attn_proj_heads(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, std::vector<Ciphertext> &bias,
+                     std::vector<Ciphertext> &outputs, int rows, int d_model, int heads, bool column_layout,
+                     CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                     GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void qk_heads(std::vector<Ciphertext> &Q, std::vector<Ciphertext> &K, std::vector<Ciphertext> &outputs, int rows,
+              int head_dim, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+              GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void sv_heads(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vector<Ciphertext> &outputs, int rows,
+              int head_dim, int d_model, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+              Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void compute_inverse_norm(Ciphertext &input, Ciphertext &output, int iters, double normalize_factor,
+                          CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                          GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void compute_softmax_rows(Ciphertext &input, int n, const std::vector<double> &keep_mask, double inv_norm,
+                          int inv_iters, Bootstrapper &bootstrapper, CKKSEncoder &encoder, Encryptor &encryptor,
+                          Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void layer_norm_rows(Ciphertext &input, Ciphertext &output, const std::vector<double> &gamma,
+                     const std::vector<double> &beta, int rows, int row_size, int newton_iters,
+                     Bootstrapper &bootstrapper, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
+                     Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void compute_gelu_block(Ciphertext &inputs, Ciphertext &outputs, double alpha, CKKSEncoder &encoder,
+                        Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                        RelinKeys &relin_keys);
+// layers.cpp
+void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std::vector<Ciphertext> &qb,
+                    std::vector<Ciphertext> &kw, std::vector<Ciphertext> &kb, std::vector<Ciphertext> &vw,
+                    std::vector<Ciphertext> &vb, std::vector<Ciphertext> &w_out, Ciphertext &b_out,
+                    const std::vector<std::vector<double>> &keep, std::vector<std::vector<Ciphertext>> &kv_cache,
+                    std::vector<Ciphertext> &outputs, int rows, int cols, int heads, int idx,
+                    const AttentionParams &params, Bootstrapper &bootstrapper, seal::KeyGenerator &keygen,
+                    CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
+                    GaloisKeys &gal_keys, RelinKeys &relin_keys);
+void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, Ciphertext b1,
+                      std::vector<Ciphertext> &W2, Ciphertext b2, std::vector<Ciphertext> &outputs, int rows, int cols,
+                      int d_ff, double gelu_alpha, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
+                      Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                      RelinKeys &relin_keys);
+void transformer_block(std::vector<Ciphertext> &x, BlockWeights &w, const std::vector<std::vector<double>> &keep,
+                       std::vector<Ciphertext> &y, const BlockDims &dims, const AttentionParams &params,
+                       Bootstrapper &bootstrapper, seal::KeyGenerator &keygen, CKKSEncoder &encoder,
+                       Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                       RelinKeys &relin_keys, BlockTrace *trace = nullptr);
+// full_gpt2.py:17-78 for one block; ciphertexts dropped to `limbs` (<= 0: kept at the top level)
+void encrypt_block_weights(const PlainBlockWeights &p, BlockWeights &w, const BlockDims &dims, CKKSEncoder &encoder,
+                           Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
+                           RelinKeys &relin_keys, int limbs);
+// the +-2^i steps every block rotation is composed from
+std::vector<int> block_rotation_steps(int logN);
 } // namespace gpt2

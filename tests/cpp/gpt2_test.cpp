@@ -364,6 +364,43 @@ static int run_all(int log_scale)
         };
         std::uniform_real_distribution<double> U(-1, 1);
         {
+            // bootstrap() accuracy against its prescale kappa, for |x| <= 1 and |x| <= 4 (kappa = 1 is the
+            // reference's util.cpp:318 behaviour)
+            const double saved_kappa = bootstrap_prescale();
+            for (double range : { 1.0, 4.0 })
+                for (double kappa : { 1.0, 8.0, 32.0, 128.0, 512.0 })
+                {
+                    set_bootstrap_prescale(kappa);
+                    std::vector<double> v(S);
+                    for (auto &x : v) x = range * U(rng);
+                    Ciphertext c = enc(v), out;
+                    while ((int)c.coeff_modulus_size() > 3) evaluator.mod_switch_to_next_inplace(c);
+                    bootstrap(c, out, bt, evaluator);
+                    const auto got = dec(out);
+                    double e = 0;
+                    for (int i = 0; i < S; i++) e = std::max(e, std::fabs(got[i] - v[i]));
+                    std::printf("   bootstrap |x| <= %.0f, kappa %4.0f: max err %.3g, %zu limbs out\n", range, kappa, e,
+                                out.coeff_modulus_size());
+                }
+            {
+                // a ciphertext rescaled (not dropped) into its last limb, bootstrapped as is
+                set_bootstrap_prescale(1.0);
+                std::vector<double> v(S);
+                for (auto &x : v) x = U(rng);
+                Ciphertext c = enc(v), out;
+                while ((int)c.coeff_modulus_size() > 2) evaluator.mod_switch_to_next_inplace(c);
+                evaluator.multiply_const_inplace(c, 1.0);
+                evaluator.rescale_to_next_inplace(c);
+                const double s_in = c.scale();
+                bootstrap(c, out, bt, evaluator);
+                const auto got = dec(out);
+                double e = 0;
+                for (int i = 0; i < S; i++) e = std::max(e, std::fabs(got[i] - v[i]));
+                std::printf("   bootstrap of a rescaled 1-limb ciphertext (scale 2^%.4f): max err %.3g\n", std::log2(s_in), e);
+            }
+            set_bootstrap_prescale(saved_kappa);
+        }
+        {
             // the reference's ComputeMax doctest inputs, then all slots random
             std::vector<double> a(S), b(S);
             const double d1[5] = { 0.1, 0.5, 0.003, 0.4, -0.2 }, d2[5] = { 0.3, 0.1, 0.1, -0.6, 0.0001 };

@@ -1,0 +1,274 @@
+"""Plain restatement of one GPT-2 transformer block as the encrypted path computes it, and the
+fixture the GPU test checks against (tests/golden/gpt2_block/block.bin + block.txt).
+
+The block follows the reference's plain pipeline (plain_approx/full_gpt2.py:94-147: layer_norm ->
+attention_layer -> residual -> layer_norm -> mlp -> residual; plain_approx/layers.py:24-116,
+plain_approx/attn.py:168-381) with the approximations the encrypted path evaluates in place of the
+exact functions:
+  * layer norm: row sums by fold + quickSum, mean and variance by 1/d, inverse square root by a
+    2nd-order Taylor start at 1 and Newton steps y <- y (1.5 - 0.5 u y^2) (plain_approx/
+    iterations.py:15-21; the reference's own start, taylor_expand, has no constant term as written in
+    IterApprox.cpp:69-120);
+  * softmax: the reference's compute_softmax (PolyApprox.cpp:533-593) on rows of T at stride 2T --
+    row max by quickMax of computeMax (Fold.cpp:47-110: 0.5((a-b) sign(0.1(a-b)) + a + b) with the
+    composite sign f(f(g(g(x))))), exp(x) ~ (1 + x/64)^64, the causal/padding mask applied
+    multiplicatively after exp (attn.py:247's extract mask) and, before the max, masked scores
+    pinned to -5 (attn.py:365 adds -1e5, which the sign step of computeMax cannot take), fold + quickSum, Goldschmidt 1/sum
+    (IterApprox.cpp:15-68) normalised by 1/T with 8 steps;
+  * GELU: the piecewise p / q / x of PolyApprox.cpp:443-504 (plain_approx/poly.py:30-35) with its
+    three signs evaluated on alpha (x + shift), alpha = 1/10 so they stay inside [-1, 1], and the last
+    piece's indicator s2 + 0.5 (the reference's 0.5 s2 returns +-x/4 there).
+Every matrix product is exact here (the encrypted path's placements only move values); softmax is
+restated slot by slot because the approximate max depends on the order quickMax combines entries.
+
+Run: python tests/golden/gpt2_block/make_fixture.py  (writes block.bin / block.txt next to itself)
+"""
+import math
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SLOTS = 32768
+
+# block dimensions (reduced GPT-2: 16 tokens, d_model 64, 4 heads of 16, d_ff 256)
+T, D, H, F = 16, 64, 4, 256
+DH = D // H
+SEED = 20261016
+GELU_ALPHA = 1.0 / 10.0
+NEWTON_ITERS = 3
+INV_ITERS = 8
+INV_NORM = 1.0 / T
+MASKED_SCORE = -5.0   # causal mask: masked scores are replaced by this before the row max
+
+# composite sign (PolyApprox.cpp:103-305, Chebyshev form)
+SIGN_F = (-0.6767578125, 1.563049316, -0.02685546875, 0.1384277344, 0.002136230469)
+SIGN_G = (-1.121704102, 1.978370667, -0.6178588867, 0.403533935, 0.3557052612)
+
+
+def cheb(x):
+    t2 = 2 * x * x - 1
+    t3 = 2 * x * t2 - x
+    t4 = 2 * t2 * t2 - 1
+    t8 = 2 * t4 * t4 - 1
+    return t2, t3, t4, t8
+
+
+def sign_poly(x, c):
+    fq1, fr1, frq2_q, frq2_r, fq3 = c
+    t2, t3, t4, t8 = cheb(x)
+    return fq1 * x * t2 + fr1 * x + (frq2_q * t3 + frq2_r * x) * t4 + fq3 * x * t8
+
+
+def sign_function(x):
+    # sign_function(2, 2): g, g, then f, f (PolyApprox.cpp:308-334)
+    return sign_poly(sign_poly(sign_poly(sign_poly(x, SIGN_G), SIGN_G), SIGN_F), SIGN_F)
+
+
+def gelu_p(x):
+    t2 = 2 * x * x - 1
+    return (-0.005337069175 * x - 0.05745879353) * t2 + (-0.4187418723 * x - 0.55528939)
+
+
+def gelu_q(x):
+    t2, _, t4, _ = cheb(x)
+    return ((-0.00324699876 * x + 0.1634058825) * t2 + (0.5027208006 * x + 0.1750485092)
+            + (0.0001533078376 * x * x + 0.0002609111473 * x - 0.004401064777) * t4)
+
+
+def gelu_block(x):
+    y = GELU_ALPHA * x
+    s2 = 0.5 * sign_function(y + GELU_ALPHA * -3.0)
+    s1 = 0.5 * sign_function(y + GELU_ALPHA * 1.95)
+    s0 = 0.5 * sign_function(y + GELU_ALPHA * 4.0)
+    b1, b2, b3 = s0 - s1, s1 - s2, s2 + 0.5
+    return b1 * gelu_p(x) + b2 * gelu_q(x) + b3 * x
+
+
+def rot(v, k):
+    """Evaluator::rotate_vector(v, k): out[i] = v[i + k]."""
+    return np.roll(v, -k)
+
+
+def quick_sum(v, n):
+    # Fold.cpp:20-45
+    out = v + rot(v, 1)
+    acc = 2
+    for _ in range(int(math.log2(n)) - 1):
+        out = out + rot(out, acc)
+        acc *= 2
+    return out
+
+
+def compute_max(a, b):
+    # Fold.cpp:47-88
+    diff = a - b
+    return 0.5 * (diff * sign_function(0.1 * diff) + a + b)
+
+
+def quick_max(v, n):
+    # Fold.cpp:91-110 (bootstrapping is the identity here)
+    acc = 1
+    for _ in range(int(math.log2(n))):
+        v = compute_max(v, rot(v, acc))
+        acc *= 2
+    return v
+
+
+def compute_exp(x, r=6):
+    y = x / 2.0 ** r + 1.0
+    for _ in range(r):
+        y = y * y
+    return y
+
+
+def goldschmidt(s, norm, iters):
+    # IterApprox.cpp:15-68 with the normalisation as a parameter
+    n = np.full_like(s, norm)
+    d = norm * s
+    for _ in range(iters):
+        f = 2.0 - d
+        n = n * f
+        d = d * f
+    return n
+
+
+def softmax_rows_slots(scores, keep):
+    """compute_softmax_rows on one head: scores (T x T) packed at row stride 2T; keep (T x T) 0/1."""
+    n = scores.shape[1]
+    v = np.zeros(SLOTS)
+    km = np.zeros(SLOTS)
+    for r in range(scores.shape[0]):
+        v[r * 2 * n:r * 2 * n + n] = scores[r]
+        km[r * 2 * n:r * 2 * n + n] = keep[r]
+    x = v + rot(v, SLOTS - n)
+    mx = quick_max(x, n)
+    exps = compute_exp(x - mx) * km
+    rolled = rot(exps, -n) + exps
+    summed = quick_sum(rolled, n)
+    out = exps * goldschmidt(summed, INV_NORM, INV_ITERS)
+    p = np.stack([out[r * 2 * n:r * 2 * n + n] for r in range(scores.shape[0])])
+    return p, {"max_abs_in": float(np.abs(x).max()), "max_row_sum": float(summed.max())}
+
+
+def layer_norm_block(x, gamma, beta):
+    d = x.shape[1]
+    mean = x.sum(axis=1, keepdims=True) * (1.0 / d)
+    z = x - mean
+    u = (z * z).sum(axis=1, keepdims=True) * (1.0 / d)
+    t = u - 1.0
+    y = (1.0 + (-0.5) * t) + 0.375 * (t * t)
+    h = -0.5 * u
+    for _ in range(NEWTON_ITERS):
+        y = y * ((y * y) * h + 1.5)
+    return (z * y) * gamma + beta, u
+
+
+def block(x, w):
+    ranges = {}
+    ln1, u1 = layer_norm_block(x, w["ln1_g"], w["ln1_b"])
+    q = ln1 @ w["qw"] + w["qb"]
+    k = ln1 @ w["kw"] + w["kb"]
+    v = ln1 @ w["vw"] + w["vb"]
+    keep = np.tril(np.ones((T, T)))
+    o = np.zeros((T, D))
+    smax_in = 0.0
+    for h in range(H):
+        sl = slice(h * DH, (h + 1) * DH)
+        s = (q[:, sl] @ k[:, sl].T) / math.sqrt(DH)
+        s = s * keep + MASKED_SCORE * (1.0 - keep)
+        p, info = softmax_rows_slots(s, keep)
+        smax_in = max(smax_in, info["max_abs_in"])
+        o[:, sl] = p @ v[:, sl]
+    attn = o @ w["ow"] + w["ob"]
+    x1 = x + attn
+    ln2, u2 = layer_norm_block(x1, w["ln2_g"], w["ln2_b"])
+    hid = ln2 @ w["fc_w"] + w["fc_b"]
+    g = gelu_block(hid)
+    f = g @ w["pj_w"] + w["pj_b"]
+    y = x1 + f
+    ranges.update(var1=(float(u1.min()), float(u1.max())), var2=(float(u2.min()), float(u2.max())),
+                  scores=smax_in, hidden=(float(hid.min()), float(hid.max())), x1=float(np.abs(x1).max()),
+                  gelu=float(np.abs(g).max()), qkv=float(max(np.abs(q).max(), np.abs(k).max(), np.abs(v).max())))
+    return {"ln1": ln1, "q": q, "k": k, "v": v, "attn": attn, "x1": x1, "ln2": ln2, "hidden": hid, "gelu": g,
+            "ffn": f, "y": y}, ranges
+
+
+def exact_block(x, w):
+    """The same block with exact layer norm (eps 0), softmax and tanh-GELU (attn.py:388-468,
+    test_layers.py:67-94), for the approximation error."""
+    def ln(a, g, b):
+        m = a.mean(axis=1, keepdims=True)
+        var = ((a - m) ** 2).mean(axis=1, keepdims=True)
+        return (a - m) / np.sqrt(var) * g + b
+
+    ln1 = ln(x, w["ln1_g"], w["ln1_b"])
+    q, k, v = ln1 @ w["qw"] + w["qb"], ln1 @ w["kw"] + w["kb"], ln1 @ w["vw"] + w["vb"]
+    o = np.zeros((T, D))
+    mask = np.tril(np.ones((T, T)))
+    for h in range(H):
+        sl = slice(h * DH, (h + 1) * DH)
+        s = (q[:, sl] @ k[:, sl].T) / math.sqrt(DH)
+        s = np.where(mask == 0, -1e10, s)
+        e = np.exp(s - s.max(axis=1, keepdims=True))
+        o[:, sl] = (e / e.sum(axis=1, keepdims=True)) @ v[:, sl]
+    x1 = x + o @ w["ow"] + w["ob"]
+    hid = ln(x1, w["ln2_g"], w["ln2_b"]) @ w["fc_w"] + w["fc_b"]
+    g = 0.5 * hid * (1 + np.tanh(math.sqrt(2 / math.pi) * (hid + 0.044715 * hid ** 3)))
+    return x1 + g @ w["pj_w"] + w["pj_b"]
+
+
+def make_inputs(seed=SEED):
+    rng = np.random.default_rng(seed)
+    x = rng.normal(0.0, 1.0, (T, D))
+    w = {
+        "ln1_g": 1.0 + 0.1 * rng.normal(size=D), "ln1_b": 0.1 * rng.normal(size=D),
+        "qw": rng.normal(0, 1.0 / math.sqrt(D), (D, D)), "qb": 0.05 * rng.normal(size=D),
+        "kw": rng.normal(0, 1.0 / math.sqrt(D), (D, D)), "kb": 0.05 * rng.normal(size=D),
+        "vw": rng.normal(0, 1.0 / math.sqrt(D), (D, D)), "vb": 0.05 * rng.normal(size=D),
+        "ow": rng.normal(0, 0.5 / math.sqrt(D), (D, D)), "ob": 0.05 * rng.normal(size=D),
+        "ln2_g": 1.0 + 0.1 * rng.normal(size=D), "ln2_b": 0.1 * rng.normal(size=D),
+        "fc_w": rng.normal(0, 0.8 / math.sqrt(D), (D, F)), "fc_b": 0.05 * rng.normal(size=F),
+        "pj_w": rng.normal(0, 0.5 / math.sqrt(F), (F, D)), "pj_b": 0.05 * rng.normal(size=D),
+    }
+    return x, w
+
+
+ORDER_IN = ["x", "ln1_g", "ln1_b", "qw", "qb", "kw", "kb", "vw", "vb", "ow", "ob", "ln2_g", "ln2_b", "fc_w", "fc_b",
+            "pj_w", "pj_b"]
+ORDER_OUT = ["ln1", "q", "k", "v", "attn", "x1", "ln2", "hidden", "gelu", "ffn", "y", "y_exact"]
+
+
+def arrays(seed=SEED):
+    x, w = make_inputs(seed)
+    outs, ranges = block(x, w)
+    outs["y_exact"] = exact_block(x, w)
+    allv = {"x": x, **w, **outs}
+    return [(k, np.atleast_2d(np.asarray(allv[k], dtype="<f8"))) for k in ORDER_IN + ORDER_OUT], ranges
+
+
+def write(dst=HERE):
+    items, ranges = arrays()
+    off = 0
+    lines = [f"# gpt2 block fixture: T {T} d {D} heads {H} d_ff {F} seed {SEED} alpha {GELU_ALPHA} "
+             f"newton {NEWTON_ITERS} inv_iters {INV_ITERS}", "# name rows cols offset(doubles)"]
+    blob = bytearray()
+    for name, a in items:
+        lines.append(f"{name} {a.shape[0]} {a.shape[1]} {off}")
+        blob += a.tobytes()
+        off += a.size
+    with open(os.path.join(dst, "block.bin"), "wb") as f:
+        f.write(bytes(blob))
+    with open(os.path.join(dst, "block.txt"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return ranges
+
+
+if __name__ == "__main__":
+    r = write()
+    items, _ = arrays()
+    d = dict(items)
+    print("ranges:", r)
+    print("approximate vs exact block: max |y - y_exact| =", float(np.abs(d["y"] - d["y_exact"]).max()))
+    sys.exit(0)

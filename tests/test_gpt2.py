@@ -29,7 +29,11 @@ def test_gpt2_symbols_exported():
                 "gpt2::qk_matmul", "gpt2::sv_matmul",
                 "gpt2::batch_matmul", "gpt2::qk_matmul_col", "gpt2::cipher_plain_128_128",
                 "gpt2::bootstrap", "gpt2::init_bootstrap", "gpt2::computeMax", "gpt2::quickMax",
-                "gpt2::compute_softmax"):
+                "gpt2::compute_softmax", "gpt2::pack_tight", "gpt2::unpack_tight", "gpt2::expand_bias",
+                "gpt2::expand_bias_head_row", "gpt2::expand_bias_head_col", "gpt2::augment_value_row",
+                "gpt2::augment_value_col", "gpt2::attentionLayer", "gpt2::FeedForwardLayer",
+                "gpt2::transformer_block", "gpt2::layer_norm_rows", "gpt2::compute_softmax_rows",
+                "gpt2::compute_gelu_block", "gpt2::qk_heads", "gpt2::sv_heads", "gpt2::attn_proj_heads"):
         assert sym in out, sym
 
 
@@ -52,3 +56,60 @@ def test_gpt2_attention_matmuls():
     print(r.stdout)
     print(r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+# ----------------------------------------------------------------------------- the block (C5)
+BLOCK_DIR = os.path.join(ROOT, "tests", "golden", "gpt2_block")
+
+
+def _fixture_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("gpt2_block_fixture", os.path.join(BLOCK_DIR, "make_fixture.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_block_fixture_regenerates_bit_identically(tmp_path):
+    """The committed block.bin / block.txt are exactly what make_fixture.py writes."""
+    m = _fixture_module()
+    m.write(str(tmp_path))
+    for name in ("block.bin", "block.txt"):
+        with open(os.path.join(BLOCK_DIR, name), "rb") as a, open(os.path.join(tmp_path, name), "rb") as b:
+            assert a.read() == b.read(), name
+
+
+def test_block_restatement_against_exact_math():
+    """The restated block (the approximations the encrypted path evaluates) stays close to the exact
+    GPT-2 block on the fixture: layer norm to 1e-6, softmax rows summing to 1 within 1e-2, the block
+    output within 0.05 (the approximation error of exp / quickMax / GELU pieces, reported)."""
+    import numpy as np
+
+    m = _fixture_module()
+    items, ranges = m.arrays()
+    d = dict(items)
+    x, w = m.make_inputs()
+    mu = x.mean(1, keepdims=True)
+    ln1 = (x - mu) / np.sqrt(((x - mu) ** 2).mean(1, keepdims=True)) * w["ln1_g"] + w["ln1_b"]
+    assert np.abs(d["ln1"] - ln1).max() < 1e-6
+    assert np.abs(d["y"] - d["y_exact"]).max() < 0.05
+    # every value the encrypted path bootstraps or feeds a sign stays in range
+    assert 0.4 < ranges["var1"][0] and ranges["var1"][1] < 2.0 and 0.4 < ranges["var2"][0] and ranges["var2"][1] < 2.0
+    assert ranges["scores"] <= 5.0 + 1e-9 and -5.0 < ranges["hidden"][0] and ranges["hidden"][1] < 6.0
+    keep = np.tril(np.ones((m.T, m.T)))
+    s = d["q"][:, :m.DH] @ d["k"][:, :m.DH].T / np.sqrt(m.DH)
+    p, _ = m.softmax_rows_slots(s * keep + m.MASKED_SCORE * (1 - keep), keep)
+    assert np.abs(p.sum(1) - 1).max() < 1e-2 and np.all(p[keep == 0] == 0)
+
+
+@pytest.mark.gpu
+def test_gpt2_block_end_to_end():
+    """GPU: packing helpers, KV cache, each block piece and the whole block (real bootstrapping)
+    against the committed restatement, every stage within 1e-3 (tests/cpp/gpt2_block_test.cpp)."""
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "gpt2_block_test"), BLOCK_DIR], capture_output=True, text=True,
+                       timeout=600, cwd=ROOT)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
