@@ -47,9 +47,9 @@ def test_gpt2_approximations_end_to_end():
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.environ.get("MHE_LONG"), reason="about 3 minutes of on-the-spot keygen; set MHE_LONG=1")
 def test_gpt2_attention_matmuls():
-    """qk_matmul / sv_matmul (MatrixMul.cpp:480-584): 16384 + 8192 surefire_rotate keys."""
+    """qk_matmul / sv_matmul (MatrixMul.cpp:480-584): 16384 + 8192 surefire_rotate placements on
+    6-limb inputs (about a minute with the rest of gpt2_test)."""
     _build()
     env = dict(os.environ, GPT2_QKV="1")
     r = subprocess.run([os.path.join(ROOT, "build", "gpt2_test")], capture_output=True, text=True, timeout=900, env=env)
