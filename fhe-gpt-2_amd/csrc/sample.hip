@@ -42,7 +42,34 @@ struct LimbMap
     int prime[64]; // context prime index of limb l
 };
 
-// 64-byte stream block `blk` (= byte offset / 64) of the PRNG seeded with `s`
+// Every 64-byte block of a 4096-byte buffer is one compression of that buffer's XOF root, and a
+// root costs two compressions, so a workgroup first computes the roots of the buffers its blocks
+// fall in (threads 0 .. nb-1, into LDS) and every block then costs one compression.
+constexpr int kMaxRoots = 8;
+
+// roots of buffers [c0, c0 + nb) (nb <= kMaxRoots) into `roots`; a workgroup-wide barrier follows
+__device__ __forceinline__ void load_roots(const Seed &s, u64 c0, int nb, u64 (*roots)[8])
+{
+    if ((int)threadIdx.x < nb)
+    {
+        u64 r[8];
+        b2b::xof_root(s.w, c0 + threadIdx.x, b2b::kPrngBuffer, r);
+#pragma unroll
+        for (int k = 0; k < 8; k++) roots[threadIdx.x][k] = r[k];
+    }
+    __syncthreads();
+}
+
+// stream block `blk` from the workgroup's roots (buffer blk >> 6 must be in [c0, c0 + nb))
+__device__ __forceinline__ void block_from_roots(const u64 (*roots)[8], u64 c0, u64 blk, u64 (&out)[8])
+{
+    u64 r[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) r[k] = roots[(blk >> 6) - c0][k];
+    b2b::xof_block(r, (u32)(blk & 63), b2b::kPrngBuffer, 64, out);
+}
+
+// 64-byte stream block `blk` (= byte offset / 64) of the PRNG seeded with `s` (root included)
 __device__ __forceinline__ void stream_block(const Seed &s, u64 blk, u64 (&out)[8])
 {
     u64 root[8];
@@ -50,15 +77,19 @@ __device__ __forceinline__ void stream_block(const Seed &s, u64 blk, u64 (&out)[
     b2b::xof_block(root, (u32)(blk & 63), b2b::kPrngBuffer, 64, out);
 }
 
-// Bulk of sample_poly_uniform over `limbs` limbs: one thread per 64-byte block (8 words).
-__global__ void k_prng_uniform(Seed s, LimbMap map, u64 *out, const PrimeDev *primes, int limbs, int log_n,
-                               u64 *rej, u32 *rej_count, u32 rej_cap)
+// Bulk of sample_poly_uniform over `limbs` limbs: one thread per 64-byte block (8 words), a
+// workgroup's 256 blocks in 4 buffers.
+__global__ __launch_bounds__(256) void k_prng_uniform(Seed s, LimbMap map, u64 *out, const PrimeDev *primes, int limbs,
+                                                      int log_n, u64 *rej, u32 *rej_count, u32 rej_cap)
 {
-    const u64 blk = (u64)blockIdx.x * 256 + threadIdx.x;
+    __shared__ u64 roots[kMaxRoots][8];
+    const u64 b0 = (u64)blockIdx.x * 256, blk = b0 + threadIdx.x;
     const u64 total = (u64)limbs << log_n;
+    const u64 last = ((total / 8 < b0 + 256) ? total / 8 : b0 + 256) - 1;
+    load_roots(s, b0 >> 6, (int)((last >> 6) - (b0 >> 6) + 1), roots);
     if (blk * 8 >= total) return;
     u64 w[8];
-    stream_block(s, blk, w);
+    block_from_roots(roots, b0 >> 6, blk, w);
 #pragma unroll
     for (int k = 0; k < 8; k++)
     {
@@ -86,13 +117,19 @@ __global__ void k_prng_apply(const u64 *fix, u32 count, u64 *out)
 // sample_poly_ternary: coefficients [0, n) from the stream bytes at byte offset `off` (64-aligned),
 // 16 coefficients (one block) per thread.  A zero word would be redrawn (Lemire); those are
 // counted in state[1] and k_prng_ternary_fix redoes the poly sequentially.
-__global__ void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs, int log_n, u32 *state)
+__global__ __launch_bounds__(256) void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs,
+                                                      int log_n, u32 *state)
 {
+    __shared__ u64 roots[kMaxRoots][8];
     const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
     const u64 n = (u64)1 << log_n;
+    const u64 first = (off >> 6) + (u64)blockIdx.x * 256;
+    const u64 nblk = n / 16, wg_end = ((u64)blockIdx.x * 256 + 256 < nblk ? (u64)blockIdx.x * 256 + 256 : nblk);
+    const u64 last = (off >> 6) + wg_end - 1;
+    load_roots(s, first >> 6, (int)((last >> 6) - (first >> 6) + 1), roots);
     if (t * 16 >= n) return;
     u64 w[8];
-    stream_block(s, (off >> 6) + t, w);
+    block_from_roots(roots, first >> 6, (off >> 6) + t, w);
 #pragma unroll
     for (int k = 0; k < 16; k++)
     {
@@ -148,36 +185,41 @@ __global__ void k_prng_ternary_fix(Seed s, u64 off, u64 *out, const PrimeDev *pr
 }
 
 // sample_poly_cbd: coefficients [0, n) from the bytes at offset off + (*extra when given), a
-// multiple of 4; 32 coefficients (192 bytes, 3-4 blocks) per thread.
-__global__ void k_prng_cbd(Seed s, u64 off, const u32 *extra, u64 *out, const PrimeDev *primes, int limbs, int log_n)
+// multiple of 4.  A workgroup owns kCbdCoeffs coefficients (6 bytes each): it computes the roots
+// of the <= 3 buffers and the <= 97 stream blocks those bytes span into LDS (one compression per
+// block), then every thread forms 4 coefficients from LDS.
+constexpr int kCbdCoeffs = 1024;
+constexpr int kCbdBlocks = (6 * kCbdCoeffs) / 64 + 1;
+__global__ __launch_bounds__(256) void k_prng_cbd(Seed s, u64 off, const u32 *extra, u64 *out, const PrimeDev *primes,
+                                                  int limbs, int log_n)
 {
-    const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+    __shared__ u64 roots[kMaxRoots][8];
+    __shared__ u64 bytes[kCbdBlocks * 8];
     const u64 n = (u64)1 << log_n;
-    if (t * 32 >= n) return;
-    const int cnt = (int)((n - t * 32) < 32 ? (n - t * 32) : 32);
-    const u64 start = off + (extra ? extra[0] : 0) + 192 * t;
+    const u64 c0 = (u64)blockIdx.x * kCbdCoeffs;
+    const u64 cnt = (n - c0) < (u64)kCbdCoeffs ? (n - c0) : (u64)kCbdCoeffs;
+    const u64 start = off + (extra ? extra[0] : 0) + 6 * c0;
     const u64 b0 = start >> 6, b1 = (start + 6 * cnt - 1) >> 6;
-    u64 w[32];
+    load_roots(s, b0 >> 6, (int)((b1 >> 6) - (b0 >> 6) + 1), roots);
+    if (threadIdx.x <= b1 - b0)
     {
-        u64 b[8];
-        for (u64 j = 0; j <= b1 - b0; j++)
-        {
-            stream_block(s, b0 + j, b);
+        u64 w[8];
+        block_from_roots(roots, b0 >> 6, b0 + threadIdx.x, w);
 #pragma unroll
-            for (int k = 0; k < 8; k++) w[8 * j + k] = b[k];
-        }
+        for (int k = 0; k < 8; k++) bytes[threadIdx.x * 8 + k] = w[k];
     }
+    __syncthreads();
     const u32 skip = (u32)(start - 64 * b0);
     auto byte_at = [&](u32 i) -> u32 {
         i += skip;
-        return (u32)(w[i >> 3] >> (8 * (i & 7))) & 0xff;
+        return (u32)(bytes[i >> 3] >> (8 * (i & 7))) & 0xff;
     };
-    for (int k = 0; k < cnt; k++)
+    for (u32 k = threadIdx.x; k < cnt; k += 256)
     {
-        const u32 c0 = 6 * k;
-        const int noise = __popc(byte_at(c0)) + __popc(byte_at(c0 + 1)) + __popc(byte_at(c0 + 2) & 0x1f) -
-                          __popc(byte_at(c0 + 3)) - __popc(byte_at(c0 + 4)) - __popc(byte_at(c0 + 5) & 0x1f);
-        const u64 i = t * 32 + k;
+        const u32 c = 6 * k;
+        const int noise = __popc(byte_at(c)) + __popc(byte_at(c + 1)) + __popc(byte_at(c + 2) & 0x1f) -
+                          __popc(byte_at(c + 3)) - __popc(byte_at(c + 4)) - __popc(byte_at(c + 5) & 0x1f);
+        const u64 i = c0 + k;
         for (int l = 0; l < limbs; l++)
         {
             const u64 q = primes[l].q;
@@ -255,7 +297,7 @@ MHE_EXPORT int mhe_prng_small(mhe_ctx *c, const uint64_t seed[8], uint64_t byte_
                            state_dev);
     }
     else if (kind == MHE_SAMPLE_CBD)
-        hipLaunchKernelGGL(k_prng_cbd, dim3((unsigned)((n / 32 + 255) / 256)), dim3(256), 0, st, s, byte_offset,
+        hipLaunchKernelGGL(k_prng_cbd, dim3((unsigned)((n + kCbdCoeffs - 1) / kCbdCoeffs)), dim3(256), 0, st, s, byte_offset,
                            (const u32 *)state_dev, out, primes, limbs, log_n);
     else
         return mhe_internal_fail(MHE_ERR_ARG, "unknown distribution");
