@@ -1737,6 +1737,21 @@ MHE_EXPORT int mhe_stream_sync(mhe_ctx *c, void *stream)
     return MHE_OK;
 }
 
+MHE_EXPORT int mhe_stream_wait(mhe_ctx *c, void *waiter, void *waitee)
+{
+    // device-side ordering: work enqueued on `waiter` after this call starts after everything
+    // enqueued on `waitee` before it (no host blocking)
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    if (waiter == waitee) return MHE_OK;
+    hipEvent_t ev;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, S(waitee));
+    if (e == hipSuccess) e = hipStreamWaitEvent(S(waiter), ev, 0);
+    (void)hipEventDestroy(ev); // released by the runtime once the recorded work completes
+    if (e != hipSuccess) return fail(MHE_ERR_DEVICE, hipGetErrorString(e));
+    return MHE_OK;
+}
+
 static int check_poly_args(mhe_ctx *c, const void *a, int polys, int limbs)
 {
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");

@@ -8,6 +8,7 @@
 //   context.cpp (modulus switching chain), ciphertext.h, plaintext.h, keygenerator.cpp,
 //   encryptor.cpp:88-166, decryptor.cpp (ckks_decrypt), ckks.h/ckks.cpp (CKKSEncoder),
 //   evaluator.cpp (all Evaluator entry points; line numbers cited per method).
+#include "stream_order.h"
 #include "seal/seal.h"
 
 #include "../../include/mhe.h"
@@ -285,20 +286,17 @@ void *PolyStore::thread_stream() const
     return SEALContext::stream_of(hold_.get());
 }
 
+// Cross-stream ordering (stream_order.h): device-side waits, no host blocking.
 void PolyStore::wait_writer(void *s) const
 {
-    if (writer_ && writer_ != s && !writer_done_)
-    {
-        chk(mhe_stream_sync(eng_, writer_));
-        writer_done_ = true;
-    }
+    for (void *w : detail::order_before<void *>(s, writer_, writer_done_, {}, detail::Access::read))
+        chk(mhe_stream_wait(eng_, s, w));
 }
 
 void PolyStore::wait_all(void *s) const
 {
-    wait_writer(s);
-    for (void *r : readers_)
-        if (r != s) chk(mhe_stream_sync(eng_, r));
+    for (void *w : detail::order_before<void *>(s, writer_, writer_done_, readers_, detail::Access::write))
+        chk(mhe_stream_wait(eng_, s, w));
     readers_.clear();
 }
 
@@ -308,8 +306,8 @@ void PolyStore::release()
     {
         std::lock_guard<std::mutex> g(*mu_);
         void *s = writer_ ? writer_ : thread_stream();
-        for (void *r : readers_)
-            if (r != s) (void)mhe_stream_sync(eng_, r);
+        for (void *w : detail::order_before<void *>(s, writer_, writer_done_, readers_, detail::Access::release))
+            (void)mhe_stream_wait(eng_, s, w);
         (void)mhe_free_async(eng_, dev_, s);
     }
     dev_ = nullptr;
@@ -390,8 +388,11 @@ const std::uint64_t *PolyStore::dev_read(void *s) const
         writer_ = s;
         writer_done_ = true;
     }
-    wait_writer(s);
-    if (writer_ != s && std::find(readers_.begin(), readers_.end(), s) == readers_.end()) readers_.push_back(s);
+    if (writer_ != s && std::find(readers_.begin(), readers_.end(), s) == readers_.end())
+    {
+        wait_writer(s); // once per (write, reading stream): the stream is then ordered after it
+        readers_.push_back(s);
+    }
     return dev_;
 }
 

@@ -69,6 +69,9 @@ int mhe_memcpy_h2d(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void 
 int mhe_memcpy_d2h(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int mhe_memcpy_d2d(mhe_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 int mhe_stream_sync(mhe_ctx *ctx, void *stream);
+/* Device-side ordering without host blocking: work enqueued on `waiter` after the call runs after
+ * everything already enqueued on `waitee` (event record + stream wait). */
+int mhe_stream_wait(mhe_ctx *ctx, void *waiter, void *waitee);
 /* A non-blocking HIP stream on the context's device (and its scratch workspace); the SEAL
  * shim gives every host thread its own, as the reference's OpenMP threads share one
  * Evaluator (cnn/infer_seal.cpp:404). */

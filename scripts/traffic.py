@@ -2,7 +2,7 @@
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half the bytes of a
 wide coalesced read -- calibrated here on k_ks_mac (known 2970 MiB read per launch) -- so
-bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024.  Usage: traffic.py <pmc_dir> <hmults_in_run> [out.json]
+bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024.  Usage: traffic.py <pmc_dir> <hmults_in_run | auto> [out.json]
 """
 import collections
 import csv
@@ -10,7 +10,17 @@ import glob
 import json
 import sys
 
-pmc_dir, hmults = sys.argv[1], int(sys.argv[2])
+pmc_dir = sys.argv[1]
+if sys.argv[2] == "auto":
+    # one k_ks_row_mac dispatch per HMult
+    ids = set()
+    for f in glob.glob(f"{pmc_dir}/FETCH_SIZE/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_ks_row_mac" in r["Kernel_Name"]:
+                ids.add(r.get("Dispatch_Id", len(ids)))
+    hmults = max(1, len(ids))
+else:
+    hmults = int(sys.argv[2])
 tot = collections.defaultdict(float)
 per_kernel = collections.defaultdict(lambda: collections.defaultdict(float))
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
