@@ -768,4 +768,63 @@ private:
 extern template void Evaluator::multiply_vector_inplace<double>(Ciphertext &, const std::vector<double> &) const;
 extern template void Evaluator::multiply_vector_inplace<std::complex<double>>(
     Ciphertext &, const std::vector<std::complex<double>> &) const;
+// seal::util::iter -- the iterator helpers the reference's bootstrapper uses for coefficient access
+// (modraise_inplace, BOOT/Bootstrapper.cpp:2894-2948; SEAL/util/iterator.h): iter(ciphertext)[poly]
+// [limb][coeff] over the host mirror (non-const access marks the device copy stale, so the next GPU
+// operation uploads it), iter(plaintext)[limb][coeff], and iter(coeff_modulus)[j].
+namespace util
+{
+template <class T>
+class CoeffIterT
+{
+public:
+    explicit CoeffIterT(T *p) : p_(p) {}
+    T &operator[](std::size_t i) const { return p_[i]; }
+    T *ptr() const noexcept { return p_; }
+    operator T *() const noexcept { return p_; }
+
+private:
+    T *p_;
+};
+template <class T>
+class RNSIterT
+{
+public:
+    RNSIterT(T *p, std::size_t n) : p_(p), n_(n) {}
+    CoeffIterT<T> operator[](std::size_t limb) const { return CoeffIterT<T>(p_ + limb * n_); }
+    std::size_t poly_modulus_degree() const noexcept { return n_; }
+
+private:
+    T *p_;
+    std::size_t n_;
+};
+template <class T>
+class PolyIterT
+{
+public:
+    PolyIterT(T *p, std::size_t n, std::size_t limbs) : p_(p), n_(n), limbs_(limbs) {}
+    RNSIterT<T> operator[](std::size_t poly) const { return RNSIterT<T>(p_ + poly * limbs_ * n_, n_); }
+    std::size_t coeff_modulus_size() const noexcept { return limbs_; }
+
+private:
+    T *p_;
+    std::size_t n_, limbs_;
+};
+using CoeffIter = CoeffIterT<std::uint64_t>;
+using ConstCoeffIter = CoeffIterT<const std::uint64_t>;
+using RNSIter = RNSIterT<std::uint64_t>;
+using ConstRNSIter = RNSIterT<const std::uint64_t>;
+using PolyIter = PolyIterT<std::uint64_t>;
+using ConstPolyIter = PolyIterT<const std::uint64_t>;
+
+inline PolyIter iter(Ciphertext &c)
+{
+    return PolyIter(c.data(), c.poly_modulus_degree(), c.coeff_modulus_size());
+}
+inline ConstPolyIter iter(const Ciphertext &c)
+{
+    return ConstPolyIter(c.data(), c.poly_modulus_degree(), c.coeff_modulus_size());
+}
+inline const std::vector<Modulus> &iter(const std::vector<Modulus> &coeff_modulus) { return coeff_modulus; }
+} // namespace util
 } // namespace seal

@@ -61,6 +61,59 @@ int main(int argc, char **argv)
     std::printf("setup (polynomials, %zu Galois steps, LT coefficients): %.2f s\n", steps.size(),
                 std::chrono::duration<double>(t1 - t0).count());
 
+    int fail = 0;
+    {
+        // modraise_inplace written against the surface's seal::util::iter, as the reference writes it
+        // (BOOT/Bootstrapper.cpp:2894-2948: centred lift of the one-limb coefficients to every prime
+        // of the first level), against the Bootstrapper's GPU version: every word equal
+        std::vector<double> v(1 << (logN - 1));
+        std::mt19937_64 gg(5);
+        std::uniform_real_distribution<double> UU(-1, 1);
+        for (auto &x : v) x = UU(gg);
+        Plaintext p;
+        encoder.encode(v, scale, p);
+        Ciphertext a;
+        encryptor.encrypt(p, a);
+        evaluator.mod_switch_to_inplace(a, context.last_parms_id());
+        Ciphertext b = a;
+        bt.modraise_inplace(b);
+        {
+            using seal::util::iter;
+            if (a.is_ntt_form()) evaluator.transform_from_ntt_inplace(a);
+            Ciphertext src(a);
+            a.resize(context, context.first_parms_id(), 2);
+            const auto &modulus = iter(context.first_context_data()->parms().coeff_modulus());
+            const std::size_t L = a.coeff_modulus_size(), N = a.poly_modulus_degree();
+            const std::uint64_t q0 = modulus[0].value();
+            for (std::size_t k = 0; k < a.size(); k++)
+            {
+                const auto s0 = iter(static_cast<const Ciphertext &>(src))[k][0];
+                const auto dst = iter(a)[k];
+                for (std::size_t j = 0; j < L; j++)
+                {
+                    const std::uint64_t q = modulus[j].value(), mq0 = j ? q - q0 % q : 0;
+                    for (std::size_t i = 0; i < N; i++)
+                    {
+                        std::uint64_t x = s0[i] % q;
+                        if (s0[i] > (q0 >> 1))
+                        {
+                            x += mq0;
+                            x -= x >= q ? q : 0;
+                        }
+                        dst[j][i] = x;
+                    }
+                }
+            }
+            evaluator.transform_to_ntt_inplace(a);
+        }
+        std::size_t diff = 0;
+        const std::uint64_t *x = a.data(), *y = b.data();
+        for (std::size_t w = 0; w < a.dyn_array_size(); w++) diff += x[w] != y[w];
+        std::printf("modraise via seal::util::iter vs Bootstrapper::modraise_inplace: %zu of %zu words differ (%zu limbs)\n",
+                    diff, a.dyn_array_size(), a.coeff_modulus_size());
+        if (diff || a.dyn_array_size() != b.dyn_array_size()) fail++;
+    }
+
     const long n = 1L << logn, Nh = 1L << (logN - 1);
     std::mt19937_64 g(2026);
     std::uniform_real_distribution<double> U(-1, 1);
@@ -74,7 +127,6 @@ int main(int argc, char **argv)
     evaluator.mod_switch_to_inplace(ct, context.last_parms_id());
     std::printf("input: %zu limb(s), scale 2^%.2f\n", ct.coeff_modulus_size(), std::log2(ct.scale()));
 
-    int fail = 0;
     if (argc > 3)
     {
         // stage-by-stage checks on fresh encryptions
