@@ -26,6 +26,28 @@
 #include "fparith.h"
 
 
+// Streaming (non-temporal) access for the key-switch streams, selected at build time (MHE_NT bit 0:
+// ModUp intermediate stores, bit 1: key loads, bit 2: intermediate loads in the fused MAC).
+#ifndef MHE_NT
+#define MHE_NT 5 // measured: +5% HMult/s (scripts/gpu_nt.sh; key loads NT lost 5%)
+#endif
+template <int BIT, class T>
+__device__ __forceinline__ void st_nt(T *p, T v)
+{
+    if constexpr ((MHE_NT >> BIT) & 1)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+template <int BIT, class T>
+__device__ __forceinline__ T ld_nt(const T *p)
+{
+    if constexpr ((MHE_NT >> BIT) & 1)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
 // Forward Harvey butterfly (dwthandler.h:122-125 with ntt.h:34-65 arithmetic).
 __device__ __forceinline__ void fwd_bfly(u64 &x, u64 &y, const Tw w, u64 q, u64 q2)
 {
@@ -428,7 +450,7 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
                                    [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
             u64 *dst = modup + (((size_t)(I - I0) * L + J) << log_n);
 #pragma unroll
-            for (int e = 0; e < E; e++) dst[c + ((u32)(E * t + e) << logC)] = ar.out(v[e]);
+            for (int e = 0; e < E; e++) st_nt<0>(&dst[c + ((u32)(E * t + e) << logC)], ar.out(v[e]));
             __syncthreads(); // lds is rewritten by the next output prime
         }
     };
@@ -674,8 +696,8 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
 #pragma unroll
             for (int e = 0; e < 8; e++)
             {
-                ka[e] = k0[lay(t, e, B_A)];
-                kb[e] = k1[lay(t, e, B_A)];
+                ka[e] = ld_nt<1>(&k0[lay(t, e, B_A)]);
+                kb[e] = ld_nt<1>(&k1[lay(t, e, B_A)]);
             }
         };
         u64 kk0[8], kk1[8];
@@ -691,7 +713,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
             {
                 const u64 *src = digit_src(J + 1);
 #pragma unroll
-                for (int e = 0; e < 8; e++) vnext[e] = src[lay(t, e, B_A)];
+                for (int e = 0; e < 8; e++) vnext[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
             }
             T d[8]; // the digit in the coalesced layout, NTT form
             if (J != I)

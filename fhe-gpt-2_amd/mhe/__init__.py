@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "libmhe.so")
+LIB_PATH = os.environ.get("MHE_LIB_PATH") or os.path.join(_PKG, "libmhe.so")  # override: build experiments
 _lib = None
 
 u64p = ctypes.POINTER(ctypes.c_uint64)
