@@ -467,7 +467,10 @@ template <int LOGR, bool FP>
 static inline void modup_col_a(const u64 *coeff, u64 *modup, const PrimeDev *primes, const Tw *tw, int L, int K,
                                int log_n, long long twd, int I0, int Icnt, int IG, hipStream_t st)
 {
-    constexpr int LOGT = LOGR <= 7 ? 3 : 4;
+#ifndef MHE_MODUP_LOGT8
+#define MHE_MODUP_LOGT8 4
+#endif
+    constexpr int LOGT = LOGR <= 7 ? 3 : MHE_MODUP_LOGT8;
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
     hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3(subs / SH::S, L, IG), dim3(256), 0, st, coeff, modup,
