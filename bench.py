@@ -152,7 +152,9 @@ def resnet_leg(device, images, streams, layers=20):
     info = runner.info()
     rng = np.random.default_rng(1000 + rank)
     imgs = rng.uniform(-2.5, 2.5, size=(images, 3072))
+    runner.key_traffic(reset=True)
     one = runner.infer_batch(imgs[:1], 1)
+    key_bytes = runner.key_traffic(reset=True)  # key-switching key bytes of one image
     if world > 1:
         dist.barrier()
     t2 = time.perf_counter()
@@ -173,6 +175,16 @@ def resnet_leg(device, images, streams, layers=20):
         "galois_keys": info["galois_keys"],
         "galois_key_GB_resident": round(info["galois_key_gb"], 2),
         "key_H2D_GB_per_image": 0.0,
+        # ResNet roofline: the key-switching key bytes one image streams (the algorithmic bytes of its
+        # dominant work, every key switch reading its L x 2 x (L+1)-limb key slice) over its 1-stream time
+        "roofline": {
+            "bound": "hbm",
+            "key_bytes_per_image": key_bytes,
+            "achieved": round(key_bytes / float(one["seconds"][0]) / 1e9, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(key_bytes / float(one["seconds"][0]) / 1e9 / HBM_PEAK_GBS, 4),
+        },
         "key_sharing": shared if shared else "single GPU: keys generated here",
         "labels": [int(x) for x in batch["labels"]],
         "reference_cpu_sec_per_image": RESNET20_CPU_S if layers == 20 else None,

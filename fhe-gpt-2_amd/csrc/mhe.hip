@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <string>
@@ -184,6 +185,7 @@ enum TimedKernel
 
 struct mhe_ctx
 {
+    std::atomic<unsigned long long> key_bytes{ 0 }; // key-switching key bytes read since reset (mhe_key_traffic)
     int device = 0;
     int log_n = 0;
     size_t n = 0;
@@ -1149,6 +1151,8 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
                           hipStream_t st, u64 *rescale_out = nullptr)
 {
     if (key_limbs < L + 1 || key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
+    // the key slice one switch streams: L digits x 2 polys x (L + 1) primes
+    c->key_bytes += 2ull * (unsigned long long)L * (unsigned long long)(L + 1) * c->n * 8ull;
     Workspace *w;
     int r = get_ws(c, st, c->K - 1, &w);
     if (r) return r;
@@ -1734,6 +1738,13 @@ MHE_EXPORT int mhe_stream_sync(mhe_ctx *c, void *stream)
 {
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
     HIP_TRY(hipStreamSynchronize(S(stream)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_key_traffic(mhe_ctx *c, uint64_t *bytes, int reset)
+{
+    if (!valid_ctx(c) || !bytes) return fail(MHE_ERR_ARG, "invalid argument");
+    *bytes = reset ? c->key_bytes.exchange(0) : c->key_bytes.load();
     return MHE_OK;
 }
 

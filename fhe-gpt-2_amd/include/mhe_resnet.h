@@ -78,6 +78,8 @@ public:
     std::size_t galois_keys() const { return galois_keys_; }
     // device bytes of the server's Galois key set (all resident in HBM: no key traffic per image)
     double galois_key_gb() const;
+    // key-switching key bytes streamed by this runner's key switches since the last reset
+    double key_traffic_bytes(bool reset);
 
     // key buffers as device memory, for sharing one key set across GPUs: kind 0 secret key [K][n],
     // 1 public key [2][K][n], 2 relinearization key [K-1][2][K][n], 3 Galois key `index` with

@@ -39,6 +39,7 @@ def seal_lib():
             "mhe_resnet_finish_import": (i32, [vp]),
             "mhe_resnet_infer_batch": (i32, [vp, dp, i32, i32, dp, ip, dp, dp, dp, dp]),
             "mhe_resnet_info": (i32, [vp, dp, dp, ip]),
+            "mhe_resnet_key_traffic": (i32, [vp, dp, i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -109,6 +110,12 @@ class Runner:
             labels.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), sec.ctypes.data_as(dp), boot.ctypes.data_as(dp),
             relu.ctypes.data_as(dp), ctypes.byref(wall)))
         return {"logits": logits, "labels": labels, "seconds": sec, "boot": boot, "relu": relu, "wall": wall.value}
+
+    def key_traffic(self, reset=False):
+        """Key-switching key bytes streamed since the last reset."""
+        b = ctypes.c_double()
+        _check(seal_lib().mhe_resnet_key_traffic(self._h, ctypes.byref(b), 1 if reset else 0))
+        return b.value
 
     def info(self):
         s, gb, nk = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()

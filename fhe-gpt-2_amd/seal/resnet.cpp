@@ -2,6 +2,8 @@
 // cnn_ckks/cpu-ckks/single-key/cnn/infer_seal.cpp over the seal:: surface.
 #include "mhe_resnet.h"
 
+#include "../../include/mhe.h"
+
 #include <atomic>
 #include <chrono>
 #include <exception>
@@ -370,6 +372,13 @@ ResNetRunner::~ResNetRunner() = default;
 double ResNetRunner::galois_key_gb() const
 {
     return impl_->gal_keys.device_bytes() / 1e9;
+}
+
+double ResNetRunner::key_traffic_bytes(bool reset)
+{
+    std::uint64_t b = 0;
+    if (mhe_key_traffic(impl_->context->engine(), &b, reset ? 1 : 0) != 0) throw std::runtime_error(mhe_last_error());
+    return (double)b;
 }
 
 ResNetResult ResNetRunner::infer(const std::vector<double> &img)

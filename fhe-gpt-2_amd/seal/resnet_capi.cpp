@@ -133,6 +133,14 @@ int mhe_resnet_infer_batch(mhe_resnet *r, const double *images, int count, int t
     });
 }
 
+int mhe_resnet_key_traffic(mhe_resnet *r, double *bytes, int reset)
+{
+    return guard([&] {
+        const double b = r->runner->key_traffic_bytes(reset != 0);
+        if (bytes) *bytes = b;
+    });
+}
+
 int mhe_resnet_info(mhe_resnet *r, double *setup_s, double *gb, int *nkeys)
 {
     return guard([&] {

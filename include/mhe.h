@@ -72,6 +72,9 @@ int mhe_stream_sync(mhe_ctx *ctx, void *stream);
 /* Device-side ordering without host blocking: work enqueued on `waiter` after the call runs after
  * everything already enqueued on `waitee` (event record + stream wait). */
 int mhe_stream_wait(mhe_ctx *ctx, void *waiter, void *waitee);
+/* Key-switching key bytes streamed by the key switches run on the context since the last reset
+ * (L digits x 2 x (L+1) primes x n x 8 per switch): the algorithmic key traffic of a workload. */
+int mhe_key_traffic(mhe_ctx *ctx, uint64_t *bytes, int reset);
 /* A non-blocking HIP stream on the context's device (and its scratch workspace); the SEAL
  * shim gives every host thread its own, as the reference's OpenMP threads share one
  * Evaluator (cnn/infer_seal.cpp:404). */

@@ -41,6 +41,8 @@ int mhe_resnet_finish_import(mhe_resnet *runner);
 int mhe_resnet_infer_batch(mhe_resnet *runner, const double *images, int count, int threads, double *logits,
                            int *labels, double *seconds, double *boot, double *relu, double *wall);
 int mhe_resnet_info(mhe_resnet *runner, double *setup_s, double *galois_key_gb, int *galois_keys);
+/* key-switching key bytes the runner's key switches streamed since the last reset (reset != 0 zeroes) */
+int mhe_resnet_key_traffic(mhe_resnet *runner, double *bytes, int reset);
 
 #ifdef __cplusplus
 }
