@@ -768,6 +768,25 @@ __global__ void k_mulplain(const u64 *a, const u64 *b, u64 *out, const PrimeDev 
     *(ulonglong2 *)(out + i) = r;
 }
 
+// acc += a * b, b broadcast over polys (multiply_plain_ntt then add_inplace, one pass)
+__global__ void k_mulplain_add(const u64 *a, const u64 *b, u64 *acc, const PrimeDev *primes, int limbs, int log_n,
+                               size_t total2)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 >= total2) return;
+    const size_t i = i2 * 2;
+    const size_t limb_words = (size_t)limbs << log_n;
+    const int l = (int)((i >> log_n) % limbs);
+    const PrimeDev p = primes[l];
+    ulonglong2 x = *(const ulonglong2 *)(a + i);
+    ulonglong2 y = *(const ulonglong2 *)(b + i % limb_words);
+    ulonglong2 z = *(const ulonglong2 *)(acc + i);
+    ulonglong2 r;
+    r.x = addmod(z.x, mulmod(x.x, y.x, p), p.q);
+    r.y = addmod(z.y, mulmod(x.y, y.y, p), p.q);
+    *(ulonglong2 *)(acc + i) = r;
+}
+
 struct ScalarTab
 {
     u64 v[64];
@@ -1831,6 +1850,19 @@ MHE_EXPORT int mhe_multiply_plain(mhe_ctx *c, const uint64_t *a, const uint64_t 
     if (!b || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_mulplain, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, out, c->primes, limbs, c->log_n,
+                       total2);
+    HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_multiply_plain_add(mhe_ctx *c, const uint64_t *a, const uint64_t *b, uint64_t *acc, int polys,
+                                      int limbs, void *s)
+{
+    int r = check_poly_args(c, a, polys, limbs);
+    if (r) return r;
+    if (!b || !acc) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
+    hipLaunchKernelGGL(k_mulplain_add, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, acc, c->primes, limbs, c->log_n,
                        total2);
     HIP_LAUNCH_CHECK();
     return MHE_OK;

@@ -215,7 +215,7 @@ public:
 
 private:
     void multiply_diag(seal::Ciphertext &ct, const std::vector<std::complex<double>> &diag, int coeff_logn,
-                       int shift, seal::Ciphertext &dest, double coeff_scale = 1.0);
+                       int shift, seal::Ciphertext &dest, double coeff_scale = 1.0, bool accumulate = false);
     struct PtKey
     {
         const void *diag;

@@ -699,6 +699,9 @@ public:
         multiply_vector_inplace(destination, value);
     }
     void add_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
+    // (not SEAL API) multiply_plain(encrypted, plain, t) + add_inplace_reduced_error(acc, t) for acc at
+    // encrypted's level, fused into one pass with bit-identical output
+    void multiply_plain_add_reduced_error(Ciphertext &acc, const Ciphertext &encrypted, const Plaintext &plain) const;
     void add_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
     {
         // evaluator.h: operands swap when destination aliases encrypted2

@@ -39,6 +39,7 @@ SIGNATURES = {
     "mhe_memcpy_d2d": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
     "mhe_stream_sync": (ctypes.c_int, [vp, vp]),
     "mhe_stream_wait": (ctypes.c_int, [vp, vp, vp]),
+    "mhe_multiply_plain_add": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_traffic": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     "mhe_stream_destroy": (ctypes.c_int, [vp, vp]),

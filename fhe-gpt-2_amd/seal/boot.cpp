@@ -966,7 +966,7 @@ bool pt_cache_on()
 } // namespace
 
 void Bootstrapper::multiply_diag(Ciphertext &ct, const std::vector<cd> &diag, int coeff_logn, int shift,
-                                 Ciphertext &dest, double coeff_scale)
+                                 Ciphertext &dest, double coeff_scale, bool accumulate)
 {
     // rotation(coeff_logn, Nh, shift, diag) + multiply_vector_reduced_error (Bootstrapper.cpp:1983-1984):
     // the diagonal is encoded at ct.scale() on the first level and kept at ct's level
@@ -994,7 +994,11 @@ void Bootstrapper::multiply_diag(Ciphertext &ct, const std::vector<cd> &diag, in
         else
             pt = &local;
     }
-    evaluator.multiply_plain(ct, *pt, dest);
+    // accumulate: dest += ct * pt (the loop's add_inplace_reduced_error fused into the product)
+    if (accumulate)
+        evaluator.multiply_plain_add_reduced_error(dest, ct, *pt);
+    else
+        evaluator.multiply_plain(ct, *pt, dest);
 }
 
 std::size_t Bootstrapper::verify_cache()
@@ -1058,14 +1062,8 @@ void Bootstrapper::bsgs_linear_transform(Ciphertext &rtncipher, Ciphertext &ciph
         for (int j = basicstart1; j <= jlast; j++)
         {
             multiply_diag(babyct[j - basicstart1], fftcoeff[(i * gs1 + j) + totlen], coeff_logn,
-                          (-i) * gs1 * basicstep, tmptmpct, coeff_scale);
-            if (!giantbool)
-            {
-                giantct = tmptmpct;
-                giantbool = true;
-            }
-            else
-                evaluator.add_inplace_reduced_error(giantct, tmptmpct);
+                          (-i) * gs1 * basicstep, giantct, coeff_scale, giantbool);
+            giantbool = true;
         }
         if (i != 0)
         {
@@ -1116,15 +1114,9 @@ void Bootstrapper::rotated_bsgs_linear_transform(Ciphertext &rtncipher, Cipherte
         const int jlast = i != giantlast2 ? gs2 - 1 : totlen - i * gs2;
         for (int j = 0; j <= jlast; j++)
         {
-            multiply_diag(babyct[j], fftcoeff[i * gs2 + j], coeff_logn, (-i) * gs2 * basicstep, tmptmpct,
-                          coeff_scale);
-            if (!giantbool)
-            {
-                giantct = tmptmpct;
-                giantbool = true;
-            }
-            else
-                evaluator.add_inplace_reduced_error(giantct, tmptmpct);
+            multiply_diag(babyct[j], fftcoeff[i * gs2 + j], coeff_logn, (-i) * gs2 * basicstep, giantct,
+                          coeff_scale, giantbool);
+            giantbool = true;
         }
         if (i != 0)
         {

@@ -218,15 +218,18 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
     const int d = static_cast<int>(log2_long(ki)), c = static_cast<int>(log2_long(ti));
     for (int i9 = 0; i9 < q; i9++)
     {
-        // filter taps
+        // filter taps: multiply_vector_reduced_error + add_inplace_reduced_error, the product and the
+        // add fused into one pass (bit-identical; every tap is at the input's level)
         for (int i1 = 0; i1 < fh; i1++)
             for (int i2 = 0; i2 < fw; i2++)
             {
-                evaluator.multiply_vector_reduced_error(*rot[fw * i1 + i2], weight_vec(i1, i2, i9), temp);
+                Ciphertext &tap = *rot[fw * i1 + i2];
+                Plaintext wp;
+                evaluator.encode_vector_for(tap, weight_vec(i1, i2, i9), wp);
                 if (i1 == 0 && i2 == 0)
-                    sum = temp;
+                    evaluator.multiply_plain(tap, wp, sum);
                 else
-                    evaluator.add_inplace_reduced_error(sum, temp);
+                    evaluator.multiply_plain_add_reduced_error(sum, tap, wp);
             }
         evaluator.rescale_to_next_inplace(sum);
         var = sum;

@@ -1939,6 +1939,28 @@ void Evaluator::multiply_const(const Ciphertext &encrypted, double value, Cipher
     destination.scale() = new_scale;
 }
 
+void Evaluator::multiply_plain_add_reduced_error(Ciphertext &acc, const Ciphertext &encrypted,
+                                                 const Plaintext &plain) const
+{
+    // multiply_plain(encrypted, plain, tmp) + add_inplace_reduced_error(acc, tmp) at equal levels,
+    // one kernel (bit-identical): acc takes the product's scale, as the reduced-error add assigns it
+    Level lv = check_ct(context_, encrypted, "encrypted");
+    Level la = check_ct(context_, acc, "encrypted1");
+    if (la.L != lv.L || acc.size() != encrypted.size())
+        throw std::invalid_argument("multiply_plain_add: acc and encrypted must share level and size");
+    if (!encrypted.is_ntt_form() || !plain.is_ntt_form() || !acc.is_ntt_form())
+        throw std::invalid_argument("NTT form mismatch");
+    if (encrypted.parms_id() != plain.parms_id())
+        throw std::invalid_argument("encrypted_ntt and plain_ntt parameter mismatch");
+    const double new_scale = encrypted.scale() * plain.scale();
+    check_scale(new_scale, lv);
+    void *s = context_.stream();
+    const std::uint64_t *b = plain.store().dev_read(s);
+    const std::uint64_t *a = encrypted.store().dev_read(s);
+    chk(mhe_multiply_plain_add(context_.engine(), a, b, acc.store().dev_write(s), (int)encrypted.size(), (int)lv.L, s));
+    acc.scale() = new_scale;
+}
+
 namespace
 {
 template <typename T>

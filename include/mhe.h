@@ -106,6 +106,10 @@ int mhe_negate(mhe_ctx *ctx, const uint64_t *a, uint64_t *out, int polys, int li
  * (evaluator.cpp:1891-1930) when a is a ciphertext and b an NTT plaintext. */
 int mhe_multiply_plain(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *out, int polys, int limbs,
                        void *stream);
+/* acc += a * b (b broadcast over the polys of a): multiply_plain_ntt followed by add_inplace in one
+ * pass, bit-identical to the two (evaluator.cpp:1891-1930, 78-120) */
+int mhe_multiply_plain_add(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *acc, int polys, int limbs,
+                           void *stream);
 /* multiply_poly_scalar_coeffmod with one scalar per limb (scalars[l] < q_l), host array;
  * used by multiply_const (evaluator.cpp:287-301). */
 int mhe_multiply_scalar(mhe_ctx *ctx, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys,

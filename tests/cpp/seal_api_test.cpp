@@ -413,6 +413,19 @@ static void test_reduced_error_ops()
     e.evaluator->rescale_to_next_inplace(vr);
     for (int i = 0; i < 4096; i++) ex[i] = 0.5 * a[i];
     CHECK(max_err(e.dec(vr), ex) < 1e-5);
+    // fused multiply_plain + add_inplace_reduced_error: the same words as the two separate ops
+    {
+        Ciphertext acc1 = e.enc(a, s), acc2 = acc1, c = e.enc(b, s), t;
+        Plaintext pw;
+        e.evaluator->encode_vector_for(c, w, pw);
+        e.evaluator->multiply_plain(c, pw, t);
+        e.evaluator->add_inplace_reduced_error(acc1, t);
+        e.evaluator->multiply_plain_add_reduced_error(acc2, c, pw);
+        const std::uint64_t *p1 = acc1.data(), *p2 = acc2.data();
+        std::size_t diff = 0;
+        for (std::size_t k = 0; k < acc1.dyn_array_size(); k++) diff += p1[k] != p2[k];
+        CHECK(diff == 0 && acc1.scale() == acc2.scale() && acc1.dyn_array_size() == acc2.dyn_array_size());
+    }
 }
 
 static void test_security_level()
