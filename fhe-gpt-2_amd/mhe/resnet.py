@@ -25,7 +25,7 @@ def seal_lib():
     global _seal
     if _seal is None:
         _mhe_lib()
-        L = ctypes.CDLL(os.path.join(os.path.dirname(_HERE), "libmhe_seal.so"))
+        L = ctypes.CDLL(os.environ.get("MHE_SEAL_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "libmhe_seal.so"))
         vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
         dp, ip, u64p = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32), ctypes.POINTER(u64)
         sig = {

@@ -106,17 +106,30 @@ void memory_save_rotate(const Ciphertext &cipher_in, Ciphertext &cipher_out, int
     const long slots = static_cast<long>(cipher_in.poly_modulus_degree() / 2);
     const long s = (steps + slots) % slots; // C++ remainder, as the reference: 0..slots-1 for steps >= -slots
     if (s == 0) return;
-    Ciphertext temp = cipher_in;
+    Ciphertext temp; // out-of-place rotations: no copy of cipher_in
     const bool split = (s >= 34 && s <= 55) || (s >= 57 && s <= 61);
     if (split)
     {
-        evaluator.rotate_vector_inplace(temp, 33, gal_keys);
+        evaluator.rotate_vector(cipher_in, 33, gal_keys, temp);
         evaluator.rotate_vector_inplace(temp, static_cast<int>(s - 33), gal_keys);
     }
     else
-        evaluator.rotate_vector_inplace(temp, static_cast<int>(s), gal_keys);
+        evaluator.rotate_vector(cipher_in, static_cast<int>(s), gal_keys, temp);
     cipher_out = std::move(temp);
 }
+
+namespace
+{
+// `out = in; memory_save_rotate(out, out, steps)` without the copy when the rotation is not zero
+void rotate_copy(const Ciphertext &in, Ciphertext &out, int steps, Evaluator &evaluator, GaloisKeys &gal_keys)
+{
+    const long slots = static_cast<long>(in.poly_modulus_degree() / 2);
+    if ((steps + slots) % slots == 0)
+        out = in;
+    else
+        memory_save_rotate(in, out, steps, evaluator, gal_keys);
+}
+} // namespace
 
 // ------------------------------------------------------------------------ convolution
 void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, int co, int st, int fh,
@@ -204,8 +217,7 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         for (int i2 = 0; i2 < fw; i2++)
         {
             Ciphertext &r = *rot[fw * i1 + i2];
-            r = ctxt_in;
-            memory_save_rotate(r, r, ki * ki * wi * (i1 - ch) + ki * (i2 - cw), evaluator, gal_keys);
+            rotate_copy(ctxt_in, r, ki * ki * wi * (i1 - ch) + ki * (i2 - cw), evaluator, gal_keys);
         }
 
     // encryption of zero at the input scale (cnn_seal.cpp:423-427)
@@ -236,8 +248,7 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
 
         // sum over the input channels held in one replica
         auto fold = [&](long step) {
-            temp = var;
-            memory_save_rotate(temp, temp, static_cast<int>(step), evaluator, gal_keys);
+            rotate_copy(var, temp, static_cast<int>(step), evaluator, gal_keys);
             evaluator.add_inplace_reduced_error(var, temp);
         };
         for (int x = 0; x < d; x++) fold(pow2(x));
@@ -247,8 +258,7 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
             sum = ct_zero;
             for (int x = 0; x < ti; x++)
             {
-                temp = var;
-                memory_save_rotate(temp, temp, ki * ki * hi * wi * x, evaluator, gal_keys);
+                rotate_copy(var, temp, ki * ki * hi * wi * x, evaluator, gal_keys);
                 evaluator.add_inplace_reduced_error(sum, temp);
             }
             var = sum;
@@ -260,8 +270,7 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         for (int i8 = 0; i8 < pi && pi * i9 + i8 < co; i8++)
         {
             const int j4 = pi * i9 + i8;
-            temp = var;
-            memory_save_rotate(temp, temp,
+            rotate_copy(var, temp,
                                (int)((n / pi) * (j4 % pi) - j4 % ko - (j4 / (ko * ko)) * ko * ko * ho * wo -
                                      ((j4 % (ko * ko)) / ko) * ko * wo),
                                evaluator, gal_keys);
@@ -281,8 +290,7 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         sum = ct_zero;
         for (int u6 = 0; u6 < po; u6++)
         {
-            temp = var;
-            memory_save_rotate(temp, temp, static_cast<int>(-u6 * (n / po)), evaluator, gal_keys);
+            rotate_copy(var, temp, static_cast<int>(-u6 * (n / po)), evaluator, gal_keys);
             evaluator.add_inplace_reduced_error(sum, temp);
         }
         var = sum;
@@ -395,8 +403,7 @@ void multiplexed_parallel_downsampling_seal(const TensorCipher &cnn_in, TensorCi
     const Ciphertext packed = sum;
     for (int u6 = 1; u6 < po; u6++)
     {
-        temp = packed;
-        memory_save_rotate(temp, temp, static_cast<int>(-(n / po) * u6), evaluator, gal_keys);
+        rotate_copy(packed, temp, static_cast<int>(-(n / po) * u6), evaluator, gal_keys);
         evaluator.add_inplace_reduced_error(sum, temp);
     }
     cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, sum);
@@ -415,22 +422,19 @@ void averagepooling_seal_scale(const TensorCipher &cnn_in, TensorCipher &cnn_out
     Ciphertext ct = cnn_in.cipher(), temp, sum;
     for (int x = 0; x < log2_long(wi); x++)
     {
-        temp = ct;
-        memory_save_rotate(temp, temp, static_cast<int>(pow2(x) * ki), evaluator, gal_keys);
+        rotate_copy(ct, temp, static_cast<int>(pow2(x) * ki), evaluator, gal_keys);
         evaluator.add_inplace_reduced_error(ct, temp);
     }
     for (int x = 0; x < log2_long(hi); x++)
     {
-        temp = ct;
-        memory_save_rotate(temp, temp, static_cast<int>(pow2(x) * ki * ki * wi), evaluator, gal_keys);
+        rotate_copy(ct, temp, static_cast<int>(pow2(x) * ki * ki * wi), evaluator, gal_keys);
         evaluator.add_inplace_reduced_error(ct, temp);
     }
     for (int s = 0; s < ki; s++)
         for (int u = 0; u < ti; u++)
         {
             const int p = ki * u + s;
-            temp = ct;
-            memory_save_rotate(temp, temp, -p * ki + ki * ki * hi * wi * u + ki * wi * s, evaluator, gal_keys);
+            rotate_copy(ct, temp, -p * ki + ki * ki * hi * wi * u + ki * wi * s, evaluator, gal_keys);
             std::vector<double> sel(n, 0.0);
             for (int i = 0; i < ki; i++) sel[(size_t)(ki * u + s) * ki + i] = B / static_cast<double>(hi * wi);
             evaluator.multiply_vector_inplace_reduced_error(temp, sel);
@@ -458,8 +462,7 @@ void matrix_multiplication_seal(const TensorCipher &cnn_in, TensorCipher &cnn_ou
     Ciphertext temp, sum;
     for (int s = 0; s < q + r - 1; s++)
     {
-        temp = ct;
-        memory_save_rotate(temp, temp, r - 1 - s, evaluator, gal_keys);
+        rotate_copy(ct, temp, r - 1 - s, evaluator, gal_keys);
         evaluator.multiply_vector_inplace_reduced_error(temp, diag[s]);
         if (s == 0)
             sum = temp;
