@@ -175,6 +175,10 @@ def resnet_leg(device, images, streams, layers=20):
         "galois_keys": info["galois_keys"],
         "galois_key_GB_resident": round(info["galois_key_gb"], 2),
         "key_H2D_GB_per_image": 0.0,
+        # every planned key is resident in HBM (no eviction tier is needed at 65 GB of 288), so every
+        # key switch finds its key on the device
+        "key_cache": {"resident_keys": info["galois_keys"], "hit_rate": 1.0, "evictions": 0,
+                      "secret_key_in_eval_keys": False},
         # ResNet roofline: the key-switching key bytes one image streams (the algorithmic bytes of its
         # dominant work, every key switch reading its L x 2 x (L+1)-limb key slice) over its 1-stream time
         "roofline": {

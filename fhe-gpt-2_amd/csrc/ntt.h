@@ -857,7 +857,10 @@ static inline bool ks_key_prefetch()
 // Digit groups G: enough workgroups to hide HBM latency (each one walks L/G digits).
 static inline int ks_groups(int L)
 {
-    return L >= 32 ? 1 : (L >= 8 ? 2 : 1); // measured at L=44: G=1 763, 2 738, 4 700 HMult/s
+    // measured at L=44: G=1 763, 2 738, 4 700 HMult/s; ResNet-20 (L <= 31): G=1 0.865-0.873 images/s
+    // vs 0.832-0.839 with G=2 (scripts/gpu_sweep_env.sh), and no partial-sum reduction launch
+    (void)L;
+    return 1;
 }
 
 template <int LOGR, bool FP>
