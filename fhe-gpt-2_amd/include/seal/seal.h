@@ -695,8 +695,9 @@ public:
     template <typename T>
     void multiply_vector(Ciphertext &encrypted, const std::vector<T> &value, Ciphertext &destination) const
     {
-        destination = encrypted;
-        multiply_vector_inplace(destination, value);
+        Plaintext plain;
+        encode_vector_for(encrypted, value, plain);
+        multiply_plain(encrypted, plain, destination);
     }
     void add_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
     // (not SEAL API) multiply_plain(encrypted, plain, t) + add_inplace_reduced_error(acc, t) for acc at
@@ -708,10 +709,7 @@ public:
         if (&encrypted2 == &destination)
             add_inplace_reduced_error(destination, encrypted1);
         else
-        {
-            destination = encrypted1;
-            add_inplace_reduced_error(destination, encrypted2);
-        }
+            reduced_error_out(encrypted1, encrypted2, destination, Rmode::add, nullptr);
     }
     void double_inplace(Ciphertext &encrypted) const { add_inplace(encrypted, encrypted); }
     void sub_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const;
@@ -722,10 +720,7 @@ public:
         if (&encrypted2 == &destination)
             sub_inplace_reduced_error(destination, encrypted1);
         else
-        {
-            destination = encrypted1;
-            sub_inplace_reduced_error(destination, encrypted2);
-        }
+            reduced_error_out(encrypted1, encrypted2, destination, Rmode::sub, nullptr);
     }
     void multiply_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2,
                                         const RelinKeys &relin_keys) const;
@@ -735,10 +730,7 @@ public:
         if (&encrypted2 == &destination)
             multiply_inplace_reduced_error(destination, encrypted1, relin_keys);
         else
-        {
-            destination = encrypted1;
-            multiply_inplace_reduced_error(destination, encrypted2, relin_keys);
-        }
+            reduced_error_out(encrypted1, encrypted2, destination, Rmode::mul, &relin_keys);
     }
     template <typename T>
     void multiply_vector_inplace_reduced_error(Ciphertext &encrypted, const std::vector<T> &value)
@@ -748,8 +740,10 @@ public:
     template <typename T>
     void multiply_vector_reduced_error(Ciphertext &encrypted, const std::vector<T> &value, Ciphertext &destination)
     {
-        destination = encrypted;
-        multiply_vector_inplace_reduced_error(destination, value);
+        // copy + multiply_vector_inplace in SEAL; the product written straight to destination here
+        Plaintext plain;
+        encode_vector_for(encrypted, value, plain);
+        multiply_plain(encrypted, plain, destination);
     }
 
 private:
@@ -760,6 +754,10 @@ private:
         mul
     };
     void reduced_error_op(Ciphertext &encrypted1, const Ciphertext &encrypted2, Rmode mode) const;
+    // destination = encrypted1 (op)_reduced_error encrypted2 without the copy of encrypted1 when the
+    // levels match (the copy + in-place op of the modified SEAL, same words)
+    void reduced_error_out(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
+                           Rmode mode, const RelinKeys *relin_keys) const;
     void switch_key(Ciphertext &encrypted, const std::uint64_t *target_dev, const KSwitchKeys &keys,
                     std::size_t index) const;
     void rotate_internal(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys) const;

@@ -2081,6 +2081,44 @@ void Evaluator::reduced_error_op(Ciphertext &encrypted1, const Ciphertext &encry
     }
 }
 
+void Evaluator::reduced_error_out(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
+                                  Rmode mode, const RelinKeys *relin_keys) const
+{
+    // equal levels: encrypted1 takes encrypted2's scale, then the op (reduced_error_op); written
+    // out of place so encrypted1 is not copied first
+    const bool same = encrypted1.coeff_modulus_size() == encrypted2.coeff_modulus_size() &&
+                      encrypted1.parms_id() == encrypted2.parms_id() && encrypted1.size() == encrypted2.size() &&
+                      encrypted1.size() == 2 && &encrypted1 != &destination && &encrypted2 != &destination;
+    if (!same)
+    {
+        destination = encrypted1;
+        reduced_error_op(destination, encrypted2, mode);
+        if (mode == Rmode::mul) relinearize_inplace(destination, *relin_keys);
+        return;
+    }
+    check_pair(context_, encrypted1, encrypted2, false);
+    void *s = context_.stream();
+    const Level lv = level_of(context_, encrypted1.parms_id(), "encrypted1");
+    const std::uint64_t *a = encrypted1.store().dev_read(s), *b = encrypted2.store().dev_read(s);
+    if (mode == Rmode::mul)
+    {
+        const double new_scale = encrypted2.scale() * encrypted2.scale();
+        check_scale(new_scale, lv);
+        fresh_dest(context_, encrypted1, destination, 3);
+        chk(mhe_ct_multiply(context_.engine(), a, b, destination.store().dev_write(s, true), (int)lv.L, s));
+        destination.scale() = new_scale;
+        relinearize_inplace(destination, *relin_keys);
+        return;
+    }
+    fresh_dest(context_, encrypted1, destination, 2);
+    std::uint64_t *d = destination.store().dev_write(s, true);
+    if (mode == Rmode::add)
+        chk(mhe_add(context_.engine(), a, b, d, 2, (int)lv.L, s));
+    else
+        chk(mhe_sub(context_.engine(), a, b, d, 2, (int)lv.L, s));
+    destination.scale() = encrypted2.scale();
+}
+
 void Evaluator::add_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
 {
     reduced_error_op(encrypted1, encrypted2, Rmode::add);

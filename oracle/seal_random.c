@@ -284,18 +284,17 @@ static void or_sample_sparse_ternary(or_prng *g, const or_ctx *c, int limbs, siz
 {
     const size_t n = c->n, total = (size_t)limbs * n;
     memset(out, 0, total * 8);
+    (void)total;
     size_t w = 0;
     while (w < hw)
     {
-        const size_t index = (size_t)or_uniform_int(g, 0, n); /* inclusive: n can be drawn */
-        if (out[index] != 0) continue;
+        /* inclusive range: n can be drawn.  SEAL then writes coefficient 0 of limbs 1.. with the
+         * previous prime's residue (and one word past the array), which is not a ring element;
+         * the engine redraws it (seal/random.cpp), and so does this restatement */
+        const size_t index = (size_t)or_uniform_int(g, 0, n);
+        if (index >= n || out[index] != 0) continue;
         const uint64_t r = 2 * or_uniform_int(g, 0, 1);
-        for (int j = 0; j < limbs; j++)
-        {
-            const size_t at = index + (size_t)j * n;
-            if (at >= total) break; /* SEAL writes one word past the array here */
-            out[at] = r == 0 ? c->mod[j].value - 1 : r - 1;
-        }
+        for (int j = 0; j < limbs; j++) out[index + (size_t)j * n] = r == 0 ? c->mod[j].value - 1 : r - 1;
         w++;
     }
 }

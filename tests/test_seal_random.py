@@ -210,20 +210,58 @@ def test_samplers_match_plain_restatement():
                 r = struct.unpack("<Q", st.take(8))[0]
             out.append(r % q)
     assert np.array_equal(oc.sample(SEED, "uniform", 3), np.array(out, np.uint64).reshape(3, n))
-    # sparse ternary (hw 5), including the inclusive position range (index n allowed)
+    # sparse ternary (hw 5): SEAL's inclusive position range (index n can be drawn), with a draw
+    # of n redrawn (SEAL would write a non-residue into limb 1's coefficient 0)
     st = _Stream(SEED)
     arr = [0] * (3 * n)
     w = 0
     while w < 5:
         idx = st.uniform_int(0, n)
-        if arr[idx] != 0:
+        if idx >= n or arr[idx] != 0:
             continue
         r = 2 * st.uniform_int(0, 1)
         for j, q in enumerate(qs):
-            if idx + j * n < 3 * n:
-                arr[idx + j * n] = q - 1 if r == 0 else r - 1
+            arr[idx + j * n] = q - 1 if r == 0 else r - 1
         w += 1
     assert np.array_equal(oc.sample(SEED, "sparse_ternary", 3, hw=5), np.array(arr, np.uint64).reshape(3, n))
+
+
+def test_sparse_ternary_redraws_position_n():
+    """SEAL's sparse sampler draws positions from [0, n] inclusive; a draw of n would write limb 1's
+    coefficient 0 with limb 0's residue (not a ring element).  For a seed whose draws hit n, the
+    oracle (like the engine, seal/random.cpp) redraws it: the key has exactly hw nonzero positions,
+    each the same +-1 in every limb."""
+    log_n = 6
+    n = 1 << log_n
+    moduli = O.coeff_modulus_create(n, [30, 40, 30])
+    oc = O.Context(log_n, moduli)
+    qs = [int(q) for q in moduli]
+    hw = 32
+    hit = None
+    for s0 in range(1, 400):
+        seed = [s0, 2, 3, 4, 5, 6, 7, 8]
+        st = _Stream(seed)
+        taken, w = set(), 0
+        drew_n = False
+        while w < hw:
+            idx = st.uniform_int(0, n)
+            if idx == n:
+                drew_n = True
+            if idx >= n or idx in taken:
+                continue
+            st.uniform_int(0, 1)
+            taken.add(idx)
+            w += 1
+        if drew_n:
+            hit = seed
+            break
+    assert hit is not None
+    key = oc.sample(hit, "sparse_ternary", 3, hw=hw).astype(object)
+    nz = [i for i in range(n) if key[0][i] != 0]
+    assert len(nz) == hw
+    for i in range(n):
+        vals = {(int(key[j][i]) + 1) % qs[j] - 1 for j in range(3)}  # residues -> {-1, 0, 1}
+        assert len(vals) == 1 and vals <= {-1, 0, 1}
 
 
 def test_uniform_rejection_path_exercised():
