@@ -205,6 +205,7 @@ struct mhe_ctx
     int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
     int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
+    int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };
@@ -1192,6 +1193,8 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
         //      column-pass output can stay in the Infinity Cache (MHE_KS_FCHUNK).
         const int G = c->ks_groups > 0 ? c->ks_groups : ks_groups(L);
         const int P = c->ks_fchunk > 0 ? c->ks_fchunk : L + 1;
+        // 48-bit intermediate (ntt.h tile16): only k_modup_col writes it, so only with column groups
+        const int pack = (c->ks_pack && c->ks_colgroups > 0) ? 1 : 0;
         for (int I0 = 0; I0 <= L; I0 += P)
         {
             const int cnt = (I0 + P <= L + 1) ? P : L + 1 - I0;
@@ -1199,7 +1202,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             if (c->ks_colgroups > 0)
             {
                 const int IG = c->ks_colgroups < cnt ? c->ks_colgroups : cnt;
-                modup_col(w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, IG, st);
+                modup_col(w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, IG, pack, st);
             }
             else
             {
@@ -1209,7 +1212,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             timing_end(tc, st);
             hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
             ks_row_mac_chunk(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, c->nm, G, I0,
-                             cnt, st);
+                             cnt, pack, st);
             timing_end(tm, st);
         }
         ks_acc_finish(w->acc, c->primes, L, c->K, G, log_n, st);
@@ -1394,6 +1397,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_KS_FCHUNK")) c->ks_fchunk = atoi(f);
     if (const char *f = getenv("MHE_HMULT_FUSED")) c->hmult_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
+    if (const char *f = getenv("MHE_KS_PACK")) c->ks_pack = atoi(f);
     if (const char *f = getenv("MHE_KS_GROUPS")) c->ks_groups = atoi(f) > 8 ? 8 : atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);

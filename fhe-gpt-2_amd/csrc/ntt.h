@@ -48,6 +48,22 @@ __device__ __forceinline__ T ld_nt(const T *p)
         return *p;
 }
 
+// Packed ModUp intermediate (key switch at n = 2^16, output prime q < 2^48): the canonical
+// residues need 48 bits, so a limb slot holds a 32-bit plane [n] followed by a 16-bit plane [n]
+// (6 of its 8 bytes per residue).  Both planes are laid out as 16 x 16 tiles of the 256 x 256
+// (row = index >> 8, column = index & 255) matrix the two NTT passes see: a column-pass lane
+// writes 16 consecutive rows of one column and a row-pass wave reads whole tile rows, so both
+// sides move contiguous 64-128 B runs.
+__device__ __forceinline__ u32 tile16(u32 idx)
+{
+    const u32 r = idx >> 8, c = idx & 255;
+    return ((((r >> 4) << 4) | (c >> 4)) << 8) | ((r & 15) << 4) | (c & 15);
+}
+__device__ __forceinline__ bool inter_packed(int pack, u64 q)
+{
+    return pack && q < (1ull << 48);
+}
+
 // Forward Harvey butterfly (dwthandler.h:122-125 with ntt.h:34-65 arithmetic).
 __device__ __forceinline__ void fwd_bfly(u64 &x, u64 &y, const Tw w, u64 q, u64 q2)
 {
@@ -393,7 +409,8 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long t
 template <int LOGR, int LOGT, bool FP>
 __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ coeff, u64 *__restrict__ modup,
                                                    const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all,
-                                                   int L, int K, int log_n, long long twd, int I0, int Icnt)
+                                                   int L, int K, int log_n, long long twd, int I0, int Icnt,
+                                                   int pack)
 {
     using SH = Shape<LOGR, LOGT>;
     using A = NttArith<FP>;
@@ -449,8 +466,29 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
                 ar.template fwd<E>(v, 1 << (LOGR - 1 - s),
                                    [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
             u64 *dst = modup + (((size_t)(I - I0) * L + J) << log_n);
+            if (inter_packed(pack, p.q)) // uniform per workgroup
+            {
+                // n = 2^16 here, so logC = 16 - LOGR is a constant and the tile offsets fold into
+                // one base per lane plus immediates
+                constexpr int LC = 16 - LOGR;
+                u32 *lo = reinterpret_cast<u32 *>(dst) + tile16(c + ((u32)(E * t) << LC));
+                unsigned short *hi = reinterpret_cast<unsigned short *>(reinterpret_cast<u32 *>(dst) + 65536) +
+                                     tile16(c + ((u32)(E * t) << LC));
 #pragma unroll
-            for (int e = 0; e < E; e++) st_nt<0>(&dst[c + ((u32)(E * t + e) << logC)], ar.out(v[e]));
+                for (int e = 0; e < E; e++)
+                {
+                    const u64 o = ar.out(v[e]);
+                    // tile16(c + ((E t + e) << LC)) - tile16(c + ((E t) << LC)), E t a multiple of 16
+                    const u32 k = ((u32)(e >> 4) << 12) | ((u32)(e & 15) << 4);
+                    st_nt<0>(&lo[k], (u32)o);
+                    st_nt<0>(&hi[k], (unsigned short)(o >> 32));
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++) st_nt<0>(&dst[c + ((u32)(E * t + e) << logC)], ar.out(v[e]));
+            }
             __syncthreads(); // lds is rewritten by the next output prime
         }
     };
@@ -465,7 +503,7 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
 
 template <int LOGR, bool FP>
 static inline void modup_col_a(const u64 *coeff, u64 *modup, const PrimeDev *primes, const Tw *tw, int L, int K,
-                               int log_n, long long twd, int I0, int Icnt, int IG, hipStream_t st)
+                               int log_n, long long twd, int I0, int Icnt, int IG, int pack, hipStream_t st)
 {
 #ifndef MHE_MODUP_LOGT8
 #define MHE_MODUP_LOGT8 4
@@ -474,27 +512,29 @@ static inline void modup_col_a(const u64 *coeff, u64 *modup, const PrimeDev *pri
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
     hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3(subs / SH::S, L, IG), dim3(256), 0, st, coeff, modup,
-                       primes, tw, L, K, log_n, twd, I0, Icnt);
+                       primes, tw, L, K, log_n, twd, I0, Icnt, pack);
 }
 
 // ModUp column pass for output primes I0 .. I0+Icnt-1 (modup holds exactly those), in IG
-// groups of output primes per digit.
+// groups of output primes per digit.  pack (n = 2^16 only): limbs of primes below 2^48 are
+// stored in the packed 48-bit form (tile16), which k_ks_row_mac must then be told as well.
 static inline void modup_col(const u64 *coeff, u64 *modup, const PrimeDev *primes, const Tw *tw, int L, int K,
-                             int log_n, const NttMode &m, int I0, int Icnt, int IG, hipStream_t st)
+                             int log_n, const NttMode &m, int I0, int Icnt, int IG, int pack, hipStream_t st)
 {
     switch ((log_n + 1) / 2)
     {
     case 6:
-        if (m.fp) modup_col_a<6, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, st);
-        else modup_col_a<6, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, st);
+        if (m.fp) modup_col_a<6, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        else modup_col_a<6, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
         break;
     case 7:
-        if (m.fp) modup_col_a<7, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, st);
-        else modup_col_a<7, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, st);
+        if (m.fp) modup_col_a<7, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        else modup_col_a<7, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
         break;
     case 8:
-        if (m.fp) modup_col_a<8, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, st);
-        else modup_col_a<8, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, st);
+        pack = (pack && log_n == 16) ? 1 : 0;
+        if (m.fp) modup_col_a<8, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, pack, st);
+        else modup_col_a<8, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, pack, st);
         break;
     }
 }
@@ -624,7 +664,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                                                        u64 *__restrict__ acc,          // [G][2][L+1][n]
                                                        const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int key_limbs,
-                                                       int log_n, long long twd, int I0)
+                                                       int log_n, long long twd, int I0, int pack)
 {
     using SH = RowMacShape<LOGR>;
     using A = NttArith<FP>;
@@ -680,15 +720,36 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                 a0[e] = a1[e] = Acc128{ 0, 0 };
         }
 
-        auto digit_src = [&](int J) -> const u64 * {
-            return (J == I) ? target + (size_t)J * n + base : inter + ((size_t)(I - I0) * L + J) * n + base;
+        // digit J of this output prime: the input limb itself (J == I, already NTT form) or the
+        // column-pass output, packed (tile16) when the column pass packed it
+        const bool pk = inter_packed(pack, p.q); // uniform per workgroup
+        auto load_digit = [&](int J, u64 (&v)[8]) {
+            if (J == I)
+            {
+                const u64 *src = target + (size_t)J * n + base;
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
+            }
+            else if (pk)
+            {
+                const u32 *lo = reinterpret_cast<const u32 *>(inter + ((size_t)(I - I0) * L + J) * n);
+                const unsigned short *hi = reinterpret_cast<const unsigned short *>(lo + n);
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    const u32 k = tile16(base + lay(t, e, B_A));
+                    v[e] = (u64)ld_nt<2>(&lo[k]) | ((u64)ld_nt<2>(&hi[k]) << 32);
+                }
+            }
+            else
+            {
+                const u64 *src = inter + ((size_t)(I - I0) * L + J) * n + base;
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
+            }
         };
         u64 vin[8];
-        {
-            const u64 *src = digit_src(j0);
-#pragma unroll
-            for (int e = 0; e < 8; e++) vin[e] = src[lay(t, e, B_A)];
-        }
+        load_digit(j0, vin);
         lds_barrier(); // twiddles visible
 
         // key limbs of a digit: issued one digit ahead (KPF) or at the top of the digit (the
@@ -712,12 +773,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                 load_key(J, kk0, kk1);
             else if (J + 1 < j1)
                 load_key(J + 1, kn0, kn1);
-            if (J + 1 < j1)
-            {
-                const u64 *src = digit_src(J + 1);
-#pragma unroll
-                for (int e = 0; e < 8; e++) vnext[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
-            }
+            if (J + 1 < j1) load_digit(J + 1, vnext);
             T d[8]; // the digit in the coalesced layout, NTT form
             if (J != I)
             {
@@ -866,39 +922,43 @@ static inline int ks_groups(int L)
 template <int LOGR, bool FP>
 static inline void ks_row_mac_a(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
                                 const Tw *tw, int L, int K, int key_limbs, int log_n, long long twd, int G, int I0,
-                                int cnt, hipStream_t st)
+                                int cnt, int pack, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
     const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, G);
     if (ks_key_prefetch())
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, inter, target, key, acc, primes, tw,
-                           L, K, key_limbs, log_n, twd, I0);
+                           L, K, key_limbs, log_n, twd, I0, pack);
     else
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, inter, target, key, acc, primes,
-                           tw, L, K, key_limbs, log_n, twd, I0);
+                           tw, L, K, key_limbs, log_n, twd, I0, pack);
 }
 
 template <int LOGR>
 static inline void ks_row_mac_m(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
                                 const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, int G, int I0,
-                                int cnt, hipStream_t st)
+                                int cnt, int pack, hipStream_t st)
 {
     if (m.fp)
-        ks_row_mac_a<LOGR, true>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m.dfwd, G, I0, cnt, st);
+        ks_row_mac_a<LOGR, true>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m.dfwd, G, I0, cnt, pack,
+                                 st);
     else
-        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, I0, cnt, st);
+        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, I0, cnt, pack, st);
 }
 
 // Fused row pass + MAC for output primes I0 .. I0+cnt-1 (inter holds exactly those).
 static inline void ks_row_mac_chunk(const u64 *inter, const u64 *target, const u64 *key, u64 *acc,
                                     const PrimeDev *primes, const Tw *tw, int L, int K, int key_limbs, int log_n,
-                                    const NttMode &m, int G, int I0, int cnt, hipStream_t st)
+                                    const NttMode &m, int G, int I0, int cnt, int pack, hipStream_t st)
 {
     switch (log_n / 2)
     {
-    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, st); break;
-    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, st); break;
-    case 8: ks_row_mac_m<8>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, st); break;
+    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, st); break;
+    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, st); break;
+    case 8:
+        ks_row_mac_m<8>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt,
+                        (pack && log_n == 16) ? 1 : 0, st);
+        break;
     }
 }
 
