@@ -746,6 +746,17 @@ public:
         multiply_plain(encrypted, plain, destination);
     }
 
+    // (not SEAL API) encode_vector_for of static operands (network weights, masks), cached: the
+    // caller names the vector by a 128-bit recipe id (a hash of everything that determines it) and
+    // make() builds it on a miss only.  Entries are keyed by (id, level, scale), are bit-identical
+    // to a fresh encode_vector_for, and live as long as the evaluator (and its copies).  Returns the
+    // cached plaintext, or `scratch` holding a fresh encoding when the cache is full or off
+    // (MHE_VEC_CACHE_GB, default 48; 0 disables).
+    const Plaintext &cached_vector_plain(const Ciphertext &encrypted, std::uint64_t id_hi, std::uint64_t id_lo,
+                                         const std::function<std::vector<double>()> &make, Plaintext &scratch) const;
+    std::size_t vector_cache_entries() const;
+    std::size_t vector_cache_bytes() const;
+
 private:
     enum class Rmode
     {
@@ -764,6 +775,8 @@ private:
     std::size_t limbs_of(const parms_id_type &id) const;
     SEALContext context_;
     CKKSEncoder &encoder_;
+    struct VecCache;
+    std::shared_ptr<VecCache> vcache_;
 };
 
 extern template void Evaluator::multiply_vector_inplace<double>(Ciphertext &, const std::vector<double> &) const;

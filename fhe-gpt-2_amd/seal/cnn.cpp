@@ -10,6 +10,8 @@
 #include "mhe_cnn.h"
 
 #include <cmath>
+#include <cstring>
+#include <functional>
 #include <iostream>
 #include <stdexcept>
 
@@ -68,6 +70,48 @@ struct Mux
     }
     bool in_tensor(const Slot &r) const { return r.local < (long)k * k * h * w * t; }
 };
+
+// 128-bit id of a static plaintext operand (Evaluator::cached_vector_plain): two independent
+// 64-bit hashes (FNV-1a and a splitmix64 chain) over everything the vector is built from.
+struct Recipe
+{
+    std::uint64_t a = 0xcbf29ce484222325ull, b = 0x243f6a8885a308d3ull;
+    Recipe &add(std::uint64_t x)
+    {
+        for (int i = 0; i < 8; i++) a = (a ^ ((x >> (8 * i)) & 0xff)) * 0x100000001b3ull;
+        std::uint64_t z = (b ^ x) + 0x9e3779b97f4a7c15ull;
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        b = z ^ (z >> 31);
+        return *this;
+    }
+    Recipe &add(double d)
+    {
+        std::uint64_t x;
+        std::memcpy(&x, &d, sizeof x);
+        return add(x);
+    }
+    Recipe &add(const std::vector<double> &v)
+    {
+        add((std::uint64_t)v.size());
+        for (double d : v) add(d);
+        return *this;
+    }
+    Recipe &ints(std::initializer_list<long> xs)
+    {
+        for (long x : xs) add((std::uint64_t)x);
+        return *this;
+    }
+};
+
+// multiply_vector_inplace(_reduced_error)(ct, make()) with the encoded vector cached under `id`
+void multiply_static_vector(Evaluator &evaluator, Ciphertext &ct, const Recipe &id,
+                            const std::function<std::vector<double>()> &make)
+{
+    Plaintext scratch;
+    const Plaintext &pt = evaluator.cached_vector_plain(ct, id.a, id.b, make, scratch);
+    evaluator.multiply_plain_inplace(ct, pt);
+}
 } // namespace
 
 // ------------------------------------------------------------------------ TensorCipher
@@ -227,6 +271,14 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         encryptor.encrypt(plain, ct_zero);
     }
 
+    // the tap weights and select vectors are static: their encodings are cached by the evaluator
+    // under a hash of what they are built from (bit-identical to encoding them per call)
+    Recipe conv_id;
+    conv_id.add((std::uint64_t)0x636f6e76u).add(data).ints({ ki, hi, wi, ci, ti, pi, logn, co, st, fh, fw });
+    Recipe sel_id;
+    sel_id.add((std::uint64_t)0x73656c63u).add(constant_weight).add(running_var).add(epsilon).ints(
+        { ko, ho, wo, to, n });
+
     const int d = static_cast<int>(log2_long(ki)), c = static_cast<int>(log2_long(ti));
     for (int i9 = 0; i9 < q; i9++)
     {
@@ -236,8 +288,11 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
             for (int i2 = 0; i2 < fw; i2++)
             {
                 Ciphertext &tap = *rot[fw * i1 + i2];
-                Plaintext wp;
-                evaluator.encode_vector_for(tap, weight_vec(i1, i2, i9), wp);
+                Plaintext scratch;
+                Recipe id = conv_id;
+                id.ints({ i1, i2, i9 });
+                const Plaintext &wp = evaluator.cached_vector_plain(
+                    tap, id.a, id.b, [&] { return weight_vec(i1, i2, i9); }, scratch);
                 if (i1 == 0 && i2 == 0)
                     evaluator.multiply_plain(tap, wp, sum);
                 else
@@ -274,7 +329,9 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
                                (int)((n / pi) * (j4 % pi) - j4 % ko - (j4 / (ko * ko)) * ko * ko * ho * wo -
                                      ((j4 % (ko * ko)) / ko) * ko * wo),
                                evaluator, gal_keys);
-            evaluator.multiply_vector_inplace_reduced_error(temp, select_vec(j4));
+            Recipe id = sel_id;
+            id.ints({ j4 });
+            multiply_static_vector(evaluator, temp, id, [&] { return select_vec(j4); });
             if (i8 == 0 && i9 == 0)
                 total_sum = temp;
             else
@@ -381,14 +438,19 @@ void multiplexed_parallel_downsampling_seal(const TensorCipher &cnn_in, TensorCi
     for (int w1 = 0; w1 < ki; w1++)
         for (int w2 = 0; w2 < ti; w2++)
         {
-            std::vector<double> sel(n, 0.0);
-            for (long s = 0; s < (long)ki * ki * hi * wi * ti; s++)
-            {
-                const Mux::Slot r = in.at(s);
-                if (r.row % 2 == 0 && r.col % 2 == 0 && r.rb % ki == w1 && r.u == w2) sel[s] = 1.0;
-            }
+            auto make_sel = [&] {
+                std::vector<double> sel(n, 0.0);
+                for (long s = 0; s < (long)ki * ki * hi * wi * ti; s++)
+                {
+                    const Mux::Slot r = in.at(s);
+                    if (r.row % 2 == 0 && r.col % 2 == 0 && r.rb % ki == w1 && r.u == w2) sel[s] = 1.0;
+                }
+                return sel;
+            };
+            Recipe id;
+            id.add((std::uint64_t)0x646f776eu).ints({ n, ki, hi, wi, ti, w1, w2 });
             temp = ct;
-            evaluator.multiply_vector_inplace_reduced_error(temp, sel);
+            multiply_static_vector(evaluator, temp, id, make_sel);
             const int w3 = ((ki * w2 + w1) % (2 * ko)) / 2, w4 = (ki * w2 + w1) % 2, w5 = (ki * w2 + w1) / (2 * ko);
             memory_save_rotate(temp, temp,
                                ki * ki * hi * wi * w2 + ki * wi * w1 - ko * ko * ho * wo * w5 - ko * wo * w3 - ki * w4 -
@@ -435,9 +497,13 @@ void averagepooling_seal_scale(const TensorCipher &cnn_in, TensorCipher &cnn_out
         {
             const int p = ki * u + s;
             rotate_copy(ct, temp, -p * ki + ki * ki * hi * wi * u + ki * wi * s, evaluator, gal_keys);
-            std::vector<double> sel(n, 0.0);
-            for (int i = 0; i < ki; i++) sel[(size_t)(ki * u + s) * ki + i] = B / static_cast<double>(hi * wi);
-            evaluator.multiply_vector_inplace_reduced_error(temp, sel);
+            Recipe id;
+            id.add((std::uint64_t)0x61766770u).add(B).ints({ n, ki, hi, wi, u, s });
+            multiply_static_vector(evaluator, temp, id, [&] {
+                std::vector<double> sel(n, 0.0);
+                for (int i = 0; i < ki; i++) sel[(size_t)(ki * u + s) * ki + i] = B / static_cast<double>(hi * wi);
+                return sel;
+            });
             if (u == 0 && s == 0)
                 sum = temp;
             else
@@ -455,15 +521,25 @@ void matrix_multiplication_seal(const TensorCipher &cnn_in, TensorCipher &cnn_ou
     if (static_cast<int>(matrix.size()) != q * r) throw std::invalid_argument("the size of matrix is not q*r");
     if (static_cast<int>(bias.size()) != q) throw std::invalid_argument("the size of bias is not q");
     const long n = 1L << cnn_in.logn();
-    std::vector<std::vector<double>> diag(q + r - 1, std::vector<double>(n, 0.0));
-    for (int i = 0; i < q; i++)
-        for (int j = 0; j < r; j++) diag[i - j + r - 1][i] = matrix[(size_t)i * r + j];
+    // diagonal s of the matrix: diag[i] = matrix[i][i + s - (r - 1)] (cached encodings)
+    Recipe fc_id;
+    fc_id.add((std::uint64_t)0x66636d6du).add(matrix).ints({ n, q, r });
     const Ciphertext ct = cnn_in.cipher();
     Ciphertext temp, sum;
     for (int s = 0; s < q + r - 1; s++)
     {
         rotate_copy(ct, temp, r - 1 - s, evaluator, gal_keys);
-        evaluator.multiply_vector_inplace_reduced_error(temp, diag[s]);
+        Recipe id = fc_id;
+        id.ints({ s });
+        multiply_static_vector(evaluator, temp, id, [&] {
+            std::vector<double> diag(n, 0.0);
+            for (int i = 0; i < q; i++)
+            {
+                const int j = i + r - 1 - s;
+                if (j >= 0 && j < r) diag[i] = matrix[(size_t)i * r + j];
+            }
+            return diag;
+        });
         if (s == 0)
             sum = temp;
         else

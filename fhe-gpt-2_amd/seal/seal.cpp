@@ -1255,9 +1255,78 @@ void check_scale(double scale, const Level &lv)
 }
 } // namespace
 
-Evaluator::Evaluator(const SEALContext &context, CKKSEncoder &encoder) : context_(context), encoder_(encoder)
+struct Evaluator::VecCache
+{
+    struct Key
+    {
+        std::uint64_t hi, lo;
+        std::size_t limbs;
+        std::uint64_t scale_bits;
+        bool operator<(const Key &o) const
+        {
+            if (hi != o.hi) return hi < o.hi;
+            if (lo != o.lo) return lo < o.lo;
+            if (limbs != o.limbs) return limbs < o.limbs;
+            return scale_bits < o.scale_bits;
+        }
+    };
+    std::mutex mu;
+    std::map<Key, Plaintext> entries;
+    std::size_t bytes = 0;
+    std::size_t cap = [] {
+        const char *e = std::getenv("MHE_VEC_CACHE_GB");
+        const double gb = e ? std::atof(e) : 48.0;
+        return gb > 0 ? (std::size_t)(gb * 1e9) : (std::size_t)0;
+    }();
+};
+
+Evaluator::Evaluator(const SEALContext &context, CKKSEncoder &encoder)
+    : context_(context), encoder_(encoder), vcache_(std::make_shared<VecCache>())
 {
     if (!context.parameters_set()) throw std::invalid_argument("encryption parameters are not set correctly");
+}
+
+const Plaintext &Evaluator::cached_vector_plain(const Ciphertext &encrypted, std::uint64_t id_hi, std::uint64_t id_lo,
+                                                const std::function<std::vector<double>()> &make,
+                                                Plaintext &scratch) const
+{
+    const Level lv = check_ct(context_, encrypted, "encrypted");
+    std::uint64_t sb;
+    const double sc = encrypted.scale();
+    std::memcpy(&sb, &sc, sizeof sb);
+    const VecCache::Key key{ id_hi, id_lo, lv.L, sb };
+    VecCache &vc = *vcache_;
+    const std::size_t sz = lv.L * lv.n * sizeof(std::uint64_t);
+    bool fits;
+    {
+        std::lock_guard<std::mutex> g(vc.mu);
+        auto it = vc.entries.find(key);
+        if (it != vc.entries.end()) return it->second;
+        fits = vc.cap > 0 && vc.bytes + sz <= vc.cap;
+    }
+    if (!fits)
+    {
+        encode_vector_for(encrypted, make(), scratch);
+        return scratch;
+    }
+    Plaintext pt;
+    encode_vector_for(encrypted, make(), pt);
+    std::lock_guard<std::mutex> g(vc.mu);
+    auto r = vc.entries.emplace(key, std::move(pt)); // another thread may have made the same entry
+    if (r.second) vc.bytes += sz;
+    return r.first->second;
+}
+
+std::size_t Evaluator::vector_cache_entries() const
+{
+    std::lock_guard<std::mutex> g(vcache_->mu);
+    return vcache_->entries.size();
+}
+
+std::size_t Evaluator::vector_cache_bytes() const
+{
+    std::lock_guard<std::mutex> g(vcache_->mu);
+    return vcache_->bytes;
 }
 
 std::size_t Evaluator::limbs_of(const parms_id_type &id) const

@@ -426,6 +426,40 @@ static void test_reduced_error_ops()
         for (std::size_t k = 0; k < acc1.dyn_array_size(); k++) diff += p1[k] != p2[k];
         CHECK(diff == 0 && acc1.scale() == acc2.scale() && acc1.dyn_array_size() == acc2.dyn_array_size());
     }
+    // cached static-vector encodings: bit-identical to encode_vector_for, built once per
+    // (id, level, scale), and the builder is not called on a hit
+    {
+        Ciphertext c = e.enc(b, s), low = e.enc(b, s);
+        e.evaluator->mod_switch_to_next_inplace(low);
+        Plaintext fresh, scratch;
+        e.evaluator->encode_vector_for(c, w, fresh);
+        int built = 0;
+        auto make = [&] {
+            built++;
+            return w;
+        };
+        const std::size_t before = e.evaluator->vector_cache_entries();
+        const Plaintext &p1 = e.evaluator->cached_vector_plain(c, 7, 11, make, scratch);
+        const Plaintext &p2 = e.evaluator->cached_vector_plain(c, 7, 11, make, scratch);
+        CHECK(&p1 == &p2 && built == 1 && e.evaluator->vector_cache_entries() == before + 1);
+        std::size_t diff = fresh.store().words() != p1.store().words();
+        for (std::size_t k = 0; !diff && k < fresh.store().words(); k++)
+            diff += fresh.store().host()[k] != p1.store().host()[k];
+        CHECK(diff == 0 && p1.scale() == fresh.scale() && p1.parms_id() == fresh.parms_id());
+        // another level (and another scale) is another entry
+        const Plaintext &p3 = e.evaluator->cached_vector_plain(low, 7, 11, make, scratch);
+        CHECK(&p3 != &p1 && built == 2 && p3.parms_id() == low.parms_id());
+        c.scale() *= 2;
+        const Plaintext &p4 = e.evaluator->cached_vector_plain(c, 7, 11, make, scratch);
+        CHECK(&p4 != &p1 && built == 3 && p4.scale() == c.scale());
+        // and a product through the cached plaintext equals multiply_vector_inplace
+        Ciphertext m1 = e.enc(a, s), m2 = m1;
+        e.evaluator->multiply_vector_inplace(m1, w);
+        e.evaluator->multiply_plain_inplace(m2, e.evaluator->cached_vector_plain(m2, 7, 12, make, scratch));
+        diff = 0;
+        for (std::size_t k = 0; k < m1.dyn_array_size(); k++) diff += m1.data()[k] != m2.data()[k];
+        CHECK(diff == 0);
+    }
 }
 
 static void test_security_level()
