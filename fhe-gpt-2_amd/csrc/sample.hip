@@ -114,33 +114,44 @@ __global__ void k_prng_apply(const u64 *fix, u32 count, u64 *out)
     if (i < count) out[fix[2 * i]] = fix[2 * i + 1];
 }
 
-// sample_poly_ternary: coefficients [0, n) from the stream bytes at byte offset `off` (64-aligned),
-// 16 coefficients (one block) per thread.  A zero word would be redrawn (Lemire); those are
-// counted in state[1] and k_prng_ternary_fix redoes the poly sequentially.
+// sample_poly_ternary: coefficients [0, n) from the stream bytes at byte offset `off` (64-aligned).
+// A workgroup owns 256 stream blocks (4096 coefficients): one thread per block draws its 16 values
+// into LDS, then the workgroup writes them coalesced to the limbs blockIdx.y, blockIdx.y +
+// gridDim.y, ... (every y redraws the same values; the limbs split keeps the grid wide).  A zero word
+// would be redrawn (Lemire); those are counted in state[1] (by y == 0) and k_prng_ternary_fix redoes
+// the poly sequentially.
 __global__ __launch_bounds__(256) void k_prng_ternary(Seed s, u64 off, u64 *out, const PrimeDev *primes, int limbs,
                                                       int log_n, u32 *state)
 {
     __shared__ u64 roots[kMaxRoots][8];
-    const u64 t = (u64)blockIdx.x * 256 + threadIdx.x;
+    __shared__ unsigned char val[256 * 16];
     const u64 n = (u64)1 << log_n;
-    const u64 first = (off >> 6) + (u64)blockIdx.x * 256;
-    const u64 nblk = n / 16, wg_end = ((u64)blockIdx.x * 256 + 256 < nblk ? (u64)blockIdx.x * 256 + 256 : nblk);
-    const u64 last = (off >> 6) + wg_end - 1;
+    const u64 nblk = n / 16, wb0 = (u64)blockIdx.x * 256;
+    const u64 wg_end = (wb0 + 256 < nblk ? wb0 + 256 : nblk);
+    const u64 first = (off >> 6) + wb0, last = (off >> 6) + wg_end - 1;
     load_roots(s, first >> 6, (int)((last >> 6) - (first >> 6) + 1), roots);
-    if (t * 16 >= n) return;
-    u64 w[8];
-    block_from_roots(roots, first >> 6, (off >> 6) + t, w);
-#pragma unroll
-    for (int k = 0; k < 16; k++)
+    if (wb0 + threadIdx.x < wg_end)
     {
-        const u32 g = (u32)(w[k >> 1] >> (32 * (k & 1)));
-        if (g == 0) atomicAdd(&state[1], 1u);
-        const u64 r = ((u64)g * 3) >> 32; // {0, 1, 2} -> {-1, 0, 1}
-        const u64 i = t * 16 + k;
-        for (int l = 0; l < limbs; l++)
+        u64 w[8];
+        block_from_roots(roots, first >> 6, first + threadIdx.x, w);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
         {
-            const u64 q = primes[l].q;
-            out[((u64)l << log_n) + i] = r == 0 ? q - 1 : r - 1;
+            const u32 g = (u32)(w[k >> 1] >> (32 * (k & 1)));
+            if (g == 0 && blockIdx.y == 0) atomicAdd(&state[1], 1u);
+            val[threadIdx.x * 16 + k] = (unsigned char)(((u64)g * 3) >> 32); // {0, 1, 2} -> {-1, 0, 1}
+        }
+    }
+    __syncthreads();
+    const u32 cnt = (u32)((wg_end - wb0) * 16);
+    for (int l = blockIdx.y; l < limbs; l += gridDim.y)
+    {
+        const u64 q = primes[l].q;
+        u64 *o = out + ((u64)l << log_n) + wb0 * 16;
+        for (u32 i = threadIdx.x; i < cnt; i += 256)
+        {
+            const u32 r = val[i];
+            o[i] = r == 0 ? q - 1 : r - 1;
         }
     }
 }
@@ -187,7 +198,8 @@ __global__ void k_prng_ternary_fix(Seed s, u64 off, u64 *out, const PrimeDev *pr
 // sample_poly_cbd: coefficients [0, n) from the bytes at offset off + (*extra when given), a
 // multiple of 4.  A workgroup owns kCbdCoeffs coefficients (6 bytes each): it computes the roots
 // of the <= 3 buffers and the <= 97 stream blocks those bytes span into LDS (one compression per
-// block), then every thread forms 4 coefficients from LDS.
+// block), forms the noise values in LDS, and writes them coalesced to the limbs blockIdx.y,
+// blockIdx.y + gridDim.y, ... (as k_prng_ternary).
 constexpr int kCbdCoeffs = 1024;
 constexpr int kCbdBlocks = (6 * kCbdCoeffs) / 64 + 1;
 __global__ __launch_bounds__(256) void k_prng_cbd(Seed s, u64 off, const u32 *extra, u64 *out, const PrimeDev *primes,
@@ -195,6 +207,7 @@ __global__ __launch_bounds__(256) void k_prng_cbd(Seed s, u64 off, const u32 *ex
 {
     __shared__ u64 roots[kMaxRoots][8];
     __shared__ u64 bytes[kCbdBlocks * 8];
+    __shared__ signed char noise[kCbdCoeffs];
     const u64 n = (u64)1 << log_n;
     const u64 c0 = (u64)blockIdx.x * kCbdCoeffs;
     const u64 cnt = (n - c0) < (u64)kCbdCoeffs ? (n - c0) : (u64)kCbdCoeffs;
@@ -217,13 +230,18 @@ __global__ __launch_bounds__(256) void k_prng_cbd(Seed s, u64 off, const u32 *ex
     for (u32 k = threadIdx.x; k < cnt; k += 256)
     {
         const u32 c = 6 * k;
-        const int noise = __popc(byte_at(c)) + __popc(byte_at(c + 1)) + __popc(byte_at(c + 2) & 0x1f) -
-                          __popc(byte_at(c + 3)) - __popc(byte_at(c + 4)) - __popc(byte_at(c + 5) & 0x1f);
-        const u64 i = c0 + k;
-        for (int l = 0; l < limbs; l++)
+        noise[k] = (signed char)(__popc(byte_at(c)) + __popc(byte_at(c + 1)) + __popc(byte_at(c + 2) & 0x1f) -
+                                 __popc(byte_at(c + 3)) - __popc(byte_at(c + 4)) - __popc(byte_at(c + 5) & 0x1f));
+    }
+    __syncthreads();
+    for (int l = blockIdx.y; l < limbs; l += gridDim.y)
+    {
+        const u64 q = primes[l].q;
+        u64 *o = out + ((u64)l << log_n) + c0;
+        for (u32 k = threadIdx.x; k < cnt; k += 256)
         {
-            const u64 q = primes[l].q;
-            out[((u64)l << log_n) + i] = noise >= 0 ? (u64)noise : q - (u64)(-noise);
+            const int v = noise[k];
+            o[k] = v >= 0 ? (u64)v : q - (u64)(-v);
         }
     }
 }
@@ -291,14 +309,14 @@ MHE_EXPORT int mhe_prng_small(mhe_ctx *c, const uint64_t seed[8], uint64_t byte_
         if (!state_dev) return mhe_internal_fail(MHE_ERR_ARG, "invalid sampling arguments");
         if (hipMemsetAsync(state_dev, 0, 8, st) != hipSuccess)
             return mhe_internal_fail(MHE_ERR_DEVICE, "sampling state reset failed");
-        hipLaunchKernelGGL(k_prng_ternary, dim3((unsigned)((n / 16 + 255) / 256)), dim3(256), 0, st, s, byte_offset, out,
-                           primes, limbs, log_n, state_dev);
+        hipLaunchKernelGGL(k_prng_ternary, dim3((unsigned)((n / 16 + 255) / 256), (unsigned)(limbs < 8 ? limbs : 8)),
+                           dim3(256), 0, st, s, byte_offset, out, primes, limbs, log_n, state_dev);
         hipLaunchKernelGGL(k_prng_ternary_fix, dim3(1), dim3(64), 0, st, s, byte_offset, out, primes, limbs, log_n,
                            state_dev);
     }
     else if (kind == MHE_SAMPLE_CBD)
-        hipLaunchKernelGGL(k_prng_cbd, dim3((unsigned)((n + kCbdCoeffs - 1) / kCbdCoeffs)), dim3(256), 0, st, s, byte_offset,
-                           (const u32 *)state_dev, out, primes, limbs, log_n);
+        hipLaunchKernelGGL(k_prng_cbd, dim3((unsigned)((n + kCbdCoeffs - 1) / kCbdCoeffs), (unsigned)(limbs < 4 ? limbs : 4)),
+                           dim3(256), 0, st, s, byte_offset, (const u32 *)state_dev, out, primes, limbs, log_n);
     else
         return mhe_internal_fail(MHE_ERR_ARG, "unknown distribution");
     return launch_check("sampling kernel launch failed");
