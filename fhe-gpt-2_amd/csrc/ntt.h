@@ -658,7 +658,16 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
 }
 
 template <int LOGR, bool FP, bool KPF>
-__global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass out
+#ifndef MHE_KS_OCC
+#define MHE_KS_OCC 2 // waves per SIMD the fused MAC is compiled for
+#endif
+#ifndef MHE_KS_XCH
+#define MHE_KS_XCH 2 // LDS transpose buffers of the fused MAC (1 or 2)
+#endif
+#ifndef MHE_KS_DPF
+#define MHE_KS_DPF 1 // fused MAC: load the next digit one digit ahead (1) or at the top of the digit (0)
+#endif
+__global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass out
                                                        const u64 *__restrict__ target, // [L][n] NTT form
                                                        const u64 *__restrict__ key,    // [digits][2][key_limbs][n]
                                                        u64 *__restrict__ acc,          // [G][2][L+1][n]
@@ -672,7 +681,10 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
     using TW = typename A::TW;
     constexpr int R = SH::R, TPS = SH::TPS, S = SH::S;
     constexpr int B_A = LOGR - 3, B_B = LOGR - 6;
-    __shared__ T xch[2][S * R];
+    // one transpose buffer is enough (every transpose stays inside one wave and a wave's LDS
+    // operations complete in order; the fences only stop the compiler from reordering them):
+    // 49 KB per workgroup fits 3 workgroups per CU, two buffers (65.6 KB) only 2
+    __shared__ T xch[MHE_KS_XCH][S * R];
     __shared__ TW twl[S * (R + 1)];
     const int G = gridDim.z, g = blockIdx.z;
     const int j0 = (L * g) / G, j1 = (L * (g + 1)) / G;
@@ -700,7 +712,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
         }
     }
     const TW *mytw = &twl[sl * (R + 1)];
-    T *x0 = &xch[0][sl * R], *x1 = &xch[1][sl * R];
+    T *x0 = &xch[0][sl * R], *x1 = &xch[MHE_KS_XCH - 1][sl * R];
 
     auto run = [&](const auto &ar) {
         // FP: the key inner products run in FP64 as well (fp_mulmod_gen); with q < 2^47 and
@@ -749,7 +761,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
             }
         };
         u64 vin[8];
-        load_digit(j0, vin);
+        if (MHE_KS_DPF) load_digit(j0, vin);
         lds_barrier(); // twiddles visible
 
         // key limbs of a digit: issued one digit ahead (KPF) or at the top of the digit (the
@@ -773,7 +785,10 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                 load_key(J, kk0, kk1);
             else if (J + 1 < j1)
                 load_key(J + 1, kn0, kn1);
-            if (J + 1 < j1) load_digit(J + 1, vnext);
+            if (!MHE_KS_DPF)
+                load_digit(J, vin); // no prefetch: occupancy hides the latency instead
+            else if (J + 1 < j1)
+                load_digit(J + 1, vnext);
             T d[8]; // the digit in the coalesced layout, NTT form
             if (J != I)
             {
@@ -781,6 +796,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
 #pragma unroll
                 for (int e = 0; e < 8; e++) w[e] = ar.in(vin[e]);
                 row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
+                wave_lds_fence(); // the previous digit's reads of x0 come first
 #pragma unroll
                 for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
                 wave_lds_fence();
@@ -791,6 +807,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                 int bl = B_B;
                 if (LOGR > 6)
                 {
+                    wave_lds_fence();
 #pragma unroll
                     for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
                     wave_lds_fence();
@@ -802,6 +819,7 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                 }
                 // back to the coalesced layout of the key stream (integer: canonical digits
                 // keep the 128-bit sums exact for any digit count below 2^8)
+                wave_lds_fence();
 #pragma unroll
                 for (int e = 0; e < 8; e++)
                 {
@@ -843,8 +861,11 @@ __global__ __launch_bounds__(256, 2) void k_ks_row_mac(const u64 *__restrict__ i
                     mac128(a1[e], d[e], kk1[e]);
                 }
             }
+            if (MHE_KS_DPF)
+            {
 #pragma unroll
-            for (int e = 0; e < 8; e++) vin[e] = vnext[e];
+                for (int e = 0; e < 8; e++) vin[e] = vnext[e];
+            }
             if (KPF)
             {
 #pragma unroll
