@@ -206,6 +206,7 @@ struct mhe_ctx
     int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
+    int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };
@@ -436,6 +437,7 @@ struct JobModDownRow
     const Tw *invq; // [K][K]
     int L, K, log_n;
     int fixed_i = -1; // >= 0: one job per poly, all on limb fixed_i
+    int c1_write = 0; // 1: ct[1] = ModDown(acc[1]) instead of += (apply_galois: ct[1] was 0)
     struct View
     {
         u64 *buf;
@@ -445,11 +447,12 @@ struct JobModDownRow
         const Tw *tw;
         Tw inv;
         bool skip;
+        bool replace;
         __device__ u64 load(u32 x) const { return buf[x]; }
         __device__ void store(u32 x, u64 t) const
         {
             u64 v = mul_shoup(accp[x] + p.four_q - t, inv.x, inv.y, p.q);
-            ctp[x] = addmod(v, ctp[x], p.q);
+            ctp[x] = replace ? v : addmod(v, ctp[x], p.q); // 0 + v = v: the same word
         }
     };
     __device__ View view(int y) const
@@ -463,6 +466,7 @@ struct JobModDownRow
         v.tw = tw + ((size_t)i << log_n);
         v.inv = invq[(size_t)(K - 1) * K + i];
         v.skip = false;
+        v.replace = c1_write && k == 1;
         return v;
     }
 };
@@ -1168,8 +1172,11 @@ static int run_ntt_inv(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limb
 // ct += KS(target) the result of rescale_to_next(ct + KS(target)) goes to rescale_out
 // [2][L-1][n] (JobMDRCol / JobMDRRow); ct limb L-1 is overwritten on the way.
 static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key, int key_limbs, int L,
-                          hipStream_t st, u64 *rescale_out = nullptr)
+                          hipStream_t st, u64 *rescale_out = nullptr, int c1_write = 0)
 {
+    // c1_write: ct[1] is taken as zero and written, not read (target may then alias ct[1]: it is
+    // last read by the key MAC, before the ModDown writes ct)
+    if (c1_write && rescale_out) return fail(MHE_ERR_ARG, "key switch: c1_write with a fused rescale");
     if (key_limbs < L + 1 || key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
     // the key slice one switch streams: L digits x 2 polys x (L + 1) primes
     c->key_bytes += 2ull * (unsigned long long)L * (unsigned long long)(L + 1) * c->n * 8ull;
@@ -1250,6 +1257,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n };
             fwd_col(dc, log_n, 2 * L, c->nm, st);
             JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
+            dr.c1_write = c1_write;
             fwd_row(dr, log_n, 2 * L, c->nm, st);
         }
         else
@@ -1398,6 +1406,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_HMULT_FUSED")) c->hmult_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
     if (const char *f = getenv("MHE_KS_PACK")) c->ks_pack = atoi(f);
+    if (const char *f = getenv("MHE_GALOIS_FUSED")) c->galois_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_GROUPS")) c->ks_groups = atoi(f) > 8 ? 8 : atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);
@@ -2003,8 +2012,8 @@ MHE_EXPORT int mhe_apply_galois(mhe_ctx *c, uint64_t *ct, uint32_t elt, const ui
     HIP_TRY(mhe_internal_copy_d2d(ct, w->tmp, ps * sizeof(u64), st));
     r = launch_galois(c, ct + ps, elt, w->tmp, 1, limbs, st);
     if (r) return r;
-    HIP_TRY(hipMemsetAsync(ct + ps, 0, ps * sizeof(u64), st));
-    return run_switch_key(c, ct, w->tmp, key, key_limbs, limbs, st);
+    if (!c->galois_fused) HIP_TRY(hipMemsetAsync(ct + ps, 0, ps * sizeof(u64), st));
+    return run_switch_key(c, ct, w->tmp, key, key_limbs, limbs, st, nullptr, c->galois_fused); // c1 <- 0 + KS_1
 }
 
 MHE_EXPORT int mhe_apply_galois_to(mhe_ctx *c, const uint64_t *in, uint64_t *out, uint32_t elt, const uint64_t *key,
@@ -2021,7 +2030,14 @@ MHE_EXPORT int mhe_apply_galois_to(mhe_ctx *c, const uint64_t *in, uint64_t *out
     r = get_ws(c, st, c->K - 1, &w);
     if (r) return r;
     const size_t ps = (size_t)limbs << c->log_n;
-    // evaluator.cpp:2193-2214: out0 <- perm(c0), tmp <- perm(c1), out1 <- 0, then out += KS(tmp)
+    // evaluator.cpp:2193-2214: out0 <- perm(c0), out1 <- perm(c1) (one launch), then the key switch
+    // of out1 with out0 += KS_0 and out1 = KS_1 (SEAL zeroes c1 and adds; same words)
+    if (c->galois_fused)
+    {
+        r = launch_galois(c, in, elt, out, 2, limbs, st);
+        if (r) return r;
+        return run_switch_key(c, out, out + ps, key, key_limbs, limbs, st, nullptr, 1);
+    }
     r = launch_galois(c, in, elt, out, 1, limbs, st);
     if (r) return r;
     r = launch_galois(c, in + ps, elt, w->tmp, 1, limbs, st);
