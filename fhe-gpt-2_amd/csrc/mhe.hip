@@ -206,6 +206,7 @@ struct mhe_ctx
     int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
+    int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
     int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
@@ -402,12 +403,13 @@ struct JobModDownCol
         u64 half, fix;
         bool reduce;
         bool skip;
-        __device__ u64 load(u32 x) const
+        __device__ u64 lift(u64 s) const
         {
-            u64 t = barrett64(src[x] + half, P);
+            u64 t = barrett64(s + half, P);
             if (reduce) t = barrett64(t, p);
             return t + fix;
         }
+        __device__ u64 load(u32 x) const { return lift(src[x]); }
         __device__ void store(u32 x, u64 v) const { dst[x] = v; }
     };
     __device__ View view(int y) const
@@ -490,12 +492,13 @@ struct JobRescaleCol
         const Tw *tw;
         bool reduce;
         bool skip;
-        __device__ u64 load(u32 x) const
+        __device__ u64 lift(u64 s) const // s canonical mod q_last
         {
-            u64 v = csub(src[x] + half, ql);
+            u64 v = csub(s + half, ql);
             if (reduce) v = barrett64(v, p);
             return v + neg_half;
         }
+        __device__ u64 load(u32 x) const { return lift(src[x]); }
         __device__ void store(u32 x, u64 v) const { dst[x] = v; }
     };
     __device__ View view(int y) const
@@ -1251,11 +1254,18 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
         JobStrided j{ w->acc + (size_t)L * n, w->acc + (size_t)L * n, (size_t)(L + 1) * n, (size_t)(L + 1) * n,
                       c->K - 1, 0, c->primes, c->itw, log_n, 0 };
         inv_row(j, log_n, 2, c->nm, st);
-        inv_col(j, log_n, 2, c->nm, st);
+        // the special limbs' inverse column pass runs inside the lift column pass (k_icol_lift)
+        // (not in the HMult tail: JobMDRCol reads the fully inverse-transformed special limbs)
+        const ColSrc cs{ w->acc + (size_t)L * n, (size_t)(L + 1) * n, c->primes, c->itw, c->K - 1 };
+        const bool fuse = c->icol_fused && (!rescale_out || L < 2);
+        if (!fuse) inv_col(j, log_n, 2, c->nm, st);
         if (!rescale_out || L < 2)
         {
             JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n };
-            fwd_col(dc, log_n, 2 * L, c->nm, st);
+            if (fuse)
+                icol_lift(cs, dc, 2, L, log_n, c->nm, st);
+            else
+                fwd_col(dc, log_n, 2 * L, c->nm, st);
             JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
             dr.c1_write = c1_write;
             fwd_row(dr, log_n, 2 * L, c->nm, st);
@@ -1291,12 +1301,19 @@ static int run_rescale(mhe_ctx *c, const u64 *in, u64 *out, int size, int L, hip
     // last[s] = INTT(in[s][L-1]) canonical -> w->coeff (size <= 3 polys)
     JobLastInv li{ in, w->coeff, c->primes, c->itw, L, log_n, 1 };
     inv_row(li, log_n, size, c->nm, st);
+    JobRescaleCol rc{ w->coeff, w->modup, c->primes, c->tw, L, log_n };
+    if (c->icol_fused)
+    {
+        // the last limb's inverse column pass runs inside the lift column pass (k_icol_lift)
+        const ColSrc cs{ w->coeff, c->n, c->primes, c->itw, L - 1 };
+        icol_lift(cs, rc, size, L - 1, log_n, c->nm, st);
+    }
+    else
     {
         JobStrided j2{ w->coeff, w->coeff, c->n, c->n, L - 1, 0, c->primes, c->itw, log_n, 1 };
         inv_col(j2, log_n, size, c->nm, st);
+        fwd_col(rc, log_n, size * (L - 1), c->nm, st);
     }
-    JobRescaleCol rc{ w->coeff, w->modup, c->primes, c->tw, L, log_n };
-    fwd_col(rc, log_n, size * (L - 1), c->nm, st);
     JobRescaleRow rr{ w->modup, in, out, c->primes, c->tw, c->invq, L, c->K, log_n };
     fwd_row(rr, log_n, size * (L - 1), c->nm, st);
     HIP_LAUNCH_CHECK();
@@ -1407,6 +1424,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
     if (const char *f = getenv("MHE_KS_PACK")) c->ks_pack = atoi(f);
     if (const char *f = getenv("MHE_GALOIS_FUSED")) c->galois_fused = atoi(f);
+    if (const char *f = getenv("MHE_ICOL_FUSED")) c->icol_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_GROUPS")) c->ks_groups = atoi(f) > 8 ? 8 : atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);

@@ -400,6 +400,98 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long t
     for (int e = 0; e < E; e++) V.store(c + ((u32)(t + TPS * e) << logC), ar.out(v[e]));
 }
 
+// ------------------------------------ inverse column pass fused with a lift + forward column pass
+// ModDown (evaluator.cpp:2466-2524) and rescale (rns.cpp:737-808) both take one limb (the special
+// prime's accumulator / the last limb) through an INTT, lift it into every other prime and
+// forward-transform it.  After the inverse column stages a lane holds exactly the positions the
+// forward column pass loads, so one workgroup per (column block, poly, group of output primes)
+// finishes the INTT of its columns once (canonical), then for each output prime lifts (the job's
+// View::lift) and runs the forward column stages: the separate inverse-column launch and its HBM
+// round trip disappear, and the outputs are the same words.
+struct ColSrc
+{
+    const u64 *src;       // poly s at src + s * stride, after the inverse row pass
+    size_t stride;
+    const PrimeDev *primes;
+    const Tw *itw;        // inverse twiddle rows
+    int pi;               // prime index of the source limb
+};
+
+template <int LOGR, int LOGT, class Job, bool FP>
+__global__ __launch_bounds__(256) void k_icol_lift(ColSrc cs, Job job, int cnt, int log_n, long long dinv,
+                                                   long long dfwd)
+{
+    using SH = Shape<LOGR, LOGT>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
+    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
+    __shared__ T lds[S * LD];
+    const int tid = threadIdx.x, sl = tid % S, t = tid / S;
+    const int logC = log_n - LOGR;
+    const u32 c = blockIdx.x * S + sl;
+    const int s = blockIdx.y;
+    const int IG = gridDim.z, g = blockIdx.z;
+    const int i_lo = (cnt * g) / IG, i_hi = (cnt * (g + 1)) / IG;
+    u64 x[E];
+    {
+        // the inverse column pass of k_inv_col, canonical output
+        const PrimeDev P = cs.primes[cs.pi];
+        const A ai(P, cs.itw + ((size_t)cs.pi << log_n), dinv);
+        const u64 *src = cs.src + (size_t)s * cs.stride;
+        T v[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) v[e] = ai.in(src[c + ((u32)(E * t + e) << logC)]);
+#pragma unroll
+        for (int st = LOGR - 1; st >= LOGE; st--)
+            ai.template inv<E>(v, 1 << (LOGR - 1 - st), [&](int e) { return (1 << st) + ((E * t + e) >> (LOGR - st)); });
+#pragma unroll
+        for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; e++) v[e] = lds[sl * LD + t + TPS * e];
+#pragma unroll
+        for (int st = LOGE - 1; st >= 1; st--)
+            ai.template inv<E>(v, 1 << (LOGE - 1 - st), [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+        {
+            constexpr int gap = E / 2;
+#pragma unroll
+            for (int e = 0; e < gap; e++) ai.inv_last(v[e], v[e + gap], P);
+        }
+#pragma unroll
+        for (int e = 0; e < E; e++)
+        {
+            if constexpr (FP)
+                x[e] = ai.out(v[e]);
+            else
+                x[e] = ai.canon(v[e]);
+        }
+    }
+    // x[e] is the coefficient at c + ((t + TPS e) << logC): the forward column pass's load order
+    for (int i = i_lo; i < i_hi; i++)
+    {
+        const auto V = job.view(s * cnt + i);
+        const A ar(V.p, V.tw, dfwd);
+        T v[E];
+#pragma unroll
+        for (int e = 0; e < E; e++) v[e] = ar.in(V.lift(x[e]));
+#pragma unroll
+        for (int st = 0; st < LOGE; st++)
+            ar.template fwd<E>(v, 1 << (LOGE - 1 - st), [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+        __syncthreads(); // lds still holds the previous prime's (or the inverse pass's) transpose
+#pragma unroll
+        for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+#pragma unroll
+        for (int st = LOGE; st < LOGR; st++)
+            ar.template fwd<E>(v, 1 << (LOGR - 1 - st),
+                               [&](int e) { return (1 << st) + ((E * t + e) >> (LOGR - st)); });
+#pragma unroll
+        for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
+    }
+}
+
 // ------------------------------------------------- key-switch ModUp, digit-major column pass
 // Column pass of the ModUp (evaluator.cpp:2386-2408) with one workgroup per (column block,
 // digit J, group of output primes): the digit's columns are read once into registers and
@@ -594,6 +686,47 @@ static inline void launch_row(const Job &job, int log_n, int jobs, const NttMode
     }
 }
 
+// k_icol_lift over `polys` source polys and `cnt` output primes each (job index s * cnt + i), the
+// column-pass shape of launch_col; IG groups of output primes per (column block, poly)
+template <int LOGR, class Job, bool FP>
+static inline void icol_lift_a(const ColSrc &cs, const Job &job, int polys, int cnt, int log_n, long long dinv,
+                               long long dfwd, hipStream_t st)
+{
+    constexpr int LOGT = LOGR <= 7 ? 3 : 4;
+    using SH = Shape<LOGR, LOGT>;
+    const int subs = 1 << (log_n - LOGR);
+    // one output prime per group (MHE_ICOL_GROUP primes per group): the grid stays as wide as the
+    // separate forward column pass's, and each workgroup redoes the cheap inverse stages of its
+    // columns from L2
+    static const int per = [] {
+        const char *e = getenv("MHE_ICOL_GROUP");
+        return e && atoi(e) > 0 ? atoi(e) : 1;
+    }();
+    const int IG = (cnt + per - 1) / per;
+    hipLaunchKernelGGL((k_icol_lift<LOGR, LOGT, Job, FP>), dim3(subs / SH::S, polys, IG), dim3(256), 0, st, cs, job,
+                       cnt, log_n, dinv, dfwd);
+}
+template <class Job>
+static inline void icol_lift(const ColSrc &cs, const Job &job, int polys, int cnt, int log_n, const NttMode &m,
+                             hipStream_t st)
+{
+    if (cnt <= 0 || polys <= 0) return;
+    switch ((log_n + 1) / 2)
+    {
+    case 6:
+        if (m.fp) icol_lift_a<6, Job, true>(cs, job, polys, cnt, log_n, m.dinv, m.dfwd, st);
+        else icol_lift_a<6, Job, false>(cs, job, polys, cnt, log_n, 0, 0, st);
+        break;
+    case 7:
+        if (m.fp) icol_lift_a<7, Job, true>(cs, job, polys, cnt, log_n, m.dinv, m.dfwd, st);
+        else icol_lift_a<7, Job, false>(cs, job, polys, cnt, log_n, 0, 0, st);
+        break;
+    case 8:
+        if (m.fp) icol_lift_a<8, Job, true>(cs, job, polys, cnt, log_n, m.dinv, m.dfwd, st);
+        else icol_lift_a<8, Job, false>(cs, job, polys, cnt, log_n, 0, 0, st);
+        break;
+    }
+}
 template <class Job> static inline void fwd_col(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_col<FWD_COL>(j, log_n, jobs, m, st); }
 template <class Job> static inline void fwd_row(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_row<FWD_ROW>(j, log_n, jobs, m, st); }
 template <class Job> static inline void inv_row(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_row<INV_ROW>(j, log_n, jobs, m, st); }
