@@ -492,6 +492,50 @@ def test_engine_variants_bit_exact(variant):
     assert np.array_equal(ch.down(ch.eng.ntt_inverse(ch.up(x))), ch.oc.ntt(x, O.NTT_INV))
 
 
+# ------------------------------ n = 2^16 variants: packed intermediate, fused ModDown / galois
+# The 48-bit ModUp intermediate (ntt.h tile16) only exists at n = 2^16 for output primes < 2^48,
+# so these run on the 7+1-prime chain at log n = 16 (four 46-bit primes): the integer path with
+# packing, and each fusion switched off, all against the oracle word for word.
+N16_VARIANTS = [
+    {},                                                # defaults: FP64, packed, fused
+    {"MHE_FP": "0"},                                   # integer butterflies + packed intermediate
+    {"MHE_KS_PACK": "0"},                              # 64-bit intermediate
+    {"MHE_ICOL_FUSED": "0", "MHE_GALOIS_FUSED": "0"},  # separate inverse column pass, SEAL's galois order
+    {"MHE_ICOL_FUSED": "1", "MHE_HMULT_FUSED": "0"},   # fused inverse column pass in the plain ModDown
+]
+
+
+@pytest.mark.parametrize("variant", range(len(N16_VARIANTS)))
+def test_n16_variants_bit_exact(variant):
+    import os
+
+    env = N16_VARIANTS[variant]
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ch = Chain(16, SMALL_BITS, seed=70 + variant)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    key = ch.rand_key()
+    for L in (2, ch.K - 1):
+        ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+        got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
+        assert np.array_equal(got, ch.oc.switch_key(ct, target, key)), (env, L)
+    L = ch.K - 1
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    assert np.array_equal(ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key))), ch.oc.hmult(a, b, key)), env
+    x = ch.rand(2, L, ch.n)
+    assert np.array_equal(ch.down(ch.eng.rescale_to_next(ch.up(x))), ch.oc.rescale(x)), env
+    elt = mhe.galois_elt_from_step(16, 3)
+    want = ch.oc.apply_galois(x, elt, key)
+    assert np.array_equal(ch.down(ch.eng.apply_galois_to(ch.up(x), elt, ch.up(key))), want), env
+    assert np.array_equal(ch.down(ch.eng.apply_galois(ch.up(x), elt, ch.up(key))), want), env
+
+
 # ----------------------------------------------------------------- CKKS encode (A13, A14)
 @pytest.mark.parametrize("kind", ["real", "complex", "partial"])
 def test_ckks_encode_bit_exact(small, kind):
