@@ -35,17 +35,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 MIB = 1 << 20
 
 
-def hmult_bytes(L):
+def hmult_bytes(L, key_bytes=None):
     """Algorithmic HBM bytes of one HMult: 2 input cts (2L MiB) + relin key
-    slice (L(L+1) MiB) + output ct ((L-1) MiB) = L^2 + 4L - 1 MiB."""
-    return (L * L + 4 * L - 1) * MIB
+    slice (L(L+1) MiB in SEAL's layout) + output ct ((L-1) MiB) = L^2 + 4L - 1 MiB; with a
+    prepared key the key term is the prepared slice's bytes (ks_row_mac_key_bytes)."""
+    if key_bytes is None:
+        return (L * L + 4 * L - 1) * MIB
+    return (3 * L - 1) * MIB + key_bytes
 
 
-def ks_row_mac_key_bytes(L, n):
+def ks_row_mac_key_bytes(L, n, moduli=None, prepared=False):
     """Algorithmic HBM bytes of one k_ks_row_mac launch (SURVEY.md §8(d) key slice): every key
-    limb it multiplies against is read once, 2 polys x L digits x (L+1) primes x n x 8 B; the
-    ModUp intermediate it also reads is not algorithmic (it is what fusion should remove)."""
-    return 2 * L * (L + 1) * n * 8
+    limb it multiplies against is read once, 2 polys x L digits x (L+1) primes x n residues, 8 B
+    each in SEAL's layout; a prepared key (mhe_key_prepare) holds the limbs of primes below 2^48
+    in 6 B.  The ModUp intermediate the kernel also reads is not algorithmic."""
+    if not prepared:
+        return 2 * L * (L + 1) * n * 8
+    primes = list(moduli[:L]) + [moduli[-1]]
+    return sum(2 * L * n * (6 if q < (1 << 48) else 8) for q in primes)
 
 
 def rand_residues(shape, moduli_t, gen):
@@ -228,6 +235,9 @@ def main():
                     help="20: config C3 (ResNet-20); 110: config C4's network (ResNet-110, one image per GPU "
                          "with --resnet-images 1 --resnet-streams 1)")
     ap.add_argument("--resnet-streams", type=int, default=4, help="images in flight per GPU (one stream each)")
+    ap.add_argument("--key-format", choices=("prepared", "seal"), default="prepared",
+                    help="relin key as the engine's prepared format (mhe_key_prepare, 48-bit planes for "
+                         "primes < 2^48; bit-identical results) or SEAL's u64 layout")
     ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams the batch is spread over (round robin; 4 = the hardware queues per process)")
     args = ap.parse_args()
@@ -258,6 +268,10 @@ def main():
         g0.manual_seed(7)
         key.copy_(rand_residues((K - 1, 2, K, n), q_t, g0))
     broadcast_key(key, src=0)
+    prepared = args.key_format == "prepared"
+    if prepared:  # one-time conversion to the engine's key format, outside the timed region
+        eng.key_prepare(key)
+        torch.cuda.synchronize(dev)
     B = args.batch
     a = rand_residues((B, 2, L, n), q_t[:L], gen)
     b = rand_residues((B, 2, L, n), q_t[:L], gen)
@@ -346,8 +360,9 @@ def main():
     hmults_per_gpu = B * args.steps
     value = world * hmults_per_gpu / elapsed
     per_hmult_s = gpu_s / hmults_per_gpu  # HIP-event time per HMult (batch over its streams)
-    achieved = hmult_bytes(L) / per_hmult_s / 1e9
-    km_bytes = ks_row_mac_key_bytes(L, n)
+    km_bytes = ks_row_mac_key_bytes(L, n, moduli, prepared)
+    hm_bytes = hmult_bytes(L, km_bytes)
+    achieved = hm_bytes / per_hmult_s / 1e9
     km_achieved = km_bytes / (km_avg_us * 1e-6) / 1e9 if km_avg_us > 0 else 0.0
     result = {
         "metric": "homomorphic ciphertext mults/sec (N=2^16, L limbs)",
@@ -381,6 +396,8 @@ def main():
             "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, gfx950-corrected)",
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": km_bytes,
+            "key_format": args.key_format,
+            "seal_layout_key_bytes_per_launch": ks_row_mac_key_bytes(L, n),
             "avg_launch_us": round(km_avg_us, 2),
             "launches_timed": km_n.value,
             "timing": "HIP events around each launch on its stream; single-stream pass when --streams > 1",
@@ -394,7 +411,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "traffic_unit": "HBM bytes per HMult (PMC)",
-            "algorithmic_bytes_per_hmult": hmult_bytes(L),
+            "algorithmic_bytes_per_hmult": hm_bytes,
             "us_per_hmult": round(per_hmult_s * 1e6, 2),
         },
     }

@@ -212,6 +212,30 @@ struct mhe_ctx
     std::map<hipStream_t, Workspace> ws;
 };
 
+// Key limbs of a prepared key that the fused MAC reads packed: primes below 2^48 (ntt.h load_key).
+static bool key_limb_packed(const mhe_ctx *c, int limb, int key_limbs)
+{
+    const int pi = (limb == key_limbs - 1) ? c->K - 1 : limb;
+    return c->q[pi] < (1ull << 48);
+}
+
+// Is `key` in the prepared format?  Reads the tag word of its first packed slot (host sync:
+// only prepare / unprepare and the separate-MAC debugging path ask).
+static int key_tagged(mhe_ctx *c, const u64 *key, int key_limbs, hipStream_t st, int *tagged)
+{
+    *tagged = 0;
+    for (int l = 0; l < key_limbs; l++)
+        if (key_limb_packed(c, l, key_limbs))
+        {
+            u64 w = 0;
+            HIP_TRY(hipMemcpyAsync(&w, key + (size_t)l * c->n + c->n - 1, 8, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            *tagged = (w == KEY_PACK_TAG) ? 1 : 0;
+            return MHE_OK;
+        }
+    return MHE_OK;
+}
+
 // Events around a launch of kernel kind k on stream st when timing is on.
 static hipEvent_t *timing_slot(mhe_ctx *c, Workspace *w, int k, hipStream_t st)
 {
@@ -1181,6 +1205,18 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
     // last read by the key MAC, before the ModDown writes ct)
     if (c1_write && rescale_out) return fail(MHE_ERR_ARG, "key switch: c1_write with a fused rescale");
     if (key_limbs < L + 1 || key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
+    // a prepared key (mhe_key_prepare) is recognised by the fused MAC itself (KEY_PACK_TAG in
+    // each packed slot); the separate-MAC debugging path reads SEAL's layout only
+    int kpack = 1;
+    if (!c->ks_fused)
+    {
+        int tagged = 0;
+        int r0 = key_tagged(c, key, key_limbs, st, &tagged);
+        if (r0) return r0;
+        kpack = tagged;
+    }
+    if (kpack && !c->ks_fused) return fail(MHE_ERR_ARG, "key switch: prepared keys need the fused key MAC");
+    if (!c->ks_fused) kpack = 0;
     // the key slice one switch streams: L digits x 2 polys x (L + 1) primes
     c->key_bytes += 2ull * (unsigned long long)L * (unsigned long long)(L + 1) * c->n * 8ull;
     Workspace *w;
@@ -1222,7 +1258,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             timing_end(tc, st);
             hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
             ks_row_mac_chunk(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, c->nm, G, I0,
-                             cnt, pack, st);
+                             cnt, pack, kpack, st);
             timing_end(tm, st);
         }
         ks_acc_finish(w->acc, c->primes, L, c->K, G, log_n, st);
@@ -1796,6 +1832,90 @@ MHE_EXPORT int mhe_key_traffic(mhe_ctx *c, uint64_t *bytes, int reset)
     if (!valid_ctx(c) || !bytes) return fail(MHE_ERR_ARG, "invalid argument");
     *bytes = reset ? c->key_bytes.exchange(0) : c->key_bytes.load();
     return MHE_OK;
+}
+
+// Pack (dir 1) or unpack (dir 0) the limb slots of one digit of a key: src is a copy of the
+// digit's 2 x key_limbs slots, dst the key's.  Packed slot of a prime below 2^48: a 32-bit plane
+// [n] then a 16-bit plane [n] (natural order); other slots are copied unchanged.
+__global__ void k_key_pack(const u64 *__restrict__ src, u64 *__restrict__ dst, const unsigned char *__restrict__ packed,
+                           int key_limbs, int log_n, int dir)
+{
+    const size_t n = (size_t)1 << log_n;
+    const int slot = blockIdx.y; // poly * key_limbs + limb
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const u64 *s = src + (size_t)slot * n;
+    u64 *d = dst + (size_t)slot * n;
+    if (!packed[slot % key_limbs])
+    {
+        d[i] = s[i];
+        return;
+    }
+    if (dir)
+    {
+        const u64 v = s[i];
+        reinterpret_cast<u32 *>(d)[i] = (u32)v;
+        reinterpret_cast<unsigned short *>(reinterpret_cast<u32 *>(d) + n)[i] = (unsigned short)(v >> 32);
+        if (i == n - 1) d[n - 1] = KEY_PACK_TAG; // in the slot's unused last quarter
+    }
+    else
+    {
+        const u32 lo = reinterpret_cast<const u32 *>(s)[i];
+        const unsigned short hi = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(s) + n)[i];
+        d[i] = (u64)lo | ((u64)hi << 32);
+    }
+}
+
+static int key_pack_run(mhe_ctx *c, u64 *key, int digits, int key_limbs, int dir, hipStream_t st)
+{
+    const size_t n = c->n, slots = 2 * (size_t)key_limbs;
+    std::vector<unsigned char> pk(key_limbs);
+    for (int l = 0; l < key_limbs; l++) pk[l] = key_limb_packed(c, l, key_limbs) ? 1 : 0;
+    HIP_TRY(hipSetDevice(c->device));
+    u64 *tmp = nullptr;
+    unsigned char *pkd = nullptr;
+    if (hipMalloc(&tmp, slots * n * sizeof(u64) + 256) != hipSuccess) return fail(MHE_ERR_MEMORY, "key prepare: scratch allocation failed");
+    pkd = reinterpret_cast<unsigned char *>(tmp + slots * n);
+    int rc = MHE_OK;
+    if (hipMemcpyAsync(pkd, pk.data(), key_limbs, hipMemcpyHostToDevice, st) != hipSuccess) rc = fail(MHE_ERR_DEVICE, "key prepare: copy");
+    for (int J = 0; J < digits && rc == MHE_OK; J++)
+    {
+        u64 *dg = key + (size_t)J * slots * n;
+        if (hipMemcpyAsync(tmp, dg, slots * n * sizeof(u64), hipMemcpyDeviceToDevice, st) != hipSuccess)
+        {
+            rc = fail(MHE_ERR_DEVICE, "key prepare: copy");
+            break;
+        }
+        hipLaunchKernelGGL(k_key_pack, dim3((unsigned)((n + 255) / 256), (unsigned)slots), dim3(256), 0, st, tmp, dg,
+                           pkd, key_limbs, c->log_n, dir);
+        if (hipGetLastError() != hipSuccess) rc = fail(MHE_ERR_DEVICE, "key prepare: launch");
+    }
+    // the scratch is freed only after the stream has used it
+    if (hipStreamSynchronize(st) != hipSuccess && rc == MHE_OK) rc = fail(MHE_ERR_DEVICE, "key prepare: sync");
+    (void)hipFree(tmp);
+    return rc;
+}
+
+MHE_EXPORT int mhe_key_prepare(mhe_ctx *c, uint64_t *key, int digits, int key_limbs, void *s)
+{
+    if (!valid_ctx(c) || !key || digits < 1 || key_limbs < 2 || key_limbs > c->K || digits > key_limbs - 1)
+        return fail(MHE_ERR_ARG, "invalid argument");
+    int tagged = 0;
+    int r = key_tagged(c, key, key_limbs, S(s), &tagged);
+    if (r) return r;
+    if (tagged) return fail(MHE_ERR_ARG, "key prepare: key is already prepared");
+    return key_pack_run(c, key, digits, key_limbs, 1, S(s));
+}
+
+MHE_EXPORT int mhe_key_unprepare(mhe_ctx *c, uint64_t *key, int digits, int key_limbs, void *s)
+{
+    if (!valid_ctx(c) || !key || digits < 1 || key_limbs < 2 || key_limbs > c->K || digits > key_limbs - 1)
+        return fail(MHE_ERR_ARG, "invalid argument");
+    int tagged = 0;
+    int r = key_tagged(c, key, key_limbs, S(s), &tagged);
+    if (r) return r;
+    if (!tagged) return fail(MHE_ERR_ARG, "key unprepare: key is not prepared");
+    return key_pack_run(c, key, digits, key_limbs, 0, S(s));
 }
 
 MHE_EXPORT int mhe_stream_wait(mhe_ctx *c, void *waiter, void *waitee)

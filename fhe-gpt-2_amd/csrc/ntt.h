@@ -59,6 +59,10 @@ __device__ __forceinline__ u32 tile16(u32 idx)
     const u32 r = idx >> 8, c = idx & 255;
     return ((((r >> 4) << 4) | (c >> 4)) << 8) | ((r & 15) << 4) | (c & 15);
 }
+// Prepared key (mhe_key_prepare): every limb slot of a prime below 2^48 holds a 32-bit plane [n],
+// a 16-bit plane [n] and, in its last word, this tag -- never a residue of a SEAL key (>= 2^63),
+// so the key MAC tells a prepared key from SEAL's layout by itself.
+#define KEY_PACK_TAG 0xF0E1D2C3B4A59687ull
 __device__ __forceinline__ bool inter_packed(int pack, u64 q)
 {
     return pack && q < (1ull << 48);
@@ -806,7 +810,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__res
                                                        u64 *__restrict__ acc,          // [G][2][L+1][n]
                                                        const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int key_limbs,
-                                                       int log_n, long long twd, int I0, int pack)
+                                                       int log_n, long long twd, int I0, int pack, int kpack)
 {
     using SH = RowMacShape<LOGR>;
     using A = NttArith<FP>;
@@ -899,14 +903,34 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__res
 
         // key limbs of a digit: issued one digit ahead (KPF) or at the top of the digit (the
         // fewer-VGPR variant), consumed after the digit's NTT
+        // a prepared key (mhe_key_prepare) holds the limbs of primes below 2^48 as a 32-bit plane
+        // [n] and a 16-bit plane [n] in natural order (6 of the slot's 8 bytes per residue)
+        const bool kpk = kpack && p.q < (1ull << 48) && key[(size_t)ki * n + n - 1] == KEY_PACK_TAG; // uniform
         auto load_key = [&](int J, u64 (&ka)[8], u64 (&kb)[8]) {
-            const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n + base;
+            const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
             const u64 *k1 = k0 + kstride;
-#pragma unroll
-            for (int e = 0; e < 8; e++)
+            if (kpk)
             {
-                ka[e] = ld_nt<1>(&k0[lay(t, e, B_A)]);
-                kb[e] = ld_nt<1>(&k1[lay(t, e, B_A)]);
+                const u32 *l0 = reinterpret_cast<const u32 *>(k0) + base;
+                const u32 *l1 = reinterpret_cast<const u32 *>(k1) + base;
+                const unsigned short *h0 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k0) + n) + base;
+                const unsigned short *h1 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k1) + n) + base;
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    const u32 r = lay(t, e, B_A);
+                    ka[e] = (u64)ld_nt<1>(&l0[r]) | ((u64)ld_nt<1>(&h0[r]) << 32);
+                    kb[e] = (u64)ld_nt<1>(&l1[r]) | ((u64)ld_nt<1>(&h1[r]) << 32);
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    ka[e] = ld_nt<1>(&k0[base + lay(t, e, B_A)]);
+                    kb[e] = ld_nt<1>(&k1[base + lay(t, e, B_A)]);
+                }
             }
         };
         u64 kk0[8], kk1[8];
@@ -1076,42 +1100,43 @@ static inline int ks_groups(int L)
 template <int LOGR, bool FP>
 static inline void ks_row_mac_a(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
                                 const Tw *tw, int L, int K, int key_limbs, int log_n, long long twd, int G, int I0,
-                                int cnt, int pack, hipStream_t st)
+                                int cnt, int pack, int kpack, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
     const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, G);
     if (ks_key_prefetch())
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, inter, target, key, acc, primes, tw,
-                           L, K, key_limbs, log_n, twd, I0, pack);
+                           L, K, key_limbs, log_n, twd, I0, pack, kpack);
     else
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, inter, target, key, acc, primes,
-                           tw, L, K, key_limbs, log_n, twd, I0, pack);
+                           tw, L, K, key_limbs, log_n, twd, I0, pack, kpack);
 }
 
 template <int LOGR>
 static inline void ks_row_mac_m(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
                                 const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, int G, int I0,
-                                int cnt, int pack, hipStream_t st)
+                                int cnt, int pack, int kpack, hipStream_t st)
 {
     if (m.fp)
         ks_row_mac_a<LOGR, true>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m.dfwd, G, I0, cnt, pack,
-                                 st);
+                                 kpack, st);
     else
-        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, I0, cnt, pack, st);
+        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, I0, cnt, pack,
+                                  kpack, st);
 }
 
 // Fused row pass + MAC for output primes I0 .. I0+cnt-1 (inter holds exactly those).
 static inline void ks_row_mac_chunk(const u64 *inter, const u64 *target, const u64 *key, u64 *acc,
                                     const PrimeDev *primes, const Tw *tw, int L, int K, int key_limbs, int log_n,
-                                    const NttMode &m, int G, int I0, int cnt, int pack, hipStream_t st)
+                                    const NttMode &m, int G, int I0, int cnt, int pack, int kpack, hipStream_t st)
 {
     switch (log_n / 2)
     {
-    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, st); break;
-    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, st); break;
+    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, kpack, st); break;
+    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, kpack, st); break;
     case 8:
         ks_row_mac_m<8>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt,
-                        (pack && log_n == 16) ? 1 : 0, st);
+                        (pack && log_n == 16) ? 1 : 0, kpack, st);
         break;
     }
 }

@@ -41,6 +41,8 @@ SIGNATURES = {
     "mhe_stream_wait": (ctypes.c_int, [vp, vp, vp]),
     "mhe_multiply_plain_add": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_traffic": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "mhe_key_prepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_key_unprepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     "mhe_stream_destroy": (ctypes.c_int, [vp, vp]),
     "mhe_ntt_forward": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]),
@@ -287,6 +289,17 @@ class Engine:
     @staticmethod
     def _key_limbs(key):
         return key.shape[2]  # [digits][2][key_limbs][n]
+
+    def key_prepare(self, key):
+        """mhe_key_prepare: convert `key` [digits][2][key_limbs][n] in place to the engine's packed
+        key format (48-bit planes for primes below 2^48); switches given it stay bit-identical."""
+        _check(lib().mhe_key_prepare(self._h, _ptr(key), key.shape[0], self._key_limbs(key), self.stream()))
+        return key
+
+    def key_unprepare(self, key):
+        """mhe_key_unprepare: back to SEAL's key layout."""
+        _check(lib().mhe_key_unprepare(self._h, _ptr(key), key.shape[0], self._key_limbs(key), self.stream()))
+        return key
 
     def switch_key(self, ct, target, key):
         _check(lib().mhe_switch_key(self._h, _ptr(ct), _ptr(target), _ptr(key), self._key_limbs(key), ct.shape[1],

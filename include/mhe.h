@@ -132,6 +132,16 @@ int mhe_ct_square(mhe_ctx *ctx, const uint64_t *a, uint64_t *out3, int limbs, vo
  * limb i is limb i.  A full SEAL key has key_limbs = chain count and digits = count-1; a
  * level-truncated slice for L-limb ciphertexts may keep only L digits and L+1 limbs. */
 
+/* Engine key format (optional, no SEAL counterpart; the role of SEAL's KSwitchKeys
+ * storage, keygenerator.cpp:384-414).  Converts a key of `digits` digits and `key_limbs` limbs
+ * in place: each limb slot of a prime below 2^48 then holds a 32-bit plane [n], a 16-bit plane
+ * [n] and a tag word (>= 2^63, never a residue) in its unused last quarter, so the key MAC
+ * streams 6 instead of 8 bytes per residue and recognises the format by itself; every key
+ * switch stays bit-identical.  The buffer is not a SEAL key again until mhe_key_unprepare.
+ * Preparing a prepared key (or unpreparing a SEAL key) fails with MHE_ERR_ARG. */
+int mhe_key_prepare(mhe_ctx *ctx, uint64_t *key, int digits, int key_limbs, void *stream);
+int mhe_key_unprepare(mhe_ctx *ctx, uint64_t *key, int digits, int key_limbs, void *stream);
+
 /* Evaluator::switch_key_inplace (evaluator.cpp:2281-2525): ct[2][L][n] += KS(target[L][n]). */
 int mhe_switch_key(mhe_ctx *ctx, uint64_t *ct, const uint64_t *target, const uint64_t *key, int key_limbs,
                    int limbs, void *stream);

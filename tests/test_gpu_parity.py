@@ -284,6 +284,46 @@ def test_hmult_small(small):
     assert np.array_equal(got, ch.oc.hmult(a, b, key))
 
 
+def test_prepared_key_bit_exact(small):
+    """mhe_key_prepare (engine key format: 48-bit planes for primes below 2^48) leaves every key
+    switch bit-identical -- full and level-truncated keys, switch / relinearize / rotate / HMult --
+    and mhe_key_unprepare restores SEAL's layout word for word."""
+    ch = small
+    key = ch.rand_key()
+    dkey = ch.up(key)
+    ch.eng.key_prepare(dkey)
+    packed = ch.down(dkey)
+    assert not np.array_equal(packed, key)  # the 46-bit limbs are repacked and tagged
+    assert np.array_equal(packed[:, :, 0], key[:, :, 0]) and np.array_equal(packed[:, :, -1], key[:, :, -1])  # 51-bit
+    lo = packed[:, :, 1].view(np.uint32)[..., : ch.n]
+    hi = packed[:, :, 1].view(np.uint16)[..., 2 * ch.n: 3 * ch.n]
+    assert np.array_equal(lo.astype(np.uint64) | (hi.astype(np.uint64) << 32), key[:, :, 1])
+    assert (packed[:, :, 1, -1] == 0xF0E1D2C3B4A59687).all()
+    for L in (1, 5, ch.K - 1):
+        ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+        got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), dkey))
+        assert np.array_equal(got, ch.oc.switch_key(ct, target, key)), L
+    L = ch.K - 1
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    assert np.array_equal(ch.down(ch.eng.hmult(ch.up(a), ch.up(b), dkey)), ch.oc.hmult(a, b, key))
+    elt = mhe.galois_elt_from_step(ch.log_n, 3)
+    ct = ch.rand(2, 5, ch.n)
+    assert np.array_equal(ch.down(ch.eng.apply_galois_to(ch.up(ct), elt, dkey)), ch.oc.apply_galois(ct, elt, key))
+    with pytest.raises(mhe.MheError):
+        ch.eng.key_prepare(dkey)  # already prepared
+    ch.eng.key_unprepare(dkey)
+    assert np.array_equal(ch.down(dkey), key)
+    # a level-truncated slice, prepared on its own
+    Lt = 4
+    trunc = np.concatenate([key[:Lt, :, :Lt], key[:Lt, :, -1:]], axis=2).copy()
+    dt = ch.eng.key_prepare(ch.up(trunc))
+    ct, target = ch.rand(2, Lt, ch.n), ch.rand(Lt, ch.n)
+    got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), dt))
+    assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
+    ch.eng.key_unprepare(dt)
+    assert np.array_equal(ch.down(dt), trunc)
+
+
 def test_errors_are_reported(small):
     ch = small
     key = ch.up(ch.rand_key())
@@ -345,6 +385,18 @@ def test_hmult_c2_full_bit_exact(c2):
     got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
     want = ch.oc.hmult(a, b, key)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.slow
+def test_hmult_c2_prepared_key_bit_exact(c2):
+    """The bench's key format (mhe_key_prepare) at the C2 size: HMult bit-identical to the oracle."""
+    ch = c2
+    L = ch.K - 1
+    key = ch.rand_key()
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    dkey = ch.eng.key_prepare(ch.up(key))
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), dkey))
+    assert np.array_equal(got, ch.oc.hmult(a, b, key))
 
 
 @pytest.mark.slow
