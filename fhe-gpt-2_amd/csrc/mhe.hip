@@ -186,6 +186,7 @@ enum TimedKernel
 struct mhe_ctx
 {
     std::atomic<unsigned long long> key_bytes{ 0 }; // key-switching key bytes read since reset (mhe_key_traffic)
+    std::atomic<unsigned long long> key_bytes_prep{ 0 }; // the same slices' bytes in the prepared key format
     int device = 0;
     int log_n = 0;
     size_t n = 0;
@@ -1219,6 +1220,11 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
     if (!c->ks_fused) kpack = 0;
     // the key slice one switch streams: L digits x 2 polys x (L + 1) primes
     c->key_bytes += 2ull * (unsigned long long)L * (unsigned long long)(L + 1) * c->n * 8ull;
+    {
+        unsigned long long per = 0; // bytes per residue over the slice's L + 1 limbs, prepared format
+        for (int l = 0; l <= L; l++) per += key_limb_packed(c, l == L ? key_limbs - 1 : l, key_limbs) ? 6 : 8;
+        c->key_bytes_prep += 2ull * (unsigned long long)L * c->n * per;
+    }
     Workspace *w;
     int r = get_ws(c, st, c->K - 1, &w);
     if (r) return r;
@@ -1916,6 +1922,19 @@ MHE_EXPORT int mhe_key_unprepare(mhe_ctx *c, uint64_t *key, int digits, int key_
     if (r) return r;
     if (!tagged) return fail(MHE_ERR_ARG, "key unprepare: key is not prepared");
     return key_pack_run(c, key, digits, key_limbs, 0, S(s));
+}
+
+MHE_EXPORT int mhe_key_traffic_prepared(mhe_ctx *c, uint64_t *bytes, int reset)
+{
+    if (!valid_ctx(c) || !bytes) return fail(MHE_ERR_ARG, "invalid argument");
+    *bytes = reset ? c->key_bytes_prep.exchange(0) : c->key_bytes_prep.load();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_key_is_prepared(mhe_ctx *c, const uint64_t *key, int key_limbs, int *prepared, void *s)
+{
+    if (!valid_ctx(c) || !key || !prepared || key_limbs < 2 || key_limbs > c->K) return fail(MHE_ERR_ARG, "invalid argument");
+    return key_tagged(c, key, key_limbs, S(s), prepared);
 }
 
 MHE_EXPORT int mhe_stream_wait(mhe_ctx *c, void *waiter, void *waitee)

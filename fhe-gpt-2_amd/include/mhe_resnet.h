@@ -92,16 +92,19 @@ public:
     };
     std::vector<KeyBlob> export_keys() const;
     void import_key(const KeyBlob &blob); // device-to-device copy from blob.dev (this runner's device)
-    void copy_key(const KeyBlob &blob, void *dst_dev) const; // blob -> dst_dev, synchronous
+    // blob -> dst_dev in SEAL's key layout (a prepared key is unprepared in dst), synchronous
+    void copy_key(const KeyBlob &blob, void *dst_dev) const;
     void finish_import();                 // after the last import_key (KeySource::import)
 
 private:
     void finish_setup(bool plan_galois_keys);
+    void prepare_keys(); // relinearization and Galois keys -> the engine's prepared key format
     struct Impl;
     std::unique_ptr<Impl> impl_;
     std::chrono::steady_clock::time_point t0_;
     double setup_s_ = 0, plan_s_ = 0, keygen_s_ = 0;
     std::size_t galois_keys_ = 0;
+    bool keys_prepared_ = false;
 };
 
 // infer_seal.cpp:234-577 entry point: images [start, end] from ../../../testFile/test_values.txt

@@ -43,6 +43,8 @@ SIGNATURES = {
     "mhe_key_traffic": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_key_prepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_unprepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_key_is_prepared": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), vp]),
+    "mhe_key_traffic_prepared": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
     "mhe_stream_destroy": (ctypes.c_int, [vp, vp]),
     "mhe_ntt_forward": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]),
@@ -300,6 +302,11 @@ class Engine:
         """mhe_key_unprepare: back to SEAL's key layout."""
         _check(lib().mhe_key_unprepare(self._h, _ptr(key), key.shape[0], self._key_limbs(key), self.stream()))
         return key
+
+    def key_is_prepared(self, key):
+        v = ctypes.c_int()
+        _check(lib().mhe_key_is_prepared(self._h, _ptr(key), self._key_limbs(key), ctypes.byref(v), self.stream()))
+        return bool(v.value)
 
     def switch_key(self, ct, target, key):
         _check(lib().mhe_switch_key(self._h, _ptr(ct), _ptr(target), _ptr(key), self._key_limbs(key), ct.shape[1],

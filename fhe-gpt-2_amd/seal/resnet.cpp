@@ -283,6 +283,7 @@ void ResNetRunner::finish_setup(bool plan_galois_keys)
         keygen_s_ = std::chrono::duration<double>(t3 - t2).count();
     }
     galois_keys_ = m.gal_keys.usage().size();
+    prepare_keys();
     setup_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count();
 }
 
@@ -360,6 +361,38 @@ void ResNetRunner::copy_key(const KeyBlob &b, void *dst) const
     if (mhe_memcpy_d2d(m.context->engine(), dst, b.dev, b.words * 8, s) != MHE_OK ||
         mhe_stream_sync(m.context->engine(), s) != MHE_OK)
         throw std::runtime_error(mhe_last_error());
+    if (b.kind == 2 || b.kind == 3)
+    {
+        int prepared = 0;
+        if (mhe_key_is_prepared(m.context->engine(), b.dev, (int)b.limbs, &prepared, s) != MHE_OK)
+            throw std::runtime_error(mhe_last_error());
+        if (prepared && mhe_key_unprepare(m.context->engine(), static_cast<std::uint64_t *>(dst), (int)b.limbs - 1,
+                                          (int)b.limbs, s) != MHE_OK)
+            throw std::runtime_error(mhe_last_error());
+    }
+}
+
+void ResNetRunner::prepare_keys()
+{
+    // The server's evaluation keys in the engine's prepared format (mhe_key_prepare): the key MAC
+    // streams 6 instead of 8 bytes per residue for the 46-bit primes; results are bit-identical.
+    // MHE_KEY_PREPARE=0 keeps SEAL's layout.
+    const char *e = getenv("MHE_KEY_PREPARE");
+    if (e && atoi(e) == 0) return;
+    Impl &m = *impl_;
+    mhe_ctx *eng = m.context->engine();
+    void *s = m.context->stream();
+    auto prep = [&](PolyStore &ps, std::size_t limbs) {
+        int prepared = 0;
+        std::uint64_t *p = ps.dev_write(s);
+        if (mhe_key_is_prepared(eng, p, (int)limbs, &prepared, s) != MHE_OK) throw std::runtime_error(mhe_last_error());
+        if (!prepared && mhe_key_prepare(eng, p, (int)limbs - 1, (int)limbs, s) != MHE_OK)
+            throw std::runtime_error(mhe_last_error());
+    };
+    if (m.relin_keys.has_index(0)) prep(m.relin_keys.key_mut(0), m.relin_keys.limbs_of(0));
+    for (const auto &kv : m.gal_keys.usage()) prep(m.gal_keys.key_mut(kv.first), kv.second);
+    mhe_stream_sync(eng, s);
+    keys_prepared_ = true;
 }
 
 void ResNetRunner::finish_import()
@@ -377,7 +410,12 @@ double ResNetRunner::galois_key_gb() const
 double ResNetRunner::key_traffic_bytes(bool reset)
 {
     std::uint64_t b = 0;
-    if (mhe_key_traffic(impl_->context->engine(), &b, reset ? 1 : 0) != 0) throw std::runtime_error(mhe_last_error());
+    // the bytes the switches stream: counted in the prepared format when the keys are prepared
+    std::uint64_t other = 0;
+    mhe_ctx *eng = impl_->context->engine();
+    const int rc = keys_prepared_ ? mhe_key_traffic_prepared(eng, &b, reset ? 1 : 0) | mhe_key_traffic(eng, &other, reset ? 1 : 0)
+                                  : mhe_key_traffic(eng, &b, reset ? 1 : 0) | mhe_key_traffic_prepared(eng, &other, reset ? 1 : 0);
+    if (rc != 0) throw std::runtime_error(mhe_last_error());
     return (double)b;
 }
 

@@ -75,6 +75,9 @@ int mhe_stream_wait(mhe_ctx *ctx, void *waiter, void *waitee);
 /* Key-switching key bytes streamed by the key switches run on the context since the last reset
  * (L digits x 2 x (L+1) primes x n x 8 per switch): the algorithmic key traffic of a workload. */
 int mhe_key_traffic(mhe_ctx *ctx, uint64_t *bytes, int reset);
+/* The same key slices counted in the prepared key format (mhe_key_prepare): 6 B per residue for
+ * primes below 2^48, 8 B otherwise -- the bytes a switch streams when its key is prepared. */
+int mhe_key_traffic_prepared(mhe_ctx *ctx, uint64_t *bytes, int reset);
 /* A non-blocking HIP stream on the context's device (and its scratch workspace); the SEAL
  * shim gives every host thread its own, as the reference's OpenMP threads share one
  * Evaluator (cnn/infer_seal.cpp:404). */
@@ -141,6 +144,8 @@ int mhe_ct_square(mhe_ctx *ctx, const uint64_t *a, uint64_t *out3, int limbs, vo
  * Preparing a prepared key (or unpreparing a SEAL key) fails with MHE_ERR_ARG. */
 int mhe_key_prepare(mhe_ctx *ctx, uint64_t *key, int digits, int key_limbs, void *stream);
 int mhe_key_unprepare(mhe_ctx *ctx, uint64_t *key, int digits, int key_limbs, void *stream);
+/* *prepared = 1 when `key` is in the prepared format (reads one tag word; host sync). */
+int mhe_key_is_prepared(mhe_ctx *ctx, const uint64_t *key, int key_limbs, int *prepared, void *stream);
 
 /* Evaluator::switch_key_inplace (evaluator.cpp:2281-2525): ct[2][L][n] += KS(target[L][n]). */
 int mhe_switch_key(mhe_ctx *ctx, uint64_t *ct, const uint64_t *target, const uint64_t *key, int key_limbs,
