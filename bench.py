@@ -184,6 +184,7 @@ def resnet_leg(device, images, streams, layers=20):
         "key_H2D_GB_per_image": 0.0,
         # every planned key is resident in HBM (no eviction tier is needed at 65 GB of 288), so every
         # key switch finds its key on the device
+        "key_format": "prepared (mhe_key_prepare: 46-bit limbs streamed in 6 B); key bytes below in SEAL's layout",
         "key_cache": {"resident_keys": info["galois_keys"], "hit_rate": 1.0, "evictions": 0,
                       "secret_key_in_eval_keys": False},
         # ResNet roofline: the key-switching key bytes one image streams (the algorithmic bytes of its
@@ -309,7 +310,9 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     km_ms, km_n = mhe.ctypes.c_double(), mhe.ctypes.c_int()
+    mc_ms, mc_n = mhe.ctypes.c_double(), mhe.ctypes.c_int()  # k_modup_col, the second key-switch kernel
     lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))  # drop the warmup launches
+    lib.mhe_kernel_time(eng._h, 1, mhe.ctypes.byref(mc_ms), mhe.ctypes.byref(mc_n))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -333,6 +336,7 @@ def main():
     # single-stream pass after the timed region (the rocprofv3 summary under profiles/ is of
     # the same single-stream command: bench.py --streams 1).
     lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))
+    lib.mhe_kernel_time(eng._h, 1, mhe.ctypes.byref(mc_ms), mhe.ctypes.byref(mc_n))
     if len(sps) > 1:
         for _ in range(min(args.steps, 4)):
             for i in range(B):
@@ -341,7 +345,9 @@ def main():
                     raise mhe.MheError(rc, lib.mhe_last_error().decode())
         torch.cuda.synchronize(dev)
         lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))
+        lib.mhe_kernel_time(eng._h, 1, mhe.ctypes.byref(mc_ms), mhe.ctypes.byref(mc_n))
     km_avg_us = km_ms.value * 1e3 / max(km_n.value, 1)
+    mc_avg_us = mc_ms.value * 1e3 / max(mc_n.value, 1)
 
     # HBM traffic per HMult from the committed PMC passes of the same workload (rocprofv3
     # FETCH_SIZE/WRITE_SIZE, gfx950-corrected; scripts/gpu_round.sh + scripts/traffic.py)
@@ -360,8 +366,11 @@ def main():
     hmults_per_gpu = B * args.steps
     value = world * hmults_per_gpu / elapsed
     per_hmult_s = gpu_s / hmults_per_gpu  # HIP-event time per HMult (batch over its streams)
-    km_bytes = ks_row_mac_key_bytes(L, n, moduli, prepared)
-    hm_bytes = hmult_bytes(L, km_bytes)
+    # algorithmic bytes as SURVEY.md §8(d) defines them (SEAL's u64 key layout); a prepared key
+    # streams fewer (streamed_key_bytes_per_launch), which is what the format buys
+    km_bytes = ks_row_mac_key_bytes(L, n)
+    km_streamed = ks_row_mac_key_bytes(L, n, moduli, prepared)
+    hm_bytes = hmult_bytes(L)
     achieved = hm_bytes / per_hmult_s / 1e9
     km_achieved = km_bytes / (km_avg_us * 1e-6) / 1e9 if km_avg_us > 0 else 0.0
     result = {
@@ -397,8 +406,9 @@ def main():
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": km_bytes,
             "key_format": args.key_format,
-            "seal_layout_key_bytes_per_launch": ks_row_mac_key_bytes(L, n),
+            "streamed_key_bytes_per_launch": km_streamed,
             "avg_launch_us": round(km_avg_us, 2),
+            "modup_col_avg_launch_us": round(mc_avg_us, 2),
             "launches_timed": km_n.value,
             "timing": "HIP events around each launch on its stream; single-stream pass when --streams > 1",
         },

@@ -524,6 +524,14 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
 #pragma unroll
     for (int e = 0; e < E; e++) x[e] = src[c + ((u32)(t + TPS * e) << logC)];
     const u64 qJ = primes[J].q;
+    // FP: the digit residues (< 2^51, exact in a double) are converted once, not once per output
+    // prime (u64 -> f64 is several VALU instructions)
+    double xd[E];
+    if constexpr (FP)
+    {
+#pragma unroll
+        for (int e = 0; e < E; e++) xd[e] = (double)x[e];
+    }
     // two sweeps over the group's output primes when FP: first the q < 2^47 ones with the lazy
     // forward butterflies, then the rest, so each loop body has one arithmetic variant
     auto sweep = [&](auto mode) {
@@ -541,7 +549,7 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
             if constexpr (M != 0)
             {
 #pragma unroll
-                for (int e = 0; e < E; e++) v[e] = fp_reduce((double)x[e], ar.q, ar.qinv);
+                for (int e = 0; e < E; e++) v[e] = fp_reduce(xd[e], ar.q, ar.qinv);
             }
             else
             {

@@ -410,11 +410,11 @@ double ResNetRunner::galois_key_gb() const
 double ResNetRunner::key_traffic_bytes(bool reset)
 {
     std::uint64_t b = 0;
-    // the bytes the switches stream: counted in the prepared format when the keys are prepared
+    // SURVEY 8(d)'s algorithmic figure: every slice counted in SEAL's u64 layout, prepared or not
+    // (a prepared key streams 6 of those 8 bytes for the 46-bit primes: mhe_key_traffic_prepared)
     std::uint64_t other = 0;
     mhe_ctx *eng = impl_->context->engine();
-    const int rc = keys_prepared_ ? mhe_key_traffic_prepared(eng, &b, reset ? 1 : 0) | mhe_key_traffic(eng, &other, reset ? 1 : 0)
-                                  : mhe_key_traffic(eng, &b, reset ? 1 : 0) | mhe_key_traffic_prepared(eng, &other, reset ? 1 : 0);
+    const int rc = mhe_key_traffic(eng, &b, reset ? 1 : 0) | mhe_key_traffic_prepared(eng, &other, reset ? 1 : 0);
     if (rc != 0) throw std::runtime_error(mhe_last_error());
     return (double)b;
 }

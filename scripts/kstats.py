@@ -14,11 +14,16 @@ def load(path):
 if sys.argv[1] == "diff":
     a, b = load(sys.argv[2]), load(sys.argv[3])
     d = {k: (b[k][0] - a.get(k, (0, 0))[0], b[k][1] - a.get(k, (0, 0))[1]) for k in b}
-    tot_ns = sum(v[1] for v in d.values())
+    # a kernel whose time difference is negative ran slower in the shorter run (e.g. a rare
+    # sequential PRNG redraw during key generation): listed apart, not netted into the total
+    neg = {k: v for k, v in d.items() if v[1] < 0}
+    tot_ns = sum(v[1] for v in d.values() if v[1] >= 0)
     tot_calls = sum(v[0] for v in d.values())
-    print(f"difference: {tot_calls} launches, {tot_ns / 1e6:.1f} ms of kernel time")
+    print(f"difference: {tot_calls} launches, {tot_ns / 1e6:.1f} ms of kernel time"
+          + (f" (excluding {len(neg)} kernel(s) slower in the shorter run: "
+             + ", ".join(f"{k.replace('void ', '')[:60]} {v[1] / 1e6:.1f} ms" for k, v in neg.items()) + ")" if neg else ""))
     for k, (c, ns) in sorted(d.items(), key=lambda kv: -kv[1][1]):
-        if c <= 0:
+        if c <= 0 or ns < 0:
             continue
         print(f"{100 * ns / tot_ns:6.2f}%  calls={c:>6}  total={ns / 1e6:8.1f} ms  avg={ns / c / 1e3:7.1f} us  "
               f"{k.replace('void ', '')[:90]}")

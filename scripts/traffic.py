@@ -21,6 +21,9 @@ if sys.argv[2] == "auto":
     hmults = max(1, len(ids))
 else:
     hmults = int(sys.argv[2])
+# one-time setup kernels of the bench process (key preparation), not part of any HMult
+SETUP = ("k_key_pack",)
+setup = collections.defaultdict(float)
 tot = collections.defaultdict(float)
 per_kernel = collections.defaultdict(lambda: collections.defaultdict(float))
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -29,6 +32,9 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             if r["Counter_Name"] != c:
                 continue
             v = float(r["Counter_Value"]) * 1024 * (2 if c == "FETCH_SIZE" else 1)
+            if any(k in r["Kernel_Name"] for k in SETUP):
+                setup[c] += v
+                continue
             tot[c] += v
             per_kernel[r["Kernel_Name"].replace("void ", "").split("(")[0]][c] += v
 hbm = (tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) / hmults
@@ -37,6 +43,7 @@ res = {
     "read_bytes_per_hmult": tot["FETCH_SIZE"] / hmults,
     "write_bytes_per_hmult": tot["WRITE_SIZE"] / hmults,
     "correction": "FETCH_SIZE x2 (gfx950 wide-load undercount), WRITE_SIZE x1",
+    "setup_kernels_excluded": {k: None for k in SETUP} | {"bytes_total": setup["FETCH_SIZE"] + setup["WRITE_SIZE"]},
     "per_kernel_GB_per_hmult": {k: round((v["FETCH_SIZE"] + v["WRITE_SIZE"]) / hmults / 1e9, 4)
                                 for k, v in sorted(per_kernel.items(), key=lambda kv: -sum(kv[1].values()))},
 }
