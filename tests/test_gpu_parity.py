@@ -292,6 +292,7 @@ def test_prepared_key_bit_exact(small):
     key = ch.rand_key()
     dkey = ch.up(key)
     ch.eng.key_prepare(dkey)
+    assert ch.eng.key_is_prepared(dkey)
     packed = ch.down(dkey)
     assert not np.array_equal(packed, key)  # the 46-bit limbs are repacked and tagged
     assert np.array_equal(packed[:, :, 0], key[:, :, 0]) and np.array_equal(packed[:, :, -1], key[:, :, -1])  # 51-bit
@@ -322,6 +323,22 @@ def test_prepared_key_bit_exact(small):
     assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
     ch.eng.key_unprepare(dt)
     assert np.array_equal(ch.down(dt), trunc)
+
+
+def test_prepared_key_errors_and_noop():
+    """Unpreparing a SEAL-layout key fails with SEAL-style argument errors; on a chain with no
+    prime below 2^48 preparation leaves the key as it is (nothing to pack) and switches still match."""
+    ch = Chain(12, [51] * 5, seed=11)
+    key = ch.rand_key()
+    dkey = ch.up(key)
+    assert not ch.eng.key_is_prepared(dkey)
+    with pytest.raises(mhe.MheError):
+        ch.eng.key_unprepare(dkey)
+    ch.eng.key_prepare(dkey)
+    assert np.array_equal(ch.down(dkey), key) and not ch.eng.key_is_prepared(dkey)
+    ct, target = ch.rand(2, 4, ch.n), ch.rand(4, ch.n)
+    assert np.array_equal(ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), dkey)),
+                          ch.oc.switch_key(ct, target, key))
 
 
 def test_errors_are_reported(small):
