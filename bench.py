@@ -225,7 +225,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=8, help="independent HMults per GPU per step")
+    ap.add_argument("--batch", type=int, default=32, help="independent HMults per GPU per step")
     ap.add_argument("--limbs", type=int, default=44)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host cores for the CPU baseline (16 = one GPU's share of the box's CPUs)")
