@@ -539,6 +539,30 @@ static void test_threads()
     }
 }
 
+// without an explicit seed every KeyGenerator / Encryptor draws a fresh
+// 512-bit Blake2xb seed from the OS (getrandom, seal/random.cpp): two of them never collide
+static void test_fresh_seeds_differ()
+{
+    Env e(4096, BITS);
+    KeyGenerator kg2(*e.ctx);
+    const SecretKey &s1 = e.keygen->secret_key(), &s2 = kg2.secret_key();
+    std::size_t same = 0, words = s1.data().coeff_count();
+    for (std::size_t k = 0; k < words; k++) same += s1.data().data()[k] == s2.data().data()[k];
+    CHECK(words > 0 && same < words); // sparse keys share zeros, never every word
+    Plaintext p;
+    e.encoder->encode(rand_vec(rng, 2048, 1.0), std::pow(2.0, 40), p);
+    Ciphertext c1, c2;
+    e.encryptor->encrypt(p, c1);
+    Encryptor enc2(*e.ctx, e.pk);
+    enc2.encrypt(p, c2);
+    std::size_t eq = 0;
+    for (std::size_t k = 0; k < c1.dyn_array_size(); k++) eq += c1.data()[k] == c2.data()[k];
+    CHECK(eq * 1000 < c1.dyn_array_size()); // fresh u, e0, e1: essentially every residue differs
+    prng_seed_type a = UniformRandomGeneratorFactory::DefaultFactory()->next_seed();
+    prng_seed_type b = UniformRandomGeneratorFactory::DefaultFactory()->next_seed();
+    CHECK(a != b);
+}
+
 int main()
 {
     struct T
@@ -555,7 +579,8 @@ int main()
                   { "reduced_error_ops", test_reduced_error_ops },
                   { "sparse_secret_and_slots", test_sparse_secret_and_slots },
                   { "security_level", test_security_level },
-                  { "threads", test_threads } };
+                  { "threads", test_threads },
+                  { "fresh_seeds_differ", test_fresh_seeds_differ } };
     for (auto &t : tests)
     {
         const int before = g_fail;
