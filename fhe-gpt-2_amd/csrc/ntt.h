@@ -506,7 +506,7 @@ template <int LOGR, int LOGT, bool FP>
 __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ coeff, u64 *__restrict__ modup,
                                                    const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all,
                                                    int L, int K, int log_n, long long twd, int I0, int Icnt,
-                                                   int pack)
+                                                   int pack, int X, int IG, int xcd)
 {
     using SH = Shape<LOGR, LOGT>;
     using A = NttArith<FP>;
@@ -515,9 +515,28 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
     __shared__ T lds[S * LD];
     const int tid = threadIdx.x, sl = tid % S, t = tid / S;
     const int logC = log_n - LOGR;
-    const u32 c = blockIdx.x * S + sl;
-    const int J = blockIdx.y;
-    const int IG = gridDim.z, g = blockIdx.z;
+    // 1-D grid of X column blocks x L digits x IG output-prime groups.  xcd: the IG groups of one
+    // (column block, digit) get ids i, i + 8, ..., i + 8 (IG - 1) -- workgroups are dealt to the 8
+    // XCDs round robin, so they run on one XCD close in time and share its L2 copy of the digit
+    u32 bj;
+    int g;
+    {
+        const u32 id = blockIdx.x;
+        if (xcd)
+        {
+            const u32 per = 8u * (u32)IG, r = id % per;
+            g = (int)(r / 8);
+            bj = (id / per) * 8 + r % 8;
+        }
+        else
+        {
+            const u32 XL = (u32)X * (u32)L;
+            bj = id % XL;
+            g = (int)(id / XL);
+        }
+    }
+    const u32 c = (bj % (u32)X) * S + sl;
+    const int J = (int)(bj / (u32)X);
     const int i_lo = I0 + (Icnt * g) / IG, i_hi = I0 + (Icnt * (g + 1)) / IG;
     const u64 *src = coeff + ((size_t)J << log_n);
     u64 x[E];
@@ -615,8 +634,14 @@ static inline void modup_col_a(const u64 *coeff, u64 *modup, const PrimeDev *pri
     constexpr int LOGT = LOGR <= 7 ? 3 : MHE_MODUP_LOGT8;
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
-    hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3(subs / SH::S, L, IG), dim3(256), 0, st, coeff, modup,
-                       primes, tw, L, K, log_n, twd, I0, Icnt, pack);
+    static const int xcd_env = [] {
+        const char *e = getenv("MHE_MODUP_XCD");
+        return e ? atoi(e) : 1;
+    }();
+    const int X = subs / SH::S;
+    const int xcd = (xcd_env && (X * L) % 8 == 0) ? 1 : 0;
+    hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3((unsigned)(X * L * IG)), dim3(256), 0, st, coeff, modup,
+                       primes, tw, L, K, log_n, twd, I0, Icnt, pack, X, IG, xcd);
 }
 
 // ModUp column pass for output primes I0 .. I0+Icnt-1 (modup holds exactly those), in IG
