@@ -63,6 +63,15 @@ __device__ __forceinline__ u32 tile16(u32 idx)
 // a 16-bit plane [n] and, in its last word, this tag -- never a residue of a SEAL key (>= 2^63),
 // so the key MAC tells a prepared key from SEAL's layout by itself.
 #define KEY_PACK_TAG 0xF0E1D2C3B4A59687ull
+// The 16-bit plane pairs rows instead: in a tile, u32 word (r/2, c) holds the high halves of rows
+// r and r+1 of column c (u16 index returned), so a column-pass lane, which holds both rows, writes
+// one u32 per row pair and 16 lanes fill a whole 64-byte segment (2-byte stores left 32-byte
+// half-segments and ~0.17 GB of extra write traffic per HMult).
+__device__ __forceinline__ u32 tile16h(u32 idx)
+{
+    const u32 r = idx >> 8, c = idx & 255;
+    return ((((r >> 4) << 4) | (c >> 4)) << 8) | (((r & 15) >> 1) << 5) | ((c & 15) << 1) | (r & 1);
+}
 __device__ __forceinline__ bool inter_packed(int pack, u64 q)
 {
     return pack && q < (1ull << 48);
@@ -595,16 +604,20 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
                 // one base per lane plus immediates
                 constexpr int LC = 16 - LOGR;
                 u32 *lo = reinterpret_cast<u32 *>(dst) + tile16(c + ((u32)(E * t) << LC));
-                unsigned short *hi = reinterpret_cast<unsigned short *>(reinterpret_cast<u32 *>(dst) + 65536) +
-                                     tile16(c + ((u32)(E * t) << LC));
+                // word index of the lane's first row pair (E t is a multiple of 16: tile16h is even)
+                u32 *hi = reinterpret_cast<u32 *>(dst) + 65536 + (tile16h(c + ((u32)(E * t) << LC)) >> 1);
 #pragma unroll
-                for (int e = 0; e < E; e++)
+                for (int e = 0; e < E; e += 2)
                 {
-                    const u64 o = ar.out(v[e]);
+                    const u64 o0 = ar.out(v[e]), o1 = ar.out(v[e + 1]);
                     // tile16(c + ((E t + e) << LC)) - tile16(c + ((E t) << LC)), E t a multiple of 16
-                    const u32 k = ((u32)(e >> 4) << 12) | ((u32)(e & 15) << 4);
-                    st_nt<0>(&lo[k], (u32)o);
-                    st_nt<0>(&hi[k], (unsigned short)(o >> 32));
+                    const u32 k0 = ((u32)(e >> 4) << 12) | ((u32)(e & 15) << 4);
+                    const u32 k1 = ((u32)((e + 1) >> 4) << 12) | ((u32)((e + 1) & 15) << 4);
+                    st_nt<0>(&lo[k0], (u32)o0);
+                    st_nt<0>(&lo[k1], (u32)o1);
+                    // the same difference for tile16h in words: row pair (e & 15) / 2 of tile row e / 16
+                    const u32 kw = ((u32)(e >> 4) << 11) | ((u32)((e & 15) >> 1) << 4);
+                    st_nt<0>(&hi[kw], (u32)(o0 >> 32) | ((u32)(o1 >> 32) << 16));
                 }
             }
             else
@@ -919,8 +932,8 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__res
 #pragma unroll
                 for (int e = 0; e < 8; e++)
                 {
-                    const u32 k = tile16(base + lay(t, e, B_A));
-                    v[e] = (u64)ld_nt<2>(&lo[k]) | ((u64)ld_nt<2>(&hi[k]) << 32);
+                    const u32 idx = base + lay(t, e, B_A);
+                    v[e] = (u64)ld_nt<2>(&lo[tile16(idx)]) | ((u64)ld_nt<2>(&hi[tile16h(idx)]) << 32);
                 }
             }
             else
