@@ -596,6 +596,7 @@ struct JobMDRCol
     const Tw *tw;
     const Tw *invq; // [K][K]
     int L, K, log_n;
+    int fp = 0; // every prime < 2^51 (NttMode::fp): the lift in exact FP64 (fparith.h)
     struct View
     {
         const u64 *accP, *lastp;
@@ -604,9 +605,20 @@ struct JobMDRCol
         const Tw *tw;
         Tw pinv;
         u64 halfP, fixP, ql, halfL, neg_halfL;
-        bool redP, redL, skip;
+        bool redP, redL, skip, fp;
+        double pd, pi, pinvd;
         __device__ u64 load(u32 x) const
         {
+            if (fp)
+            {
+                // accP in [0, 2P) -> a mod P canonical by two conditional subtractions; t + fixP
+                // and the rescale lift r + neg_halfL are exact doubles (< 2^52), the product by
+                // P^-1 is in (-2p, 2p), the sum below 2^53: one canonicalisation, the same residue
+                const u64 t = csub(csub(accP[x] + halfP, 2 * P.q), P.q);
+                const u64 r = csub(lastp[x] + halfL, ql);
+                const double u = fp_mulmod_gen((double)(t + fixP), pinvd, pd, pi) + (double)(r + neg_halfL);
+                return fp_canon(u, pd, pi);
+            }
             u64 t = barrett64(accP[x] + halfP, P);
             if (redP) t = barrett64(t, p);
             t += fixP;                                  // ModDown lift, [0, 2q)
@@ -637,6 +649,10 @@ struct JobMDRCol
         v.neg_halfL = v.p.q - barrett64(v.halfL, v.p);
         v.redL = v.p.q < v.ql;
         v.skip = false;
+        v.fp = fp != 0;
+        v.pd = (double)v.p.q;
+        v.pi = 1.0 / v.pd;
+        v.pinvd = (double)v.pinv.x;
         return v;
     }
 };
@@ -1324,7 +1340,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             inv_row(li, log_n, 2, c->nm, st);
             JobStrided j2{ w->coeff, w->coeff, n, n, L - 1, 0, c->primes, c->itw, log_n, 1 };
             inv_col(j2, log_n, 2, c->nm, st);
-            JobMDRCol mc{ w->acc, w->coeff, w->modup, c->primes, c->tw, c->invq, L, c->K, log_n };
+            JobMDRCol mc{ w->acc, w->coeff, w->modup, c->primes, c->tw, c->invq, L, c->K, log_n, c->nm.fp ? 1 : 0 };
             fwd_col(mc, log_n, 2 * (L - 1), c->nm, st);
             JobMDRRow mr{ w->modup, w->acc, ct, rescale_out, c->primes, c->tw, c->invq, L, c->K, log_n };
             fwd_row(mr, log_n, 2 * (L - 1), c->nm, st);
