@@ -465,6 +465,7 @@ struct JobModDownRow
     int L, K, log_n;
     int fixed_i = -1; // >= 0: one job per poly, all on limb fixed_i
     int c1_write = 0; // 1: ct[1] = ModDown(acc[1]) instead of += (apply_galois: ct[1] was 0)
+    int fp = 0;       // every prime < 2^51: the epilogue in exact FP64 (fparith.h)
     struct View
     {
         u64 *buf;
@@ -475,9 +476,19 @@ struct JobModDownRow
         Tw inv;
         bool skip;
         bool replace;
+        bool fp;
+        double pd, pi, invd;
         __device__ u64 load(u32 x) const { return buf[x]; }
         __device__ void store(u32 x, u64 t) const
         {
+            if (fp)
+            {
+                // acc and t canonical: (acc - t) P^-1 in (-1.25p, 1.25p), plus c < p, one
+                // canonicalisation (|.| < 2^53): the residue of the integer form
+                const double v = fp_mulmod_gen((double)accp[x] - (double)t, invd, pd, pi);
+                ctp[x] = fp_canon(replace ? v : v + (double)ctp[x], pd, pi);
+                return;
+            }
             u64 v = mul_shoup(accp[x] + p.four_q - t, inv.x, inv.y, p.q);
             ctp[x] = replace ? v : addmod(v, ctp[x], p.q); // 0 + v = v: the same word
         }
@@ -494,6 +505,10 @@ struct JobModDownRow
         v.inv = invq[(size_t)(K - 1) * K + i];
         v.skip = false;
         v.replace = c1_write && k == 1;
+        v.fp = fp != 0;
+        v.pd = (double)v.p.q;
+        v.pi = 1.0 / v.pd;
+        v.invd = (double)v.inv.x;
         return v;
     }
 };
@@ -552,6 +567,7 @@ struct JobRescaleRow
     const Tw *tw;
     const Tw *invq;
     int L, K, log_n;
+    int fp = 0; // every prime < 2^51: the epilogue in exact FP64 (fparith.h)
     struct View
     {
         u64 *buf;
@@ -560,9 +576,16 @@ struct JobRescaleRow
         PrimeDev p;
         const Tw *tw;
         Tw inv;
-        bool skip;
+        bool skip, fp;
+        double pd, pi, invd;
         __device__ u64 load(u32 x) const { return buf[x]; }
-        __device__ void store(u32 x, u64 t) const { outp[x] = mul_shoup(inp[x] + p.four_q - t, inv.x, inv.y, p.q); }
+        __device__ void store(u32 x, u64 t) const
+        {
+            if (fp) // in and t canonical: (in - t) q_last^-1 in (-1.25p, 1.25p), canonicalised
+                outp[x] = fp_canon(fp_mulmod_gen((double)inp[x] - (double)t, invd, pd, pi), pd, pi);
+            else
+                outp[x] = mul_shoup(inp[x] + p.four_q - t, inv.x, inv.y, p.q);
+        }
     };
     __device__ View view(int y) const
     {
@@ -575,6 +598,10 @@ struct JobRescaleRow
         v.tw = tw + ((size_t)i << log_n);
         v.inv = invq[(size_t)(L - 1) * K + i];
         v.skip = false;
+        v.fp = fp != 0;
+        v.pd = (double)v.p.q;
+        v.pi = 1.0 / v.pd;
+        v.invd = (double)v.inv.x;
         return v;
     }
 };
@@ -667,6 +694,7 @@ struct JobMDRRow
     const Tw *tw;
     const Tw *invq;
     int L, K, log_n;
+    int fp = 0; // every prime < 2^51: the epilogue in exact FP64 (fparith.h)
     struct View
     {
         u64 *buf;
@@ -675,10 +703,20 @@ struct JobMDRRow
         PrimeDev p;
         const Tw *tw;
         Tw pinv, qlinv;
-        bool skip;
+        bool skip, fp;
+        double pd, pi, pinvd, qlinvd;
         __device__ u64 load(u32 x) const { return buf[x]; }
         __device__ void store(u32 x, u64 U) const
         {
+            if (fp)
+            {
+                // acc_i P^-1 in (-1.25p, 1.25p); c + a - U is an exact integer below 2^53; its
+                // centered residue times q_{L-1}^-1, canonicalised: the residue of the integer form
+                const double a = fp_mulmod_gen((double)accp[x], pinvd, pd, pi);
+                const double v = fp_reduce((double)ctp[x] + a - (double)U, pd, pi);
+                outp[x] = fp_canon(fp_mulmod_gen(v, qlinvd, pd, pi), pd, pi);
+                return;
+            }
             const u64 a = mul_shoup(accp[x], pinv.x, pinv.y, p.q);  // acc_i P^-1
             const u64 v = ctp[x] + a + p.four_q - U;                // < 6q
             outp[x] = mul_shoup(v, qlinv.x, qlinv.y, p.q);
@@ -697,6 +735,11 @@ struct JobMDRRow
         v.pinv = invq[(size_t)(K - 1) * K + i];
         v.qlinv = invq[(size_t)(L - 1) * K + i];
         v.skip = false;
+        v.fp = fp != 0;
+        v.pd = (double)v.p.q;
+        v.pi = 1.0 / v.pd;
+        v.pinvd = (double)v.pinv.x;
+        v.qlinvd = (double)v.qlinv.x;
         return v;
     }
 };
@@ -1325,6 +1368,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             else
                 fwd_col(dc, log_n, 2 * L, c->nm, st);
             JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
+            dr.fp = c->nm.fp ? 1 : 0;
             dr.c1_write = c1_write;
             fwd_row(dr, log_n, 2 * L, c->nm, st);
         }
@@ -1335,6 +1379,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n, L - 1 };
             fwd_col(dc, log_n, 2, c->nm, st);
             JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n, L - 1 };
+            dr.fp = c->nm.fp ? 1 : 0;
             fwd_row(dr, log_n, 2, c->nm, st);
             JobLastInv li{ ct, w->coeff, c->primes, c->itw, L, log_n, 1 };
             inv_row(li, log_n, 2, c->nm, st);
@@ -1342,7 +1387,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             inv_col(j2, log_n, 2, c->nm, st);
             JobMDRCol mc{ w->acc, w->coeff, w->modup, c->primes, c->tw, c->invq, L, c->K, log_n, c->nm.fp ? 1 : 0 };
             fwd_col(mc, log_n, 2 * (L - 1), c->nm, st);
-            JobMDRRow mr{ w->modup, w->acc, ct, rescale_out, c->primes, c->tw, c->invq, L, c->K, log_n };
+            JobMDRRow mr{ w->modup, w->acc, ct, rescale_out, c->primes, c->tw, c->invq, L, c->K, log_n, c->nm.fp ? 1 : 0 };
             fwd_row(mr, log_n, 2 * (L - 1), c->nm, st);
         }
     }
@@ -1373,6 +1418,7 @@ static int run_rescale(mhe_ctx *c, const u64 *in, u64 *out, int size, int L, hip
         fwd_col(rc, log_n, size * (L - 1), c->nm, st);
     }
     JobRescaleRow rr{ w->modup, in, out, c->primes, c->tw, c->invq, L, c->K, log_n };
+    rr.fp = c->nm.fp ? 1 : 0;
     fwd_row(rr, log_n, size * (L - 1), c->nm, st);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
