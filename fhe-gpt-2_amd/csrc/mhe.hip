@@ -10,6 +10,7 @@
 // Scratch workspaces are per stream (see Workspace).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -162,13 +163,23 @@ static u32 rev_bits(u32 x, int bits)
 } // namespace host
 
 // ============================================================================= context
+// Per batch entry (a key switch / rescale of one ciphertext inside a batched launch).
+struct WsEntry
+{
+    u64 *coeff = nullptr; // [L][n]        INTT(target); the rescale's / ModDown's INTT'd last limbs
+    u64 *modup = nullptr; // [L+1][L][n]   lifted + NTT'd digits; reused by mod-down/rescale
+    u64 *acc = nullptr;   // [2][L+1][n]   key inner products
+};
+
 struct Workspace
 {
     int max_limbs = 0;
+    int entries = 0;      // batch entries the scratch is sized for (<= MHE_MAXB)
     u64 *base = nullptr;
-    u64 *coeff = nullptr; // [L][n]        INTT(target)
-    u64 *modup = nullptr; // [L+1][L][n]   lifted + NTT'd digits; reused by mod-down/rescale
-    u64 *acc = nullptr;   // [2][L+1][n]   key inner products
+    WsEntry e[MHE_MAXB];
+    u64 *coeff = nullptr; // entry 0's buffers under their old names
+    u64 *modup = nullptr;
+    u64 *acc = nullptr;
     u64 *tmp = nullptr;   // [L][n]        permuted c1 for Galois
     u64 *ct3 = nullptr;   // [3][L][n]     tensor output for hmult
     // kernel timing (mhe_ctx_set_timing): event pairs recorded around the two dominant
@@ -204,7 +215,6 @@ struct mhe_ctx
     int timing = 0;      // record HIP events around the key-switch kernels (mhe_ctx_set_timing)
     int hmult_fused = 1; // HMult: ModDown fused with the rescale (MHE_HMULT_FUSED=0: separate)
     int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
-    int ks_groups = 0; // fused path: digit groups (MHE_KS_GROUPS; <= 0 = by L)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
@@ -258,35 +268,59 @@ static void timing_end(hipEvent_t *pair, hipStream_t st)
     if (pair) (void)hipEventRecord(pair[1], st);
 }
 
-static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out)
+// The scratch of stream st, for ciphertexts of up to `limbs` limbs and `entries` batch entries.
+static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int entries = 1)
 {
     std::lock_guard<std::mutex> g(c->mu);
     Workspace &w = c->ws[st];
-    if (w.max_limbs < limbs)
+    if (w.max_limbs < limbs || w.entries < entries)
     {
         if (w.base) HIP_TRY(hipFree(w.base));
         w.base = nullptr;
-        const size_t n = c->n, L = limbs;
+        const int E = std::max(entries, w.entries);
+        const size_t n = c->n, L = std::max(limbs, w.max_limbs);
         const size_t Lc = L < 3 ? 3 : L;
-        size_t words = Lc * n + (L + 1) * L * n + 8 * 2 * (L + 1) * n + L * n + 3 * L * n;
+        const size_t per = Lc * n + (L + 1) * L * n + 2 * (L + 1) * n;
+        size_t words = (size_t)E * per + L * n + 3 * L * n;
         HIP_TRY(hipSetDevice(c->device));
         if (hipMalloc(&w.base, words * sizeof(u64)) != hipSuccess)
         {
             w.max_limbs = 0;
+            w.entries = 0;
             return fail(MHE_ERR_MEMORY, "workspace allocation failed");
         }
-        w.coeff = w.base;
-        w.modup = w.coeff + Lc * n;
-        w.acc = w.modup + (L + 1) * L * n;
-        w.tmp = w.acc + 8 * 2 * (L + 1) * n; // acc holds up to 8 digit-group partials
+        for (int i = 0; i < E; i++)
+        {
+            w.e[i].coeff = w.base + (size_t)i * per;
+            w.e[i].modup = w.e[i].coeff + Lc * n;
+            w.e[i].acc = w.e[i].modup + (L + 1) * L * n;
+        }
+        w.coeff = w.e[0].coeff;
+        w.modup = w.e[0].modup;
+        w.acc = w.e[0].acc;
+        w.tmp = w.base + (size_t)E * per;
         w.ct3 = w.tmp + L * n;
-        w.max_limbs = limbs;
+        w.max_limbs = (int)L;
+        w.entries = E;
     }
     *out = &w;
     return MHE_OK;
 }
 
 // ================================================================================ jobs
+// A batch of jobs of one kind: entry e owns job indices [e * per, (e + 1) * per) of the launch and
+// its own buffers (pointers inside j[e]); the shared geometry (level, primes) is the same for all.
+template <class Job>
+struct JobB
+{
+    Job j[MHE_MAXB];
+    int per = 1; // jobs per entry
+    __device__ auto view(int y) const
+    {
+        const int e = y / per;
+        return j[e].view(y - e * per);
+    }
+};
 // Plain transform over [poly][limb][n] with limb l on prime l (optionally src != dst).
 struct JobPlain
 {
@@ -1002,6 +1036,30 @@ __global__ void k_galois(const u64 *in, u64 *out, u32 elt, int log_n, size_t tot
     out[g] = in[base + src];
 }
 
+// The same for up to MHE_MAXB independent (in, out, element) entries, entry = blockIdx.y.
+struct GalPtrs
+{
+    const u64 *in[MHE_MAXB];
+    u64 *out[MHE_MAXB];
+    u32 elt[MHE_MAXB];
+};
+
+__global__ void k_galois_b(GalPtrs P, int log_n, size_t total)
+{
+    size_t g = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (g >= total) return;
+    const u64 *in = P.in[blockIdx.y];
+    u64 *out = P.out[blockIdx.y];
+    const u32 elt = P.elt[blockIdx.y];
+    const u32 n = 1u << log_n;
+    const u32 i = (u32)(g & (n - 1));
+    const size_t base = g - i;
+    const u32 reversed = __builtin_bitreverse32(n + i) >> (31 - log_n);
+    const u32 idx = (u32)(((u64)elt * reversed) >> 1) & (n - 1);
+    const u32 src = __builtin_bitreverse32(idx) >> (32 - log_n);
+    out[g] = in[base + src];
+}
+
 // Bootstrapper::modraise_inplace (ckks_bootstrapping/Bootstrapper.cpp:2894-2948): the single-limb
 // coefficient-form polynomial x (mod q_0, canonical) is lifted centered, v = x - q_0 if
 // x > q_0/2, and reduced mod every prime of the target level.
@@ -1254,58 +1312,104 @@ static int run_ntt_inv(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limb
     return MHE_OK;
 }
 
-// switch_key_inplace: ct[2][L][n] += KS(target[L][n]) (evaluator.cpp:2281-2525).
-// rescale_out != nullptr (HMult): ct is the first two polys of a product, and instead of
-// ct += KS(target) the result of rescale_to_next(ct + KS(target)) goes to rescale_out
-// [2][L-1][n] (JobMDRCol / JobMDRRow); ct limb L-1 is overwritten on the way.
-static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key, int key_limbs, int L,
-                          hipStream_t st, u64 *rescale_out = nullptr, int c1_write = 0)
+// One entry of a (batched) key switch.
+struct KsJob
 {
-    // c1_write: ct[1] is taken as zero and written, not read (target may then alias ct[1]: it is
-    // last read by the key MAC, before the ModDown writes ct)
-    if (c1_write && rescale_out) return fail(MHE_ERR_ARG, "key switch: c1_write with a fused rescale");
-    if (key_limbs < L + 1 || key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
+    u64 *ct;               // [2][L][n]
+    const u64 *target;     // [L][n], NTT form
+    const u64 *key;        // [digits][2][key_limbs][n]
+    int key_limbs;
+    u64 *rescale_out;      // HMult: [2][L-1][n] (see run_switch_key_batch), else nullptr
+};
+
+static int ks_check_key(mhe_ctx *c, const KsJob &j, int L, hipStream_t st, int *kpack)
+{
+    if (j.key_limbs < L + 1 || j.key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
     // a prepared key (mhe_key_prepare) is recognised by the fused MAC itself (KEY_PACK_TAG in
     // each packed slot); the separate-MAC debugging path reads SEAL's layout only
-    int kpack = 1;
+    *kpack = 1;
     if (!c->ks_fused)
     {
         int tagged = 0;
-        int r0 = key_tagged(c, key, key_limbs, st, &tagged);
+        int r0 = key_tagged(c, j.key, j.key_limbs, st, &tagged);
         if (r0) return r0;
-        kpack = tagged;
+        if (tagged) return fail(MHE_ERR_ARG, "key switch: prepared keys need the fused key MAC");
+        *kpack = 0;
     }
-    if (kpack && !c->ks_fused) return fail(MHE_ERR_ARG, "key switch: prepared keys need the fused key MAC");
-    if (!c->ks_fused) kpack = 0;
     // the key slice one switch streams: L digits x 2 polys x (L + 1) primes
     c->key_bytes += 2ull * (unsigned long long)L * (unsigned long long)(L + 1) * c->n * 8ull;
+    unsigned long long per = 0; // bytes per residue over the slice's L + 1 limbs, prepared format
+    for (int l = 0; l <= L; l++) per += key_limb_packed(c, l == L ? j.key_limbs - 1 : l, j.key_limbs) ? 6 : 8;
+    c->key_bytes_prep += 2ull * (unsigned long long)L * c->n * per;
+    return MHE_OK;
+}
+
+// switch_key_inplace (evaluator.cpp:2281-2525) for B <= MHE_MAXB independent entries of one
+// level L, every kernel launched once for all of them: ct_e[2][L][n] += KS(target_e[L][n]).
+// rescale_out != nullptr (HMult; all entries or none): ct_e is the first two polys of a product,
+// and instead of ct += KS(target) the result of rescale_to_next(ct + KS(target)) goes to
+// rescale_out [2][L-1][n] (JobMDRCol / JobMDRRow); ct limb L-1 is overwritten on the way.
+// c1_write: ct[1] is taken as zero and written, not read (target may then alias ct[1]: it is last
+// read by the key MAC, before the ModDown writes ct).
+static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hipStream_t st, int c1_write = 0)
+{
+    if (B < 1 || B > MHE_MAXB) return fail(MHE_ERR_ARG, "key switch: batch size out of range");
+    const bool hm = jobs[0].rescale_out != nullptr;
+    for (int e = 0; e < B; e++)
+        if ((jobs[e].rescale_out != nullptr) != hm) return fail(MHE_ERR_ARG, "key switch: mixed fused-rescale batch");
+    if (c1_write && hm) return fail(MHE_ERR_ARG, "key switch: c1_write with a fused rescale");
+    if (!c->ks_fused && B > 1)
     {
-        unsigned long long per = 0; // bytes per residue over the slice's L + 1 limbs, prepared format
-        for (int l = 0; l <= L; l++) per += key_limb_packed(c, l == L ? key_limbs - 1 : l, key_limbs) ? 6 : 8;
-        c->key_bytes_prep += 2ull * (unsigned long long)L * c->n * per;
+        // the separate-MAC debugging path runs one entry at a time
+        for (int e = 0; e < B; e++)
+        {
+            int r = run_switch_key_batch(c, jobs + e, 1, L, st, c1_write);
+            if (r) return r;
+        }
+        return MHE_OK;
+    }
+    int kpack = 1;
+    for (int e = 0; e < B; e++)
+    {
+        int r = ks_check_key(c, jobs[e], L, st, &kpack);
+        if (r) return r;
     }
     Workspace *w;
-    int r = get_ws(c, st, c->K - 1, &w);
+    int r = get_ws(c, st, c->K - 1, &w, B);
     if (r) return r;
     const int log_n = c->log_n;
     const size_t n = c->n;
     // 1. t_target = INTT(target), canonical (evaluator.cpp:2351-2354)
     {
-        JobStrided j{ target, w->coeff, n, n, 0, 1, c->primes, c->itw, log_n, 0 };
-        inv_row(j, log_n, L, c->nm, st);
-        j.src = w->coeff;
-        j.mode = 1;
-        inv_col(j, log_n, L, c->nm, st);
+        JobB<JobStrided> j;
+        j.per = L;
+        for (int e = 0; e < B; e++) j.j[e] = JobStrided{ jobs[e].target, w->e[e].coeff, n, n, 0, 1, c->primes, c->itw, log_n, 0 };
+        inv_row(j, log_n, B * L, c->nm, st);
+        for (int e = 0; e < B; e++)
+        {
+            j.j[e].src = w->e[e].coeff;
+            j.j[e].mode = 1;
+        }
+        inv_col(j, log_n, B * L, c->nm, st);
     }
     if (c->ks_fused)
     {
         // 2+3. ModUp column pass, then its row pass fused with the key MAC so NTT'd digits
         //      never leave registers; optionally in chunks of output primes so a chunk's
         //      column-pass output can stay in the Infinity Cache (MHE_KS_FCHUNK).
-        const int G = c->ks_groups > 0 ? c->ks_groups : ks_groups(L);
         const int P = c->ks_fchunk > 0 ? c->ks_fchunk : L + 1;
         // 48-bit intermediate (ntt.h tile16): only k_modup_col writes it, so only with column groups
         const int pack = (c->ks_pack && c->ks_colgroups > 0) ? 1 : 0;
+        KsPtrs kp{};
+        for (int e = 0; e < B; e++)
+        {
+            kp.coeff[e] = w->e[e].coeff;
+            kp.inter[e] = w->e[e].modup;
+            kp.target[e] = jobs[e].target;
+            kp.key[e] = jobs[e].key;
+            kp.acc[e] = w->e[e].acc;
+            kp.key_limbs[e] = jobs[e].key_limbs;
+        }
         for (int I0 = 0; I0 <= L; I0 += P)
         {
             const int cnt = (I0 + P <= L + 1) ? P : L + 1 - I0;
@@ -1313,20 +1417,20 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             if (c->ks_colgroups > 0)
             {
                 const int IG = c->ks_colgroups < cnt ? c->ks_colgroups : cnt;
-                modup_col(w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, IG, pack, st);
+                modup_col(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, IG, pack, st);
             }
             else
             {
-                JobModUpCol j{ w->coeff, w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
-                fwd_col(j, log_n, cnt * L, c->nm, st);
+                JobB<JobModUpCol> j;
+                j.per = cnt * L;
+                for (int e = 0; e < B; e++) j.j[e] = JobModUpCol{ w->e[e].coeff, w->e[e].modup, c->primes, c->tw, L, c->K, log_n, I0 };
+                fwd_col(j, log_n, B * cnt * L, c->nm, st);
             }
             timing_end(tc, st);
             hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
-            ks_row_mac_chunk(w->modup, target, key, w->acc, c->primes, c->tw, L, c->K, key_limbs, log_n, c->nm, G, I0,
-                             cnt, pack, kpack, st);
+            ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, pack, kpack, st);
             timing_end(tm, st);
         }
-        ks_acc_finish(w->acc, c->primes, L, c->K, G, log_n, st);
     }
     else
     {
@@ -1335,7 +1439,7 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
         //      acc[k][I] = sum_J digit * key[J][k][I] (evaluator.cpp:2410-2463).  The chunk
         //      scratch is reused, so the column-pass output and the NTT'd digits of a chunk
         //      stay in the Infinity Cache between the three kernels instead of round-tripping
-        //      through HBM; only the key streams from HBM.
+        //      through HBM; only the key streams from HBM.  (One entry: B == 1 here.)
         const int P = c->ks_chunk > 0 ? c->ks_chunk : L + 1;
         for (int I0 = 0; I0 <= L; I0 += P)
         {
@@ -1345,83 +1449,148 @@ static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key
             JobModUpRow r2{ w->modup, c->primes, c->tw, L, c->K, log_n, I0 };
             fwd_row(r2, log_n, cnt * L, c->nm, st);
             dim3 grid((unsigned)(n / 512), cnt);
-            hipLaunchKernelGGL(k_ks_mac, grid, dim3(256), 0, st, w->modup, target, key, w->acc, c->primes, L, c->K,
-                               key_limbs, log_n, I0);
+            hipLaunchKernelGGL(k_ks_mac, grid, dim3(256), 0, st, w->modup, jobs[0].target, jobs[0].key, w->acc, c->primes, L,
+                               c->K, jobs[0].key_limbs, log_n, I0);
         }
     }
     // 4. ModDown (evaluator.cpp:2466-2524): INTT_lazy of the special limbs, then fused
     //    lift + NTT + (c + 4q - t) * P^-1 + add.
     {
-        JobStrided j{ w->acc + (size_t)L * n, w->acc + (size_t)L * n, (size_t)(L + 1) * n, (size_t)(L + 1) * n,
-                      c->K - 1, 0, c->primes, c->itw, log_n, 0 };
-        inv_row(j, log_n, 2, c->nm, st);
+        JobB<JobStrided> j;
+        j.per = 2;
+        for (int e = 0; e < B; e++)
+            j.j[e] = JobStrided{ w->e[e].acc + (size_t)L * n, w->e[e].acc + (size_t)L * n, (size_t)(L + 1) * n,
+                                 (size_t)(L + 1) * n, c->K - 1, 0, c->primes, c->itw, log_n, 0 };
+        inv_row(j, log_n, 2 * B, c->nm, st);
         // the special limbs' inverse column pass runs inside the lift column pass (k_icol_lift)
         // (not in the HMult tail: JobMDRCol reads the fully inverse-transformed special limbs)
-        const ColSrc cs{ w->acc + (size_t)L * n, (size_t)(L + 1) * n, c->primes, c->itw, c->K - 1 };
-        const bool fuse = c->icol_fused && (!rescale_out || L < 2);
-        if (!fuse) inv_col(j, log_n, 2, c->nm, st);
-        if (!rescale_out || L < 2)
+        ColSrc cs{};
+        cs.stride = (size_t)(L + 1) * n;
+        cs.per = 2;
+        cs.primes = c->primes;
+        cs.itw = c->itw;
+        cs.pi = c->K - 1;
+        for (int e = 0; e < B; e++) cs.src[e] = w->e[e].acc + (size_t)L * n;
+        const bool fuse = c->icol_fused && (!hm || L < 2);
+        if (!fuse) inv_col(j, log_n, 2 * B, c->nm, st);
+        if (!hm || L < 2)
         {
-            JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n };
+            JobB<JobModDownCol> dc;
+            dc.per = 2 * L;
+            JobB<JobModDownRow> dr;
+            dr.per = 2 * L;
+            for (int e = 0; e < B; e++)
+            {
+                dc.j[e] = JobModDownCol{ w->e[e].acc, w->e[e].modup, c->primes, c->tw, L, c->K, log_n };
+                dr.j[e] = JobModDownRow{ w->e[e].modup, w->e[e].acc, jobs[e].ct, c->primes, c->tw, c->invq, L, c->K, log_n };
+                dr.j[e].fp = c->nm.fp ? 1 : 0;
+                dr.j[e].c1_write = c1_write;
+            }
             if (fuse)
-                icol_lift(cs, dc, 2, L, log_n, c->nm, st);
+                icol_lift(cs, dc, 2 * B, L, log_n, c->nm, st);
             else
-                fwd_col(dc, log_n, 2 * L, c->nm, st);
-            JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n };
-            dr.fp = c->nm.fp ? 1 : 0;
-            dr.c1_write = c1_write;
-            fwd_row(dr, log_n, 2 * L, c->nm, st);
+                fwd_col(dc, log_n, 2 * L * B, c->nm, st);
+            fwd_row(dr, log_n, 2 * L * B, c->nm, st);
         }
         else
         {
             // ModDown of limb L-1 only, its INTT (the rescale's "last"), then ModDown and
             // rescale of the other limbs through one forward NTT each
-            JobModDownCol dc{ w->acc, w->modup, c->primes, c->tw, L, c->K, log_n, L - 1 };
-            fwd_col(dc, log_n, 2, c->nm, st);
-            JobModDownRow dr{ w->modup, w->acc, ct, c->primes, c->tw, c->invq, L, c->K, log_n, L - 1 };
-            dr.fp = c->nm.fp ? 1 : 0;
-            fwd_row(dr, log_n, 2, c->nm, st);
-            JobLastInv li{ ct, w->coeff, c->primes, c->itw, L, log_n, 1 };
-            inv_row(li, log_n, 2, c->nm, st);
-            JobStrided j2{ w->coeff, w->coeff, n, n, L - 1, 0, c->primes, c->itw, log_n, 1 };
-            inv_col(j2, log_n, 2, c->nm, st);
-            JobMDRCol mc{ w->acc, w->coeff, w->modup, c->primes, c->tw, c->invq, L, c->K, log_n, c->nm.fp ? 1 : 0 };
-            fwd_col(mc, log_n, 2 * (L - 1), c->nm, st);
-            JobMDRRow mr{ w->modup, w->acc, ct, rescale_out, c->primes, c->tw, c->invq, L, c->K, log_n, c->nm.fp ? 1 : 0 };
-            fwd_row(mr, log_n, 2 * (L - 1), c->nm, st);
+            JobB<JobModDownCol> dc;
+            dc.per = 2;
+            JobB<JobModDownRow> dr;
+            dr.per = 2;
+            JobB<JobLastInv> li;
+            li.per = 2;
+            JobB<JobStrided> j2;
+            j2.per = 2;
+            JobB<JobMDRCol> mc;
+            mc.per = 2 * (L - 1);
+            JobB<JobMDRRow> mr;
+            mr.per = 2 * (L - 1);
+            for (int e = 0; e < B; e++)
+            {
+                dc.j[e] = JobModDownCol{ w->e[e].acc, w->e[e].modup, c->primes, c->tw, L, c->K, log_n, L - 1 };
+                dr.j[e] = JobModDownRow{ w->e[e].modup, w->e[e].acc, jobs[e].ct, c->primes, c->tw, c->invq, L, c->K, log_n, L - 1 };
+                dr.j[e].fp = c->nm.fp ? 1 : 0;
+                li.j[e] = JobLastInv{ jobs[e].ct, w->e[e].coeff, c->primes, c->itw, L, log_n, 1 };
+                j2.j[e] = JobStrided{ w->e[e].coeff, w->e[e].coeff, n, n, L - 1, 0, c->primes, c->itw, log_n, 1 };
+                mc.j[e] = JobMDRCol{ w->e[e].acc, w->e[e].coeff, w->e[e].modup, c->primes, c->tw, c->invq, L, c->K, log_n,
+                                     c->nm.fp ? 1 : 0 };
+                mr.j[e] = JobMDRRow{ w->e[e].modup, w->e[e].acc, jobs[e].ct, jobs[e].rescale_out, c->primes, c->tw, c->invq,
+                                     L, c->K, log_n, c->nm.fp ? 1 : 0 };
+            }
+            fwd_col(dc, log_n, 2 * B, c->nm, st);
+            fwd_row(dr, log_n, 2 * B, c->nm, st);
+            inv_row(li, log_n, 2 * B, c->nm, st);
+            inv_col(j2, log_n, 2 * B, c->nm, st);
+            fwd_col(mc, log_n, 2 * (L - 1) * B, c->nm, st);
+            fwd_row(mr, log_n, 2 * (L - 1) * B, c->nm, st);
         }
     }
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }
 
-static int run_rescale(mhe_ctx *c, const u64 *in, u64 *out, int size, int L, hipStream_t st)
+static int run_switch_key(mhe_ctx *c, u64 *ct, const u64 *target, const u64 *key, int key_limbs, int L,
+                          hipStream_t st, u64 *rescale_out = nullptr, int c1_write = 0)
 {
+    const KsJob j{ ct, target, key, key_limbs, rescale_out };
+    return run_switch_key_batch(c, &j, 1, L, st, c1_write);
+}
+
+// rescale_to_next (util/rns.cpp:737-808) of B <= MHE_MAXB independent ciphertexts of `size` polys
+// at L limbs, in[e] -> out[e] ([size][L-1][n]), every kernel launched once for all of them.
+static int run_rescale_batch(mhe_ctx *c, const u64 *const *in, u64 *const *out, int B, int size, int L, hipStream_t st)
+{
+    if (B < 1 || B > MHE_MAXB) return fail(MHE_ERR_ARG, "rescale: batch size out of range");
     Workspace *w;
-    int r = get_ws(c, st, c->K - 1, &w);
+    int r = get_ws(c, st, c->K - 1, &w, B);
     if (r) return r;
     const int log_n = c->log_n;
-    // last[s] = INTT(in[s][L-1]) canonical -> w->coeff (size <= 3 polys)
-    JobLastInv li{ in, w->coeff, c->primes, c->itw, L, log_n, 1 };
-    inv_row(li, log_n, size, c->nm, st);
-    JobRescaleCol rc{ w->coeff, w->modup, c->primes, c->tw, L, log_n };
+    // last[s] = INTT(in[s][L-1]) canonical -> the entry's coeff (size <= 3 polys)
+    JobB<JobLastInv> li;
+    li.per = size;
+    JobB<JobRescaleCol> rc;
+    rc.per = size * (L - 1);
+    JobB<JobRescaleRow> rr;
+    rr.per = size * (L - 1);
+    ColSrc cs{};
+    cs.stride = c->n;
+    cs.per = size;
+    cs.primes = c->primes;
+    cs.itw = c->itw;
+    cs.pi = L - 1;
+    for (int e = 0; e < B; e++)
+    {
+        li.j[e] = JobLastInv{ in[e], w->e[e].coeff, c->primes, c->itw, L, log_n, 1 };
+        rc.j[e] = JobRescaleCol{ w->e[e].coeff, w->e[e].modup, c->primes, c->tw, L, log_n };
+        rr.j[e] = JobRescaleRow{ w->e[e].modup, in[e], out[e], c->primes, c->tw, c->invq, L, c->K, log_n };
+        rr.j[e].fp = c->nm.fp ? 1 : 0;
+        cs.src[e] = w->e[e].coeff;
+    }
+    inv_row(li, log_n, size * B, c->nm, st);
     if (c->icol_fused)
     {
         // the last limb's inverse column pass runs inside the lift column pass (k_icol_lift)
-        const ColSrc cs{ w->coeff, c->n, c->primes, c->itw, L - 1 };
-        icol_lift(cs, rc, size, L - 1, log_n, c->nm, st);
+        icol_lift(cs, rc, size * B, L - 1, log_n, c->nm, st);
     }
     else
     {
-        JobStrided j2{ w->coeff, w->coeff, c->n, c->n, L - 1, 0, c->primes, c->itw, log_n, 1 };
-        inv_col(j2, log_n, size, c->nm, st);
-        fwd_col(rc, log_n, size * (L - 1), c->nm, st);
+        JobB<JobStrided> j2;
+        j2.per = size;
+        for (int e = 0; e < B; e++) j2.j[e] = JobStrided{ w->e[e].coeff, w->e[e].coeff, c->n, c->n, L - 1, 0, c->primes, c->itw, log_n, 1 };
+        inv_col(j2, log_n, size * B, c->nm, st);
+        fwd_col(rc, log_n, size * (L - 1) * B, c->nm, st);
     }
-    JobRescaleRow rr{ w->modup, in, out, c->primes, c->tw, c->invq, L, c->K, log_n };
-    rr.fp = c->nm.fp ? 1 : 0;
-    fwd_row(rr, log_n, size * (L - 1), c->nm, st);
+    fwd_row(rr, log_n, size * (L - 1) * B, c->nm, st);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
+}
+
+static int run_rescale(mhe_ctx *c, const u64 *in, u64 *out, int size, int L, hipStream_t st)
+{
+    return run_rescale_batch(c, &in, &out, 1, size, L, st);
 }
 
 // ================================================================ internal (encode.hip)
@@ -1529,7 +1698,6 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_KS_PACK")) c->ks_pack = atoi(f);
     if (const char *f = getenv("MHE_GALOIS_FUSED")) c->galois_fused = atoi(f);
     if (const char *f = getenv("MHE_ICOL_FUSED")) c->icol_fused = atoi(f);
-    if (const char *f = getenv("MHE_KS_GROUPS")) c->ks_groups = atoi(f) > 8 ? 8 : atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);
     for (int k = 0; k < count; k++)
@@ -2005,6 +2173,7 @@ MHE_EXPORT int mhe_stream_wait(mhe_ctx *c, void *waiter, void *waitee)
     // enqueued on `waitee` before it (no host blocking)
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
     if (waiter == waitee) return MHE_OK;
+    HIP_TRY(hipSetDevice(c->device)); // the event must belong to the engine's device
     hipEvent_t ev;
     HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     hipError_t e = hipEventRecord(ev, S(waitee));
@@ -2263,6 +2432,96 @@ MHE_EXPORT int mhe_apply_galois_to(mhe_ctx *c, const uint64_t *in, uint64_t *out
     if (r) return r;
     HIP_TRY(hipMemsetAsync(out + ps, 0, ps * sizeof(u64), st));
     return run_switch_key(c, out, w->tmp, key, key_limbs, limbs, st);
+}
+
+MHE_EXPORT int mhe_apply_galois_batch(mhe_ctx *c, int count, const uint64_t *const *in, uint64_t *const *out,
+                                      const uint32_t *elts, const uint64_t *const *keys, const int *key_limbs, int limbs,
+                                      void *s)
+{
+    int r = check_limbs(c, limbs, 1);
+    if (r) return r;
+    if (count < 0 || (count && (!in || !out || !elts || !keys || !key_limbs))) return fail(MHE_ERR_ARG, "invalid argument");
+    hipStream_t st = S(s);
+    const size_t ps = (size_t)limbs << c->log_n;
+    for (int i = 0; i < count; i++)
+    {
+        if (!in[i] || !out[i] || !keys[i]) return fail(MHE_ERR_ARG, "Galois key not present");
+        if (!(elts[i] & 1) || elts[i] >= 2 * c->n) return fail(MHE_ERR_ARG, "Galois element is not valid");
+        // outputs must be disjoint from every input and from each other (all are written before the
+        // first key switch reads its input's permutation back from its own output)
+        for (int j = 0; j < count; j++)
+        {
+            const bool ov_in = out[i] < in[j] + 2 * ps && in[j] < out[i] + 2 * ps;
+            const bool ov_out = j != i && out[i] < out[j] + 2 * ps && out[j] < out[i] + 2 * ps;
+            if (ov_in || ov_out) return fail(MHE_ERR_ARG, "result cannot point to the same value as operand");
+        }
+    }
+    if (!c->galois_fused)
+    {
+        for (int i = 0; i < count; i++)
+            if ((r = mhe_apply_galois_to(c, in[i], out[i], elts[i], keys[i], key_limbs[i], limbs, s))) return r;
+        return MHE_OK;
+    }
+    for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
+    {
+        const int B = std::min(MHE_MAXB, count - i0);
+        // out_e <- perm_e(in_e), both polys, one launch (evaluator.cpp:2193-2214; SEAL zeroes c1 and
+        // adds KS_1, the same words as writing it)
+        GalPtrs gp{};
+        KsJob jobs[MHE_MAXB];
+        for (int e = 0; e < B; e++)
+        {
+            gp.in[e] = in[i0 + e];
+            gp.out[e] = out[i0 + e];
+            gp.elt[e] = elts[i0 + e];
+            jobs[e] = KsJob{ out[i0 + e], out[i0 + e] + ps, keys[i0 + e], key_limbs[i0 + e], nullptr };
+        }
+        const size_t total = 2 * ps;
+        hipLaunchKernelGGL(k_galois_b, dim3((unsigned)((total + 255) / 256), (unsigned)B), dim3(256), 0, st, gp, c->log_n,
+                           total);
+        HIP_LAUNCH_CHECK();
+        if ((r = run_switch_key_batch(c, jobs, B, limbs, st, 1))) return r;
+    }
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_rescale_batch(mhe_ctx *c, int count, const uint64_t *const *in, uint64_t *const *out, int size,
+                                 int limbs, void *s)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (limbs < 2) return fail(MHE_ERR_RANGE, "end of modulus switching chain reached");
+    if (limbs > c->K || size < 1 || size > 3 || count < 0 || (count && (!in || !out)))
+        return fail(MHE_ERR_ARG, "encrypted is not valid for encryption parameters");
+    for (int i = 0; i < count; i++)
+    {
+        if (!in[i] || !out[i]) return fail(MHE_ERR_ARG, "encrypted is not valid for encryption parameters");
+        if (in[i] == out[i]) return fail(MHE_ERR_ARG, "rescale output must not alias its input");
+    }
+    for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
+    {
+        const int B = std::min(MHE_MAXB, count - i0);
+        int r = run_rescale_batch(c, in + i0, out + i0, B, size, limbs, S(s));
+        if (r) return r;
+    }
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_switch_key_batch(mhe_ctx *c, int count, uint64_t *const *ct, const uint64_t *const *target,
+                                    const uint64_t *const *keys, const int *key_limbs, int limbs, void *s)
+{
+    int r = check_limbs(c, limbs, 1);
+    if (r) return r;
+    if (count < 0 || (count && (!ct || !target || !keys || !key_limbs))) return fail(MHE_ERR_ARG, "invalid argument");
+    for (int i = 0; i < count; i++)
+        if (!ct[i] || !target[i] || !keys[i]) return fail(MHE_ERR_ARG, "target_iter");
+    for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
+    {
+        const int B = std::min(MHE_MAXB, count - i0);
+        KsJob jobs[MHE_MAXB];
+        for (int e = 0; e < B; e++) jobs[e] = KsJob{ ct[i0 + e], target[i0 + e], keys[i0 + e], key_limbs[i0 + e], nullptr };
+        if ((r = run_switch_key_batch(c, jobs, B, limbs, S(s)))) return r;
+    }
+    return MHE_OK;
 }
 
 MHE_EXPORT int mhe_rescale_to_next(mhe_ctx *c, const uint64_t *in, uint64_t *out, int size, int limbs, void *s)

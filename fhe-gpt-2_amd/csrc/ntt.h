@@ -25,6 +25,11 @@
 #include "arith.h"
 #include "fparith.h"
 
+// Batched launches: one launch of a key-switch / rescale kernel serves up to MHE_MAXB independent
+// ciphertexts of the same level (per-entry pointers in the kernel arguments, entry = a grid
+// dimension), so small-level work from independent rotations or images fills the chip.
+#define MHE_MAXB 8
+
 
 // Streaming (non-temporal) access for the key-switch streams, selected at build time (MHE_NT bit 0:
 // ModUp intermediate stores, bit 1: key loads, bit 2: intermediate loads in the fused MAC).
@@ -423,11 +428,17 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long t
 // round trip disappear, and the outputs are the same words.
 struct ColSrc
 {
-    const u64 *src;       // poly s at src + s * stride, after the inverse row pass
+    const u64 *src[MHE_MAXB]; // poly s of batch entry e at src[e] + s * stride, after the inverse row pass
     size_t stride;
+    int per;                  // polys per batch entry
     const PrimeDev *primes;
-    const Tw *itw;        // inverse twiddle rows
-    int pi;               // prime index of the source limb
+    const Tw *itw;            // inverse twiddle rows
+    int pi;                   // prime index of the source limb
+    __device__ const u64 *poly(int y) const
+    {
+        const int e = y / per;
+        return src[e] + (size_t)(y - e * per) * stride;
+    }
 };
 
 template <int LOGR, int LOGT, class Job, bool FP>
@@ -450,7 +461,7 @@ __global__ __launch_bounds__(256) void k_icol_lift(ColSrc cs, Job job, int cnt, 
         // the inverse column pass of k_inv_col, canonical output
         const PrimeDev P = cs.primes[cs.pi];
         const A ai(P, cs.itw + ((size_t)cs.pi << log_n), dinv);
-        const u64 *src = cs.src + (size_t)s * cs.stride;
+        const u64 *src = cs.poly(s);
         T v[E];
 #pragma unroll
         for (int e = 0; e < E; e++) v[e] = ai.in(src[c + ((u32)(E * t + e) << logC)]);
@@ -511,12 +522,25 @@ __global__ __launch_bounds__(256) void k_icol_lift(ColSrc cs, Job job, int cnt, 
 // lifted + transformed for every output prime I of the group (I == J skipped: the MAC reads
 // the input NTT form).  Reading each digit once instead of once per output prime removes
 // L(L+1) - L limb reads (~1 GB at L=44) from the key switch.
-template <int LOGR, int LOGT, bool FP>
-__global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ coeff, u64 *__restrict__ modup,
-                                                   const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all,
-                                                   int L, int K, int log_n, long long twd, int I0, int Icnt,
-                                                   int pack, int X, int IG, int xcd)
+// Per-entry buffers of a (batched) key switch: entry e is blockIdx.y of the ModUp column pass and
+// blockIdx.z of the fused row pass + MAC.
+struct KsPtrs
 {
+    const u64 *coeff[MHE_MAXB];  // INTT(target), canonical [L][n]
+    u64 *inter[MHE_MAXB];        // ModUp column-pass output [Icnt][L][n]
+    const u64 *target[MHE_MAXB]; // target, NTT form [L][n]
+    const u64 *key[MHE_MAXB];    // [digits][2][key_limbs][n]
+    u64 *acc[MHE_MAXB];          // key inner products [2][L+1][n]
+    int key_limbs[MHE_MAXB];
+};
+
+template <int LOGR, int LOGT, bool FP>
+__global__ __launch_bounds__(256, 3) void k_modup_col(KsPtrs P, const PrimeDev *__restrict__ primes,
+                                                   const Tw *__restrict__ tw_all, int L, int K, int log_n,
+                                                   long long twd, int I0, int Icnt, int pack, int X, int IG, int xcd)
+{
+    const u64 *__restrict__ coeff = P.coeff[blockIdx.y];
+    u64 *__restrict__ modup = P.inter[blockIdx.y];
     using SH = Shape<LOGR, LOGT>;
     using A = NttArith<FP>;
     using T = typename A::T;
@@ -638,7 +662,7 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(const u64 *__restrict__ co
 }
 
 template <int LOGR, bool FP>
-static inline void modup_col_a(const u64 *coeff, u64 *modup, const PrimeDev *primes, const Tw *tw, int L, int K,
+static inline void modup_col_a(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K,
                                int log_n, long long twd, int I0, int Icnt, int IG, int pack, hipStream_t st)
 {
 #ifndef MHE_MODUP_LOGT8
@@ -653,30 +677,31 @@ static inline void modup_col_a(const u64 *coeff, u64 *modup, const PrimeDev *pri
     }();
     const int X = subs / SH::S;
     const int xcd = (xcd_env && (X * L) % 8 == 0) ? 1 : 0;
-    hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3((unsigned)(X * L * IG)), dim3(256), 0, st, coeff, modup,
+    hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3((unsigned)(X * L * IG), (unsigned)B), dim3(256), 0, st, P,
                        primes, tw, L, K, log_n, twd, I0, Icnt, pack, X, IG, xcd);
 }
 
-// ModUp column pass for output primes I0 .. I0+Icnt-1 (modup holds exactly those), in IG
-// groups of output primes per digit.  pack (n = 2^16 only): limbs of primes below 2^48 are
-// stored in the packed 48-bit form (tile16), which k_ks_row_mac must then be told as well.
-static inline void modup_col(const u64 *coeff, u64 *modup, const PrimeDev *primes, const Tw *tw, int L, int K,
+// ModUp column pass for output primes I0 .. I0+Icnt-1 (each entry's inter holds exactly those), in
+// IG groups of output primes per digit, over B batch entries.  pack (n = 2^16 only): limbs of
+// primes below 2^48 are stored in the packed 48-bit form (tile16), which k_ks_row_mac must then be
+// told as well.
+static inline void modup_col(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K,
                              int log_n, const NttMode &m, int I0, int Icnt, int IG, int pack, hipStream_t st)
 {
     switch ((log_n + 1) / 2)
     {
     case 6:
-        if (m.fp) modup_col_a<6, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
-        else modup_col_a<6, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
+        if (m.fp) modup_col_a<6, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        else modup_col_a<6, false>(P, B, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
         break;
     case 7:
-        if (m.fp) modup_col_a<7, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
-        else modup_col_a<7, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
+        if (m.fp) modup_col_a<7, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        else modup_col_a<7, false>(P, B, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
         break;
     case 8:
         pack = (pack && log_n == 16) ? 1 : 0;
-        if (m.fp) modup_col_a<8, true>(coeff, modup, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, pack, st);
-        else modup_col_a<8, false>(coeff, modup, primes, tw, L, K, log_n, 0, I0, Icnt, IG, pack, st);
+        if (m.fp) modup_col_a<8, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, pack, st);
+        else modup_col_a<8, false>(P, B, primes, tw, L, K, log_n, 0, I0, Icnt, IG, pack, st);
         break;
     }
 }
@@ -736,8 +761,9 @@ static inline void launch_row(const Job &job, int log_n, int jobs, const NttMode
     }
 }
 
-// k_icol_lift over `polys` source polys and `cnt` output primes each (job index s * cnt + i), the
-// column-pass shape of launch_col; IG groups of output primes per (column block, poly)
+// k_icol_lift over `polys` source polys (all batch entries: cs.per polys each) and `cnt` output
+// primes each (job index s * cnt + i), the column-pass shape of launch_col; IG groups of output
+// primes per (column block, poly)
 template <int LOGR, class Job, bool FP>
 static inline void icol_lift_a(const ColSrc &cs, const Job &job, int polys, int cnt, int log_n, long long dinv,
                                long long dfwd, hipStream_t st)
@@ -786,7 +812,7 @@ template <class Job> static inline void inv_col(const Job &j, int log_n, int job
 // Fused key-switching ModUp row pass + key inner product (evaluator.cpp:2386-2463).
 //
 // One workgroup owns output prime I (blockIdx.y; I == L is the special prime) and S blocks of
-// R = 2^LOGR coefficients; blockIdx.z selects a range of digits J.  For every digit it takes
+// R = 2^LOGR coefficients; blockIdx.z is the batch entry (KsPtrs).  For every digit J it takes
 // the column-pass output of (I, J) (or, for I == J, the input target limb, already in NTT
 // form), finishes the forward NTT in registers, and multiply-accumulates with key[J][0][I] and
 // key[J][1][I] into 128-bit accumulators.  NTT'd digits never touch HBM; each key residue is
@@ -850,14 +876,17 @@ template <int LOGR, bool FP, bool KPF>
 #ifndef MHE_KS_DPF
 #define MHE_KS_DPF 1 // fused MAC: load the next digit one digit ahead (1) or at the top of the digit (0)
 #endif
-__global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__restrict__ inter, // [L+1][L][n] column-pass out
-                                                       const u64 *__restrict__ target, // [L][n] NTT form
-                                                       const u64 *__restrict__ key,    // [digits][2][key_limbs][n]
-                                                       u64 *__restrict__ acc,          // [G][2][L+1][n]
-                                                       const PrimeDev *__restrict__ primes,
-                                                       const Tw *__restrict__ tw_all, int L, int K, int key_limbs,
-                                                       int log_n, long long twd, int I0, int pack, int kpack)
+__global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
+                                                       const Tw *__restrict__ tw_all, int L, int K, int log_n,
+                                                       long long twd, int I0, int pack, int kpack)
 {
+    // batch entry blockIdx.z: inter [cnt][L][n] column-pass output, target [L][n] NTT form,
+    // key [digits][2][key_limbs][n], acc [2][L+1][n]
+    const u64 *__restrict__ inter = P.inter[blockIdx.z];
+    const u64 *__restrict__ target = P.target[blockIdx.z];
+    const u64 *__restrict__ key = P.key[blockIdx.z];
+    u64 *__restrict__ acc = P.acc[blockIdx.z];
+    const int key_limbs = P.key_limbs[blockIdx.z];
     using SH = RowMacShape<LOGR>;
     using A = NttArith<FP>;
     using T = typename A::T;
@@ -869,8 +898,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__res
     // 49 KB per workgroup fits 3 workgroups per CU, two buffers (65.6 KB) only 2
     __shared__ T xch[MHE_KS_XCH][S * R];
     __shared__ TW twl[S * (R + 1)];
-    const int G = gridDim.z, g = blockIdx.z;
-    const int j0 = (L * g) / G, j1 = (L * (g + 1)) / G;
+    const int j0 = 0, j1 = L;
     const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
     const u32 b = blockIdx.x * S + sl;
     const u32 base = b << LOGR;
@@ -1079,7 +1107,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__res
                 }
             }
         }
-        u64 *o0 = acc + (size_t)(2 * g * (L + 1) + I) * n + base;
+        u64 *o0 = acc + (size_t)I * n + base;
         u64 *o1 = o0 + (size_t)(L + 1) * n;
 #pragma unroll
         for (int e = 0; e < 8; e++)
@@ -1110,20 +1138,6 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(const u64 *__res
         run(ar0);
 }
 
-// Sum the G partial accumulators: acc[0] += acc[1..G-1] mod q (prime of each limb).
-__global__ void k_acc_reduce(u64 *acc, const PrimeDev *primes, int L, int K, int G, int log_n)
-{
-    const size_t n = (size_t)1 << log_n;
-    const size_t per = (size_t)2 * (L + 1) * n;
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= per) return;
-    const int limb = (int)((i >> log_n) % (L + 1));
-    const u64 q = primes[limb == L ? K - 1 : limb].q;
-    u64 s = acc[i];
-    for (int g = 1; g < G; g++) s = addmod(s, acc[g * per + i], q);
-    acc[i] = s;
-}
-
 // Key prefetch distance of the fused kernel: none (default; measured equal, fewer VGPRs) or one digit ahead (MHE_KS_KPF=1).
 static inline bool ks_key_prefetch()
 {
@@ -1134,66 +1148,41 @@ static inline bool ks_key_prefetch()
     return v;
 }
 
-// Digit groups G: enough workgroups to hide HBM latency (each one walks L/G digits).
-static inline int ks_groups(int L)
-{
-    // measured at L=44: G=1 763, 2 738, 4 700 HMult/s; ResNet-20 (L <= 31): G=1 0.865-0.873 images/s
-    // vs 0.832-0.839 with G=2 (scripts/gpu_sweep_env.sh), and no partial-sum reduction launch
-    (void)L;
-    return 1;
-}
-
+// measured at L=44: G=1 763, 2 738, 4 700 HMult/s (digit groups with a partial-sum reduction, since
+// removed); ResNet-20 (L <= 31): G=1 0.865-0.873 images/s vs 0.832-0.839 with G=2
 template <int LOGR, bool FP>
-static inline void ks_row_mac_a(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
-                                const Tw *tw, int L, int K, int key_limbs, int log_n, long long twd, int G, int I0,
-                                int cnt, int pack, int kpack, hipStream_t st)
+static inline void ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
+                                long long twd, int I0, int cnt, int pack, int kpack, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
-    const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, G);
+    const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, B);
     if (ks_key_prefetch())
-        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, inter, target, key, acc, primes, tw,
-                           L, K, key_limbs, log_n, twd, I0, pack, kpack);
+        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
+                           pack, kpack);
     else
-        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, inter, target, key, acc, primes,
-                           tw, L, K, key_limbs, log_n, twd, I0, pack, kpack);
+        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
+                           pack, kpack);
 }
 
 template <int LOGR>
-static inline void ks_row_mac_m(const u64 *inter, const u64 *target, const u64 *key, u64 *acc, const PrimeDev *primes,
-                                const Tw *tw, int L, int K, int key_limbs, int log_n, const NttMode &m, int G, int I0,
-                                int cnt, int pack, int kpack, hipStream_t st)
+static inline void ks_row_mac_m(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
+                                const NttMode &m, int I0, int cnt, int pack, int kpack, hipStream_t st)
 {
     if (m.fp)
-        ks_row_mac_a<LOGR, true>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m.dfwd, G, I0, cnt, pack,
-                                 kpack, st);
+        ks_row_mac_a<LOGR, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, st);
     else
-        ks_row_mac_a<LOGR, false>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, 0, G, I0, cnt, pack,
-                                  kpack, st);
+        ks_row_mac_a<LOGR, false>(P, B, primes, tw, L, K, log_n, 0, I0, cnt, pack, kpack, st);
 }
 
-// Fused row pass + MAC for output primes I0 .. I0+cnt-1 (inter holds exactly those).
-static inline void ks_row_mac_chunk(const u64 *inter, const u64 *target, const u64 *key, u64 *acc,
-                                    const PrimeDev *primes, const Tw *tw, int L, int K, int key_limbs, int log_n,
-                                    const NttMode &m, int G, int I0, int cnt, int pack, int kpack, hipStream_t st)
+// Fused row pass + MAC for output primes I0 .. I0+cnt-1 (each entry's inter holds exactly those),
+// over B batch entries.
+static inline void ks_row_mac_chunk(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K,
+                                    int log_n, const NttMode &m, int I0, int cnt, int pack, int kpack, hipStream_t st)
 {
     switch (log_n / 2)
     {
-    case 6: ks_row_mac_m<6>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, kpack, st); break;
-    case 7: ks_row_mac_m<7>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt, 0, kpack, st); break;
-    case 8:
-        ks_row_mac_m<8>(inter, target, key, acc, primes, tw, L, K, key_limbs, log_n, m, G, I0, cnt,
-                        (pack && log_n == 16) ? 1 : 0, kpack, st);
-        break;
-    }
-}
-
-// Sum of the G digit-group partials (after every chunk has run).
-static inline void ks_acc_finish(u64 *acc, const PrimeDev *primes, int L, int K, int G, int log_n, hipStream_t st)
-{
-    if (G > 1)
-    {
-        const size_t per = (size_t)2 * (L + 1) << log_n;
-        hipLaunchKernelGGL(k_acc_reduce, dim3((unsigned)((per + 255) / 256)), dim3(256), 0, st, acc, primes, L, K, G,
-                           log_n);
+    case 6: ks_row_mac_m<6>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, st); break;
+    case 7: ks_row_mac_m<7>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, st); break;
+    case 8: ks_row_mac_m<8>(P, B, primes, tw, L, K, log_n, m, I0, cnt, (pack && log_n == 16) ? 1 : 0, kpack, st); break;
     }
 }

@@ -214,6 +214,9 @@ public:
     std::size_t verify_cache(); // debugging aid: re-encode and compare every cached plaintext
 
 private:
+    // the giant-step rotations of a BSGS transform in batched launches, then the outer sum
+    void giant_rotate_sum(std::vector<seal::Ciphertext> &giantct, std::vector<seal::Ciphertext> &rotct, int first,
+                          int gs, int basicstep, seal::Ciphertext &rtncipher);
     void multiply_diag(seal::Ciphertext &ct, const std::vector<std::complex<double>> &diag, int coeff_logn,
                        int shift, seal::Ciphertext &dest, double coeff_scale = 1.0, bool accumulate = false);
     struct PtKey

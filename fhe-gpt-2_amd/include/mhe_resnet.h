@@ -37,6 +37,10 @@ void import_parameters_cifar10(std::vector<double> &linear_weight, std::vector<d
                                std::size_t end_num, const std::string &dir = "../../pretrained_parameters");
 // The same values from one float64 file in import order (tests/golden/make_resnet_params.py).
 ResNetParams load_resnet_params_bin(const std::string &path, std::size_t layer_num);
+// The network in plain doubles with the exact ReLU (the output check of an encrypted inference:
+// the reference prints decrypted logits next to the label, infer_seal.cpp:543-575): image is
+// 3 x 32 x 32 values before the /B of infer_seal.cpp:444; returns the 10 logits.
+std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector<double> &image, std::size_t layer_num);
 
 struct ResNetResult
 {
@@ -80,6 +84,10 @@ public:
     double galois_key_gb() const;
     // key-switching key bytes streamed by this runner's key switches since the last reset
     double key_traffic_bytes(bool reset);
+    // the evaluation keys are in the engine's prepared format (mhe_key_prepare) rather than SEAL's
+    bool keys_prepared() const { return keys_prepared_; }
+    // resnet_plain_logits with this runner's parameters
+    std::vector<double> plain_logits(const std::vector<double> &image) const;
 
     // key buffers as device memory, for sharing one key set across GPUs: kind 0 secret key [K][n],
     // 1 public key [2][K][n], 2 relinearization key [K-1][2][K][n], 3 Galois key `index` with

@@ -677,6 +677,15 @@ public:
                          Ciphertext &destination) const;
     void rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                        Ciphertext &destination, MemoryPoolHandle = {}) const;
+    // (not SEAL API) independent rotations in batched launches: *destinations[i] =
+    // rotate_vector(*encrypted[i], steps[i]) for every i, bit-identical to the one-by-one calls.
+    // Entries of one level with a key present run together (mhe_apply_galois_batch); a zero step,
+    // a missing key (NAF decomposition) or a lone level falls back to rotate_vector.  Destinations
+    // must be distinct objects, none of them an input.
+    void rotate_vectors(const std::vector<const Ciphertext *> &encrypted, const std::vector<int> &steps,
+                        const GaloisKeys &galois_keys, const std::vector<Ciphertext *> &destinations) const;
+    // (not SEAL API) rescale_to_next_inplace of independent ciphertexts in batched launches
+    void rescale_to_next_inplace_many(const std::vector<Ciphertext *> &encrypted) const;
     void complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKeys &galois_keys, MemoryPoolHandle = {}) const;
     void complex_conjugate(const Ciphertext &encrypted, const GaloisKeys &galois_keys, Ciphertext &destination,
                            MemoryPoolHandle = {}) const;

@@ -64,6 +64,11 @@ SIGNATURES = {
     "mhe_apply_galois_to": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_permute_galois": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_rescale_to_next": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_apply_galois_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, ctypes.POINTER(ctypes.c_uint32), vp,
+                                              ctypes.POINTER(ctypes.c_int), ctypes.c_int, vp]),
+    "mhe_rescale_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_switch_key_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                            vp]),
     "mhe_mod_switch_drop": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_modraise": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_hmult": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]),
@@ -328,6 +333,33 @@ class Engine:
         _check(lib().mhe_apply_galois_to(self._h, _ptr(ct), _ptr(out), elt, _ptr(key), self._key_limbs(key),
                                          ct.shape[1], self.stream()))
         return out
+
+    @staticmethod
+    def _ptrs(ts):
+        return (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
+
+    def apply_galois_batch(self, cts, elts, keys, outs=None):
+        """mhe_apply_galois_batch: one batched launch sequence for len(cts) independent rotations."""
+        outs = [self.empty(*c.shape) for c in cts] if outs is None else outs
+        cnt = len(cts)
+        e = (ctypes.c_uint32 * cnt)(*[int(x) for x in elts])
+        kl = (ctypes.c_int * cnt)(*[self._key_limbs(k) for k in keys])
+        _check(lib().mhe_apply_galois_batch(self._h, cnt, self._ptrs(cts), self._ptrs(outs), e, self._ptrs(keys), kl,
+                                            cts[0].shape[1], self.stream()))
+        return outs
+
+    def rescale_batch(self, cts, outs=None):
+        size, L = cts[0].shape[0], cts[0].shape[1]
+        outs = [self.empty(size, L - 1, self.n) for _ in cts] if outs is None else outs
+        _check(lib().mhe_rescale_batch(self._h, len(cts), self._ptrs(cts), self._ptrs(outs), size, L, self.stream()))
+        return outs
+
+    def switch_key_batch(self, cts, targets, keys):
+        cnt = len(cts)
+        kl = (ctypes.c_int * cnt)(*[self._key_limbs(k) for k in keys])
+        _check(lib().mhe_switch_key_batch(self._h, cnt, self._ptrs(cts), self._ptrs(targets), self._ptrs(keys), kl,
+                                          cts[0].shape[1], self.stream()))
+        return cts
 
     def permute_galois(self, a, elt, out=None):
         out = self.empty(*a.shape) if out is None else out

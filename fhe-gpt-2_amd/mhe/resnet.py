@@ -40,6 +40,8 @@ def seal_lib():
             "mhe_resnet_infer_batch": (i32, [vp, dp, i32, i32, dp, ip, dp, dp, dp, dp]),
             "mhe_resnet_info": (i32, [vp, dp, dp, ip]),
             "mhe_resnet_key_traffic": (i32, [vp, dp, i32]),
+            "mhe_resnet_key_format": (i32, [vp, ip]),
+            "mhe_resnet_plain_logits": (i32, [vp, dp, dp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -116,6 +118,34 @@ class Runner:
         b = ctypes.c_double()
         _check(seal_lib().mhe_resnet_key_traffic(self._h, ctypes.byref(b), 1 if reset else 0))
         return b.value
+
+    def keys_prepared(self):
+        """True when the evaluation keys are in the engine's prepared format (mhe_key_prepare)."""
+        p = ctypes.c_int()
+        _check(seal_lib().mhe_resnet_key_format(self._h, ctypes.byref(p)))
+        return bool(p.value)
+
+    def plain_logits(self, image):
+        """The network in plain doubles (exact ReLU) on one 3072-value image -> 10 logits."""
+        img = np.ascontiguousarray(image, dtype=np.float64).reshape(3072)
+        out = np.zeros(10)
+        dp = ctypes.POINTER(ctypes.c_double)
+        _check(seal_lib().mhe_resnet_plain_logits(self._h, img.ctypes.data_as(dp), out.ctypes.data_as(dp)))
+        return out
+
+    def check_logits(self, images, logits, tol=0.05):
+        """Decrypted logits vs the plain network: max |error| per image must stay below
+        tol * max(1, max |plain logit|) (tests/cpp/resnet_test.cpp's band for ResNet-20; 0.08 is
+        used for the deeper networks).  Returns (max relative error, [per-image errors]); raises on a miss."""
+        errs = []
+        for img, got in zip(images, logits):
+            want = self.plain_logits(img)
+            err = float(np.max(np.abs(np.asarray(got) - want)))
+            bound = tol * max(1.0, float(np.max(np.abs(want))))
+            errs.append(round(err, 5))
+            if not err < bound:
+                raise RuntimeError(f"encrypted ResNet logits off the plain network: max |error| {err:.4g} >= {bound:.4g}")
+        return errs
 
     def info(self):
         s, gb, nk = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()

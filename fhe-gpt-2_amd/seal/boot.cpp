@@ -1046,15 +1046,28 @@ void Bootstrapper::bsgs_linear_transform(Ciphertext &rtncipher, Ciphertext &ciph
     const int giantlast1 = (int)std::floor((2 * totlen + 0.0) / (gs1 + 0.0)) + giantfirst1;
     const int nh = (int)Nh;
     std::vector<Ciphertext> babyct(gs1);
-    Ciphertext giantct, tmpct, tmptmpct;
-    bool tmpctbool = false;
-    for (int i = basicstart1; i < basicstart1 + gs1; i++)
+    // the baby-step rotations of one input are independent: batched launches
     {
-        if (i == 0)
-            babyct[i - basicstart1] = cipher;
-        else
-            evaluator.rotate_vector(cipher, (nh + i * basicstep) % nh, gal_keys, babyct[i - basicstart1]);
+        std::vector<const Ciphertext *> in;
+        std::vector<int> st;
+        std::vector<Ciphertext *> out;
+        for (int i = basicstart1; i < basicstart1 + gs1; i++)
+        {
+            if (i == 0)
+                babyct[i - basicstart1] = cipher;
+            else
+            {
+                in.push_back(&cipher);
+                st.push_back((nh + i * basicstep) % nh);
+                out.push_back(&babyct[i - basicstart1]);
+            }
+        }
+        evaluator.rotate_vectors(in, st, gal_keys, out);
     }
+    // every giant step's inner sum first, then their rotations (independent) in batched launches,
+    // then the outer sum in the reference's order: the same operations on the same words
+    const int ng = giantlast1 - giantfirst1 + 1;
+    std::vector<Ciphertext> giantct(ng), rotct(ng);
     for (int i = giantfirst1; i <= giantlast1; i++)
     {
         bool giantbool = false;
@@ -1062,30 +1075,39 @@ void Bootstrapper::bsgs_linear_transform(Ciphertext &rtncipher, Ciphertext &ciph
         for (int j = basicstart1; j <= jlast; j++)
         {
             multiply_diag(babyct[j - basicstart1], fftcoeff[(i * gs1 + j) + totlen], coeff_logn,
-                          (-i) * gs1 * basicstep, giantct, coeff_scale, giantbool);
+                          (-i) * gs1 * basicstep, giantct[i - giantfirst1], coeff_scale, giantbool);
             giantbool = true;
         }
-        if (i != 0)
-        {
-            evaluator.rotate_vector(giantct, (nh + i * gs1 * basicstep) % nh, gal_keys, tmptmpct);
-            if (!tmpctbool)
-            {
-                tmpct = tmptmpct;
-                tmpctbool = true;
-            }
-            else
-                evaluator.add_inplace_reduced_error(tmpct, tmptmpct);
-        }
+    }
+    giant_rotate_sum(giantct, rotct, giantfirst1, gs1, basicstep, rtncipher);
+}
+
+void Bootstrapper::giant_rotate_sum(std::vector<Ciphertext> &giantct, std::vector<Ciphertext> &rotct, int first,
+                                    int gs, int basicstep, Ciphertext &rtncipher)
+{
+    // giant step i = first + k: rotate its inner sum by i * gs * basicstep (i != 0), then
+    // tmpct = sum over k in order (Bootstrapper.cpp:1990-2015 / 2059-2084)
+    const int nh = (int)Nh;
+    std::vector<const Ciphertext *> in;
+    std::vector<int> st;
+    std::vector<Ciphertext *> out;
+    for (std::size_t k = 0; k < giantct.size(); k++)
+    {
+        const int i = first + (int)k;
+        if (i == 0) continue;
+        in.push_back(&giantct[k]);
+        st.push_back((nh + i * gs * basicstep) % nh);
+        out.push_back(&rotct[k]);
+    }
+    evaluator.rotate_vectors(in, st, gal_keys, out);
+    Ciphertext tmpct;
+    for (std::size_t k = 0; k < giantct.size(); k++)
+    {
+        const Ciphertext &term = (first + (int)k != 0) ? rotct[k] : giantct[k];
+        if (k == 0)
+            tmpct = term;
         else
-        {
-            if (!tmpctbool)
-            {
-                tmpct = giantct;
-                tmpctbool = true;
-            }
-            else
-                evaluator.add_inplace_reduced_error(tmpct, giantct);
-        }
+            evaluator.add_inplace_reduced_error(tmpct, term);
     }
     rtncipher = tmpct;
 }
@@ -1099,48 +1121,36 @@ void Bootstrapper::rotated_bsgs_linear_transform(Ciphertext &rtncipher, Cipherte
     const int giantlast2 = (int)std::floor((totlen + 0.0) / (gs2 + 0.0));
     const int nh = (int)Nh;
     std::vector<Ciphertext> babyct(gs2);
-    Ciphertext giantct, tmpct, tmptmpct;
-    bool tmpctbool = false;
-    for (int i = 0; i < gs2; i++)
     {
-        if (i == 0)
-            babyct[i] = cipher;
-        else
-            evaluator.rotate_vector(cipher, (nh + i * basicstep) % nh, gal_keys, babyct[i]);
+        std::vector<const Ciphertext *> in;
+        std::vector<int> st;
+        std::vector<Ciphertext *> out;
+        for (int i = 0; i < gs2; i++)
+        {
+            if (i == 0)
+                babyct[i] = cipher;
+            else
+            {
+                in.push_back(&cipher);
+                st.push_back((nh + i * basicstep) % nh);
+                out.push_back(&babyct[i]);
+            }
+        }
+        evaluator.rotate_vectors(in, st, gal_keys, out);
     }
+    std::vector<Ciphertext> giantct(giantlast2 + 1), rotct(giantlast2 + 1);
     for (int i = 0; i <= giantlast2; i++)
     {
         bool giantbool = false;
         const int jlast = i != giantlast2 ? gs2 - 1 : totlen - i * gs2;
         for (int j = 0; j <= jlast; j++)
         {
-            multiply_diag(babyct[j], fftcoeff[i * gs2 + j], coeff_logn, (-i) * gs2 * basicstep, giantct,
+            multiply_diag(babyct[j], fftcoeff[i * gs2 + j], coeff_logn, (-i) * gs2 * basicstep, giantct[i],
                           coeff_scale, giantbool);
             giantbool = true;
         }
-        if (i != 0)
-        {
-            evaluator.rotate_vector(giantct, (nh + i * gs2 * basicstep) % nh, gal_keys, tmptmpct);
-            if (!tmpctbool)
-            {
-                tmpct = tmptmpct;
-                tmpctbool = true;
-            }
-            else
-                evaluator.add_inplace_reduced_error(tmpct, tmptmpct);
-        }
-        else
-        {
-            if (!tmpctbool)
-            {
-                tmpct = giantct;
-                tmpctbool = true;
-            }
-            else
-                evaluator.add_inplace_reduced_error(tmpct, giantct);
-        }
     }
-    rtncipher = tmpct;
+    giant_rotate_sum(giantct, rotct, 0, gs2, basicstep, rtncipher);
 }
 
 void Bootstrapper::sfl_half_3(Ciphertext &rtncipher, Ciphertext &cipher)

@@ -173,6 +173,47 @@ void rotate_copy(const Ciphertext &in, Ciphertext &out, int steps, Evaluator &ev
     else
         memory_save_rotate(in, out, steps, evaluator, gal_keys);
 }
+
+// rotate_copy(*ins[i], *outs[i], steps[i]) for every i, the independent rotations in batched
+// launches (Evaluator::rotate_vectors): first every rotation by s (or by 33 for
+// memory_save_rotate's split steps), then the second rotation of the split ones -- the same words
+// as the one-by-one calls.  outs must be distinct and not inputs, except an out that is its own
+// input with a zero step.
+void rotate_copies(const std::vector<const Ciphertext *> &ins, const std::vector<int> &steps,
+                   const std::vector<Ciphertext *> &outs, Evaluator &evaluator, GaloisKeys &gal_keys)
+{
+    if (ins.empty()) return;
+    const long slots = static_cast<long>(ins[0]->poly_modulus_degree() / 2);
+    std::vector<Ciphertext> mid(steps.size());
+    std::vector<const Ciphertext *> in1, in2;
+    std::vector<int> st1, st2;
+    std::vector<Ciphertext *> out1, out2;
+    for (std::size_t i = 0; i < steps.size(); i++)
+    {
+        const long s = (steps[i] + slots) % slots;
+        if (s == 0) continue;
+        const bool split = (s >= 34 && s <= 55) || (s >= 57 && s <= 61);
+        in1.push_back(ins[i]);
+        st1.push_back(split ? 33 : static_cast<int>(s));
+        out1.push_back(split ? &mid[i] : outs[i]);
+        if (split)
+        {
+            in2.push_back(&mid[i]);
+            st2.push_back(static_cast<int>(s - 33));
+            out2.push_back(outs[i]);
+        }
+    }
+    evaluator.rotate_vectors(in1, st1, gal_keys, out1);
+    if (!in2.empty()) evaluator.rotate_vectors(in2, st2, gal_keys, out2);
+    for (std::size_t i = 0; i < steps.size(); i++)
+        if ((steps[i] + slots) % slots == 0 && outs[i] != ins[i]) *outs[i] = *ins[i];
+}
+
+void rotate_copies(const Ciphertext &in, const std::vector<int> &steps, const std::vector<Ciphertext *> &outs,
+                   Evaluator &evaluator, GaloisKeys &gal_keys)
+{
+    rotate_copies(std::vector<const Ciphertext *>(steps.size(), &in), steps, outs, evaluator, gal_keys);
+}
 } // namespace
 
 // ------------------------------------------------------------------------ convolution
@@ -257,12 +298,13 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
             const int idx = fw * i1 + i2, centre = fw * ch + cw;
             rot[idx] = idx == centre ? &ctxt_in : &cipher_pool[6 + (idx > centre ? idx - 1 : idx)];
         }
-    for (int i1 = 0; i1 < fh; i1++)
-        for (int i2 = 0; i2 < fw; i2++)
-        {
-            Ciphertext &r = *rot[fw * i1 + i2];
-            rotate_copy(ctxt_in, r, ki * ki * wi * (i1 - ch) + ki * (i2 - cw), evaluator, gal_keys);
-        }
+    {
+        // the fh*fw - 1 input rotations are independent: batched launches
+        std::vector<int> steps;
+        for (int i1 = 0; i1 < fh; i1++)
+            for (int i2 = 0; i2 < fw; i2++) steps.push_back(ki * ki * wi * (i1 - ch) + ki * (i2 - cw));
+        rotate_copies(ctxt_in, steps, rot, evaluator, gal_keys);
+    }
 
     // encryption of zero at the input scale (cnn_seal.cpp:423-427)
     {
@@ -311,31 +353,45 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         if (c == -1)
         {
             sum = ct_zero;
+            std::vector<Ciphertext> parts(ti);
+            std::vector<Ciphertext *> pp;
+            std::vector<int> steps;
             for (int x = 0; x < ti; x++)
             {
-                rotate_copy(var, temp, ki * ki * hi * wi * x, evaluator, gal_keys);
-                evaluator.add_inplace_reduced_error(sum, temp);
+                pp.push_back(&parts[x]);
+                steps.push_back(ki * ki * hi * wi * x);
             }
+            rotate_copies(var, steps, pp, evaluator, gal_keys);
+            for (int x = 0; x < ti; x++) evaluator.add_inplace_reduced_error(sum, parts[x]);
             var = sum;
         }
         else
             for (int x = 0; x < c; x++) fold(pow2(x) * ki * ki * hi * wi);
 
-        // gather each output channel into its slots of the output layout
+        // gather each output channel into its slots of the output layout (the rotations of var
+        // are independent: batched launches, then the products and sums in the reference's order)
+        std::vector<Ciphertext> gathered(pi);
+        std::vector<Ciphertext *> gp;
+        std::vector<int> gsteps;
         for (int i8 = 0; i8 < pi && pi * i9 + i8 < co; i8++)
         {
             const int j4 = pi * i9 + i8;
-            rotate_copy(var, temp,
-                               (int)((n / pi) * (j4 % pi) - j4 % ko - (j4 / (ko * ko)) * ko * ko * ho * wo -
-                                     ((j4 % (ko * ko)) / ko) * ko * wo),
-                               evaluator, gal_keys);
+            gp.push_back(&gathered[i8]);
+            gsteps.push_back((int)((n / pi) * (j4 % pi) - j4 % ko - (j4 / (ko * ko)) * ko * ko * ho * wo -
+                                   ((j4 % (ko * ko)) / ko) * ko * wo));
+        }
+        rotate_copies(var, gsteps, gp, evaluator, gal_keys);
+        for (int i8 = 0; i8 < pi && pi * i9 + i8 < co; i8++)
+        {
+            const int j4 = pi * i9 + i8;
+            Ciphertext &g = gathered[i8];
             Recipe id = sel_id;
             id.ints({ j4 });
-            multiply_static_vector(evaluator, temp, id, [&] { return select_vec(j4); });
+            multiply_static_vector(evaluator, g, id, [&] { return select_vec(j4); });
             if (i8 == 0 && i9 == 0)
-                total_sum = temp;
+                total_sum = g;
             else
-                evaluator.add_inplace_reduced_error(total_sum, temp);
+                evaluator.add_inplace_reduced_error(total_sum, g);
         }
     }
     evaluator.rescale_to_next_inplace(total_sum);
@@ -345,11 +401,16 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
     if (!end)
     {
         sum = ct_zero;
+        std::vector<Ciphertext> reps(po);
+        std::vector<Ciphertext *> rp;
+        std::vector<int> rsteps;
         for (int u6 = 0; u6 < po; u6++)
         {
-            rotate_copy(var, temp, static_cast<int>(-u6 * (n / po)), evaluator, gal_keys);
-            evaluator.add_inplace_reduced_error(sum, temp);
+            rp.push_back(&reps[u6]);
+            rsteps.push_back(static_cast<int>(-u6 * (n / po)));
         }
+        rotate_copies(var, rsteps, rp, evaluator, gal_keys);
+        for (int u6 = 0; u6 < po; u6++) evaluator.add_inplace_reduced_error(sum, reps[u6]);
         var = sum;
     }
     cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, var);
@@ -435,6 +496,12 @@ void multiplexed_parallel_downsampling_seal(const TensorCipher &cnn_in, TensorCi
     const Mux in{ n, ki, hi, wi, ti, 1 };
     const Ciphertext ct = cnn_in.cipher();
     Ciphertext sum, temp;
+    // the ki*ti select products, then their (independent) rotations in batched launches, then the
+    // sum in the reference's order
+    std::vector<Ciphertext> prod((size_t)ki * ti), rotd((size_t)ki * ti);
+    std::vector<const Ciphertext *> pin;
+    std::vector<Ciphertext *> pout;
+    std::vector<int> psteps;
     for (int w1 = 0; w1 < ki; w1++)
         for (int w2 = 0; w2 < ti; w2++)
         {
@@ -449,24 +516,36 @@ void multiplexed_parallel_downsampling_seal(const TensorCipher &cnn_in, TensorCi
             };
             Recipe id;
             id.add((std::uint64_t)0x646f776eu).ints({ n, ki, hi, wi, ti, w1, w2 });
-            temp = ct;
-            multiply_static_vector(evaluator, temp, id, make_sel);
+            Ciphertext &pr = prod[(size_t)w1 * ti + w2];
+            pr = ct;
+            multiply_static_vector(evaluator, pr, id, make_sel);
             const int w3 = ((ki * w2 + w1) % (2 * ko)) / 2, w4 = (ki * w2 + w1) % 2, w5 = (ki * w2 + w1) / (2 * ko);
-            memory_save_rotate(temp, temp,
-                               ki * ki * hi * wi * w2 + ki * wi * w1 - ko * ko * ho * wo * w5 - ko * wo * w3 - ki * w4 -
-                                   ko * ko * ho * wo * (ti / 8),
-                               evaluator, gal_keys);
-            if (w1 == 0 && w2 == 0)
-                sum = temp;
-            else
-                evaluator.add_inplace_reduced_error(sum, temp);
+            pin.push_back(&pr);
+            pout.push_back(&rotd[(size_t)w1 * ti + w2]);
+            psteps.push_back(ki * ki * hi * wi * w2 + ki * wi * w1 - ko * ko * ho * wo * w5 - ko * wo * w3 - ki * w4 -
+                             ko * ko * ho * wo * (ti / 8));
         }
+    rotate_copies(pin, psteps, pout, evaluator, gal_keys);
+    for (std::size_t k = 0; k < rotd.size(); k++)
+    {
+        if (k == 0)
+            sum = rotd[k];
+        else
+            evaluator.add_inplace_reduced_error(sum, rotd[k]);
+    }
     evaluator.rescale_to_next_inplace(sum);
     const Ciphertext packed = sum;
-    for (int u6 = 1; u6 < po; u6++)
     {
-        rotate_copy(packed, temp, static_cast<int>(-(n / po) * u6), evaluator, gal_keys);
-        evaluator.add_inplace_reduced_error(sum, temp);
+        std::vector<Ciphertext> reps(po > 1 ? po - 1 : 0);
+        std::vector<Ciphertext *> rp;
+        std::vector<int> rsteps;
+        for (int u6 = 1; u6 < po; u6++)
+        {
+            rp.push_back(&reps[u6 - 1]);
+            rsteps.push_back(static_cast<int>(-(n / po) * u6));
+        }
+        rotate_copies(packed, rsteps, rp, evaluator, gal_keys);
+        for (auto &r : reps) evaluator.add_inplace_reduced_error(sum, r);
     }
     cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, sum);
 }
@@ -492,11 +571,22 @@ void averagepooling_seal_scale(const TensorCipher &cnn_in, TensorCipher &cnn_out
         rotate_copy(ct, temp, static_cast<int>(pow2(x) * ki * ki * wi), evaluator, gal_keys);
         evaluator.add_inplace_reduced_error(ct, temp);
     }
+    std::vector<Ciphertext> gath((size_t)ki * ti);
+    {
+        std::vector<Ciphertext *> gp;
+        std::vector<int> gs;
+        for (int s = 0; s < ki; s++)
+            for (int u = 0; u < ti; u++)
+            {
+                gp.push_back(&gath[(size_t)s * ti + u]);
+                gs.push_back(-(ki * u + s) * ki + ki * ki * hi * wi * u + ki * wi * s);
+            }
+        rotate_copies(ct, gs, gp, evaluator, gal_keys);
+    }
     for (int s = 0; s < ki; s++)
         for (int u = 0; u < ti; u++)
         {
-            const int p = ki * u + s;
-            rotate_copy(ct, temp, -p * ki + ki * ki * hi * wi * u + ki * wi * s, evaluator, gal_keys);
+            Ciphertext &temp = gath[(size_t)s * ti + u];
             Recipe id;
             id.add((std::uint64_t)0x61766770u).add(B).ints({ n, ki, hi, wi, u, s });
             multiply_static_vector(evaluator, temp, id, [&] {
@@ -525,10 +615,21 @@ void matrix_multiplication_seal(const TensorCipher &cnn_in, TensorCipher &cnn_ou
     Recipe fc_id;
     fc_id.add((std::uint64_t)0x66636d6du).add(matrix).ints({ n, q, r });
     const Ciphertext ct = cnn_in.cipher();
-    Ciphertext temp, sum;
+    Ciphertext sum;
+    std::vector<Ciphertext> rots((size_t)(q + r - 1));
+    {
+        std::vector<Ciphertext *> rp;
+        std::vector<int> rs;
+        for (int s = 0; s < q + r - 1; s++)
+        {
+            rp.push_back(&rots[s]);
+            rs.push_back(r - 1 - s);
+        }
+        rotate_copies(ct, rs, rp, evaluator, gal_keys);
+    }
     for (int s = 0; s < q + r - 1; s++)
     {
-        rotate_copy(ct, temp, r - 1 - s, evaluator, gal_keys);
+        Ciphertext &temp = rots[s];
         Recipe id = fc_id;
         id.ints({ s });
         multiply_static_vector(evaluator, temp, id, [&] {

@@ -170,6 +170,100 @@ ResNetParams load_resnet_params_bin(const std::string &path, std::size_t layer_n
     return p;
 }
 
+// ------------------------------------------------------------------------------ plain network
+namespace
+{
+std::vector<double> plain_conv(const std::vector<double> &in, const std::vector<double> &wt, int h, int ci, int co,
+                               int st)
+{
+    // 3 x 3, zero padding 1, stride st; weights [co][ci][3][3] (the reference's import layout)
+    const int ho = h / st;
+    std::vector<double> out((std::size_t)co * ho * ho, 0.0);
+    for (int b = 0; b < co; b++)
+        for (int y = 0; y < ho; y++)
+            for (int x = 0; x < ho; x++)
+            {
+                double s = 0;
+                for (int a = 0; a < ci; a++)
+                    for (int i1 = 0; i1 < 3; i1++)
+                        for (int i2 = 0; i2 < 3; i2++)
+                        {
+                            const int yy = st * y + i1 - 1, xx = st * x + i2 - 1;
+                            if (yy < 0 || yy >= h || xx < 0 || xx >= h) continue;
+                            s += wt[((std::size_t)(b * ci + a) * 3 + i1) * 3 + i2] * in[(std::size_t)a * h * h + yy * h + xx];
+                        }
+                out[(std::size_t)b * ho * ho + y * ho + x] = s;
+            }
+    return out;
+}
+
+void plain_bn(std::vector<double> &v, const ResNetParams &p, int s, int c, int hw)
+{
+    for (int b = 0; b < c; b++)
+    {
+        const double g = p.bn_weight[s][b] / std::sqrt(p.bn_running_var[s][b] + 1e-5);
+        for (int i = 0; i < hw; i++)
+            v[(std::size_t)b * hw + i] = (v[(std::size_t)b * hw + i] - p.bn_running_mean[s][b]) * g + p.bn_bias[s][b];
+    }
+}
+
+void plain_relu(std::vector<double> &v)
+{
+    for (auto &x : v) x = x > 0 ? x : 0.0;
+}
+} // namespace
+
+std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector<double> &img, std::size_t layer_num)
+{
+    // the block structure of infer_seal.cpp:445-540 (conv, BN, ReLU; option-A shortcut with a
+    // stride-2 subsample for the first block of stages 2 and 3), then average pooling and FC
+    const int end_num = (int)end_num_of(layer_num);
+    std::vector<double> x = plain_conv(img, p.conv_weight[0], 32, 3, 16, 1);
+    int h = 32, c = 16;
+    plain_bn(x, p, 0, c, h * h);
+    plain_relu(x);
+    for (int j = 0; j < 3; j++)
+        for (int k = 0; k <= end_num; k++)
+        {
+            const int s1 = 2 * ((end_num + 1) * j + k) + 1, s2 = s1 + 1;
+            const int co = j == 0 ? 16 : j == 1 ? 32 : 64, st = (j >= 1 && k == 0) ? 2 : 1;
+            std::vector<double> temp = x;
+            std::vector<double> y = plain_conv(x, p.conv_weight[s1], h, c, co, st);
+            const int ho = h / st;
+            plain_bn(y, p, s1, co, ho * ho);
+            plain_relu(y);
+            y = plain_conv(y, p.conv_weight[s2], ho, co, co, 1);
+            plain_bn(y, p, s2, co, ho * ho);
+            if (st == 2)
+            {
+                // input channel a -> output channel a + c/2, even pixels
+                std::vector<double> ds((std::size_t)co * ho * ho, 0.0);
+                for (int a = 0; a < c; a++)
+                    for (int yy = 0; yy < ho; yy++)
+                        for (int xx = 0; xx < ho; xx++)
+                            ds[(std::size_t)(a + c / 2) * ho * ho + yy * ho + xx] = temp[(std::size_t)a * h * h + 2 * yy * h + 2 * xx];
+                temp = ds;
+            }
+            for (std::size_t i = 0; i < y.size(); i++) y[i] += temp[i];
+            plain_relu(y);
+            x = y;
+            h = ho;
+            c = co;
+        }
+    std::vector<double> f(64, 0.0), logits(10, 0.0);
+    for (int b = 0; b < 64; b++)
+    {
+        for (int i = 0; i < h * h; i++) f[b] += x[(std::size_t)b * h * h + i];
+        f[b] /= h * h;
+    }
+    for (int i = 0; i < 10; i++)
+    {
+        logits[i] = p.linear_bias[i];
+        for (int b = 0; b < 64; b++) logits[i] += p.linear_weight[(std::size_t)i * 64 + b] * f[b];
+    }
+    return logits;
+}
+
 // ------------------------------------------------------------------------------------ runner
 struct ResNetRunner::Impl
 {
@@ -417,6 +511,11 @@ double ResNetRunner::key_traffic_bytes(bool reset)
     const int rc = mhe_key_traffic(eng, &b, reset ? 1 : 0) | mhe_key_traffic_prepared(eng, &other, reset ? 1 : 0);
     if (rc != 0) throw std::runtime_error(mhe_last_error());
     return (double)b;
+}
+
+std::vector<double> ResNetRunner::plain_logits(const std::vector<double> &image) const
+{
+    return resnet_plain_logits(impl_->prm, image, impl_->layer_num);
 }
 
 ResNetResult ResNetRunner::infer(const std::vector<double> &img)

@@ -141,6 +141,23 @@ int mhe_resnet_key_traffic(mhe_resnet *r, double *bytes, int reset)
     });
 }
 
+int mhe_resnet_key_format(mhe_resnet *r, int *prepared)
+{
+    return guard([&] {
+        if (!prepared) throw std::invalid_argument("null argument");
+        *prepared = r->runner->keys_prepared() ? 1 : 0;
+    });
+}
+
+int mhe_resnet_plain_logits(mhe_resnet *r, const double *image, double *logits)
+{
+    return guard([&] {
+        if (!image || !logits) throw std::invalid_argument("null argument");
+        const std::vector<double> out = r->runner->plain_logits(std::vector<double>(image, image + 3072));
+        for (int k = 0; k < 10; k++) logits[k] = out[k];
+    });
+}
+
 int mhe_resnet_info(mhe_resnet *r, double *setup_s, double *gb, int *nkeys)
 {
     return guard([&] {

@@ -13,6 +13,7 @@
 
 #include "../../include/mhe.h"
 #include "random_internal.h"
+#include "trace.h"
 
 #include <algorithm>
 #include <cmath>
@@ -25,6 +26,44 @@
 
 namespace seal
 {
+namespace
+{
+// One traced operation (trace.h): the input ids are taken at entry, the output id at a normal exit;
+// nested operations (depth > 0) and operations that throw leave no record.
+template <class F>
+class TraceOp
+{
+public:
+    TraceOp(const char *op, F out) : op_(op), out_(out), unc_(std::uncaught_exceptions()) {}
+    bool top() const { return sc_.top(); }
+    void in(std::initializer_list<std::string> v) { in_.assign(v.begin(), v.end()); }
+    std::string extra;
+    ~TraceOp()
+    {
+        if (!sc_.top() || std::uncaught_exceptions() != unc_) return;
+        try
+        {
+            trace::record(op_, in_, out_(), extra);
+        }
+        catch (...)
+        {
+        }
+    }
+
+private:
+    trace::Scope sc_;
+    const char *op_;
+    F out_;
+    std::vector<std::string> in_;
+    int unc_;
+};
+} // namespace
+#define TRACE_OP(NAME, OUT, ...)                                                   \
+    TraceOp trace_op_(NAME, [&]() -> std::string { return OUT; });             \
+    if (trace_op_.top()) trace_op_.in({ __VA_ARGS__ })
+#define TRACE_EXTRA(S) \
+    if (trace_op_.top()) trace_op_.extra = (S)
+
 const parms_id_type parms_id_zero = { 0, 0, 0, 0 };
 
 namespace
@@ -1028,6 +1067,8 @@ void CKKSEncoder::encode_internal(const double *re, const double *im, std::size_
 void CKKSEncoder::encode(const std::vector<double> &values, parms_id_type parms_id, double scale,
                          Plaintext &destination, MemoryPoolHandle)
 {
+    TRACE_OP("encode", trace::pt(destination), trace::vec(values.data(), nullptr, values.size()));
+    TRACE_EXTRA("\"scale\": " + trace::num(scale));
     encode_internal(values.data(), nullptr, values.size(), parms_id, scale, destination);
 }
 
@@ -1040,6 +1081,8 @@ void CKKSEncoder::encode(const std::vector<std::complex<double>> &values, parms_
         re[i] = values[i].real();
         im[i] = values[i].imag();
     }
+    TRACE_OP("encode", trace::pt(destination), trace::vec(re.data(), im.data(), re.size()));
+    TRACE_EXTRA("\"scale\": " + trace::num(scale));
     encode_internal(re.data(), im.data(), values.size(), parms_id, scale, destination);
 }
 
@@ -1056,6 +1099,9 @@ void CKKSEncoder::encode(const std::vector<std::complex<double>> &values, double
 
 void CKKSEncoder::encode(double value, parms_id_type parms_id, double scale, Plaintext &destination, MemoryPoolHandle)
 {
+    TRACE_OP("encode_const", trace::pt(destination));
+    TRACE_EXTRA("\"value\": " + trace::num(value) + ", \"scale\": " + trace::num(scale) + ", \"limbs\": " +
+                std::to_string(ctx_.get_context_data(parms_id) ? ctx_.get_context_data(parms_id)->parms().coeff_modulus().size() : 0));
     auto cd = ctx_.get_context_data(parms_id);
     if (!cd) throw std::invalid_argument("parms_id is not valid for encryption parameters");
     const std::size_t L = cd->parms().coeff_modulus().size();
@@ -1172,6 +1218,7 @@ void Encryptor::encrypt_zero(Ciphertext &destination, MemoryPoolHandle pool) con
 
 void Encryptor::encrypt(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle) const
 {
+    TRACE_OP("encrypt", trace::ct(destination), trace::pt(plain));
     // encrypt_internal (encryptor.cpp:168-239), CKKS branch
     if (!plain.is_ntt_form()) throw std::invalid_argument("plain must be in NTT form");
     auto cd = ctx_.get_context_data(plain.parms_id());
@@ -1348,6 +1395,7 @@ void fresh_dest(const SEALContext &ctx, const Ciphertext &src, Ciphertext &dst, 
 
 void Evaluator::negate_inplace(Ciphertext &encrypted) const
 {
+    TRACE_OP("negate", trace::ct(encrypted), trace::ct(encrypted));
     // evaluator.cpp:78-101
     Level lv = check_ct(context_, encrypted, "encrypted");
     void *s = context_.stream();
@@ -1357,6 +1405,7 @@ void Evaluator::negate_inplace(Ciphertext &encrypted) const
 
 void Evaluator::negate(const Ciphertext &encrypted, Ciphertext &destination) const
 {
+    TRACE_OP("negate", trace::ct(destination), trace::ct(encrypted));
     if (&encrypted == &destination) return negate_inplace(destination);
     Level lv = check_ct(context_, encrypted, "encrypted");
     void *s = context_.stream();
@@ -1379,6 +1428,7 @@ void check_pair(const SEALContext &ctx, const Ciphertext &a, const Ciphertext &b
 
 void Evaluator::add_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
 {
+    TRACE_OP("add", trace::ct(encrypted1), trace::ct(encrypted1), trace::ct(encrypted2));
     // evaluator.cpp:103-164
     check_pair(context_, encrypted1, encrypted2, true);
     const std::size_t L = encrypted1.coeff_modulus_size(), n = encrypted1.poly_modulus_degree();
@@ -1393,6 +1443,7 @@ void Evaluator::add_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2
 
 void Evaluator::add(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
 {
+    TRACE_OP("add", trace::ct(destination), trace::ct(encrypted1), trace::ct(encrypted2));
     if (&encrypted2 == &destination)
         add_inplace(destination, encrypted1);
     else if (&encrypted1 != &destination && encrypted1.size() == encrypted2.size())
@@ -1426,6 +1477,7 @@ void Evaluator::add_many(const std::vector<Ciphertext> &encrypteds, Ciphertext &
 
 void Evaluator::sub_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
 {
+    TRACE_OP("sub", trace::ct(encrypted1), trace::ct(encrypted1), trace::ct(encrypted2));
     // evaluator.cpp:187-246
     check_pair(context_, encrypted1, encrypted2, true);
     const std::size_t L = encrypted1.coeff_modulus_size(), n = encrypted1.poly_modulus_degree();
@@ -1441,6 +1493,7 @@ void Evaluator::sub_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2
 
 void Evaluator::sub(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
 {
+    TRACE_OP("sub", trace::ct(destination), trace::ct(encrypted1), trace::ct(encrypted2));
     if (&encrypted2 == &destination)
     {
         sub_inplace(destination, encrypted1);
@@ -1455,6 +1508,7 @@ void Evaluator::sub(const Ciphertext &encrypted1, const Ciphertext &encrypted2, 
 
 void Evaluator::multiply_inplace(Ciphertext &encrypted1, const Ciphertext &encrypted2, MemoryPoolHandle) const
 {
+    TRACE_OP("multiply", trace::ct(encrypted1), trace::ct(encrypted1), trace::ct(encrypted2));
     // evaluator.cpp:248-285, ckks_multiply :673-773 (size 2 x size 2 -> 3)
     check_ct(context_, encrypted1, "encrypted1");
     check_ct(context_, encrypted2, "encrypted2");
@@ -1481,6 +1535,7 @@ void Evaluator::multiply_inplace(Ciphertext &encrypted1, const Ciphertext &encry
 void Evaluator::multiply(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
                          MemoryPoolHandle) const
 {
+    TRACE_OP("multiply", trace::ct(destination), trace::ct(encrypted1), trace::ct(encrypted2));
     if (&encrypted1 != &destination && &encrypted2 != &destination && encrypted1.size() == 2 &&
         encrypted2.size() == 2)
     {
@@ -1535,6 +1590,7 @@ void Evaluator::exponentiate_inplace(Ciphertext &encrypted, std::uint64_t expone
 
 void Evaluator::square_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
 {
+    TRACE_OP("square", trace::ct(encrypted), trace::ct(encrypted));
     // evaluator.cpp:816-845, ckks_square :1000-1059
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
@@ -1553,6 +1609,7 @@ void Evaluator::square_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
 
 void Evaluator::square(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle) const
 {
+    TRACE_OP("square", trace::ct(destination), trace::ct(encrypted));
     if (&encrypted == &destination) return square_inplace(destination);
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
@@ -1580,6 +1637,7 @@ void Evaluator::switch_key(Ciphertext &encrypted, const std::uint64_t *target, c
 
 void Evaluator::relinearize_inplace(Ciphertext &encrypted, const RelinKeys &relin_keys, MemoryPoolHandle) const
 {
+    TRACE_OP("relinearize", trace::ct(encrypted), trace::ct(encrypted));
     // relinearize_internal (evaluator.cpp:1061-1116)
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (relin_keys.parms_id() != context_.key_parms_id())
@@ -1608,12 +1666,14 @@ void Evaluator::relinearize_inplace(Ciphertext &encrypted, const RelinKeys &reli
 void Evaluator::relinearize(const Ciphertext &encrypted, const RelinKeys &relin_keys, Ciphertext &destination,
                             MemoryPoolHandle) const
 {
+    TRACE_OP("relinearize", trace::ct(destination), trace::ct(encrypted));
     destination = encrypted;
     relinearize_inplace(destination, relin_keys);
 }
 
 void Evaluator::mod_switch_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
 {
+    TRACE_OP("mod_switch", trace::ct(encrypted), trace::ct(encrypted));
     // mod_switch_drop_to_next (evaluator.cpp:1183-1246) -- CKKS mod_switch_to_next
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (!encrypted.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
@@ -1634,12 +1694,14 @@ void Evaluator::mod_switch_to_next_inplace(Ciphertext &encrypted, MemoryPoolHand
 
 void Evaluator::mod_switch_to_next(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle) const
 {
+    TRACE_OP("mod_switch", trace::ct(destination), trace::ct(encrypted));
     destination = encrypted;
     mod_switch_to_next_inplace(destination);
 }
 
 void Evaluator::mod_switch_to_next_inplace(Plaintext &plain) const
 {
+    TRACE_OP("pt_mod_switch", trace::pt(plain), trace::pt(plain));
     // mod_switch_drop_to_next(Plaintext) (evaluator.cpp:1248-1281)
     if (!plain.is_ntt_form()) throw std::invalid_argument("plain is not in NTT form");
     Level lv = level_of(context_, plain.parms_id(), "plain");
@@ -1652,6 +1714,7 @@ void Evaluator::mod_switch_to_next_inplace(Plaintext &plain) const
 
 void Evaluator::mod_switch_to_inplace(Ciphertext &encrypted, parms_id_type parms_id, MemoryPoolHandle) const
 {
+    TRACE_OP("mod_switch", trace::ct(encrypted), trace::ct(encrypted));
     // evaluator.cpp:1326-1348
     Level cur = check_ct(context_, encrypted, "encrypted");
     auto target = context_.get_context_data(parms_id);
@@ -1679,12 +1742,14 @@ void Evaluator::mod_switch_to_inplace(Ciphertext &encrypted, parms_id_type parms
 void Evaluator::mod_switch_to(const Ciphertext &encrypted, parms_id_type parms_id, Ciphertext &destination,
                               MemoryPoolHandle) const
 {
+    TRACE_OP("mod_switch", trace::ct(destination), trace::ct(encrypted));
     destination = encrypted;
     mod_switch_to_inplace(destination, parms_id);
 }
 
 void Evaluator::mod_switch_to_inplace(Plaintext &plain, parms_id_type parms_id) const
 {
+    TRACE_OP("pt_mod_switch", trace::pt(plain), trace::pt(plain));
     // evaluator.cpp:1350-1376
     auto cur = context_.get_context_data(plain.parms_id());
     auto target = context_.get_context_data(parms_id);
@@ -1702,6 +1767,7 @@ void Evaluator::mod_switch_to_inplace(Plaintext &plain, parms_id_type parms_id) 
 
 void Evaluator::rescale_to_next(const Ciphertext &encrypted, Ciphertext &destination, MemoryPoolHandle) const
 {
+    TRACE_OP("rescale", trace::ct(destination), trace::ct(encrypted));
     // evaluator.cpp:1378-1414, mod_switch_scale_to_next :1118-1181
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (context_.last_parms_id() == encrypted.parms_id())
@@ -1733,6 +1799,7 @@ void Evaluator::rescale_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle)
 
 void Evaluator::rescale_to_inplace(Ciphertext &encrypted, parms_id_type parms_id, MemoryPoolHandle) const
 {
+    TRACE_OP("rescale", trace::ct(encrypted), trace::ct(encrypted));
     // evaluator.cpp:1416-1466
     Level cur = check_ct(context_, encrypted, "encrypted");
     auto target = context_.get_context_data(parms_id);
@@ -1750,6 +1817,7 @@ void Evaluator::multiply_plain_inplace(Ciphertext &encrypted, const Plaintext &p
 void Evaluator::multiply_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination,
                                MemoryPoolHandle) const
 {
+    TRACE_OP("multiply_plain", trace::ct(destination), trace::ct(encrypted), trace::pt(plain));
     // evaluator.cpp:1726-1761, multiply_plain_ntt :1891-1930 (out of place: no copy of encrypted)
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (plain.is_ntt_form()) level_of(context_, plain.parms_id(), "plain");
@@ -1798,28 +1866,33 @@ void add_sub_plain(const SEALContext &ctx, Ciphertext &encrypted, const Plaintex
 
 void Evaluator::add_plain_inplace(Ciphertext &encrypted, const Plaintext &plain) const
 {
+    TRACE_OP("add_plain", trace::ct(encrypted), trace::ct(encrypted), trace::pt(plain));
     add_sub_plain(context_, encrypted, plain, false);
 }
 
 void Evaluator::add_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination) const
 {
+    TRACE_OP("add_plain", trace::ct(destination), trace::ct(encrypted), trace::pt(plain));
     destination = encrypted;
     add_plain_inplace(destination, plain);
 }
 
 void Evaluator::sub_plain_inplace(Ciphertext &encrypted, const Plaintext &plain) const
 {
+    TRACE_OP("sub_plain", trace::ct(encrypted), trace::ct(encrypted), trace::pt(plain));
     add_sub_plain(context_, encrypted, plain, true);
 }
 
 void Evaluator::sub_plain(const Ciphertext &encrypted, const Plaintext &plain, Ciphertext &destination) const
 {
+    TRACE_OP("sub_plain", trace::ct(destination), trace::ct(encrypted), trace::pt(plain));
     destination = encrypted;
     sub_plain_inplace(destination, plain);
 }
 
 void Evaluator::transform_to_ntt_inplace(Ciphertext &encrypted) const
 {
+    TRACE_OP("ntt_fwd", trace::ct(encrypted), trace::ct(encrypted));
     // evaluator.cpp:2025-2071
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (encrypted.is_ntt_form()) throw std::invalid_argument("encrypted is already in NTT form");
@@ -1830,6 +1903,7 @@ void Evaluator::transform_to_ntt_inplace(Ciphertext &encrypted) const
 
 void Evaluator::transform_from_ntt_inplace(Ciphertext &encrypted) const
 {
+    TRACE_OP("ntt_inv", trace::ct(encrypted), trace::ct(encrypted));
     // evaluator.cpp:2073-2118
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (!encrypted.is_ntt_form()) throw std::invalid_argument("encrypted is not in NTT form");
@@ -1841,6 +1915,8 @@ void Evaluator::transform_from_ntt_inplace(Ciphertext &encrypted) const
 void Evaluator::apply_galois_inplace(Ciphertext &encrypted, std::uint32_t galois_elt, const GaloisKeys &galois_keys,
                                      MemoryPoolHandle) const
 {
+    TRACE_OP("galois", trace::ct(encrypted), trace::ct(encrypted));
+    TRACE_EXTRA("\"elt\": " + std::to_string(galois_elt));
     // evaluator.cpp:2120-2222
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (galois_keys.parms_id() != context_.key_parms_id())
@@ -1890,12 +1966,16 @@ void Evaluator::rotate_internal(Ciphertext &encrypted, int steps, const GaloisKe
 void Evaluator::rotate_vector_inplace(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                                       MemoryPoolHandle) const
 {
+    TRACE_OP("rotate", trace::ct(encrypted), trace::ct(encrypted));
+    TRACE_EXTRA("\"step\": " + std::to_string(steps));
     rotate_internal(encrypted, steps, galois_keys);
 }
 
 void Evaluator::apply_galois_to(const Ciphertext &encrypted, std::uint32_t galois_elt, const GaloisKeys &galois_keys,
                                 Ciphertext &destination) const
 {
+    TRACE_OP("galois", trace::ct(destination), trace::ct(encrypted));
+    TRACE_EXTRA("\"elt\": " + std::to_string(galois_elt));
     // apply_galois_inplace (evaluator.cpp:2120-2222) reading encrypted and writing destination
     Level lv = check_ct(context_, encrypted, "encrypted");
     if (galois_keys.parms_id() != context_.key_parms_id())
@@ -1915,6 +1995,8 @@ void Evaluator::apply_galois_to(const Ciphertext &encrypted, std::uint32_t galoi
 void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                               Ciphertext &destination, MemoryPoolHandle) const
 {
+    TRACE_OP("rotate", trace::ct(destination), trace::ct(encrypted));
+    TRACE_EXTRA("\"step\": " + std::to_string(steps));
     if (&encrypted != &destination && steps != 0)
     {
         Level lv = level_of(context_, encrypted.parms_id(), "encrypted");
@@ -1928,8 +2010,141 @@ void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const Galo
     rotate_vector_inplace(destination, steps, galois_keys);
 }
 
+void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted, const std::vector<int> &steps,
+                               const GaloisKeys &galois_keys, const std::vector<Ciphertext *> &destinations) const
+{
+    if (encrypted.size() != steps.size() || encrypted.size() != destinations.size())
+        throw std::invalid_argument("encrypted, steps and destinations must have the same size");
+    for (std::size_t i = 0; i < destinations.size(); i++)
+    {
+        if (!encrypted[i] || !destinations[i]) throw std::invalid_argument("null ciphertext");
+        for (std::size_t j = 0; j < destinations.size(); j++)
+            if ((j != i && destinations[i] == destinations[j]) || destinations[i] == encrypted[j])
+                throw std::invalid_argument("destinations must be distinct and must not be inputs");
+    }
+    if (galois_keys.parms_id() != context_.key_parms_id())
+        throw std::invalid_argument("galois_keys is not valid for encryption parameters");
+    // traced as one "rotate" record per entry (the fallbacks below are nested)
+    trace::Scope tsc;
+    std::vector<std::string> tin;
+    if (tsc.top())
+        for (const Ciphertext *c : encrypted) tin.push_back(trace::ct(*c));
+    // entries that run batched, grouped by level (chain index)
+    std::map<std::size_t, std::vector<std::size_t>> groups;
+    std::vector<std::uint32_t> elt(encrypted.size(), 0);
+    for (std::size_t i = 0; i < encrypted.size(); i++)
+    {
+        Level lv = level_of(context_, encrypted[i]->parms_id(), "encrypted");
+        if (steps[i] == 0) continue;
+        const std::uint32_t e = mhe_galois_elt_from_step(__builtin_ctzll(lv.n), steps[i]);
+        if (!e) throw std::invalid_argument("step count too large");
+        if (!galois_keys.has_key(e)) continue;
+        elt[i] = e;
+        groups[lv.L].push_back(i);
+    }
+    void *s = context_.stream();
+    std::vector<bool> done(encrypted.size(), false);
+    for (auto &g : groups)
+    {
+        const std::vector<std::size_t> &idx = g.second;
+        if (idx.size() < 2) continue;
+        const std::size_t L = g.first;
+        std::vector<const std::uint64_t *> in, keys;
+        std::vector<std::uint64_t *> out;
+        std::vector<std::uint32_t> elts;
+        std::vector<int> kls;
+        for (std::size_t i : idx)
+        {
+            const Ciphertext &c = *encrypted[i];
+            check_ct(context_, c, "encrypted");
+            if (c.size() > 2) throw std::invalid_argument("encrypted size must be 2");
+            if (!c.is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+            std::size_t kl = 0;
+            keys.push_back(galois_keys.key_for(GaloisKeys::get_index(elt[i]), L, s, kl));
+            kls.push_back((int)kl);
+            elts.push_back(elt[i]);
+        }
+        // inputs are read, then destinations re-sized and written (no destination is an input)
+        for (std::size_t i : idx) in.push_back(encrypted[i]->store().dev_read(s));
+        for (std::size_t i : idx)
+        {
+            fresh_dest(context_, *encrypted[i], *destinations[i], 2);
+            out.push_back(destinations[i]->store().dev_write(s, true));
+        }
+        chk(mhe_apply_galois_batch(context_.engine(), (int)idx.size(), in.data(), out.data(), elts.data(), keys.data(),
+                                   kls.data(), (int)L, s));
+        for (std::size_t i : idx) done[i] = true;
+    }
+    for (std::size_t i = 0; i < encrypted.size(); i++)
+        if (!done[i]) rotate_vector(*encrypted[i], steps[i], galois_keys, *destinations[i]);
+    if (tsc.top())
+        for (std::size_t i = 0; i < encrypted.size(); i++)
+            trace::record("rotate", { tin[i] }, trace::ct(*destinations[i]), "\"step\": " + std::to_string(steps[i]));
+}
+
+void Evaluator::rescale_to_next_inplace_many(const std::vector<Ciphertext *> &encrypted) const
+{
+    // rescale_to_next of every entry; entries of one level and size run as one batched launch
+    trace::Scope tsc; // traced as one "rescale" record per entry
+    std::vector<std::string> tin;
+    if (tsc.top())
+        for (const Ciphertext *c : encrypted) tin.push_back(c ? trace::ct(*c) : std::string());
+    std::map<std::pair<std::size_t, std::size_t>, std::vector<Ciphertext *>> groups;
+    for (Ciphertext *c : encrypted)
+    {
+        if (!c) throw std::invalid_argument("null ciphertext");
+        Level lv = check_ct(context_, *c, "encrypted");
+        groups[{ lv.L, c->size() }].push_back(c);
+    }
+    void *s = context_.stream();
+    for (auto &g : groups)
+    {
+        std::vector<Ciphertext *> &v = g.second;
+        if (v.size() < 2)
+        {
+            for (Ciphertext *c : v) rescale_to_next_inplace(*c);
+            continue;
+        }
+        const std::size_t size = g.first.second;
+        std::vector<PolyStore> outs(v.size());
+        std::vector<const std::uint64_t *> in;
+        std::vector<std::uint64_t *> out;
+        std::vector<double> scales;
+        parms_id_type next_id{};
+        for (std::size_t i = 0; i < v.size(); i++)
+        {
+            Ciphertext &c = *v[i];
+            Level lv = check_ct(context_, c, "encrypted");
+            if (context_.last_parms_id() == c.parms_id()) throw std::invalid_argument("end of modulus switching chain reached");
+            if (!c.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
+            auto next = lv.cd->next_context_data();
+            const double new_scale = c.scale() / (double)lv.cd->parms().coeff_modulus().back().value();
+            check_scale(new_scale, level_of(context_, next->parms_id(), "parms_id"));
+            scales.push_back(new_scale);
+            next_id = next->parms_id();
+            outs[i].bind(context_);
+            outs[i].resize_words(size * (lv.L - 1) * lv.n, false);
+            in.push_back(c.store().dev_read(s));
+            out.push_back(outs[i].dev_write(s, true));
+        }
+        chk(mhe_rescale_batch(context_.engine(), (int)v.size(), in.data(), out.data(), (int)size, (int)g.first.first, s));
+        for (std::size_t i = 0; i < v.size(); i++)
+        {
+            const bool ntt = v[i]->is_ntt_form();
+            v[i]->store() = std::move(outs[i]);
+            v[i]->resize(context_, next_id, size);
+            v[i]->scale() = scales[i];
+            v[i]->is_ntt_form() = ntt;
+        }
+    }
+    if (tsc.top())
+        for (std::size_t i = 0; i < encrypted.size(); i++) trace::record("rescale", { tin[i] }, trace::ct(*encrypted[i]));
+}
+
 void Evaluator::complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKeys &galois_keys, MemoryPoolHandle) const
 {
+    TRACE_OP("galois", trace::ct(encrypted), trace::ct(encrypted));
+    TRACE_EXTRA("\"elt\": " + std::to_string(2 * encrypted.poly_modulus_degree() - 1));
     const std::size_t n = level_of(context_, encrypted.parms_id(), "encrypted").n;
     apply_galois_inplace(encrypted, (std::uint32_t)(2 * n - 1), galois_keys);
 }
@@ -1937,6 +2152,8 @@ void Evaluator::complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKey
 void Evaluator::complex_conjugate(const Ciphertext &encrypted, const GaloisKeys &galois_keys, Ciphertext &destination,
                                   MemoryPoolHandle) const
 {
+    TRACE_OP("galois", trace::ct(destination), trace::ct(encrypted));
+    TRACE_EXTRA("\"elt\": " + std::to_string(2 * encrypted.poly_modulus_degree() - 1));
     if (&encrypted == &destination) return complex_conjugate_inplace(destination, galois_keys);
     const std::size_t n = level_of(context_, encrypted.parms_id(), "encrypted").n;
     apply_galois_to(encrypted, (std::uint32_t)(2 * n - 1), galois_keys, destination);
@@ -1948,6 +2165,8 @@ void Evaluator::complex_conjugate(const Ciphertext &encrypted, const GaloisKeys 
 // first level) and applies them per limb without materialising the constant polynomial.
 void Evaluator::add_const_inplace(Ciphertext &encrypted, double value) const
 {
+    TRACE_OP("add_const", trace::ct(encrypted), trace::ct(encrypted));
+    TRACE_EXTRA("\"value\": " + trace::num(value));
     Level lv = check_ct(context_, encrypted, "encrypted");
     const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
     std::vector<std::uint64_t> r(lv.L);
@@ -1960,6 +2179,8 @@ void Evaluator::add_const_inplace(Ciphertext &encrypted, double value) const
 
 void Evaluator::add_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const
 {
+    TRACE_OP("add_const", trace::ct(destination), trace::ct(encrypted));
+    TRACE_EXTRA("\"value\": " + trace::num(value));
     if (&encrypted == &destination) return add_const_inplace(destination, value);
     Level lv = check_ct(context_, encrypted, "encrypted");
     const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
@@ -1978,6 +2199,8 @@ void Evaluator::add_const(const Ciphertext &encrypted, double value, Ciphertext 
 
 void Evaluator::multiply_const_inplace(Ciphertext &encrypted, double value) const
 {
+    TRACE_OP("multiply_const", trace::ct(encrypted), trace::ct(encrypted));
+    TRACE_EXTRA("\"value\": " + trace::num(value));
     Level lv = check_ct(context_, encrypted, "encrypted");
     const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
     std::vector<std::uint64_t> r(lv.L);
@@ -1993,6 +2216,8 @@ void Evaluator::multiply_const_inplace(Ciphertext &encrypted, double value) cons
 
 void Evaluator::multiply_const(const Ciphertext &encrypted, double value, Ciphertext &destination) const
 {
+    TRACE_OP("multiply_const", trace::ct(destination), trace::ct(encrypted));
+    TRACE_EXTRA("\"value\": " + trace::num(value));
     if (&encrypted == &destination) return multiply_const_inplace(destination, value);
     Level lv = check_ct(context_, encrypted, "encrypted");
     const std::size_t L1 = context_.first_context_data()->parms().coeff_modulus().size();
@@ -2011,6 +2236,7 @@ void Evaluator::multiply_const(const Ciphertext &encrypted, double value, Cipher
 void Evaluator::multiply_plain_add_reduced_error(Ciphertext &acc, const Ciphertext &encrypted,
                                                  const Plaintext &plain) const
 {
+    TRACE_OP("multiply_plain_add", trace::ct(acc), trace::ct(acc), trace::ct(encrypted), trace::pt(plain));
     // multiply_plain(encrypted, plain, tmp) + add_inplace_reduced_error(acc, tmp) at equal levels,
     // one kernel (bit-identical): acc takes the product's scale, as the reduced-error add assigns it
     Level lv = check_ct(context_, encrypted, "encrypted");
@@ -2074,6 +2300,8 @@ void Evaluator::encode_vector_for(const Ciphertext &encrypted, const std::vector
     if (value.size() > lv.n / 2) throw std::invalid_argument("values_size is too large");
     std::vector<double> re, im;
     split<T>(value, re, im);
+    TRACE_OP("encode_for", trace::pt(plain), trace::vec(re.data(), im.empty() ? nullptr : im.data(), re.size()));
+    TRACE_EXTRA("\"scale\": " + trace::num(encrypted.scale()) + ", \"limbs\": " + std::to_string(lv.L));
     void *s = context_.stream();
     plain.set_level(context_, encrypted.parms_id(), lv.L);
     plain.scale() = encrypted.scale();
@@ -2153,6 +2381,8 @@ void Evaluator::reduced_error_op(Ciphertext &encrypted1, const Ciphertext &encry
 void Evaluator::reduced_error_out(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
                                   Rmode mode, const RelinKeys *relin_keys) const
 {
+    TRACE_OP(mode == Rmode::add ? "add_re" : mode == Rmode::sub ? "sub_re" : "mul_re", trace::ct(destination),
+             trace::ct(encrypted1), trace::ct(encrypted2));
     // equal levels: encrypted1 takes encrypted2's scale, then the op (reduced_error_op); written
     // out of place so encrypted1 is not copied first
     const bool same = encrypted1.coeff_modulus_size() == encrypted2.coeff_modulus_size() &&
@@ -2190,17 +2420,20 @@ void Evaluator::reduced_error_out(const Ciphertext &encrypted1, const Ciphertext
 
 void Evaluator::add_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
 {
+    TRACE_OP("add_re", trace::ct(encrypted1), trace::ct(encrypted1), trace::ct(encrypted2));
     reduced_error_op(encrypted1, encrypted2, Rmode::add);
 }
 
 void Evaluator::sub_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2) const
 {
+    TRACE_OP("sub_re", trace::ct(encrypted1), trace::ct(encrypted1), trace::ct(encrypted2));
     reduced_error_op(encrypted1, encrypted2, Rmode::sub);
 }
 
 void Evaluator::multiply_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2,
                                                const RelinKeys &relin_keys) const
 {
+    TRACE_OP("mul_re", trace::ct(encrypted1), trace::ct(encrypted1), trace::ct(encrypted2));
     reduced_error_op(encrypted1, encrypted2, Rmode::mul);
     relinearize_inplace(encrypted1, relin_keys);
 }

@@ -160,6 +160,24 @@ int mhe_apply_galois(mhe_ctx *ctx, uint64_t *ct, uint32_t galois_elt, const uint
 /* The same with the input left untouched: out[2][L][n] = KS-rotated in (out must not alias in). */
 int mhe_apply_galois_to(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, uint32_t galois_elt, const uint64_t *key,
                         int key_limbs, int limbs, void *stream);
+/* Batched launches: `count` independent operations of one level run as one launch per kernel
+ * (up to 8 entries per launch; larger counts run in groups of 8), bit-identical to `count` calls
+ * of the single-ciphertext entry point.  This is how independent rotations of the reference's
+ * callers run on the GPU: the conv input rotations and output-channel gathers
+ * (cnn/cnn_seal.cpp:423-430, 499-526), the BSGS baby and giant steps
+ * (ckks_bootstrapping/Bootstrapper.cpp:1952-2087), and the same operation of several images
+ * (cnn/infer_seal.cpp:404).  Pointer arrays are host arrays of device pointers. */
+/* mhe_apply_galois_to for each i: out[i][2][L][n] = rotated in[i] with Galois element elts[i]
+ * and key keys[i] (key_limbs[i]); outputs disjoint from every input and from each other. */
+int mhe_apply_galois_batch(mhe_ctx *ctx, int count, const uint64_t *const *in, uint64_t *const *out,
+                           const uint32_t *elts, const uint64_t *const *keys, const int *key_limbs, int limbs,
+                           void *stream);
+/* mhe_rescale_to_next for each i: in[i][size][L][n] -> out[i][size][L-1][n]. */
+int mhe_rescale_batch(mhe_ctx *ctx, int count, const uint64_t *const *in, uint64_t *const *out, int size, int limbs,
+                      void *stream);
+/* mhe_switch_key for each i: ct[i][2][L][n] += KS(target[i][L][n]) with keys[i]. */
+int mhe_switch_key_batch(mhe_ctx *ctx, int count, uint64_t *const *ct, const uint64_t *const *target,
+                         const uint64_t *const *keys, const int *key_limbs, int limbs, void *stream);
 /* GaloisTool::apply_galois_ntt alone on [polys][limbs][n] (out must not alias in). */
 int mhe_permute_galois(mhe_ctx *ctx, const uint64_t *in, uint32_t galois_elt, uint64_t *out, int polys, int limbs,
                        void *stream);

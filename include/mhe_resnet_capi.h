@@ -43,6 +43,12 @@ int mhe_resnet_infer_batch(mhe_resnet *runner, const double *images, int count, 
 int mhe_resnet_info(mhe_resnet *runner, double *setup_s, double *galois_key_gb, int *galois_keys);
 /* key-switching key bytes the runner's key switches streamed since the last reset (reset != 0 zeroes) */
 int mhe_resnet_key_traffic(mhe_resnet *runner, double *bytes, int reset);
+/* *prepared = 1 when the runner's evaluation keys are in the engine's prepared format
+ * (mhe_key_prepare), 0 when they are in SEAL's layout (MHE_KEY_PREPARE=0). */
+int mhe_resnet_key_format(mhe_resnet *runner, int *prepared);
+/* The same network in plain doubles with the exact ReLU (the check of a decrypted inference,
+ * infer_seal.cpp:543-575 prints decrypted logits against the label): image 3 x 32 x 32 -> logits[10]. */
+int mhe_resnet_plain_logits(mhe_resnet *runner, const double *image, double *logits);
 
 #ifdef __cplusplus
 }

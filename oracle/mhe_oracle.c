@@ -929,6 +929,27 @@ OR_API int or_ctx_hmult_batch(const or_ctx *c, const uint64_t *a, const uint64_t
     return used;
 }
 
+/* The same over every host core: `batch` independent HMults drawn cyclically from `distinct`
+ * input pairs (so B can be the core count without B distinct inputs in memory); the output of
+ * HMult i goes to the slot of the thread that ran it (out: [threads][2][L-1][n]). */
+OR_API int or_ctx_hmult_batch_cyclic(const or_ctx *c, const uint64_t *a, const uint64_t *b, int distinct,
+                                     const uint64_t *key, uint64_t *out, int L, int batch, int threads)
+{
+    size_t in_stride = (size_t)2 * L * c->n, out_stride = (size_t)2 * (L - 1) * c->n;
+    if (threads > 0) omp_set_num_threads(threads);
+    int used = 1;
+#pragma omp parallel
+    {
+#pragma omp single
+        used = omp_get_num_threads();
+        uint64_t *o = out + (size_t)omp_get_thread_num() * out_stride;
+#pragma omp for schedule(dynamic, 1)
+        for (int i = 0; i < batch; i++)
+            or_ctx_hmult(c, a + (i % distinct) * in_stride, b + (i % distinct) * in_stride, key, o, L);
+    }
+    return used;
+}
+
 /* ------------------------------------------------------------------------------------------
  * CKKS encoder (ckks.cpp:10-60 constructor tables, ckks.h:457-640 encode_internal,
  * ckks.cpp:78-200 encode_internal(double), util/croots.cpp ComplexRoots,

@@ -70,6 +70,8 @@ def lib():
             "or_ctx_multiply_plain": (None, [ctypes.c_void_p, u64p, u64p, ctypes.c_int, ctypes.c_int]),
             "or_ctx_hmult": (ctypes.c_int, [ctypes.c_void_p, u64p, u64p, u64p, u64p, ctypes.c_int]),
             "or_ctx_hmult_batch": (ctypes.c_int, [ctypes.c_void_p, u64p, u64p, u64p, u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+            "or_ctx_hmult_batch_cyclic": (ctypes.c_int, [ctypes.c_void_p, u64p, u64p, ctypes.c_int, u64p, u64p, ctypes.c_int,
+                                                         ctypes.c_int, ctypes.c_int]),
             "or_encoder_create": (ctypes.c_void_p, [ctypes.c_int]),
             "or_encoder_destroy": (None, [ctypes.c_void_p]),
             "or_ckks_encode": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
@@ -415,3 +417,13 @@ class Context:
         used = lib().or_ctx_hmult_batch(self._h, _p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), _p(key),
                                         _p(out), L, B, threads)
         return out, used
+
+    def hmult_batch_cyclic(self, a, b, key, batch, threads, out=None):
+        """`batch` independent HMults over the a[i % D], b[i % D] pairs (a, b: [D][2][L][n]) on
+        `threads` OpenMP threads; each thread writes its slot of out [threads][2][L-1][n] (pass a
+        pre-touched buffer to keep page faults out of a timing).  Returns the threads used."""
+        D, _, L = a.shape[:3]
+        if out is None:
+            out = np.zeros((threads, 2, L - 1, self.n), np.uint64)
+        return lib().or_ctx_hmult_batch_cyclic(self._h, _p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), D,
+                                               _p(key), _p(out), L, batch, threads)

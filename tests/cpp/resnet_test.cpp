@@ -16,92 +16,6 @@
 #include <cstdlib>
 #include <random>
 
-static std::vector<double> conv(const std::vector<double> &in, const std::vector<double> &wt, int h, int w, int ci,
-                                int co, int st)
-{
-    const int ho = h / st, wo = w / st;
-    std::vector<double> out((size_t)co * ho * wo, 0.0);
-    for (int b = 0; b < co; b++)
-        for (int y = 0; y < ho; y++)
-            for (int x = 0; x < wo; x++)
-            {
-                double s = 0;
-                for (int a = 0; a < ci; a++)
-                    for (int i1 = 0; i1 < 3; i1++)
-                        for (int i2 = 0; i2 < 3; i2++)
-                        {
-                            const int yy = st * y + i1 - 1, xx = st * x + i2 - 1;
-                            if (yy < 0 || yy >= h || xx < 0 || xx >= w) continue;
-                            s += wt[((size_t)(b * ci + a) * 3 + i1) * 3 + i2] * in[(size_t)a * h * w + yy * w + xx];
-                        }
-                out[(size_t)b * ho * wo + y * wo + x] = s;
-            }
-    return out;
-}
-
-static void bn(std::vector<double> &v, const ResNetParams &p, int s, int c, int hw)
-{
-    for (int b = 0; b < c; b++)
-    {
-        const double g = p.bn_weight[s][b] / std::sqrt(p.bn_running_var[s][b] + 1e-5);
-        for (int i = 0; i < hw; i++)
-            v[(size_t)b * hw + i] = (v[(size_t)b * hw + i] - p.bn_running_mean[s][b]) * g + p.bn_bias[s][b];
-    }
-}
-
-static void relu(std::vector<double> &v)
-{
-    for (auto &x : v) x = std::max(x, 0.0);
-}
-
-static std::vector<double> plain_resnet(const ResNetParams &p, const std::vector<double> &img, int end_num)
-{
-    std::vector<double> x = conv(img, p.conv_weight[0], 32, 32, 3, 16, 1);
-    int h = 32, c = 16;
-    bn(x, p, 0, c, h * h);
-    relu(x);
-    for (int j = 0; j < 3; j++)
-        for (int k = 0; k <= end_num; k++)
-        {
-            const int s1 = 2 * ((end_num + 1) * j + k) + 1, s2 = s1 + 1;
-            const int co = j == 0 ? 16 : j == 1 ? 32 : 64, st = (j >= 1 && k == 0) ? 2 : 1;
-            std::vector<double> temp = x;
-            std::vector<double> y = conv(x, p.conv_weight[s1], h, h, c, co, st);
-            const int ho = h / st;
-            bn(y, p, s1, co, ho * ho);
-            relu(y);
-            y = conv(y, p.conv_weight[s2], ho, ho, co, co, 1);
-            bn(y, p, s2, co, ho * ho);
-            if (st == 2)
-            {
-                // option-A shortcut: stride-2 subsample, input channel a -> output channel a + c/2
-                std::vector<double> ds((size_t)co * ho * ho, 0.0);
-                for (int a = 0; a < c; a++)
-                    for (int yy = 0; yy < ho; yy++)
-                        for (int xx = 0; xx < ho; xx++)
-                            ds[(size_t)(a + c / 2) * ho * ho + yy * ho + xx] = temp[(size_t)a * h * h + 2 * yy * h + 2 * xx];
-                temp = ds;
-            }
-            for (size_t i = 0; i < y.size(); i++) y[i] += temp[i];
-            relu(y);
-            x = y;
-            h = ho;
-            c = co;
-        }
-    std::vector<double> f(64, 0.0), logits(10, 0.0);
-    for (int b = 0; b < 64; b++)
-    {
-        for (int i = 0; i < h * h; i++) f[b] += x[(size_t)b * h * h + i];
-        f[b] /= h * h;
-    }
-    for (int i = 0; i < 10; i++)
-    {
-        logits[i] = p.linear_bias[i];
-        for (int b = 0; b < 64; b++) logits[i] += p.linear_weight[(size_t)i * 64 + b] * f[b];
-    }
-    return logits;
-}
-
 static void on_fault(int sig)
 {
     // a host fault (seen only under rocprofv3 so far): print the call stack before dying
@@ -126,7 +40,6 @@ int main(int argc, char **argv)
     const int images = argc > 3 ? std::atoi(argv[3]) : 1;
     const std::size_t layers = argc > 4 ? std::atoi(argv[4]) : 20;
     const int threads = argc > 5 ? std::atoi(argv[5]) : 0;
-    const int end_num = (int)(layers - 2) / 6 - 1; // infer_seal.cpp: 20 -> 2, 110 -> 17
     const ResNetParams prm = load_resnet_params_bin(argv[1], layers);
     if (images < 0)
     {
@@ -167,7 +80,7 @@ int main(int argc, char **argv)
         std::vector<double> img(3072);
         for (auto &x : img) x = U(g);
         const ResNetResult r = runner.infer(img);
-        const std::vector<double> want = plain_resnet(prm, img, end_num);
+        const std::vector<double> want = resnet_plain_logits(prm, img, layers);
         double err = 0, mag = 0;
         std::size_t wl = 0;
         for (int i = 0; i < 10; i++)
@@ -205,7 +118,7 @@ int main(int argc, char **argv)
         const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int id = 0; id < images; id++)
         {
-            const std::vector<double> want = plain_resnet(prm, batch[id], end_num);
+            const std::vector<double> want = resnet_plain_logits(prm, batch[id], layers);
             double err = 0, mag = 0;
             for (int i = 0; i < 10; i++)
             {

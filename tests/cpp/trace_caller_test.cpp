@@ -1,0 +1,122 @@
+// Caller-sequence trace for the oracle replay (tests/test_trace_parity.py): runs one multiplexed
+// convolution at 3 limbs (cnn/cnn_seal.cpp:284-530, with its top-level encryption of zero, so the
+// unequal-level branch of add_inplace_reduced_error runs -- SEAL/evaluator.cpp:312-362), one batch
+// norm (cnn_seal.cpp:531-576) and one ReLU polynomial (comp/SEALcomp.cpp:3-60 with one component:
+// comp/SEALfunc.cpp:59-260, then x (1 + sgn x) / 2) through the seal:: surface on the GPU with
+// MHE_EVAL_TRACE=<dir>, so every evaluator operation of the sequence is written out (seal/trace.h),
+// with seeded keys (Blake2xbPRNGFactory {1..8}) and seeded data.  The evaluation keys the sequence
+// used are written next to the trace: key_relin.bin, key_gal_<elt>.bin (u64 header: digits, limbs,
+// n; then [digits][2][limbs][n] in SEAL's layout, the special prime last).
+//   trace_caller_test <log N: 12 | 16> <dir> <comp_dir>
+#include "mhe_cnn.h"
+#include "mhe_comp.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <random>
+#include <string>
+
+using namespace seal;
+
+static void write_key(const std::string &path, const PolyStore &key, std::size_t limbs, std::size_t n)
+{
+    const std::uint64_t hdr[3] = { limbs - 1, limbs, n };
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char *>(hdr), sizeof hdr);
+    f.write(reinterpret_cast<const char *>(key.host()), (std::streamsize)(key.words() * 8));
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 4)
+    {
+        std::fprintf(stderr, "usage: trace_caller_test <log N> <dir> <comp_dir>\n");
+        return 2;
+    }
+    const int logN = std::atoi(argv[1]);
+    const std::string dir = argv[2];
+    setenv("MHE_EVAL_TRACE", dir.c_str(), 1); // before the first evaluator operation
+    setenv("MHE_COMP_DIR", argv[3], 1);
+    const std::size_t N = (std::size_t)1 << logN;
+    // {51} + 8 x {46} + {51}: the ResNet chain's shape (cnn/infer_seal.cpp:288-316), shortened; 2^46 scale
+    std::vector<int> bits{ 51 };
+    for (int i = 0; i < 8; i++) bits.push_back(46);
+    bits.push_back(51);
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(N);
+    parms.set_coeff_modulus(CoeffModulus::Create(N, bits));
+    parms.set_secret_key_hamming_weight(logN >= 16 ? 192 : 64);
+    parms.set_random_generator(
+        std::make_shared<Blake2xbPRNGFactory>(std::array<std::uint64_t, 8>{ 1, 2, 3, 4, 5, 6, 7, 8 }));
+    SEALContext ctx(parms, true, sec_level_type::none);
+    KeyGenerator keygen(ctx);
+    PublicKey pk;
+    keygen.create_public_key(pk);
+    RelinKeys rlk;
+    keygen.create_relin_keys(rlk);
+    GaloisKeys glk;
+    keygen.create_deferred_galois_keys(glk); // materialised at the level of first use
+    CKKSEncoder encoder(ctx);
+    Encryptor encryptor(ctx, pk);
+    Decryptor decryptor(ctx, keygen.secret_key());
+    Evaluator evaluator(ctx, encoder);
+    const double scale = std::pow(2.0, 46);
+    const int logn = logN - 1;
+    const long n = 1L << logn;
+
+    std::mt19937_64 g(20261017);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    // 1. conv: k = 1, h = w = 8 (N = 2^12) or 16 (N = 2^16), ci = co = 4, t = 4, p = n / (h w t)
+    const int h = logN >= 16 ? 16 : 8, ci = 4, co = 4, t = 4, p = (int)(n / (h * h * t));
+    std::vector<double> img(n, 0.0), wt(9 * ci * co), var(co), gamma(co), bias(co), mean(co);
+    for (int r = 0; r < p; r++)
+        for (int i = 0; i < ci * h * h; i++) img[(std::size_t)r * (n / p) + i] = 0.5 * U(g);
+    for (auto &v : wt) v = 0.3 * U(g);
+    for (int b = 0; b < co; b++)
+    {
+        var[b] = 1.25 + 0.75 * U(g);
+        gamma[b] = 1.0 + 0.5 * U(g);
+        bias[b] = 0.1 * U(g);
+        mean[b] = 0.1 * U(g);
+    }
+    TensorCipher in(logn, 1, h, h, ci, t, p, img, encryptor, encoder, 46);
+    Ciphertext c = in.cipher();
+    evaluator.mod_switch_to_inplace(c, ctx.get_context_data(ctx.first_parms_id())->next_context_data()->parms_id());
+    while (c.coeff_modulus_size() > 3) evaluator.mod_switch_to_next_inplace(c);
+    in.set_ciphertext(c);
+    std::vector<Ciphertext> pool(16);
+    TensorCipher out;
+    multiplexed_parallel_convolution_seal(in, out, co, 1, 3, 3, wt, var, gamma, 1e-5, encoder, encryptor, evaluator, glk,
+                                          pool);
+    // 2. batch norm on the conv output
+    TensorCipher bn;
+    multiplexed_parallel_batch_norm_seal(out, bn, bias, mean, var, gamma, 1e-5, encoder, encryptor, evaluator, 40.0);
+    // 3. one ReLU polynomial (the first component of the alpha = 13 composite) on a fresh input
+    std::vector<double> x(n);
+    for (auto &v : x) v = U(g);
+    Plaintext px;
+    encoder.encode(x, scale, px);
+    Ciphertext cx, cr;
+    encryptor.encrypt(px, cx);
+    std::vector<Tree> tree(1);
+    upgrade_oddbaby(15, tree[0]);
+    SecretKey sk = keygen.secret_key();
+    minimax_ReLU_seal(1, { 15 }, 13, tree, 1.7, 46, encryptor, evaluator, decryptor, encoder, pk, sk, rlk, cx, cr);
+
+    // keys the sequence used, for the replay
+    write_key(dir + "/key_relin.bin", rlk.key(0), rlk.limbs_of(0), N);
+    std::size_t gal = 0;
+    for (const auto &kv : glk.usage())
+    {
+        write_key(dir + "/key_gal_" + std::to_string(2 * kv.first + 1) + ".bin", glk.key(kv.first), kv.second, N);
+        gal++;
+    }
+    std::ofstream meta(dir + "/meta.json");
+    meta << "{\"log_n\": " << logN << ", \"moduli\": [";
+    const auto &q = ctx.key_context_data()->parms().coeff_modulus();
+    for (std::size_t i = 0; i < q.size(); i++) meta << (i ? ", " : "") << q[i].value();
+    meta << "], \"first_limbs\": " << ctx.first_context_data()->parms().coeff_modulus().size() << "}\n";
+    std::printf("trace written to %s (%zu Galois keys used)\n", dir.c_str(), gal);
+    return 0;
+}

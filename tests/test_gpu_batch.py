@@ -1,0 +1,120 @@
+"""GPU parity of the batched launches (include/mhe.h mhe_apply_galois_batch / mhe_rescale_batch /
+mhe_switch_key_batch): `count` independent operations of one level in one launch per kernel must
+give, entry for entry, the same words as the oracle's single-ciphertext restatement of
+apply_galois_inplace / divide_and_round_q_last_ntt_inplace / switch_key_inplace
+(SEAL/evaluator.cpp:2120-2222, 2281-2525; SEAL/util/rns.cpp:737-808).  Batches larger than one
+launch's 8 entries run in groups, so 9 and 11 cover the split."""
+import numpy as np
+import pytest
+
+import mhe
+import oracle as O
+from test_gpu_parity import RESNET_BITS, SMALL_BITS, Chain
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def small():
+    return Chain(12, SMALL_BITS, seed=11)
+
+
+@pytest.fixture(scope="module")
+def resnet():
+    return Chain(16, RESNET_BITS, seed=12)
+
+
+def truncated(key, L):
+    """The level-L slice of a key: L digits, data primes 0..L-1 and the special prime."""
+    return np.ascontiguousarray(np.concatenate([key[:L, :, :L], key[:L, :, -1:]], axis=2))
+
+
+@pytest.mark.parametrize("L", [1, 3, 7])
+@pytest.mark.parametrize("count", [1, 3, 8, 11])
+def test_rotate_batch_one_input(small, L, count):
+    """The conv / BSGS baby-step shape: one input rotated by `count` different steps."""
+    ch = small
+    ct = ch.rand(2, L, ch.n)
+    steps = [1, -1, 3, 100, 0, 7, -5, 64, 2, 9, 31][:count]
+    elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
+    keys = [ch.rand_key() for _ in steps]
+    dkeys = [ch.up(k if i % 2 else truncated(k, L)) for i, k in enumerate(keys)]  # full and level-truncated
+    src = ch.up(ct)
+    outs = ch.eng.apply_galois_batch([src] * count, elts, dkeys)
+    for i in range(count):
+        assert np.array_equal(ch.down(outs[i]), ch.oc.apply_galois(ct, elts[i], keys[i])), f"entry {i} step {steps[i]}"
+    assert np.array_equal(ch.down(src), ct)  # inputs untouched
+
+
+@pytest.mark.parametrize("count", [2, 9])
+def test_rotate_batch_many_inputs(small, count):
+    """The multi-image / giant-step shape: different inputs, the same or different keys."""
+    ch = small
+    L = 5
+    key = ch.rand_key()
+    cts = [ch.rand(2, L, ch.n) for _ in range(count)]
+    elts = [mhe.galois_elt_from_step(ch.log_n, 1 + (i % 3)) for i in range(count)]
+    dk = ch.up(key)
+    outs = ch.eng.apply_galois_batch([ch.up(c) for c in cts], elts, [dk] * count)
+    for i in range(count):
+        assert np.array_equal(ch.down(outs[i]), ch.oc.apply_galois(cts[i], elts[i], key))
+
+
+def test_rotate_batch_prepared_keys_n16(resnet):
+    """N = 2^16 on the ResNet chain with prepared (48-bit) keys: the packed ModUp intermediate and
+    key planes per entry, at a bootstrap-like level."""
+    ch = resnet
+    L = 6
+    ct = ch.rand(2, L, ch.n)
+    steps = [1, 2, 4, 8]
+    elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
+    keys = [truncated(ch.rand_key(digits=L), L) for _ in steps]
+    dkeys = [ch.eng.key_prepare(ch.up(k)) for k in keys]
+    outs = ch.eng.apply_galois_batch([ch.up(ct)] * len(steps), elts, dkeys)
+    full = [np.zeros((L, 2, ch.K, ch.n), np.uint64) for _ in keys]
+    for f, k in zip(full, keys):  # the truncated slice inside a full-shape key for the oracle
+        f[:, :, :L] = k[:, :, :L]
+        f[:, :, -1] = k[:, :, -1]
+    for i in range(len(steps)):
+        assert np.array_equal(ch.down(outs[i]), ch.oc.apply_galois(ct, elts[i], full[i]))
+
+
+@pytest.mark.parametrize("size", [1, 2, 3])
+@pytest.mark.parametrize("count", [1, 5, 9])
+def test_rescale_batch(small, size, count):
+    ch = small
+    L = 6
+    cts = [ch.rand(size, L, ch.n) for _ in range(count)]
+    outs = ch.eng.rescale_batch([ch.up(c) for c in cts])
+    for c, o in zip(cts, outs):
+        assert np.array_equal(ch.down(o), ch.oc.rescale(c))
+
+
+@pytest.mark.parametrize("L", [1, 4])
+def test_switch_key_batch(small, L):
+    ch = small
+    count = 3
+    keys = [ch.rand_key() for _ in range(count)]
+    cts = [ch.rand(2, L, ch.n) for _ in range(count)]
+    tgs = [ch.rand(L, ch.n) for _ in range(count)]
+    dct = [ch.up(c) for c in cts]
+    ch.eng.switch_key_batch(dct, [ch.up(t) for t in tgs], [ch.up(k) for k in keys])
+    for i in range(count):
+        assert np.array_equal(ch.down(dct[i]), ch.oc.switch_key(cts[i], tgs[i], keys[i]))
+
+
+def test_batch_errors(small):
+    ch = small
+    L = 3
+    a = ch.up(ch.rand(2, L, ch.n))
+    key = ch.up(ch.rand_key())
+    elt = mhe.galois_elt_from_step(ch.log_n, 1)
+    with pytest.raises(mhe.MheError, match="same value"):
+        ch.eng.apply_galois_batch([a], [elt], [key], outs=[a])  # out aliases in
+    o = ch.eng.empty(2, L, ch.n)
+    with pytest.raises(mhe.MheError, match="same value"):
+        ch.eng.apply_galois_batch([a, a], [elt, elt], [key, key], outs=[o, o])  # two outputs alias
+    with pytest.raises(mhe.MheError, match="Galois element"):
+        ch.eng.apply_galois_batch([a], [4], [key])
+    with pytest.raises(mhe.MheError):
+        ch.eng.rescale_batch([a], outs=[a])
