@@ -83,8 +83,8 @@ def cpu_baseline(moduli, L_main, threads):
     """SURVEY.md §8(d) CPU baseline: the repo's CPU restatement of the reference algorithm (oracle/,
     "port", bit-exact with the GPU path), compiled on this host with -O3 -march=native, timed in
     this run on `threads` host cores (the box's CPU share for one GPU): single-thread HMult/s,
-    B in {1, 8, 32} independent HMults (one per OpenMP thread) for L in {44, 31, 17, 3}, and B = every
-    host core's worth of HMults on all host cores at L in {44, 31} (`all_cores`)."""
+    B in {1, 8, 32} independent HMults (one per OpenMP thread) for L in {44, 31, 17, 3}, and the
+    same on every host core this process may use at L in {44, 31} (`all_cores`)."""
     import tempfile
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -114,20 +114,31 @@ def cpu_baseline(moduli, L_main, threads):
             row[str(B)] = round(B / dt, 4)
             walls[(L, B)] = (dt, used)
         table[str(L)] = row
-    # all host cores: B = the cores this process may run on, independent HMults
-    # cycled over the 32 input pairs, one per OpenMP thread, at L = 44 and the CNN top level L = 31
+    # all host cores: the cores this process may actually use -- the CPU
+    # affinity capped by the cgroup quota (the GPU box gives one GPU's job 16 of its nproc CPUs; more
+    # threads than that only time-share them: 256 threads measured 4.8 HMult/s at L=44 against 10.5
+    # on 16, r03c) -- with B = 32 independent HMults on that many threads, at L = 44 and L = 31
     host = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    all_cores = {"threads": host, "batch": host, "cgroup_cpu_max": cgroup_cpu_max()}
+    quota = cgroup_cpu_max()
+    usable = host
+    try:
+        q, per = quota.split()
+        if q != "max":
+            usable = max(1, min(host, -(-int(q) // int(per))))
+    except (AttributeError, ValueError):
+        pass
+    all_cores = {"usable_cpus": usable, "affinity_cpus": host, "cgroup_cpu_max": quota, "batch": 32}
     for L in (44, 31):
+        if usable == threads and str(L) in table:
+            all_cores[str(L)] = {"hmult_per_s": table[str(L)]["32"], "threads": usable, "note": "= per_L[L][32]"}
+            continue
         kL = np.ascontiguousarray(key[:L])
         a = np.ascontiguousarray(a_all[:, :, :L])
         b = np.ascontiguousarray(b_all[:, :, :L])
-        out = np.zeros((host, 2, L - 1, n), np.uint64)  # touched before the timing
         t0 = time.perf_counter()
-        used = oc.hmult_batch_cyclic(a, b, kL, host, host, out)
+        _, used = oc.hmult_batch(a, b, kL, threads=usable)
         dt = time.perf_counter() - t0
-        all_cores[str(L)] = {"hmult_per_s": round(host / dt, 3), "wall_s": round(dt, 2), "threads_used": int(used)}
-        del out
+        all_cores[str(L)] = {"hmult_per_s": round(32 / dt, 3), "wall_s": round(dt, 2), "threads": int(used)}
     a1 = np.ascontiguousarray(a_all[:1, :, :L_main])
     b1 = np.ascontiguousarray(b_all[:1, :, :L_main])
     t0 = time.perf_counter()

@@ -56,18 +56,31 @@ __device__ __forceinline__ double fp_reduce(double x, double q, double qinv)
     return __builtin_fma(-fp_rint(x * qinv), q, x);
 }
 
-// canonical [0, q) from |x| <= 2^53, as u64.
+// 2^52: a double in [2^52, 2^53) holds the integer d - 2^52 in its 52 mantissa bits
+#define FP_TWO52 4503599627370496.0
+
+// canonical [0, q) from |x| <= 2^53, as u64.  The centered residue r is shifted into [2^52, 2^53)
+// (r + 2^52, or r + q + 2^52 when negative: exact integers below 2^53), whose mantissa field IS
+// the residue -- one add and a mask instead of gfx950's multi-instruction f64 -> u64 conversion.
 __device__ __forceinline__ uint64_t fp_canon(double x, double q, double qinv)
 {
-    double r = fp_reduce(x, q, qinv); // [-q/2 - 1, q/2 + 1]
-    r = r < 0 ? r + q : r;
-    return (uint64_t)r;
+    const double r = fp_reduce(x, q, qinv); // [-q/2 - 1, q/2 + 1]
+    const double d = r + (r < 0 ? q + FP_TWO52 : FP_TWO52);
+    return (uint64_t)__double_as_longlong(d) & 0x000FFFFFFFFFFFFFull;
 }
 
 // exact double of a u64 < 2^53
 __device__ __forceinline__ double fp_from_u64(uint64_t x)
 {
     return (double)x;
+}
+
+// exact double of a u64 < 2^52 (every canonical residue of a prime below 2^51): the exponent of
+// 2^52 OR-ed over x gives 2^52 + x, one subtraction leaves x -- instead of two u32 conversions,
+// an ldexp and an add
+__device__ __forceinline__ double fp_from_u52(uint64_t x)
+{
+    return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - FP_TWO52;
 }
 
 // Forward Cooley-Tukey butterfly (the mathematics of dwthandler.h:122-125).

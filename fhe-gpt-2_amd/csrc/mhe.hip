@@ -519,8 +519,8 @@ struct JobModDownRow
             {
                 // acc and t canonical: (acc - t) P^-1 in (-1.25p, 1.25p), plus c < p, one
                 // canonicalisation (|.| < 2^53): the residue of the integer form
-                const double v = fp_mulmod_gen((double)accp[x] - (double)t, invd, pd, pi);
-                ctp[x] = fp_canon(replace ? v : v + (double)ctp[x], pd, pi);
+                const double v = fp_mulmod_gen(fp_from_u52(accp[x]) - fp_from_u52(t), invd, pd, pi);
+                ctp[x] = fp_canon(replace ? v : v + fp_from_u52(ctp[x]), pd, pi);
                 return;
             }
             u64 v = mul_shoup(accp[x] + p.four_q - t, inv.x, inv.y, p.q);
@@ -616,7 +616,7 @@ struct JobRescaleRow
         __device__ void store(u32 x, u64 t) const
         {
             if (fp) // in and t canonical: (in - t) q_last^-1 in (-1.25p, 1.25p), canonicalised
-                outp[x] = fp_canon(fp_mulmod_gen((double)inp[x] - (double)t, invd, pd, pi), pd, pi);
+                outp[x] = fp_canon(fp_mulmod_gen(fp_from_u52(inp[x]) - fp_from_u52(t), invd, pd, pi), pd, pi);
             else
                 outp[x] = mul_shoup(inp[x] + p.four_q - t, inv.x, inv.y, p.q);
         }
@@ -677,7 +677,7 @@ struct JobMDRCol
                 // P^-1 is in (-2p, 2p), the sum below 2^53: one canonicalisation, the same residue
                 const u64 t = csub(csub(accP[x] + halfP, 2 * P.q), P.q);
                 const u64 r = csub(lastp[x] + halfL, ql);
-                const double u = fp_mulmod_gen((double)(t + fixP), pinvd, pd, pi) + (double)(r + neg_halfL);
+                const double u = fp_mulmod_gen(fp_from_u52(t + fixP), pinvd, pd, pi) + fp_from_u52(r + neg_halfL);
                 return fp_canon(u, pd, pi);
             }
             u64 t = barrett64(accP[x] + halfP, P);
@@ -746,8 +746,8 @@ struct JobMDRRow
             {
                 // acc_i P^-1 in (-1.25p, 1.25p); c + a - U is an exact integer below 2^53; its
                 // centered residue times q_{L-1}^-1, canonicalised: the residue of the integer form
-                const double a = fp_mulmod_gen((double)accp[x], pinvd, pd, pi);
-                const double v = fp_reduce((double)ctp[x] + a - (double)U, pd, pi);
+                const double a = fp_mulmod_gen(fp_from_u52(accp[x]), pinvd, pd, pi);
+                const double v = fp_reduce(fp_from_u52(ctp[x]) + a - fp_from_u52(U), pd, pi);
                 outp[x] = fp_canon(fp_mulmod_gen(v, qlinvd, pd, pi), pd, pi);
                 return;
             }

@@ -180,6 +180,7 @@ struct NttArith<false>
     const Tw *tw;
     __device__ NttArith(const PrimeDev &p, const Tw *t, long long) : q(p.q), q2(p.two_q), tw(t) {}
     __device__ T in(u64 x) const { return x; }
+    __device__ T in52(u64 x) const { return x; }
     __device__ u64 out(T x) const { return x; }
     __device__ u64 canon(T x) const { return csub(csub(x, q2), q); }
     template <int E, class Ix>
@@ -212,6 +213,7 @@ struct NttArithF
     {
     }
     __device__ T in(u64 x) const { return (double)x; }
+    __device__ T in52(u64 x) const { return fp_from_u52(x); } // x < 2^52: a canonical residue
     __device__ u64 out(T x) const { return fp_canon(x, q, qinv); }
     __device__ u64 canon(T x) const { return fp_canon(x, q, qinv); }
     template <int E, class Ix>
@@ -582,7 +584,7 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(KsPtrs P, const PrimeDev *
     if constexpr (FP)
     {
 #pragma unroll
-        for (int e = 0; e < E; e++) xd[e] = (double)x[e];
+        for (int e = 0; e < E; e++) xd[e] = fp_from_u52(x[e]); // canonical INTT output
     }
     // two sweeps over the group's output primes when FP: first the q < 2^47 ones with the lazy
     // forward butterflies, then the rest, so each loop body has one arithmetic variant
@@ -1025,7 +1027,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             {
                 T w[8];
 #pragma unroll
-                for (int e = 0; e < 8; e++) w[e] = ar.in(vin[e]);
+                for (int e = 0; e < 8; e++) w[e] = ar.in52(vin[e]); // canonical column-pass output
                 row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
                 wave_lds_fence(); // the previous digit's reads of x0 come first
 #pragma unroll
@@ -1066,7 +1068,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             else
             {
 #pragma unroll
-                for (int e = 0; e < 8; e++) d[e] = ar.in(vin[e]);
+                for (int e = 0; e < 8; e++) d[e] = ar.in52(vin[e]); // the target: a canonical ciphertext limb
             }
             if constexpr (FP)
             {
@@ -1074,8 +1076,8 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
                 for (int e = 0; e < 8; e++)
                 {
                     const double dv = LZ ? d[e] : fp_reduce(d[e], ar.q, ar.qinv);
-                    a0[e] += fp_mulmod_gen(dv, (double)kk0[e], ar.q, ar.qinv);
-                    a1[e] += fp_mulmod_gen(dv, (double)kk1[e], ar.q, ar.qinv);
+                    a0[e] += fp_mulmod_gen(dv, fp_from_u52(kk0[e]), ar.q, ar.qinv); // canonical key residues
+                    a1[e] += fp_mulmod_gen(dv, fp_from_u52(kk1[e]), ar.q, ar.qinv);
                     if (!LZ && ((J - j0) & 1))
                     {
                         a0[e] = fp_reduce(a0[e], ar.q, ar.qinv);

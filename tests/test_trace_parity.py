@@ -1,0 +1,36 @@
+"""Caller-sequence parity at ciphertext level: one multiplexed
+convolution at 3 limbs (cnn/cnn_seal.cpp:284-530, whose top-level encryption of zero takes
+add_inplace_reduced_error's unequal-level branch, SEAL/evaluator.cpp:312-362), one batch norm
+(cnn_seal.cpp:531-576) and one ReLU polynomial (comp/SEALcomp.cpp:3-60, comp/SEALfunc.cpp:59-260)
+run on the GPU through the seal:: surface with seeded keys (Blake2xbPRNGFactory {1..8}) and the
+evaluator trace on (build/trace_caller_test, seal/trace.h); every recorded operation -- encodes,
+rotations, plaintext products, reduced-error adds / subs / multiplies with their scale forcing,
+rescales, relinearizations -- is then recomputed by the CPU oracle (tests/trace_replay.py over
+oracle/evaluator.py) from the recorded inputs and must match word for word, scale for scale."""
+import os
+import subprocess
+
+import pytest
+
+from trace_replay import Replayer
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("log_n", [12, 16])
+def test_conv_bn_relu_sequence_matches_oracle(tmp_path, log_n):
+    d = tmp_path / f"trace{log_n}"
+    d.mkdir()
+    exe = os.path.join(ROOT, "build", "trace_caller_test")
+    r = subprocess.run([exe, str(log_n), str(d), os.path.join(ROOT, "tests", "golden", "comp")], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rp = Replayer(str(d))
+    checked, counts = rp.replay()
+    print(f"N=2^{log_n}: {checked} operations match the oracle: {counts}")
+    # the sequence must have exercised the operations A11 / A19 / A20 name
+    for op in ("rotate", "multiply_plain", "multiply_plain_add", "add_re", "sub_re", "mul_re", "rescale",
+               "encode_for", "multiply_const"):
+        assert counts.get(op, 0) > 0, f"{op} not exercised: {counts}"

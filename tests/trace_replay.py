@@ -1,0 +1,225 @@
+"""Oracle replay of an evaluator trace (fhe-gpt-2_amd/seal/trace.h; TEST INFRASTRUCTURE).
+
+The GPU surface, run with MHE_EVAL_TRACE=<dir>, writes one record per top-level evaluator /
+encoder / encryptor operation (trace.jsonl) and every ciphertext, plaintext and vector it read or
+wrote (content-addressed .bin files).  `replay(dir)` recomputes every record with the CPU oracle's
+restatement of the modified SEAL evaluator (oracle/evaluator.py over oracle/mhe_oracle.c), from the
+recorded inputs, and compares the output words and scale with the GPU's, so a caller's whole
+operation sequence (conv, BN, ReLU polynomial, ...) is checked op by op, in its own order.
+Encryptions are leaves (their randomness is pinned separately by tests/test_gpu_random.py).
+"""
+import json
+import os
+import struct
+
+import numpy as np
+
+import oracle as O
+from evaluator import Evaluator, OCt
+
+
+def _read(path, hwords):
+    raw = open(path, "rb").read()
+    hdr = struct.unpack("<%dQ" % hwords, raw[: 8 * hwords])
+    return hdr, raw[8 * hwords:]
+
+
+class Store:
+    def __init__(self, d):
+        self.d = d
+        self.cache = {}
+
+    def get(self, oid):
+        if oid in self.cache:
+            return self.cache[oid]
+        path = os.path.join(self.d, oid + ".bin")
+        kind = oid[0]
+        if kind == "c":
+            (size, L, n, sb, ntt), body = _read(path, 5)
+            scale = struct.unpack("<d", struct.pack("<Q", sb))[0]
+            v = (OCt(np.frombuffer(body, np.uint64).reshape(size, L, n).copy(), scale), bool(ntt))
+        elif kind == "p":
+            (L, words, sb), body = _read(path, 3)
+            scale = struct.unpack("<d", struct.pack("<Q", sb))[0]
+            v = (np.frombuffer(body, np.uint64).reshape(L, -1).copy(), scale)
+        elif kind == "v":
+            (cnt, cplx), body = _read(path, 2)
+            a = np.frombuffer(body, np.float64)
+            v = a[:cnt] + 1j * a[cnt:2 * cnt] if cplx else a[:cnt].copy()
+        else:
+            raise ValueError(oid)
+        self.cache[oid] = v
+        return v
+
+
+def load_key(path, K):
+    """key_*.bin (trace_caller_test.cpp): [digits][2][limbs][n], special prime last -> the
+    full-shape [digits][2][K][n] the oracle indexes (the primes a truncated key lacks stay 0)."""
+    (digits, limbs, n), body = _read(path, 3)
+    k = np.frombuffer(body, np.uint64).reshape(digits, 2, limbs, n)
+    full = np.zeros((digits, 2, K, n), np.uint64)
+    full[:, :, : limbs - 1] = k[:, :, : limbs - 1]
+    full[:, :, K - 1] = k[:, :, limbs - 1]
+    return full
+
+
+def naf(steps):
+    """util/numth.h:22-42 (the NAF the evaluator uses when a rotation key is absent)."""
+    out, sign, v, i = [], steps < 0, abs(steps), 0
+    while v:
+        zi = (2 - (v & 3)) if (v & 1) else 0
+        v = (v - zi) >> 1
+        if zi:
+            out.append((-zi if sign else zi) * (1 << i))
+        i += 1
+    return out
+
+
+class Replayer:
+    def __init__(self, d):
+        meta = json.load(open(os.path.join(d, "meta.json")))
+        self.d = d
+        self.n = 1 << meta["log_n"]
+        self.moduli = meta["moduli"]
+        self.K = len(self.moduli)
+        self.ctx = O.Context(meta["log_n"], self.moduli)
+        keys = {}
+        for f in os.listdir(d):
+            if f.startswith("key_gal_"):
+                keys[int(f[8:-4])] = load_key(os.path.join(d, f), self.K)
+        self.ev = Evaluator(self.ctx, meta["first_limbs"], load_key(os.path.join(d, "key_relin.bin"), self.K), keys)
+        self.store = Store(d)
+        self.counts = {}
+
+    def _ct(self, oid):
+        c, _ = self.store.get(oid)
+        return c.copy()
+
+    def _rotate(self, a, step):
+        if step == 0:
+            return a
+        elt = O.galois_elt_from_step(self.n, step)
+        if elt in self.ev.galois_keys:
+            return OCt(self.ctx.apply_galois(a.data, elt, self.ev.galois_keys[elt]), a.scale)
+        for s in naf(step):
+            if abs(s) != self.n // 2:
+                a = self._rotate(a, s)
+        return a
+
+    def _addsub(self, a, b, sub):
+        """add_inplace / sub_inplace (evaluator.cpp:103-246) with unequal sizes: the longer tail is
+        copied (add) or negated (sub)."""
+        if a.L != b.L:
+            raise ValueError("encrypted1 and encrypted2 parameter mismatch")
+        from evaluator import are_close
+        if not are_close(a.scale, b.scale):
+            raise ValueError("scale mismatch")
+        m = min(a.size, b.size)
+        head = self.ctx.sub(a.data[:m], b.data[:m]) if sub else self.ctx.add(a.data[:m], b.data[:m])
+        tail = a.data[m:] if a.size > b.size else (self.ctx.negate(b.data[m:]) if sub else b.data[m:])
+        return OCt(np.concatenate([head, tail]) if len(tail) else head, a.scale)
+
+    def expect(self, rec):
+        """The oracle's output (OCt, or (words, scale) for a plaintext) for one record."""
+        op, ins, ex = rec["op"], rec["in"], rec
+        ev, ctx = self.ev, self.ctx
+        if op == "encode":
+            v = self.store.get(ins[0])
+            L = self.store.get(rec["out"])[0].shape[0]
+            return ctx.encode(v, ex["scale"], L), ex["scale"]
+        if op == "encode_for":
+            v = self.store.get(ins[0])
+            return ctx.encode(v, ex["scale"], ev.first)[: ex["limbs"]], ex["scale"]
+        if op == "encode_const":
+            # CKKSEncoder::encode(double, parms_id, scale) at that level (ckks.cpp:78-200)
+            r = ctx.encode_scalar(ex["value"], ex["scale"], ex["limbs"])
+            return np.repeat(np.array(r, np.uint64)[:, None], self.n, axis=1), ex["scale"]
+        if op == "pt_mod_switch":
+            w, s = self.store.get(ins[0])
+            L = self.store.get(rec["out"])[0].shape[0]
+            return w[:L], s
+        a = self._ct(ins[0])
+        if op in ("add", "sub"):
+            return self._addsub(a, self._ct(ins[1]), op == "sub")
+        if op == "negate":
+            return OCt(ctx.negate(a.data), a.scale)
+        if op == "multiply":
+            b = self._ct(ins[1])
+            ev.multiply_inplace(a, b)
+            return a
+        if op == "square":
+            ev.multiply_inplace(a, a)
+            return a
+        if op == "relinearize":
+            ev.relinearize_inplace(a)
+            return a
+        if op == "mod_switch":
+            L = self.store.get(rec["out"])[0].L
+            ev.mod_switch_to_inplace(a, L)
+            return a
+        if op == "rescale":
+            L = self.store.get(rec["out"])[0].L
+            while a.L > L:
+                ev.rescale_to_next_inplace(a)
+            return a
+        if op == "multiply_plain":
+            w, s = self.store.get(ins[1])
+            ev.multiply_plain_inplace(a, w, s)
+            return a
+        if op == "multiply_plain_add":
+            x = self._ct(ins[1])
+            w, s = self.store.get(ins[2])
+            ev.multiply_plain_inplace(x, w, s)
+            return OCt(ctx.add(a.data, x.data), x.scale)
+        if op in ("add_plain", "sub_plain"):
+            w, s = self.store.get(ins[1])
+            from evaluator import are_close
+            if not are_close(a.scale, s):
+                raise ValueError("scale mismatch")
+            a.data = a.data.copy()
+            a.data[0] = ctx.sub(a.data[0], w) if op == "sub_plain" else ctx.add(a.data[0], w)
+            return a
+        if op == "ntt_fwd":
+            return OCt(ctx.ntt(a.data, O.NTT_FWD), a.scale)
+        if op == "ntt_inv":
+            return OCt(ctx.ntt(a.data, O.NTT_INV), a.scale)
+        if op == "galois":
+            return OCt(ctx.apply_galois(a.data, ex["elt"], ev.galois_keys[ex["elt"]]), a.scale)
+        if op == "rotate":
+            return self._rotate(a, ex["step"])
+        if op == "add_const":
+            ev.add_const_inplace(a, ex["value"])
+            return a
+        if op == "multiply_const":
+            return ev.multiply_const(a, ex["value"])
+        if op in ("add_re", "sub_re", "mul_re"):
+            b = self._ct(ins[1])
+            {"add_re": ev.add_inplace_reduced_error, "sub_re": ev.sub_inplace_reduced_error,
+             "mul_re": ev.multiply_inplace_reduced_error}[op](a, b)
+            return a
+        raise ValueError("unknown op " + op)
+
+    def replay(self):
+        """Returns (records checked, {op: count}); raises AssertionError at the first mismatch."""
+        recs = [json.loads(l) for l in open(os.path.join(self.d, "trace.jsonl"))]
+        checked = 0
+        for i, rec in enumerate(recs):
+            op = rec["op"]
+            self.counts[op] = self.counts.get(op, 0) + 1
+            if op == "encrypt":
+                continue  # leaf
+            want = self.expect(rec)
+            got = self.store.get(rec["out"])
+            if rec["out"][0] == "p":
+                gw, gs = got
+                ww, ws = want
+                assert np.array_equal(gw, ww), f"record {i} ({op}): plaintext words differ"
+                assert gs == ws, f"record {i} ({op}): plaintext scale {gs!r} != {ws!r}"
+            else:
+                gc, _ = got
+                assert gc.data.shape == want.data.shape, f"record {i} ({op}): shape {gc.data.shape} != {want.data.shape}"
+                bad = int((gc.data != want.data).sum())
+                assert bad == 0, f"record {i} ({op}): {bad} of {gc.data.size} words differ"
+                assert gc.scale == want.scale, f"record {i} ({op}): scale {gc.scale!r} != {want.scale!r}"
+            checked += 1
+        return checked, dict(self.counts)
