@@ -262,6 +262,14 @@ __device__ __forceinline__ void wave_lds_fence()
     asm volatile("" ::: "memory");
 }
 
+// Workgroup barrier on LDS only (s_waitcnt lgkmcnt(0) + s_barrier): __syncthreads() also waits for
+// every outstanding global memory operation (vmcnt(0)), which serialises a kernel's stores with the
+// compute that follows them (cdna_hip_programming.md §8).
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <int LOGR, int LOGT>
 struct Shape
 {
@@ -503,10 +511,10 @@ __global__ __launch_bounds__(256) void k_icol_lift(ColSrc cs, Job job, int cnt, 
 #pragma unroll
         for (int st = 0; st < LOGE; st++)
             ar.template fwd<E>(v, 1 << (LOGE - 1 - st), [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
-        __syncthreads(); // lds still holds the previous prime's (or the inverse pass's) transpose
+        lds_barrier(); // lds still holds the previous prime's (or the inverse pass's) transpose
 #pragma unroll
         for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
-        __syncthreads();
+        lds_barrier(); // LDS only: the previous prime's stores stay in flight
 #pragma unroll
         for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
@@ -616,7 +624,7 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(KsPtrs P, const PrimeDev *
                 ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
 #pragma unroll
             for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
-            __syncthreads();
+            lds_barrier(); // LDS only: the previous output prime's stores stay in flight
 #pragma unroll
             for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
@@ -651,7 +659,7 @@ __global__ __launch_bounds__(256, 3) void k_modup_col(KsPtrs P, const PrimeDev *
 #pragma unroll
                 for (int e = 0; e < E; e++) st_nt<0>(&dst[c + ((u32)(E * t + e) << logC)], ar.out(v[e]));
             }
-            __syncthreads(); // lds is rewritten by the next output prime
+            lds_barrier(); // lds is rewritten by the next output prime (its stores need not land)
         }
     };
     if constexpr (FP)
@@ -850,10 +858,6 @@ __device__ __forceinline__ u32 lay(u32 t, int e, int b_lo)
     return ((t >> b_lo) << (b_lo + 3)) | ((u32)e << b_lo) | (t & ((1u << b_lo) - 1));
 }
 
-__device__ __forceinline__ void lds_barrier()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 
 // Forward stages [s0, s1) of the local 2^LOGR transform, twiddles from the block's LDS row

@@ -22,6 +22,7 @@
 #include <iosfwd>
 #include <map>
 #include <memory>
+#include <functional>
 #include <vector>
 
 #include "seal/seal.h"
@@ -80,6 +81,13 @@ int giantstep(int M);
 void rotation(int logslot, int Nh, int shiftcount, const std::vector<std::complex<double>> &vec,
               std::vector<std::complex<double>> &rtnvec);
 
+// common/Remez.cpp's exchange for any target (the reference's Remez::function_value), in binary128:
+// the minimax polynomial sum_j c_j T_j(x / K) of f on the union of [i - 2^-log_width,
+// i + 2^-log_width], |i| < K.  RemezCos / RemezArcsin below are this with their targets.
+std::vector<double> remez_chebyshev(long K, double log_width, long deg, const std::function<__float128(__float128)> &f,
+                                    double log_scan_step_diff = 9.5, int *iterations = nullptr,
+                                    double *spread = nullptr);
+
 // ckks_bootstrapping/RemezCos.h: cos(2 pi (x - 1/4) / scale_factor) (even scale_factor) or
 // sin(2 pi x / scale_factor), approximated on the union of [i - 2^-log_width, i + 2^-log_width],
 // |i| < boundary_K, in Chebyshev polynomials of x / boundary_K.
@@ -90,6 +98,9 @@ public:
     double log_width;
     RemezCos(long boundary_K, double log_width, long deg, long scale_factor);
     void generate_optimal_poly(boot::Polynomial &poly) const;
+    // the minimax Chebyshev coefficients by the Remez exchange (common/Remez.cpp), cached per
+    // parameter set; optionally the iterations and the final relative spread of the alternation
+    std::vector<double> chebyshev_coefficients(int *iterations = nullptr, double *spread = nullptr) const;
     double max_error(const boot::Polynomial &poly) const; // over the intervals (dense scan)
 };
 

@@ -14,7 +14,10 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <functional>
+#include <map>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 
 #include "../../include/mhe.h"
@@ -441,57 +444,524 @@ void Polynomial::homomorphic_poly_evaluation(SEALContext &, CKKSEncoder &, Encry
 } // namespace boot
 
 // ===================================================================== coefficient generation
+// The multi-interval Remez exchange of cnn_ckks/common/Remez.cpp (boot::Remez, used through
+// ckks_bootstrapping/RemezCos.h and RemezArcsin.h), restated in binary128 (__float128): the
+// reference runs it in NTL RR at 1000 bits.  Same initial reference set (better_initialize), the
+// same linear solve with an alternating-sign error column (getcoeffwitherr), the same scan for
+// the error's extrema with its ternary refinement (getextreme_local), the same selection of an
+// alternating set (choosemaxs), iterated until the alternation levels agree.  The binary128 stop
+// is 2^-85 relative spread (the reference's 2^-120 is below binary128's resolution of the error);
+// the resulting polynomial is the same minimax polynomial to far more digits than the doubles the
+// homomorphic evaluation uses.
 namespace
 {
 using f128 = __float128;
-
-// least squares  min |A c - b|_2  by Householder QR in binary128 (A: rows x cols, row-major)
-std::vector<f128> lstsq(std::vector<f128> A, std::vector<f128> b, std::size_t rows, std::size_t cols)
-{
-    for (std::size_t k = 0; k < cols; k++)
-    {
-        f128 norm = 0;
-        for (std::size_t i = k; i < rows; i++) norm += A[i * cols + k] * A[i * cols + k];
-        norm = sqrtq(norm);
-        if (norm == 0) continue;
-        const f128 alpha = A[k * cols + k] > 0 ? -norm : norm;
-        std::vector<f128> v(rows - k);
-        for (std::size_t i = k; i < rows; i++) v[i - k] = A[i * cols + k];
-        v[0] -= alpha;
-        f128 vv = 0;
-        for (auto x : v) vv += x * x;
-        if (vv == 0) continue;
-        for (std::size_t j = k; j < cols; j++)
-        {
-            f128 d = 0;
-            for (std::size_t i = k; i < rows; i++) d += v[i - k] * A[i * cols + j];
-            d = 2 * d / vv;
-            for (std::size_t i = k; i < rows; i++) A[i * cols + j] -= d * v[i - k];
-        }
-        f128 d = 0;
-        for (std::size_t i = k; i < rows; i++) d += v[i - k] * b[i];
-        d = 2 * d / vv;
-        for (std::size_t i = k; i < rows; i++) b[i] -= d * v[i - k];
-    }
-    std::vector<f128> c(cols, 0);
-    for (std::size_t k = cols; k-- > 0;)
-    {
-        f128 s = b[k];
-        for (std::size_t j = k + 1; j < cols; j++) s -= A[k * cols + j] * c[j];
-        c[k] = A[k * cols + k] != 0 ? s / A[k * cols + k] : 0;
-    }
-    return c;
-}
-
-void cheb_row(f128 u, std::size_t deg, f128 *row)
-{
-    row[0] = 1;
-    if (deg >= 1) row[1] = u;
-    for (std::size_t j = 2; j <= deg; j++) row[j] = 2 * u * row[j - 1] - row[j - 2];
-}
-
 const f128 kPi = acosq(-1);
+
+struct RemezPt
+{
+    f128 x = 0, y = 0;
+    long locmm = 0;
+};
+
+// RemezParam.h defaults
+struct RemezParams
+{
+    double log_scan_step_diff = 9.5;
+    long binary_prec = 10;
+    long log_round_prec = 100;
+    double stop_log2 = -85; // binary128 stand-in for log_approx_degree = 120
+    int max_iter = 60;
+};
+
+f128 chebeval(long deg, const std::vector<f128> &c, f128 u)
+{
+    // common/func.cpp:46-58: the three-term recurrence, summed in order
+    f128 t0 = 1, t1 = u, r = c[0] * t0 + (deg >= 1 ? c[1] * t1 : 0);
+    for (long i = 2; i <= deg; i++)
+    {
+        const f128 t2 = 2 * u * t1 - t0;
+        t0 = t1;
+        t1 = t2;
+        r += c[i] * t2;
+    }
+    return r;
+}
+
+f128 fracpart(f128 x)
+{
+    return x - roundq(x); // common/func.cpp:3-5
+}
+
+class RemezExchange
+{
+public:
+    RemezExchange(long K, double log_width, long deg, std::function<f128(f128)> f, RemezParams prm = {})
+        : K_(K), deg_(deg), f_(std::move(f)), prm_(prm), sample_(deg + 2), coeff_(deg + 1)
+    {
+        width_ = powq(2, -(f128)log_width);
+        sc_ = width_ / powq(2, (f128)prm.log_scan_step_diff);
+        log_width_ = log_width;
+    }
+
+    // generate_optimal_poly (Remez.cpp:558-582): coefficients of T_j(x / K)
+    std::vector<f128> run()
+    {
+        better_initialize();
+        iterations = 0;
+        const f128 stop = powq(2, (f128)prm_.stop_log2);
+        f128 prev = -1;
+        while (iterations < prm_.max_iter)
+        {
+            getcoeffwitherr();
+            getextreme();
+            choosemaxs();
+            iterations++;
+            const f128 spread = (max_err - min_err) / min_err;
+            if (spread <= stop) break;
+            if (prev >= 0 && spread >= prev && spread < powq(2, -60)) break; // at binary128's floor
+            prev = spread;
+        }
+        getcoeffwitherr(); // the polynomial of the final reference set
+        return coeff_;
+    }
+
+    f128 max_err = 1000, min_err = 1;
+    int iterations = 0;
+    std::vector<RemezPt> extremes() const { return extreme_; }
+
+private:
+    void better_initialize()
+    {
+        // Remez.cpp:27-93: nodes per interval from the interpolation-error bound of each, then
+        // Chebyshev nodes of every interval
+        const long deg_bdd = deg_ + 2;
+        std::vector<int> nodecount(K_, 1);
+        long tot_deg = 2 * K_ - 1;
+        const double err = std::pow(2.0, -log_width_);
+        std::vector<double> bdd(K_);
+        double temp = 0;
+        for (long i = 1; i <= 2 * K_ - 1; i++) temp -= std::log2((double)i);
+        temp += (2 * K_ - 1) * std::log2(2 * M_PI);
+        temp += std::log2(err);
+        for (long i = 0; i < K_; i++)
+        {
+            bdd[i] = temp;
+            for (long j = 1; j <= K_ - 1 - i; j++) bdd[i] += std::log2((double)j + err);
+            for (long j = 1; j <= K_ - 1 + i; j++) bdd[i] += std::log2((double)j + err);
+        }
+        for (int iter = 0; iter < 200; iter++)
+        {
+            if (tot_deg >= deg_bdd) break;
+            const int maxi = (int)(std::max_element(bdd.begin(), bdd.end()) - bdd.begin());
+            if (maxi != 0)
+            {
+                if (tot_deg + 2 > deg_bdd) break;
+                for (long i = 0; i < K_; i++)
+                {
+                    bdd[i] -= std::log2((double)(tot_deg + 1));
+                    bdd[i] -= std::log2((double)(tot_deg + 2));
+                    bdd[i] += 2.0 * std::log2(2.0 * M_PI);
+                    if (i != maxi)
+                    {
+                        bdd[i] += std::log2(std::abs((double)(i - maxi)) + err);
+                        bdd[i] += std::log2((double)(i + maxi) + err);
+                    }
+                    else
+                    {
+                        bdd[i] += std::log2(err) - 1.0;
+                        bdd[i] += std::log2(2.0 * (double)i + err);
+                    }
+                }
+                tot_deg += 2;
+            }
+            else
+            {
+                bdd[0] -= std::log2((double)(tot_deg + 1));
+                bdd[0] += std::log2(err) - 1.0;
+                bdd[0] += std::log2(2.0 * M_PI);
+                for (long i = 1; i < K_; i++)
+                {
+                    bdd[i] -= std::log2((double)(tot_deg + 1));
+                    bdd[i] += std::log2(2.0 * M_PI);
+                    bdd[i] += std::log2((double)i + err);
+                }
+                tot_deg += 1;
+            }
+            nodecount[maxi] += 1;
+        }
+        if (tot_deg == deg_bdd - 1)
+        {
+            nodecount[0]++;
+            tot_deg++;
+        }
+        int cnt = 0;
+        if (nodecount[0] % 2 != 0) sample_[cnt++].x = 0;
+        for (long i = K_ - 1; i > 0; i--)
+            for (int j = 1; j <= nodecount[i]; j++)
+            {
+                const f128 t = (f128)(2 * j - 1) * kPi / (f128)(2 * nodecount[i]);
+                sample_[cnt++].x = (f128)i + width_ * cosq(t);
+                sample_[cnt++].x = (f128)(-i) - width_ * cosq(t);
+            }
+        for (int j = 1; j <= nodecount[0] / 2; j++)
+        {
+            const f128 t = (f128)(2 * j - 1) * kPi / (f128)(2 * nodecount[0]);
+            sample_[cnt++].x = width_ * cosq(t);
+            sample_[cnt++].x = -width_ * cosq(t);
+        }
+        if (cnt != deg_ + 2) throw std::logic_error("Remez: initial reference set has the wrong size");
+        std::sort(sample_.begin(), sample_.end(), [](const RemezPt &a, const RemezPt &b) { return a.x < b.x; });
+        for (auto &p : sample_) p.y = f_(p.x);
+    }
+
+    void getcoeffwitherr()
+    {
+        // Remez.cpp:178-214: sum_j c_j T_j(x_i / K) + (-1)^(i+1) E = f(x_i), i < deg + 2, by
+        // Gaussian elimination with partial pivoting
+        const long n = deg_ + 2;
+        std::vector<f128> m(n * n), v(n);
+        for (long i = 0; i < n; i++)
+        {
+            const f128 u = sample_[i].x / K_;
+            f128 *row = &m[i * n];
+            row[0] = 1;
+            if (deg_ >= 1) row[1] = u;
+            for (long j = 2; j < deg_ + 1; j++) row[j] = 2 * u * row[j - 1] - row[j - 2];
+            row[deg_ + 1] = 2 * (i % 2) - 1;
+            v[i] = sample_[i].y;
+        }
+        for (long k = 0; k < n; k++)
+        {
+            long piv = k;
+            for (long i = k + 1; i < n; i++)
+                if (fabsq(m[i * n + k]) > fabsq(m[piv * n + k])) piv = i;
+            if (piv != k)
+            {
+                for (long j = 0; j < n; j++) std::swap(m[k * n + j], m[piv * n + j]);
+                std::swap(v[k], v[piv]);
+            }
+            const f128 d = m[k * n + k];
+            if (d == 0) throw std::runtime_error("Remez: singular reference set");
+            for (long i = k + 1; i < n; i++)
+            {
+                const f128 r = m[i * n + k] / d;
+                if (r == 0) continue;
+                for (long j = k; j < n; j++) m[i * n + j] -= r * m[k * n + j];
+                v[i] -= r * v[k];
+            }
+        }
+        for (long k = n; k-- > 0;)
+        {
+            f128 t = v[k];
+            for (long j = k + 1; j < n; j++) t -= m[k * n + j] * v[j];
+            v[k] = t / m[k * n + k];
+        }
+        for (long i = 0; i <= deg_; i++) coeff_[i] = v[i];
+        const f128 sc = powq(2, (f128)prm_.log_round_prec);
+        current_err_ = floorq(sc * fabsq(v[deg_ + 1])) / sc;
+    }
+
+    f128 errf(f128 x) const { return chebeval(deg_, coeff_, x / K_) - f_(x); }
+
+    void getextreme_local(std::vector<RemezPt> &out, long k) const
+    {
+        // Remez.cpp:216-386: scan [k - w, k + w] in steps sc; at every change of the error's
+        // direction (and at the interval ends) refine the extremum by binary_prec ternary steps;
+        // keep it when |error| reaches the current level
+        long inc_1 = 0, inc_2 = 0, tmpinc;
+        f128 scan_1, scan_2 = (f128)k - width_;
+        f128 scan_y1, scan_y2 = errf(scan_2);
+        f128 detail[3], prec_sc, prec_ext = 0, prec_x, tmp;
+        long prec_iter, prec_ind, tmp_inc;
+        bool prec_end;
+        out.clear();
+        while (scan_2 < (f128)k + width_ + sc_)
+        {
+            scan_1 = scan_2;
+            scan_2 = scan_1 + sc_;
+            if (fracpart(scan_2) > width_ + sc_ / 2)
+            {
+                // past the right end: the last point's side of the interval end
+                scan_1 = roundq(scan_1) + width_;
+                scan_2 = roundq(scan_2) + 1 - width_;
+                scan_y1 = errf(scan_1);
+                scan_y2 = errf(scan_2);
+                prec_end = false;
+                prec_x = scan_1 - sc_;
+                while (!prec_end)
+                {
+                    prec_sc = (scan_1 - prec_x) / 2;
+                    prec_end = true;
+                    for (int j = 0; j < 3; j++) detail[j] = scan_1 - 2 * prec_sc + prec_sc * j;
+                    prec_iter = 0;
+                    while (prec_iter < prm_.binary_prec)
+                    {
+                        prec_ext = errf(detail[0]);
+                        prec_ind = 0;
+                        for (int j = 1; j < 3; j++)
+                        {
+                            tmp = errf(detail[j]);
+                            if ((inc_2 == 1 && prec_ext < tmp) || (inc_2 == -1 && prec_ext > tmp))
+                            {
+                                prec_ext = tmp;
+                                prec_ind = j;
+                            }
+                        }
+                        if (prec_ind != 2) prec_end = false;
+                        prec_x = detail[prec_ind];
+                        prec_sc = prec_sc / 2;
+                        for (int j = 0; j < 3; j++)
+                            detail[j] = (prec_x + prec_sc < scan_1 ? prec_x + prec_sc : scan_1) - 2 * prec_sc + prec_sc * j;
+                        prec_iter++;
+                    }
+                    tmpinc = inc_2 == 1 ? 1 : -1;
+                    if (tmpinc * prec_ext >= current_err_)
+                    {
+                        RemezPt p;
+                        p.x = prec_x;
+                        p.y = prec_ext;
+                        p.locmm = inc_2 == 1 ? 1 : -1;
+                        out.push_back(p);
+                    }
+                    if (!prec_end) inc_2 = -inc_2;
+                }
+                inc_2 = 0;
+            }
+            else
+            {
+                inc_1 = inc_2;
+                scan_y1 = scan_y2;
+                scan_y2 = errf(scan_2);
+                if (scan_y1 < scan_y2)
+                    inc_2 = 1;
+                else if (scan_y1 > scan_y2)
+                    inc_2 = -1;
+                else
+                    inc_2 = 0;
+                if ((inc_1 == 1 && inc_2 != 1) || (inc_1 == -1 && inc_2 != -1) || inc_1 == 0)
+                {
+                    prec_end = false;
+                    tmp_inc = inc_2;
+                    prec_x = scan_2;
+                    while (!prec_end)
+                    {
+                        prec_sc = (prec_x - scan_1) / 2;
+                        prec_end = true;
+                        for (int j = 0; j < 3; j++)
+                            detail[j] = inc_1 != 0 ? scan_1 - prec_sc + prec_sc * j : scan_1 + prec_sc * j;
+                        prec_iter = 0;
+                        while (prec_iter < prm_.binary_prec)
+                        {
+                            prec_ext = errf(detail[0]);
+                            prec_ind = 0;
+                            for (int j = 1; j < 3; j++)
+                            {
+                                tmp = errf(detail[j]);
+                                if ((inc_1 == 1 && prec_ext < tmp) || (inc_1 == -1 && prec_ext > tmp))
+                                {
+                                    prec_ext = tmp;
+                                    prec_ind = j;
+                                }
+                                else if (inc_1 == 0)
+                                {
+                                    if ((inc_2 == 1 && prec_ext > tmp) || (inc_2 == -1 && prec_ext < tmp))
+                                    {
+                                        prec_ext = tmp;
+                                        prec_ind = j;
+                                    }
+                                }
+                            }
+                            if (inc_1 == 0 && prec_ind != 0) prec_end = false;
+                            prec_x = detail[prec_ind];
+                            prec_sc = prec_sc / 2;
+                            for (int j = 0; j < 3; j++)
+                            {
+                                if (inc_1 == 0)
+                                    detail[j] = (prec_x - prec_sc > scan_1 ? prec_x - prec_sc : scan_1) + prec_sc * j;
+                                else
+                                    detail[j] = prec_x - prec_sc + prec_sc * j;
+                            }
+                            prec_iter++;
+                        }
+                        tmpinc = inc_2 == 1 ? -1 : 1;
+                        if (tmpinc * prec_ext >= current_err_)
+                        {
+                            RemezPt p;
+                            p.x = prec_x;
+                            p.y = prec_ext;
+                            p.locmm = inc_2 == 1 ? -1 : 1;
+                            out.push_back(p);
+                        }
+                        if (!prec_end) inc_2 = -inc_2;
+                    }
+                    inc_2 = tmp_inc;
+                }
+            }
+        }
+    }
+
+    void getextreme()
+    {
+        // Remez.cpp:388-430: every interval scanned on its own thread, then merged in x order
+        const long nint = 2 * K_ - 1;
+        std::vector<std::vector<RemezPt>> local(nint);
+        std::vector<std::thread> thr;
+        const long nt = std::max(1L, std::min<long>(nint, (long)std::thread::hardware_concurrency()));
+        for (long t = 0; t < nt; t++)
+            thr.emplace_back([&, t] {
+                for (long i = t; i < nint; i += nt) getextreme_local(local[i], i - K_ + 1);
+            });
+        for (auto &t : thr) t.join();
+        extreme_.clear();
+        for (auto &v : local) extreme_.insert(extreme_.end(), v.begin(), v.end());
+        max_err = 0;
+        for (auto &p : extreme_)
+            if (max_err < fabsq(p.y)) max_err = fabsq(p.y);
+        std::sort(extreme_.begin(), extreme_.end(), [](const RemezPt &a, const RemezPt &b) { return a.x < b.x; });
+    }
+
+    void choosemaxs()
+    {
+        // Remez.cpp:432-556: one point (the largest |error|) per run of equal sign, then drop
+        // the smallest neighbouring pairs (or an end point) until deg + 2 alternating points remain
+        const long ec = (long)extreme_.size();
+        if (ec < deg_ + 2) throw std::runtime_error("Remez: too few extrema");
+        std::vector<RemezPt> extract;
+        max_err = 0;
+        min_err = 1000;
+        std::vector<long> run;
+        auto flush = [&] {
+            f128 best = 0;
+            long bi = run[0];
+            for (long i : run)
+                if (best < fabsq(extreme_[i].y))
+                {
+                    best = fabsq(extreme_[i].y);
+                    bi = i;
+                }
+            extract.push_back(extreme_[bi]);
+            run.clear();
+        };
+        long ind = 0;
+        while (ind < ec)
+        {
+            if (run.empty() || extreme_[ind].locmm * extreme_[ind - 1].locmm == 1)
+                run.push_back(ind++);
+            else
+                flush();
+        }
+        flush();
+        long count = (long)extract.size();
+        auto erase_at = [&](long i, long k) {
+            extract.erase(extract.begin() + i, extract.begin() + i + k);
+            count -= k;
+        };
+        while (count > deg_ + 2)
+        {
+            f128 minsum = 100000;
+            long minindex = 0;
+            if (count == deg_ + 3)
+            {
+                if (fabsq(extract[0].y) > fabsq(extract[count - 1].y))
+                    erase_at(count - 1, 1);
+                else
+                    erase_at(0, 1);
+            }
+            else if (count == deg_ + 4)
+            {
+                for (long i = 0; i < count; i++)
+                {
+                    const f128 s2 = fabsq(extract[i].y) + fabsq(extract[(i + 1) % count].y);
+                    if (minsum > s2)
+                    {
+                        minsum = s2;
+                        minindex = i;
+                    }
+                }
+                if (minindex == count - 1)
+                {
+                    // the pair (last, first): drop the first and the last
+                    extract.erase(extract.begin());
+                    extract.pop_back();
+                    count -= 2;
+                }
+                else
+                    erase_at(minindex, 2);
+            }
+            else
+            {
+                for (long i = 0; i < count - 1; i++)
+                {
+                    const f128 s2 = fabsq(extract[i].y) + fabsq(extract[i + 1].y);
+                    if (minsum > s2)
+                    {
+                        minsum = s2;
+                        minindex = i;
+                    }
+                }
+                if (minindex == 0)
+                    erase_at(0, 1);
+                else if (minindex == count - 2)
+                    erase_at(count - 1, 1);
+                else
+                    erase_at(minindex, 2);
+            }
+        }
+        for (long i = 0; i < deg_ + 2; i++)
+        {
+            sample_[i].x = extract[i].x;
+            sample_[i].y = f_(sample_[i].x);
+            if (max_err < fabsq(extract[i].y)) max_err = fabsq(extract[i].y);
+            if (min_err > fabsq(extract[i].y)) min_err = fabsq(extract[i].y);
+        }
+    }
+
+    long K_, deg_;
+    std::function<f128(f128)> f_;
+    RemezParams prm_;
+    f128 width_, sc_, current_err_ = 0;
+    double log_width_;
+    std::vector<RemezPt> sample_, extreme_;
+    std::vector<f128> coeff_;
+};
+
+// arcsin by Newton on sin (common/func.cpp:19-26), to binary128 precision
+f128 arcsin_newton(f128 x)
+{
+    f128 r = x;
+    for (int i = 0; i < 200 && fabsq(sinq(r) - x) > powq(2, -110); i++) r = r - (sinq(r) - x) / cosq(r);
+    return r;
+}
+
+// one generated polynomial per parameter set (three bootstrappers share the ResNet's)
+std::mutex g_remez_mu;
+std::map<std::string, std::vector<double>> g_remez_cache;
+
+std::vector<double> remez_cached(const std::string &key, const std::function<std::vector<double>()> &make)
+{
+    std::lock_guard<std::mutex> g(g_remez_mu);
+    auto it = g_remez_cache.find(key);
+    if (it != g_remez_cache.end()) return it->second;
+    auto v = make();
+    g_remez_cache[key] = v;
+    return v;
+}
 } // namespace
+
+std::vector<double> remez_chebyshev(long K, double log_width, long deg, const std::function<f128(f128)> &f,
+                                    double log_scan_step_diff, int *iterations, double *spread)
+{
+    RemezParams prm;
+    prm.log_scan_step_diff = log_scan_step_diff;
+    RemezExchange r(K, log_width, deg, f, prm);
+    auto cq = r.run();
+    if (iterations) *iterations = r.iterations;
+    if (spread) *spread = (double)((r.max_err - r.min_err) / r.min_err);
+    std::vector<double> out(cq.size());
+    for (std::size_t j = 0; j < cq.size(); j++) out[j] = (double)cq[j];
+    return out;
+}
 
 RemezCos::RemezCos(long K, double lw, long d, long sf) : boundary_K(K), deg(d), scale_factor(sf), log_width(lw) {}
 
@@ -502,27 +972,25 @@ static f128 cos_target(f128 x, long scale_factor)
     return sinq(2 * kPi * x / scale_factor);
 }
 
+std::vector<double> RemezCos::chebyshev_coefficients(int *iterations, double *spread) const
+{
+    // Remez(boundary_K, log_width, deg) with RemezCos::function_value (RemezCos.h)
+    const std::string key = "cos " + std::to_string(boundary_K) + " " + std::to_string(log_width) + " " +
+                            std::to_string(deg) + " " + std::to_string(scale_factor);
+    int it = 0;
+    double sp = 0;
+    auto c = remez_cached(key, [&] {
+        const long sf = scale_factor;
+        return remez_chebyshev(boundary_K, log_width, deg, [sf](f128 x) { return cos_target(x, sf); }, 9.5, &it, &sp);
+    });
+    if (iterations) *iterations = it;
+    if (spread) *spread = sp;
+    return c;
+}
+
 void RemezCos::generate_optimal_poly(boot::Polynomial &poly) const
 {
-    // Target set of Remez::initialize (common/Remez.cpp:95-175): the intervals
-    // [i - w, i + w], |i| <= K-1, w = 2^-log_width; basis T_j(x / K).  Least squares on
-    // Chebyshev nodes of every interval, in binary128.
-    const int M = 10;
-    const f128 w = powq(2, -(f128)log_width);
-    std::vector<f128> xs;
-    for (long i = -(boundary_K - 1); i <= boundary_K - 1; i++)
-        for (int j = 0; j < M; j++) xs.push_back((f128)i + w * cosq((2 * j + 1) * kPi / (2 * M)));
-    const std::size_t rows = xs.size(), cols = deg + 1;
-    std::vector<f128> A(rows * cols), b(rows);
-    for (std::size_t r = 0; r < rows; r++)
-    {
-        cheb_row(xs[r] / boundary_K, deg, &A[r * cols]);
-        b[r] = cos_target(xs[r], scale_factor);
-    }
-    auto c = lstsq(std::move(A), std::move(b), rows, cols);
-    std::vector<double> cheb(cols);
-    for (std::size_t j = 0; j < cols; j++) cheb[j] = (double)c[j];
-    poly.set_chebyshev(cheb);
+    poly.set_chebyshev(chebyshev_coefficients());
 }
 
 double RemezCos::max_error(const boot::Polynomial &poly) const
@@ -542,43 +1010,13 @@ RemezArcsin::RemezArcsin(double lw, long d) : log_width(lw), deg(d) {}
 
 void RemezArcsin::generate_optimal_poly(boot::Polynomial &poly) const
 {
-    // RemezArcsin.h: arcsin(x) / (2 pi) on [-a, a], a = 2^-log_width (boundary_K = 1)
-    const f128 a = powq(2, -(f128)log_width);
-    auto g = [](f128 x) { return asinq(x) / (2 * kPi); };
-    if (deg == 1)
-    {
-        // odd linear minimax c x: equioscillation between x1 (g'(x1) = c) and a:
-        // c x1 - g(x1) = g(a) - c a, solved by bisection on c in [g(a)/a, 1/(2 pi)]... ordered
-        f128 lo = 1 / (2 * kPi), hi = g(a) / a;
-        if (lo > hi) std::swap(lo, hi);
-        for (int it = 0; it < 200; it++)
-        {
-            const f128 c = (lo + hi) / 2;
-            const f128 s = 1 / (2 * kPi * c);
-            const f128 x1 = sqrtq(1 - s * s);
-            const f128 F = c * (x1 + a) - g(x1) - g(a);
-            if (F > 0)
-                hi = c;
-            else
-                lo = c;
-        }
-        const double c1 = (double)((lo + hi) / 2);
-        poly.set_chebyshev({ 0.0, c1 });
-        return;
-    }
-    const int rows = 8 * (int)(deg + 1);
-    const std::size_t cols = deg + 1;
-    std::vector<f128> A(rows * cols), b(rows);
-    for (int r = 0; r < rows; r++)
-    {
-        const f128 x = a * cosq((2 * r + 1) * kPi / (2 * rows));
-        cheb_row(x, deg, &A[r * cols]);
-        b[r] = g(x);
-    }
-    auto c = lstsq(std::move(A), std::move(b), rows, cols);
-    std::vector<double> cheb(cols);
-    for (std::size_t j = 0; j < cols; j++) cheb[j] = (double)c[j];
-    poly.set_chebyshev(cheb);
+    // Remez(1, log_width, deg) with RemezArcsin::function_value = arcsin(x) / (2 pi)
+    // (RemezArcsin.h; ModularReducer.cpp:12-17 sets log_scan_step_diff 12 for it)
+    const std::string key = "asin " + std::to_string(log_width) + " " + std::to_string(deg);
+    auto c = remez_cached(key, [&] {
+        return remez_chebyshev(1, log_width, deg, [](f128 x) { return arcsin_newton(x) / (2 * kPi); }, 12);
+    });
+    poly.set_chebyshev(c);
 }
 
 // =========================================================================== ModularReducer

@@ -702,3 +702,45 @@ def test_ckks_decode_c2_full(c2):
     got = ch.eng.decode(ch.up(pt), 2.0 ** 46)
     assert np.array_equal(got, ch.oc.decode(pt, 2.0 ** 46))
     assert np.abs(got - v).max() < 1e-6
+
+
+# ------------------------------------------------------ extreme residues (FP64 bounds)
+@pytest.mark.parametrize("bits", [[51] * 8, [51, 46, 46, 51, 46, 51, 51, 51]], ids=["all51", "mixed"])
+@pytest.mark.parametrize("fill", ["max", "zero", "alternating", "sparse_max"])
+def test_extreme_residues_bit_exact(bits, fill):
+    """The exact-FP64 paths (fparith.h: the lazy butterflies, the key MAC, the ModDown / rescale
+    lifts and epilogues, the 2^52-offset conversions) at their bounds: every residue q-1, every
+    residue 0, alternating 0 / q-1, and mostly-0 with q-1 spikes -- in the ciphertexts, the target
+    and the key -- on chains whose primes sit just below 2^51.  HMult, switch_key, rotation and
+    rescale must equal the oracle word for word."""
+    ch = Chain(12, bits, seed=99)
+    L, n, K = ch.K - 1, ch.n, ch.K
+    q = np.array(ch.moduli, np.uint64)
+
+    def filled(shape, limbs):
+        out = np.empty(shape, np.uint64)
+        for l in range(limbs):
+            qm1 = np.uint64(int(q[l]) - 1)
+            if fill == "max":
+                v = np.full(shape[:-2] + (n,), qm1)
+            elif fill == "zero":
+                v = np.zeros(shape[:-2] + (n,), np.uint64)
+            elif fill == "alternating":
+                v = np.where(np.arange(n) % 2 == 0, qm1, np.uint64(0)) * np.ones(shape[:-2] + (1,), np.uint64)
+            else:
+                v = np.where(ch.rng.random(shape[:-2] + (n,)) < 0.01, qm1, np.uint64(0)).astype(np.uint64)
+            out[..., l, :] = v
+        return out
+
+    a, b = filled((2, L, n), L), filled((2, L, n), L)
+    key = np.empty((L, 2, K, n), np.uint64)
+    for l in range(K):
+        key[:, :, l, :] = np.uint64(int(q[l]) - 1) if fill != "zero" else np.uint64(0)
+    dkey = ch.up(key)
+    assert np.array_equal(ch.down(ch.eng.hmult(ch.up(a), ch.up(b), dkey)), ch.oc.hmult(a, b, key))
+    tgt = filled((L, n), L)
+    assert np.array_equal(ch.down(ch.eng.switch_key(ch.up(a), ch.up(tgt), dkey)), ch.oc.switch_key(a, tgt, key))
+    elt = mhe.galois_elt_from_step(ch.log_n, 3)
+    assert np.array_equal(ch.down(ch.eng.apply_galois_to(ch.up(a), elt, dkey)), ch.oc.apply_galois(a, elt, key))
+    assert np.array_equal(ch.down(ch.eng.rescale_to_next(ch.up(a))), ch.oc.rescale(a))
+    assert np.array_equal(ch.down(ch.eng.ntt_forward(ch.up(a))), ch.oc.ntt(a, O.NTT_FWD))
