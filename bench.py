@@ -55,6 +55,20 @@ def ks_row_mac_key_bytes(L, n, moduli=None, prepared=False):
     return sum(2 * L * n * (6 if q < (1 << 48) else 8) for q in primes)
 
 
+FP64_LANE_OPS_PEAK = 35e12  # v_fma_f64 lane-ops/s measured on MI355X (profiles/r01_ubench_valu.txt; spec 39.3e12)
+
+
+def ks_row_mac_valu(L, n, moduli):
+    """VALU model of one k_ks_row_mac launch (SURVEY.md §8(d) per-op work): the ModUp row pass of
+    the L^2 digit/prime pairs with I != J (8 of the 16 stages: L^2 * 8 * n/2 butterflies) and the
+    key inner products (2 * L * (L+1) * n multiply-accumulates).  FP64 lane-ops per butterfly: 8
+    (lazy form, q < 2^47) or 11; per MAC: 8 (the FP64 mulmod, its add, the key's conversion)."""
+    primes = list(moduli[:L]) + [moduli[-1]]
+    bfly = sum((L - (1 if I < L else 0)) * 8 * (n // 2) * (8 if q < (1 << 47) else 11) for I, q in enumerate(primes))
+    macs = 2 * L * (L + 1) * n
+    return {"butterflies": L * L * 8 * (n // 2), "macs": macs, "fp64_lane_ops": bfly + 8 * macs}
+
+
 def rand_residues(shape, moduli_t, gen):
     """Uniform residues on device: last two dims [limbs][n], limb l uniform in [0, q_l)."""
     hi = torch.randint(0, 2**62, shape, generator=gen, device=moduli_t.device, dtype=torch.int64)
@@ -405,6 +419,16 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
 
+    # SQ counters of the same workload (rocprofv3 --pmc SQ_INSTS_VALU ..., scripts/gpu_pmc.sh)
+    sq_valu, sq_src = None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sq_counters.json"))):
+        try:
+            t = json.load(open(f))
+            if t.get("limbs", L) == L and "k_ks_row_mac" in t.get("SQ_INSTS_VALU", {}):
+                sq_valu, sq_src = t["SQ_INSTS_VALU"]["k_ks_row_mac"], os.path.relpath(f, ROOT)
+        except (OSError, ValueError, KeyError):
+            pass
+
     hmults_per_gpu = B * args.steps
     value = world * hmults_per_gpu / elapsed
     per_hmult_s = gpu_s / hmults_per_gpu  # HIP-event time per HMult (batch over its streams)
@@ -454,6 +478,22 @@ def main():
             "launches_timed": km_n.value,
             "timing": "HIP events around each launch on its stream; single-stream pass when --streams > 1",
         },
+        # the same kernel against the FP64 VALU issue rate ("also report the int-VALU
+        # bound"; the engine's modular arithmetic runs on the FP64 pipe, csrc/fparith.h)
+        "valu_roofline": (lambda v: {
+            "bound": "valu",
+            "kernel": "k_ks_row_mac",
+            "model": "L^2*8*n/2 butterflies x 8 (q<2^47) or 11 FP64 lane-ops + 2L(L+1)n MACs x 8",
+            **v,
+            "peak_lane_ops_per_s": FP64_LANE_OPS_PEAK,
+            "peak_source": "v_fma_f64 microbenchmark, profiles/r01_ubench_valu.txt (spec 39.3e12)",
+            "floor_us": round(v["fp64_lane_ops"] / FP64_LANE_OPS_PEAK * 1e6, 2),
+            "frac": round(v["fp64_lane_ops"] / FP64_LANE_OPS_PEAK / (km_avg_us * 1e-6), 4) if km_avg_us > 0 else None,
+            "sq_insts_valu_per_launch": sq_valu,
+            "issued_lane_ops_frac": (round(sq_valu * 64 / FP64_LANE_OPS_PEAK / (km_avg_us * 1e-6), 4)
+                                     if sq_valu and km_avg_us > 0 else None),
+            "sq_source": sq_src,
+        })(ks_row_mac_valu(L, n, moduli)),
         "hmult_roofline": {
             "bound": "hbm",
             "unit_of_work": "one HMult (tensor + key switch + rescale kernel sequence)",

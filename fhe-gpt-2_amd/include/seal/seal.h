@@ -21,6 +21,7 @@
 //  * serialization (save/load) is not provided yet.
 #pragma once
 
+#include <algorithm>
 #include <array>
 #include <complex>
 #include <cstddef>
@@ -31,6 +32,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <sstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -138,6 +140,10 @@ enum class prng_type : std::uint8_t
     blake2xb = 1,
     shake256 = 2
 };
+
+// (not SEAL API) the PRNG seeds a Serializable<T> writes in place of the second polynomial of its
+// symmetric encryptions: key index -> one seed per digit (a ciphertext or public key: index 0)
+using SeedMap = std::map<std::size_t, std::vector<prng_seed_type>>;
 
 // randomgen.cpp:23-50: bytes from the kernel CSPRNG (getrandom)
 void random_bytes(seal_byte *buf, std::size_t count);
@@ -388,6 +394,10 @@ public:
     std::streamoff load(const SEALContext &context, std::istream &stream);
     std::streamoff load(const SEALContext &context, const seal_byte *in, std::size_t size);
     std::streamoff unsafe_load(const SEALContext &context, std::istream &stream) { return load(context, stream); }
+    // (not SEAL API; Serializable) the seeded form when seeds[0] holds c1's seed: c0 only, then the
+    // UniformRandomGeneratorInfo (ciphertext.cpp:148-239); load() expands it
+    std::streamoff save_size_seeded(const SeedMap &seeds, compr_mode_type compr_mode) const;
+    std::streamoff save_seeded(std::ostream &stream, const SeedMap &seeds, compr_mode_type compr_mode) const;
 
     // engine plumbing
     PolyStore &store() noexcept { return store_; }
@@ -459,6 +469,15 @@ public:
         return pk_.save(stream, m);
     }
     std::streamoff load(const SEALContext &context, std::istream &stream) { return pk_.load(context, stream); }
+    std::streamoff save_size(compr_mode_type m = Serialization::compr_mode_default) const { return pk_.save_size(m); }
+    std::streamoff save_size_seeded(const SeedMap &seeds, compr_mode_type m) const
+    {
+        return pk_.save_size_seeded(seeds, m);
+    }
+    std::streamoff save_seeded(std::ostream &stream, const SeedMap &seeds, compr_mode_type m) const
+    {
+        return pk_.save_seeded(stream, seeds, m);
+    }
 
 private:
     Ciphertext pk_;
@@ -508,6 +527,9 @@ public:
     std::streamoff save_size(compr_mode_type compr_mode = Serialization::compr_mode_default) const;
     std::streamoff save(std::ostream &stream, compr_mode_type compr_mode = Serialization::compr_mode_default) const;
     std::streamoff load(const SEALContext &context, std::istream &stream);
+    // (not SEAL API; Serializable) every PublicKey record whose index has seeds written seeded
+    std::streamoff save_size_seeded(const SeedMap &seeds, compr_mode_type compr_mode) const;
+    std::streamoff save_seeded(std::ostream &stream, const SeedMap &seeds, compr_mode_type compr_mode) const;
 
 private:
     mutable std::map<std::size_t, PolyStore> keys_;
@@ -532,6 +554,44 @@ public:
     bool has_key(std::uint32_t galois_elt) const { return has_index(get_index(galois_elt)); }
 };
 
+// Serializable<T> (SEAL/serializable.h): what SEAL's seeded creators return -- create_public_key(),
+// create_relin_keys(), create_galois_keys(...), Encryptor::encrypt_symmetric(plain) /
+// encrypt_zero_symmetric() -- an object that can only be saved.  The second polynomial of every
+// symmetric encryption of zero inside it is written as the seed of the Blake2xb PRNG that drew it
+// (SEAL: seed marker in c1, ciphertext.cpp:183-239), halving the bytes; T::load expands the seed into
+// the same words (ciphertext.cpp:305-335).  encrypt(plain) carries no seed and saves in full.
+template <class T>
+class Serializable
+{
+public:
+    std::streamoff save_size(compr_mode_type compr_mode = Serialization::compr_mode_default) const
+    {
+        return obj_.save_size_seeded(seeds_, compr_mode);
+    }
+    std::streamoff save(std::ostream &stream, compr_mode_type compr_mode = Serialization::compr_mode_default) const
+    {
+        return obj_.save_seeded(stream, seeds_, compr_mode);
+    }
+    std::streamoff save(seal_byte *out, std::size_t size,
+                        compr_mode_type compr_mode = Serialization::compr_mode_default) const
+    {
+        const std::streamoff need = save_size(compr_mode);
+        if (!out || (std::streamoff)size < need) throw std::invalid_argument("insufficient size");
+        std::ostringstream ss(std::ios::binary);
+        save(ss, compr_mode);
+        const std::string b = ss.str();
+        std::copy(b.begin(), b.end(), reinterpret_cast<char *>(out));
+        return (std::streamoff)b.size();
+    }
+
+private:
+    friend class KeyGenerator;
+    friend class Encryptor;
+    Serializable(T obj, SeedMap seeds) : obj_(std::move(obj)), seeds_(std::move(seeds)) {}
+    T obj_;
+    SeedMap seeds_;
+};
+
 class KeyGenerator
 {
 public:
@@ -539,10 +599,14 @@ public:
     KeyGenerator(const SEALContext &context, const SecretKey &secret_key);
     const SecretKey &secret_key() const { return sk_; }
     void create_public_key(PublicKey &destination);
-    PublicKey create_public_key();
+    // keygenerator.h:83-135, 250-310: the seeded forms, only for saving
+    Serializable<PublicKey> create_public_key();
     void create_relin_keys(RelinKeys &destination);
+    Serializable<RelinKeys> create_relin_keys();
     void create_galois_keys(const std::vector<int> &steps, GaloisKeys &destination);
+    Serializable<GaloisKeys> create_galois_keys(const std::vector<int> &steps);
     void create_galois_keys(GaloisKeys &destination);
+    Serializable<GaloisKeys> create_galois_keys();
     void create_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination);
     // (not SEAL API) SEAL's Galois keys truncated per element to the ciphertext level (limbs) it
     // will be used at: digits min(limbs, K-1), primes q_0..q_{digits-1} and P (see KSwitchKeys)
@@ -557,7 +621,11 @@ public:
     const GaloisKeys &power_of_two_keys();
 
 private:
-    void kswitch_key(const std::uint64_t *new_key_dev, PolyStore &dest, std::size_t digits);
+    // seeds (optional) receives each digit's public seed (the PRNG seed of its c1)
+    void kswitch_key(const std::uint64_t *new_key_dev, PolyStore &dest, std::size_t digits,
+                     std::vector<prng_seed_type> *seeds = nullptr);
+    void relin_keys_into(RelinKeys &destination, SeedMap *seeds);
+    void galois_keys_into(const std::vector<std::uint32_t> &elts, GaloisKeys &destination, SeedMap *seeds);
     SEALContext ctx_;
     SecretKey sk_;
     std::shared_ptr<UniformRandomGeneratorFactory> rng_;
@@ -601,16 +669,35 @@ class Encryptor
 public:
     Encryptor(const SEALContext &context, const PublicKey &public_key);
     Encryptor(const SEALContext &context, const SecretKey &secret_key);
+    Encryptor(const SEALContext &context, const PublicKey &public_key, const SecretKey &secret_key);
+    void set_public_key(const PublicKey &public_key);
+    void set_secret_key(const SecretKey &secret_key);
+    // encryptor.h:130-420: encrypt / encrypt_zero use the public key when one is set (else the
+    // secret key, as this library's secret-key-only Encryptor always has); the *_symmetric forms
+    // use the secret key; the Serializable forms are for saving (seeded when symmetric)
     void encrypt(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    Serializable<Ciphertext> encrypt(const Plaintext &plain, MemoryPoolHandle = {}) const;
     void encrypt_zero(Ciphertext &destination, MemoryPoolHandle = {}) const;
     void encrypt_zero(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void encrypt_symmetric(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    Serializable<Ciphertext> encrypt_symmetric(const Plaintext &plain, MemoryPoolHandle = {}) const;
+    void encrypt_zero_symmetric(Ciphertext &destination, MemoryPoolHandle = {}) const;
+    void encrypt_zero_symmetric(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle = {}) const;
+    Serializable<Ciphertext> encrypt_zero_symmetric(MemoryPoolHandle = {}) const;
+    Serializable<Ciphertext> encrypt_zero_symmetric(parms_id_type parms_id, MemoryPoolHandle = {}) const;
 
 private:
-    void encrypt_zero_at(std::size_t limbs, Ciphertext &dest) const;
+    // symmetric: secret key; public_seed (symmetric only) receives c1's PRNG seed
+    void encrypt_zero_at(std::size_t limbs, Ciphertext &dest, bool symmetric,
+                         prng_seed_type *public_seed = nullptr) const;
+    void encrypt_plain(const Plaintext &plain, Ciphertext &destination, bool symmetric,
+                       prng_seed_type *public_seed) const;
+    void zero_at(parms_id_type parms_id, Ciphertext &destination, bool symmetric, prng_seed_type *public_seed) const;
     SEALContext ctx_;
     PublicKey pk_;
     SecretKey sk_;
     bool asymmetric_;
+    bool has_sk_ = false;
     std::shared_ptr<UniformRandomGeneratorFactory> rng_;
 };
 
@@ -686,6 +773,15 @@ public:
                         const GaloisKeys &galois_keys, const std::vector<Ciphertext *> &destinations) const;
     // (not SEAL API) rescale_to_next_inplace of independent ciphertexts in batched launches
     void rescale_to_next_inplace_many(const std::vector<Ciphertext *> &encrypted) const;
+    // (not SEAL API) relinearize_inplace of independent size-3 ciphertexts: entries of one level run
+    // their key switches as one batched launch (mhe_switch_key_batch), bit-identical
+    void relinearize_inplace_many(const std::vector<Ciphertext *> &encrypted, const RelinKeys &relin_keys) const;
+    // (not SEAL API) *destinations[i] = multiply_reduced_error(*encrypted1[i], *encrypted2[i]) for
+    // every i, the relinearizations batched (relinearize_inplace_many); destinations distinct and
+    // none of them an input
+    void multiply_reduced_error_many(const std::vector<const Ciphertext *> &encrypted1,
+                                     const std::vector<const Ciphertext *> &encrypted2, const RelinKeys &relin_keys,
+                                     const std::vector<Ciphertext *> &destinations) const;
     void complex_conjugate_inplace(Ciphertext &encrypted, const GaloisKeys &galois_keys, MemoryPoolHandle = {}) const;
     void complex_conjugate(const Ciphertext &encrypted, const GaloisKeys &galois_keys, Ciphertext &destination,
                            MemoryPoolHandle = {}) const;

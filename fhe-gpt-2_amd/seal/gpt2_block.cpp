@@ -16,8 +16,11 @@
 // outside the matrices contribute zeros and are skipped.
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <map>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 
 #include "mhe_gpt2.h"
 
@@ -45,16 +48,7 @@ struct Ops
     RelinKeys &relin_keys;
 };
 
-// the value at slot `src` (times `value`) moved to slot `dst`: one masked product, one rotation
-void place_one(Ciphertext &folded, int src, int dst, double value, Ciphertext &out, Ops &o)
-{
-    std::vector<double> m(kSlots, 0.0);
-    m[src] = value;
-    o.evaluator.multiply_vector_reduced_error(folded, m, out);
-    o.evaluator.rescale_to_next_inplace(out);
-    const int k = wrap((long)src - dst);
-    if (k) o.evaluator.rotate_vector_inplace(out, k, o.gal_keys);
-}
+constexpr std::size_t kBatch = 8; // independent ciphertexts per batched launch (MHE_MAXB)
 
 struct Accum
 {
@@ -83,8 +77,158 @@ void fold_sum(Ciphertext &x, int by, int window, Ciphertext &out, Ops &o)
     quickSum(rolled, out, window, o.encoder, o.encryptor, o.decryptor, o.evaluator, o.gal_keys, o.relin_keys);
 }
 
+// fold_sum(x, by, window) of every x in xs in place, each step's rotations in one batched launch
+// (Evaluator::rotate_vectors): the same rotate / add sequence as fold_sum + quickSum (Fold.cpp:20-45)
+void fold_many(std::vector<Ciphertext> &xs, int by, int window, Ops &o)
+{
+    const std::size_t B = xs.size();
+    if (!B) return;
+    std::vector<Ciphertext> tmp(B);
+    std::vector<const Ciphertext *> in(B);
+    std::vector<Ciphertext *> out(B);
+    for (std::size_t b = 0; b < B; b++)
+    {
+        in[b] = &xs[b];
+        out[b] = &tmp[b];
+    }
+    auto step = [&](int s) {
+        o.evaluator.rotate_vectors(in, std::vector<int>(B, s), o.gal_keys, out);
+        for (std::size_t b = 0; b < B; b++) o.evaluator.add_inplace_reduced_error(xs[b], tmp[b]);
+    };
+    step(kSlots - by);
+    for (int s = 1; s < window; s *= 2) step(s);
+}
+
+// Output placement of folded products.  After fold_many(x, w, w) the dot product of a row whose
+// window starts at slot w0 sits at EVERY slot of [w0, w0 + w), so an element bound for slot `dst`
+// of output ciphertext t is read at src = w0 + ((dst - w0) mod w): its rotation k = src - dst is a
+// multiple of w.  Elements sharing (t, k) are masked into one accumulator (one fused
+// multiply_plain + add per folded ciphertext and group) and rotated once at the end, since rotation
+// is linear -- instead of one mask, rescale and rotation per element (MatrixMul.cpp:160-180).
+struct Placer
+{
+    Ops &o;
+    explicit Placer(Ops &ops) : o(ops) {}
+    std::map<std::tuple<int, int, std::size_t>, Ciphertext> groups; // (output, rotation, limbs)
+    std::map<std::pair<int, int>, std::vector<std::pair<int, double>>> staged;
+    Plaintext scratch;
+
+    void element(int w0, int width, int t, int dst, double factor)
+    {
+        const int off = (int)((((long)dst - w0) % width + width) % width), src = w0 + off;
+        staged[{ t, wrap((long)src - dst) }].push_back({ src, factor });
+    }
+    void flush(const Ciphertext &folded)
+    {
+        for (auto &kv : staged)
+        {
+            auto &el = kv.second;
+            std::sort(el.begin(), el.end());
+            // recipe id of the mask: two FNV-1a streams over its (slot, factor) pairs
+            std::uint64_t hi = 0xcbf29ce484222325ULL, lo = 0x84222325cbf29ce4ULL;
+            for (auto &e : el)
+            {
+                std::uint64_t fb;
+                std::memcpy(&fb, &e.second, 8);
+                for (std::uint64_t w : { (std::uint64_t)e.first, fb })
+                {
+                    hi = (hi ^ w) * 0x100000001b3ULL;
+                    lo = (lo ^ (w + 0x9e3779b97f4a7c15ULL)) * 0x100000001b3ULL;
+                    lo ^= lo >> 29;
+                }
+            }
+            const Plaintext &pt = o.evaluator.cached_vector_plain(
+                folded, hi, lo,
+                [&]() {
+                    std::vector<double> m(kSlots, 0.0);
+                    for (auto &e : el) m[e.first] = e.second;
+                    return m;
+                },
+                scratch);
+            const auto key = std::make_tuple(kv.first.first, kv.first.second, folded.coeff_modulus_size());
+            auto it = groups.find(key);
+            if (it == groups.end())
+                o.evaluator.multiply_plain(folded, pt, groups[key]);
+            else
+                o.evaluator.multiply_plain_add_reduced_error(it->second, folded, pt);
+        }
+        staged.clear();
+    }
+    // rescale every group, rotate it by its k (batched), sum into outputs[t]
+    void finish(std::vector<Ciphertext> &outputs, std::size_t n_out)
+    {
+        std::vector<Ciphertext *> all;
+        for (auto &g : groups) all.push_back(&g.second);
+        o.evaluator.rescale_to_next_inplace_many(all);
+        std::vector<const Ciphertext *> in;
+        std::vector<int> steps;
+        std::vector<Ciphertext> rotated;
+        rotated.reserve(groups.size());
+        std::vector<Ciphertext *> out;
+        for (auto &g : groups)
+            if (std::get<1>(g.first))
+            {
+                in.push_back(&g.second);
+                steps.push_back(std::get<1>(g.first));
+                rotated.emplace_back();
+            }
+        for (auto &r : rotated) out.push_back(&r);
+        for (std::size_t b = 0; b < in.size(); b += kBatch)
+        {
+            const std::size_t e = std::min(in.size(), b + kBatch);
+            o.evaluator.rotate_vectors(std::vector<const Ciphertext *>(in.begin() + b, in.begin() + e),
+                                       std::vector<int>(steps.begin() + b, steps.begin() + e), o.gal_keys,
+                                       std::vector<Ciphertext *>(out.begin() + b, out.begin() + e));
+        }
+        Accum acc(outputs, n_out);
+        std::size_t r = 0;
+        for (auto &g : groups)
+        {
+            const int t = std::get<0>(g.first);
+            if ((std::size_t)t >= n_out) throw std::logic_error("Placer: output index");
+            acc.add((std::size_t)t, std::get<1>(g.first) ? rotated[r++] : g.second, o.evaluator);
+        }
+        groups.clear();
+        for (std::size_t k = 0; k < n_out; k++)
+            if (!acc.has[k]) throw std::invalid_argument("packed_matmul: an output ciphertext received no element");
+    }
+};
+
+// prods[b] = a[b] x w[b] (multiply_reduced_error), relinearized and rescaled in batched launches
+void products(const std::vector<const Ciphertext *> &a, const std::vector<const Ciphertext *> &w,
+              std::vector<Ciphertext> &prods, Ops &o)
+{
+    prods.assign(a.size(), Ciphertext());
+    std::vector<Ciphertext *> p;
+    for (auto &c : prods) p.push_back(&c);
+    o.evaluator.multiply_reduced_error_many(a, w, o.relin_keys, p);
+    o.evaluator.rescale_to_next_inplace_many(p);
+}
+
+// outs[b] = x rotated by steps[b] (0: a copy), in batched launches
+void rotations_of(const Ciphertext &x, const std::vector<int> &steps, std::vector<Ciphertext> &outs, Ops &o)
+{
+    outs.assign(steps.size(), Ciphertext());
+    std::vector<const Ciphertext *> in;
+    std::vector<int> st;
+    std::vector<Ciphertext *> out;
+    for (std::size_t b = 0; b < steps.size(); b++)
+        if (steps[b])
+        {
+            in.push_back(&x);
+            st.push_back(steps[b]);
+            out.push_back(&outs[b]);
+        }
+        else
+            outs[b] = x;
+    if (!in.empty()) o.evaluator.rotate_vectors(in, st, o.gal_keys, out);
+}
+
 // MatrixMul.cpp:118-188 / matrix_mul.py:51-109 with the output placement as a parameter:
-// sink(row, col) -> {ciphertext index, destination slot, factor}; index < 0 drops the element
+// sink(row, col) -> {ciphertext index, destination slot, factor}; index < 0 drops the element.
+// Each weight ciphertext's rotations are made once and shared by every input ciphertext; the
+// products of one rotation run as a batch (products, rescales and every fold step in batched
+// launches), and the placement is grouped (Placer).
 struct Target
 {
     int index, slot;
@@ -98,36 +242,49 @@ void packed_matmul(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, int A
     if (A_cols < 1 || SA > kSlots) throw std::invalid_argument("packed_matmul: A_cols out of range");
     if ((long)A.size() * c < A_rows) throw std::invalid_argument("packed_matmul: too few input ciphertexts");
     if ((long)W.size() * c < W_cols) throw std::invalid_argument("packed_matmul: too few weight ciphertexts");
-    Accum acc(outputs, n_out);
-    Ciphertext rolled, prod, folded, placed;
-    for (std::size_t i = 0; i < A.size(); i++)
-        for (std::size_t j = 0; j < W.size(); j++)
-            for (int rots = 0; rots < c; rots++)
+    Placer pl(o);
+    Ciphertext rolled;
+    std::vector<Ciphertext> prods;
+    for (std::size_t j = 0; j < W.size(); j++)
+        for (int rots = 0; rots < c; rots++)
+        {
+            std::vector<std::size_t> is;
+            for (std::size_t i = 0; i < A.size(); i++)
             {
                 bool any = false;
                 for (int pos = 0; pos < c && !any; pos++)
                     any = (int)i * c + pos < A_rows && (int)j * c + (rots + pos) % c < W_cols;
-                if (!any) continue;
-                if (rots)
-                    o.evaluator.rotate_vector(W[j], rots * SA, o.gal_keys, rolled);
-                else
-                    rolled = W[j];
-                o.evaluator.multiply_reduced_error(A[i], rolled, o.relin_keys, prod);
-                o.evaluator.rescale_to_next_inplace(prod);
-                fold_sum(prod, R, R, folded, o);
-                for (int pos = 0; pos < c; pos++)
+                if (any) is.push_back(i);
+            }
+            if (is.empty()) continue;
+            if (rots)
+                o.evaluator.rotate_vector(W[j], rots * SA, o.gal_keys, rolled);
+            else
+                rolled = W[j];
+            for (std::size_t b0 = 0; b0 < is.size(); b0 += kBatch)
+            {
+                const std::size_t nb = std::min(kBatch, is.size() - b0);
+                std::vector<const Ciphertext *> a(nb), w(nb, &rolled);
+                for (std::size_t b = 0; b < nb; b++) a[b] = &A[is[b0 + b]];
+                products(a, w, prods, o);
+                fold_many(prods, R, R, o);
+                for (std::size_t b = 0; b < nb; b++)
                 {
-                    const int row = (int)i * c + pos, col = (int)j * c + (rots + pos) % c;
-                    if (row >= A_rows || col >= W_cols) continue;
-                    const Target t = sink(row, col);
-                    if (t.index < 0) continue;
-                    if ((std::size_t)t.index >= n_out) throw std::logic_error("packed_matmul: sink index");
-                    place_one(folded, pos * SA, t.slot, t.factor, placed, o);
-                    acc.add((std::size_t)t.index, placed, o.evaluator);
+                    const int i = (int)is[b0 + b];
+                    for (int pos = 0; pos < c; pos++)
+                    {
+                        const int row = i * c + pos, col = (int)j * c + (rots + pos) % c;
+                        if (row >= A_rows || col >= W_cols) continue;
+                        const Target t = sink(row, col);
+                        if (t.index < 0) continue;
+                        if ((std::size_t)t.index >= n_out) throw std::logic_error("packed_matmul: sink index");
+                        pl.element(pos * SA, R, t.index, t.slot, t.factor);
+                    }
+                    pl.flush(prods[b]);
                 }
             }
-    for (std::size_t k = 0; k < n_out; k++)
-        if (!acc.has[k]) throw std::invalid_argument("packed_matmul: an output ciphertext received no element");
+        }
+    pl.finish(outputs, n_out);
 }
 
 void add_bias(std::vector<Ciphertext> &outs, std::vector<Ciphertext> &bias, Evaluator &ev)
@@ -436,35 +593,42 @@ void qk_heads(std::vector<Ciphertext> &Q, std::vector<Ciphertext> &K, std::vecto
 {
     // qk_matmul (attn.py:168-204, MatrixMul.cpp:480-533): K replicated with period rows * 2 dh, rotated
     // by whole rows, multiplied with Q, folded over dh; entry (r, (r + rots) % rows) placed at
-    // r * 2 rows + col of the head's score ciphertext, scaled by 1 / sqrt(dh) (attn.py:359)
+    // r * 2 rows + col of the head's score ciphertext, scaled by 1 / sqrt(dh) (attn.py:359).  The
+    // rotations of K, the products and the folds of kBatch row offsets run as batches; placement
+    // grouped (Placer).
     Ops o{ encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys };
     const int dh = head_dim, P = rows * 2 * dh;
     if (P > kSlots || (long)rows * 2 * rows > kSlots || (kSlots % P)) throw std::invalid_argument("qk_heads: shape");
     if (K.size() < Q.size()) throw std::invalid_argument("qk_heads: one K ciphertext per Q ciphertext");
     outputs.assign(Q.size(), Ciphertext());
     const double inv_sqrt = 1.0 / std::sqrt((double)dh);
-    Ciphertext dup, rolled, prod, folded, placed;
+    Ciphertext dup;
+    std::vector<Ciphertext> rolled, prods;
     for (std::size_t h = 0; h < Q.size(); h++)
     {
-        std::vector<Ciphertext> one;
-        Accum acc(one, 1);
         dup = K[h];
         replicate(dup, P, o);
-        for (int rots = 0; rots < rows; rots++)
+        Placer pl(o);
+        for (int r0 = 0; r0 < rows; r0 += (int)kBatch)
         {
-            if (rots)
-                o.evaluator.rotate_vector(dup, rots * 2 * dh, o.gal_keys, rolled);
-            else
-                rolled = dup;
-            o.evaluator.multiply_reduced_error(Q[h], rolled, o.relin_keys, prod);
-            o.evaluator.rescale_to_next_inplace(prod);
-            fold_sum(prod, dh, dh, folded, o);
-            for (int pos = 0; pos < rows; pos++)
+            const int nb = std::min((int)kBatch, rows - r0);
+            std::vector<int> steps(nb);
+            for (int b = 0; b < nb; b++) steps[b] = (r0 + b) * 2 * dh;
+            rotations_of(dup, steps, rolled, o);
+            std::vector<const Ciphertext *> a(nb, &Q[h]), w(nb);
+            for (int b = 0; b < nb; b++) w[b] = &rolled[b];
+            products(a, w, prods, o);
+            fold_many(prods, dh, dh, o);
+            for (int b = 0; b < nb; b++)
             {
-                place_one(folded, pos * 2 * dh, pos * 2 * rows + (pos + rots) % rows, inv_sqrt, placed, o);
-                acc.add(0, placed, o.evaluator);
+                const int rots = r0 + b;
+                for (int pos = 0; pos < rows; pos++)
+                    pl.element(pos * 2 * dh, dh, 0, pos * 2 * rows + (pos + rots) % rows, inv_sqrt);
+                pl.flush(prods[b]);
             }
         }
+        std::vector<Ciphertext> one;
+        pl.finish(one, 1);
         outputs[h] = one[0];
     }
 }
@@ -475,35 +639,43 @@ void sv_heads(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vecto
 {
     // sv_matmul (attn.py:271-316, MatrixMul.cpp:535-584): V (column layout) replicated with period
     // dh * 2 rows, rotated by whole rows, multiplied with the scores, folded over rows; entry
-    // (r, (r + rots) % dh) of head h placed at row r, column h dh + that of the row-packed output
+    // (r, (r + rots) % dh) of head h placed at row r, column h dh + that of the row-packed output.
+    // Batched and grouped as qk_heads.
     Ops o{ encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys };
     const int dh = head_dim, P = dh * 2 * rows, SO = 2 * round_to_2(d_model), cO = kSlots / SO;
     if (P > kSlots || (kSlots % P)) throw std::invalid_argument("sv_heads: shape");
     if (V.size() < S.size()) throw std::invalid_argument("sv_heads: one V ciphertext per score ciphertext");
     const std::size_t n_out = (std::size_t)(rows + cO - 1) / cO;
-    Accum acc(outputs, n_out);
-    Ciphertext dup, rolled, prod, folded, placed;
+    Placer pl(o);
+    Ciphertext dup;
+    std::vector<Ciphertext> rolled, prods;
     for (std::size_t h = 0; h < S.size(); h++)
     {
         dup = V[h];
         replicate(dup, P, o);
-        for (int rots = 0; rots < dh; rots++)
+        for (int r0 = 0; r0 < dh; r0 += (int)kBatch)
         {
-            if (rots)
-                o.evaluator.rotate_vector(dup, rots * 2 * rows, o.gal_keys, rolled);
-            else
-                rolled = dup;
-            o.evaluator.multiply_reduced_error(S[h], rolled, o.relin_keys, prod);
-            o.evaluator.rescale_to_next_inplace(prod);
-            fold_sum(prod, rows, rows, folded, o);
-            for (int pos = 0; pos < rows; pos++)
+            const int nb = std::min((int)kBatch, dh - r0);
+            std::vector<int> steps(nb);
+            for (int b = 0; b < nb; b++) steps[b] = (r0 + b) * 2 * rows;
+            rotations_of(dup, steps, rolled, o);
+            std::vector<const Ciphertext *> a(nb, &S[h]), w(nb);
+            for (int b = 0; b < nb; b++) w[b] = &rolled[b];
+            products(a, w, prods, o);
+            fold_many(prods, rows, rows, o);
+            for (int b = 0; b < nb; b++)
             {
-                const int col = (int)h * dh + (pos + rots) % dh;
-                place_one(folded, pos * 2 * rows, (pos % cO) * SO + col, 1.0, placed, o);
-                acc.add((std::size_t)(pos / cO), placed, o.evaluator);
+                const int rots = r0 + b;
+                for (int pos = 0; pos < rows; pos++)
+                {
+                    const int col = (int)h * dh + (pos + rots) % dh;
+                    pl.element(pos * 2 * rows, rows, pos / cO, (pos % cO) * SO + col, 1.0);
+                }
+                pl.flush(prods[b]);
             }
         }
     }
+    pl.finish(outputs, n_out);
 }
 
 void compute_inverse_norm(Ciphertext &input, Ciphertext &output, int iters, double normalize_factor,

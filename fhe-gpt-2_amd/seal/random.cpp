@@ -222,6 +222,19 @@ void sample_uniform_dev(mhe_ctx *eng, const prng_seed_type &seed, const std::vec
     sample_uniform_dev(eng, seed, moduli, prime, slot, n, out, s);
 }
 
+void sample_uniform_host(mhe_ctx *eng, const prng_seed_type &seed, const std::vector<std::uint64_t> &moduli,
+                         const std::vector<int> &prime_of_limb, const std::vector<int> &slot_of_limb, std::size_t n,
+                         std::uint64_t *out, void *s)
+{
+    int kept = 0;
+    for (int v : slot_of_limb) kept = std::max(kept, v + 1);
+    if (!kept) return;
+    Scratch dev(eng, s, (std::size_t)kept * n * 8);
+    sample_uniform_dev(eng, seed, moduli, prime_of_limb, slot_of_limb, n, static_cast<std::uint64_t *>(dev.p), s);
+    check(mhe_memcpy_d2h(eng, out, dev.p, (std::size_t)kept * n * 8, s));
+    check(mhe_stream_sync(eng, s));
+}
+
 void sample_cbd_dev(mhe_ctx *eng, const prng_seed_type &seed, std::uint64_t byte_offset, std::size_t limbs,
                     std::uint64_t *out, void *s)
 {

@@ -22,6 +22,10 @@ void sample_uniform_dev(mhe_ctx *eng, const prng_seed_type &seed, const std::vec
 // ... over limbs 0..limbs-1 of the context, all kept
 void sample_uniform_dev(mhe_ctx *eng, const prng_seed_type &seed, const std::vector<std::uint64_t> &moduli,
                         std::size_t limbs, std::size_t n, std::uint64_t *out, void *s);
+// sample_uniform_dev into host memory out[slot][n] (the expansion of a saved seed on load)
+void sample_uniform_host(mhe_ctx *eng, const prng_seed_type &seed, const std::vector<std::uint64_t> &moduli,
+                         const std::vector<int> &prime_of_limb, const std::vector<int> &slot_of_limb, std::size_t n,
+                         std::uint64_t *out, void *s);
 // sample_poly_cbd from stream byte `byte_offset` (64-aligned) over limbs 0..limbs-1, on the device
 void sample_cbd_dev(mhe_ctx *eng, const prng_seed_type &seed, std::uint64_t byte_offset, std::size_t limbs,
                     std::uint64_t *out, void *s);

@@ -661,7 +661,7 @@ void upload(mhe_ctx *eng, void *s, std::uint64_t *dst, const std::vector<std::ui
 // encrypt_zero_symmetric (rlwe.cpp:289-373) at a level of `limbs` primes, NTT form, no seed
 // saved: bootstrap PRNG <- `seed`; its first 64 bytes seed the PRNG of a = c1 (sample_poly_uniform,
 // NTT form directly); e = sample_poly_cbd from the bootstrap PRNG's next bytes; c0 = -(a*s + e).
-void encrypt_zero_symmetric(const SEALContext &ctx, const prng_seed_type &seed, const std::uint64_t *sk,
+void sym_encrypt_zero(const SEALContext &ctx, const prng_seed_type &seed, const std::uint64_t *sk,
                             std::size_t limbs, std::uint64_t *c0, std::uint64_t *c1, void *s)
 {
     mhe_ctx *eng = ctx.engine();
@@ -700,7 +700,7 @@ void make_kswitch_key(const SEALContext &ctx, const std::function<prng_seed_type
     for (std::size_t j = 0; j < digits; j++)
     {
         std::uint64_t *c0 = full ? d + j * 2 * K * n : tmp.p, *c1 = c0 + K * n;
-        encrypt_zero_symmetric(ctx, next_seed(), sk, K, c0, c1, s);
+        sym_encrypt_zero(ctx, next_seed(), sk, K, c0, c1, s);
         std::vector<std::uint64_t> f(K, 0);
         f[j] = P % cm[j].value();
         chk(mhe_multiply_scalar(eng, new_key, f.data(), t.p, 1, (int)K, s));
@@ -863,33 +863,58 @@ KeyGenerator::KeyGenerator(const SEALContext &context, const SecretKey &secret_k
     rng_ = factory_of(context);
 }
 
-void KeyGenerator::create_public_key(PublicKey &destination)
+namespace
 {
-    // generate_pk (keygenerator.cpp:87-112): encrypt_zero_symmetric at the key level
-    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
-    void *s = ctx_.stream();
+// generate_pk (keygenerator.cpp:87-112): encrypt_zero_symmetric at the key level
+prng_seed_type make_public_key(const SEALContext &ctx, UniformRandomGeneratorFactory &rng, const SecretKey &sk,
+                               PublicKey &destination)
+{
+    const std::size_t K = ctx.key_size(), n = ctx.key_context_data()->parms().poly_modulus_degree();
+    void *s = ctx.stream();
     Ciphertext &pk = destination.data();
-    pk.resize(ctx_, ctx_.key_parms_id(), 2);
+    pk.resize(ctx, ctx.key_parms_id(), 2);
     pk.is_ntt_form() = true;
     pk.scale() = 1.0;
     std::uint64_t *d = pk.store().dev_write(s, true);
-    encrypt_zero_symmetric(ctx_, rng_->next_seed(), sk_.data().store().dev_read(s), K, d, d + K * n, s);
+    const prng_seed_type seed = rng.next_seed();
+    sym_encrypt_zero(ctx, seed, sk.data().store().dev_read(s), K, d, d + K * n, s);
+    return rnd::stream_prefix_seed(seed);
 }
+} // namespace
 
-PublicKey KeyGenerator::create_public_key()
+void KeyGenerator::create_public_key(PublicKey &destination) { make_public_key(ctx_, *rng_, sk_, destination); }
+
+Serializable<PublicKey> KeyGenerator::create_public_key()
 {
     PublicKey pk;
-    create_public_key(pk);
-    return pk;
+    const prng_seed_type seed = make_public_key(ctx_, *rng_, sk_, pk);
+    return Serializable<PublicKey>(std::move(pk), SeedMap{ { 0, { seed } } });
 }
 
-void KeyGenerator::kswitch_key(const std::uint64_t *new_key, PolyStore &dest, std::size_t digits)
+void KeyGenerator::kswitch_key(const std::uint64_t *new_key, PolyStore &dest, std::size_t digits,
+                               std::vector<prng_seed_type> *seeds)
 {
     make_kswitch_key(
-        ctx_, [&] { return rng_->next_seed(); }, sk_.data().store().dev_read(ctx_.stream()), new_key, digits, dest);
+        ctx_,
+        [&] {
+            const prng_seed_type sd = rng_->next_seed();
+            if (seeds) seeds->push_back(rnd::stream_prefix_seed(sd));
+            return sd;
+        },
+        sk_.data().store().dev_read(ctx_.stream()), new_key, digits, dest);
 }
 
-void KeyGenerator::create_relin_keys(RelinKeys &destination)
+void KeyGenerator::create_relin_keys(RelinKeys &destination) { relin_keys_into(destination, nullptr); }
+
+Serializable<RelinKeys> KeyGenerator::create_relin_keys()
+{
+    RelinKeys rk;
+    SeedMap seeds;
+    relin_keys_into(rk, &seeds);
+    return Serializable<RelinKeys>(std::move(rk), std::move(seeds));
+}
+
+void KeyGenerator::relin_keys_into(RelinKeys &destination, SeedMap *seeds)
 {
     // create_relin_keys (keygenerator.cpp:115-149): key-switching key of s^2
     const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
@@ -898,7 +923,7 @@ void KeyGenerator::create_relin_keys(RelinKeys &destination)
     const std::uint64_t *sk = sk_.data().store().dev_read(s);
     chk(mhe_multiply_plain(ctx_.engine(), sk, sk, s2.p, 1, (int)K, s));
     PolyStore key;
-    kswitch_key(s2.p, key, K - 1);
+    kswitch_key(s2.p, key, K - 1, seeds ? &(*seeds)[RelinKeys::get_index(2)] : nullptr);
     destination.insert(RelinKeys::get_index(2), std::move(key), K);
     destination.parms_id() = ctx_.key_parms_id();
     destination.set_key_limbs(K);
@@ -932,9 +957,29 @@ void KeyGenerator::create_galois_keys(const std::vector<std::pair<std::uint32_t,
 
 void KeyGenerator::create_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination)
 {
-    std::vector<std::pair<std::uint32_t, std::size_t>> full;
-    for (std::uint32_t e : elts) full.emplace_back(e, ctx_.key_size() - 1);
-    create_galois_keys(full, destination);
+    galois_keys_into(elts, destination, nullptr);
+}
+
+void KeyGenerator::galois_keys_into(const std::vector<std::uint32_t> &elts, GaloisKeys &destination, SeedMap *seeds)
+{
+    // create_galois_keys (keygenerator.cpp:152-190) with SEAL's full keys; seeds receives every
+    // digit's public seed per key index
+    const std::size_t K = ctx_.key_size(), n = ctx_.key_context_data()->parms().poly_modulus_degree();
+    if (K < 2) throw std::logic_error("keyswitching is not supported by the context");
+    void *s = ctx_.stream();
+    DevBuf rot(ctx_.engine(), s, K * n);
+    for (std::uint32_t elt : elts)
+    {
+        if (!(elt & 1) || elt >= 2 * n) throw std::invalid_argument("Galois element is not valid");
+        if (destination.has_key(elt)) continue;
+        const std::uint64_t *sk = sk_.data().store().dev_read(s);
+        chk(mhe_permute_galois(ctx_.engine(), sk, elt, rot.p, 1, (int)K, s));
+        PolyStore key;
+        kswitch_key(rot.p, key, K - 1, seeds ? &(*seeds)[GaloisKeys::get_index(elt)] : nullptr);
+        destination.insert(GaloisKeys::get_index(elt), std::move(key), K);
+    }
+    destination.parms_id() = ctx_.key_parms_id();
+    destination.set_key_limbs(K);
 }
 
 void KeyGenerator::create_deferred_galois_keys_from_elts(const std::vector<std::uint32_t> &elts, GaloisKeys &destination)
@@ -1004,6 +1049,22 @@ void KeyGenerator::create_galois_keys(const std::vector<int> &steps, GaloisKeys 
 void KeyGenerator::create_galois_keys(GaloisKeys &destination)
 {
     create_galois_keys_from_elts(elts_all(ctx_), destination);
+}
+
+Serializable<GaloisKeys> KeyGenerator::create_galois_keys(const std::vector<int> &steps)
+{
+    GaloisKeys gk;
+    SeedMap seeds;
+    galois_keys_into(elts_from_steps(ctx_, steps), gk, &seeds);
+    return Serializable<GaloisKeys>(std::move(gk), std::move(seeds));
+}
+
+Serializable<GaloisKeys> KeyGenerator::create_galois_keys()
+{
+    GaloisKeys gk;
+    SeedMap seeds;
+    galois_keys_into(elts_all(ctx_), gk, &seeds);
+    return Serializable<GaloisKeys>(std::move(gk), std::move(seeds));
 }
 
 void KeyGenerator::create_deferred_galois_keys(const std::vector<int> &steps, GaloisKeys &destination)
@@ -1156,7 +1217,7 @@ Encryptor::Encryptor(const SEALContext &context, const PublicKey &public_key)
 }
 
 Encryptor::Encryptor(const SEALContext &context, const SecretKey &secret_key)
-    : ctx_(context), sk_(secret_key), asymmetric_(false)
+    : ctx_(context), sk_(secret_key), asymmetric_(false), has_sk_(true)
 {
     require_set(context);
     if (secret_key.parms_id() != context.key_parms_id())
@@ -1164,7 +1225,29 @@ Encryptor::Encryptor(const SEALContext &context, const SecretKey &secret_key)
     rng_ = factory_of(context);
 }
 
-void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
+Encryptor::Encryptor(const SEALContext &context, const PublicKey &public_key, const SecretKey &secret_key)
+    : Encryptor(context, public_key)
+{
+    set_secret_key(secret_key);
+}
+
+void Encryptor::set_public_key(const PublicKey &public_key)
+{
+    if (public_key.parms_id() != ctx_.key_parms_id())
+        throw std::invalid_argument("public key is not valid for encryption parameters");
+    pk_ = public_key;
+    asymmetric_ = true;
+}
+
+void Encryptor::set_secret_key(const SecretKey &secret_key)
+{
+    if (secret_key.parms_id() != ctx_.key_parms_id())
+        throw std::invalid_argument("secret key is not valid for encryption parameters");
+    sk_ = secret_key;
+    has_sk_ = true;
+}
+
+void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest, bool symmetric, prng_seed_type *public_seed) const
 {
     // encryptor.cpp:88-166 (encrypt_zero_internal): public-key encryption runs one level up
     // (the key level for the first data level) and is divided and rounded down by the dropped
@@ -1174,11 +1257,14 @@ void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
     void *s = ctx_.stream();
     std::uint64_t *d = dest.store().dev_write(s, true);
     const prng_seed_type seed = rng_->next_seed();
-    if (!asymmetric_)
+    if (symmetric)
     {
-        encrypt_zero_symmetric(ctx_, seed, sk_.data().store().dev_read(s), L, d, d + L * n, s);
+        if (!has_sk_) throw std::logic_error("secret key is not set");
+        sym_encrypt_zero(ctx_, seed, sk_.data().store().dev_read(s), L, d, d + L * n, s);
+        if (public_seed) *public_seed = rnd::stream_prefix_seed(seed);
         return;
     }
+    if (!asymmetric_) throw std::logic_error("public key is not set");
     // encrypt_zero_asymmetric (rlwe.cpp:220-286): one PRNG; u ternary, then e_0, e_1 (CBD)
     const std::size_t m = L < K ? L + 1 : L;
     const std::uint64_t *pk = pk_.data().store().dev_read(s);
@@ -1201,14 +1287,20 @@ void Encryptor::encrypt_zero_at(std::size_t L, Ciphertext &dest) const
         chk(mhe_rescale_to_next(eng, c.p, d, 2, (int)m, s));
 }
 
-void Encryptor::encrypt_zero(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle) const
+void Encryptor::zero_at(parms_id_type parms_id, Ciphertext &destination, bool symmetric,
+                        prng_seed_type *public_seed) const
 {
     auto cd = ctx_.get_context_data(parms_id);
     if (!cd) throw std::invalid_argument("parms_id is not valid for encryption parameters");
     destination.resize(ctx_, parms_id, 2);
     destination.is_ntt_form() = true;
     destination.scale() = 1.0;
-    encrypt_zero_at(cd->parms().coeff_modulus().size(), destination);
+    encrypt_zero_at(cd->parms().coeff_modulus().size(), destination, symmetric, public_seed);
+}
+
+void Encryptor::encrypt_zero(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle) const
+{
+    zero_at(parms_id, destination, !asymmetric_, nullptr);
 }
 
 void Encryptor::encrypt_zero(Ciphertext &destination, MemoryPoolHandle pool) const
@@ -1216,15 +1308,67 @@ void Encryptor::encrypt_zero(Ciphertext &destination, MemoryPoolHandle pool) con
     encrypt_zero(ctx_.first_parms_id(), destination, pool);
 }
 
+void Encryptor::encrypt_zero_symmetric(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle) const
+{
+    zero_at(parms_id, destination, true, nullptr);
+}
+
+void Encryptor::encrypt_zero_symmetric(Ciphertext &destination, MemoryPoolHandle pool) const
+{
+    encrypt_zero_symmetric(ctx_.first_parms_id(), destination, pool);
+}
+
+Serializable<Ciphertext> Encryptor::encrypt_zero_symmetric(parms_id_type parms_id, MemoryPoolHandle) const
+{
+    Ciphertext c;
+    prng_seed_type seed{};
+    zero_at(parms_id, c, true, &seed);
+    return Serializable<Ciphertext>(std::move(c), SeedMap{ { 0, { seed } } });
+}
+
+Serializable<Ciphertext> Encryptor::encrypt_zero_symmetric(MemoryPoolHandle pool) const
+{
+    return encrypt_zero_symmetric(ctx_.first_parms_id(), pool);
+}
+
 void Encryptor::encrypt(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle) const
 {
+    encrypt_plain(plain, destination, !asymmetric_, nullptr);
+}
+
+Serializable<Ciphertext> Encryptor::encrypt(const Plaintext &plain, MemoryPoolHandle) const
+{
+    // a public-key encryption has no seed to save; a secret-key-only Encryptor saves it seeded
+    Ciphertext c;
+    prng_seed_type seed{};
+    encrypt_plain(plain, c, !asymmetric_, &seed);
+    return Serializable<Ciphertext>(std::move(c), asymmetric_ ? SeedMap{} : SeedMap{ { 0, { seed } } });
+}
+
+void Encryptor::encrypt_symmetric(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle) const
+{
+    encrypt_plain(plain, destination, true, nullptr);
+}
+
+Serializable<Ciphertext> Encryptor::encrypt_symmetric(const Plaintext &plain, MemoryPoolHandle) const
+{
+    Ciphertext c;
+    prng_seed_type seed{};
+    encrypt_plain(plain, c, true, &seed);
+    return Serializable<Ciphertext>(std::move(c), SeedMap{ { 0, { seed } } });
+}
+
+void Encryptor::encrypt_plain(const Plaintext &plain, Ciphertext &destination, bool symmetric,
+                              prng_seed_type *public_seed) const
+{
     TRACE_OP("encrypt", trace::ct(destination), trace::pt(plain));
-    // encrypt_internal (encryptor.cpp:168-239), CKKS branch
+    // encrypt_internal (encryptor.cpp:168-239), CKKS branch: the plaintext is added to c0 only, so a
+    // symmetric encryption keeps c1 = the seeded uniform polynomial
     if (!plain.is_ntt_form()) throw std::invalid_argument("plain must be in NTT form");
     auto cd = ctx_.get_context_data(plain.parms_id());
     if (!cd) throw std::invalid_argument("plain is not valid for encryption parameters");
     const std::size_t L = cd->parms().coeff_modulus().size();
-    encrypt_zero(plain.parms_id(), destination);
+    zero_at(plain.parms_id(), destination, symmetric, public_seed);
     void *s = ctx_.stream();
     std::uint64_t *d = destination.store().dev_write(s);
     chk(mhe_add(ctx_.engine(), d, plain.store().dev_read(s), d, 1, (int)L, s));
@@ -2080,6 +2224,106 @@ void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted,
     if (tsc.top())
         for (std::size_t i = 0; i < encrypted.size(); i++)
             trace::record("rotate", { tin[i] }, trace::ct(*destinations[i]), "\"step\": " + std::to_string(steps[i]));
+}
+
+void Evaluator::relinearize_inplace_many(const std::vector<Ciphertext *> &encrypted, const RelinKeys &relin_keys) const
+{
+    // relinearize_inplace of every entry; size-3 entries of one level share one batched key switch
+    trace::Scope tsc; // traced as one "relinearize" record per entry
+    std::vector<std::string> tin;
+    if (tsc.top())
+        for (const Ciphertext *c : encrypted) tin.push_back(c ? trace::ct(*c) : std::string());
+    if (relin_keys.parms_id() != context_.key_parms_id())
+        throw std::invalid_argument("relin_keys is not valid for encryption parameters");
+    std::map<std::size_t, std::vector<Ciphertext *>> groups;
+    for (std::size_t i = 0; i < encrypted.size(); i++)
+    {
+        Ciphertext *c = encrypted[i];
+        if (!c) throw std::invalid_argument("null ciphertext");
+        for (std::size_t j = 0; j < i; j++)
+            if (encrypted[j] == c) throw std::invalid_argument("entries must be distinct");
+        Level lv = check_ct(context_, *c, "encrypted");
+        if (!c->is_ntt_form()) throw std::invalid_argument("encrypted must be in NTT form");
+        if (c->size() == 3) groups[lv.L].push_back(c);
+    }
+    void *s = context_.stream();
+    for (auto &g : groups)
+    {
+        std::vector<Ciphertext *> &v = g.second;
+        if (v.size() < 2) continue; // relinearized one by one below
+        const std::size_t L = g.first;
+        std::vector<std::uint64_t *> ct;
+        std::vector<const std::uint64_t *> target, keys;
+        std::vector<int> kls;
+        for (Ciphertext *c : v)
+        {
+            std::size_t kl = 0;
+            keys.push_back(relin_keys.key_for(RelinKeys::get_index(2), L, s, kl));
+            kls.push_back((int)kl);
+            std::uint64_t *d = c->store().dev_write(s);
+            ct.push_back(d);
+            target.push_back(d + 2 * L * c->poly_modulus_degree());
+        }
+        chk(mhe_switch_key_batch(context_.engine(), (int)v.size(), ct.data(), target.data(), keys.data(), kls.data(),
+                                 (int)L, s));
+        for (Ciphertext *c : v) c->resize(2);
+    }
+    for (Ciphertext *c : encrypted)
+        if (c->size() > 2) relinearize_inplace(*c, relin_keys);
+    if (tsc.top())
+        for (std::size_t i = 0; i < encrypted.size(); i++) trace::record("relinearize", { tin[i] }, trace::ct(*encrypted[i]));
+}
+
+void Evaluator::multiply_reduced_error_many(const std::vector<const Ciphertext *> &encrypted1,
+                                            const std::vector<const Ciphertext *> &encrypted2,
+                                            const RelinKeys &relin_keys,
+                                            const std::vector<Ciphertext *> &destinations) const
+{
+    if (encrypted1.size() != encrypted2.size() || encrypted1.size() != destinations.size())
+        throw std::invalid_argument("encrypted1, encrypted2 and destinations must have the same size");
+    for (std::size_t i = 0; i < destinations.size(); i++)
+    {
+        if (!encrypted1[i] || !encrypted2[i] || !destinations[i]) throw std::invalid_argument("null ciphertext");
+        for (std::size_t j = 0; j < destinations.size(); j++)
+            if ((j != i && destinations[i] == destinations[j]) || destinations[i] == encrypted1[j] ||
+                destinations[i] == encrypted2[j])
+                throw std::invalid_argument("destinations must be distinct and must not be inputs");
+    }
+    trace::Scope tsc; // traced as one "mul_re" record per entry
+    std::vector<std::string> t1, t2;
+    if (tsc.top())
+        for (std::size_t i = 0; i < encrypted1.size(); i++)
+        {
+            t1.push_back(trace::ct(*encrypted1[i]));
+            t2.push_back(trace::ct(*encrypted2[i]));
+        }
+    // the products as multiply_reduced_error makes them (size 3), then one batched relinearization
+    void *s = context_.stream();
+    for (std::size_t i = 0; i < destinations.size(); i++)
+    {
+        const Ciphertext &a = *encrypted1[i], &b = *encrypted2[i];
+        Ciphertext &d = *destinations[i];
+        const bool same = a.coeff_modulus_size() == b.coeff_modulus_size() && a.parms_id() == b.parms_id() &&
+                          a.size() == 2 && b.size() == 2;
+        if (!same)
+        {
+            d = a;
+            reduced_error_op(d, b, Rmode::mul);
+            continue;
+        }
+        check_pair(context_, a, b, false);
+        const Level lv = level_of(context_, a.parms_id(), "encrypted1");
+        const double new_scale = b.scale() * b.scale();
+        check_scale(new_scale, lv);
+        const std::uint64_t *pa = a.store().dev_read(s), *pb = b.store().dev_read(s);
+        fresh_dest(context_, a, d, 3);
+        chk(mhe_ct_multiply(context_.engine(), pa, pb, d.store().dev_write(s, true), (int)lv.L, s));
+        d.scale() = new_scale;
+    }
+    relinearize_inplace_many(destinations, relin_keys);
+    if (tsc.top())
+        for (std::size_t i = 0; i < destinations.size(); i++)
+            trace::record("mul_re", { t1[i], t2[i] }, trace::ct(*destinations[i]));
 }
 
 void Evaluator::rescale_to_next_inplace_many(const std::vector<Ciphertext *> &encrypted) const

@@ -8,13 +8,21 @@
 //               u64 | coeff_modulus_size u64 | scale f64 | DynArray
 //   Plaintext members  = parms_id | coeff_count u64 | scale f64 | DynArray
 //   DynArray  = SEALHeader + element count u64 + elements (u64, [poly][limb][n])
-// Only compr_mode_type::none is written or accepted.  Seeded (half-size) ciphertexts are not
-// produced by this library's Encryptor, so they are rejected on load.
+// Only compr_mode_type::none is written or accepted.
+//
+// Seeded objects (Serializable<T>: encrypt_symmetric, create_public_key(), create_relin_keys(),
+// create_galois_keys(...)): a size-2 ciphertext written with only c0 in its DynArray, followed by a
+// UniformRandomGeneratorInfo (SEALHeader + prng_type byte + 64-byte seed, randomgen.cpp:99-121) --
+// ciphertext.cpp:148-239; on load a DynArray of exactly n * L words means "seeded" and c1 is
+// sample_poly_uniform(Blake2xbPRNG(seed)) over the ciphertext's primes (ciphertext.cpp:305-335,
+// rlwe.cpp:133-162).  A key's PublicKey records are seeded the same way, per digit.
 //
 // parms_id (SEAL/encryptionparams.cpp:124-158, util/hash.h:30-37) is BLAKE2b with a 32-byte digest
 // over the u64 words [scheme, poly_modulus_degree, coeff moduli..., plain modulus (0 for CKKS)].
 // BLAKE2b itself follows RFC 7693 (12 rounds, SHA-512 IV, no key).
 #include "seal/seal.h"
+
+#include "random_internal.h"
 
 #include <cstring>
 #include <istream>
@@ -148,6 +156,48 @@ std::streamoff load_from_buffer(Obj &o, const SEALContext &ctx, const seal_byte 
     return o.load(ctx, ss);
 }
 
+// UniformRandomGeneratorInfo (randomgen.cpp:99-158): header + prng_type + seed
+constexpr std::streamoff kInfo = kHeader + 1 + (std::streamoff)prng_seed_byte_count;
+void write_info(std::ostream &s, const prng_seed_type &seed)
+{
+    write_header(s, (std::uint64_t)kInfo, compr_mode_type::none);
+    put<std::uint8_t>(s, (std::uint8_t)prng_type::blake2xb);
+    s.write(reinterpret_cast<const char *>(seed.data()), (std::streamsize)prng_seed_byte_count);
+}
+prng_seed_type read_info(std::istream &s)
+{
+    const auto h = read_header(s);
+    if (h.size != (std::uint64_t)kInfo) throw std::logic_error("ciphertext data is invalid");
+    const auto t = get<std::uint8_t>(s);
+    if (t == (std::uint8_t)prng_type::shake256) throw std::logic_error("unsupported prng_type");
+    if (t != (std::uint8_t)prng_type::blake2xb) throw std::logic_error("prng_type is invalid");
+    prng_seed_type seed;
+    s.read(reinterpret_cast<char *>(seed.data()), (std::streamsize)prng_seed_byte_count);
+    if (!s) throw std::runtime_error("I/O error");
+    return seed;
+}
+// c1 = sample_poly_uniform(Blake2xbPRNG(seed)) drawn over the key-level primes listed in `prime`
+// (limb order of the draw), limb l kept at out[slot[l]][n] when slot[l] >= 0 (host memory)
+void expand_uniform(const SEALContext &ctx, const prng_seed_type &seed, const std::vector<int> &prime,
+                    const std::vector<int> &slot, std::size_t n, std::uint64_t *out)
+{
+    std::vector<std::uint64_t> moduli;
+    for (const auto &m : ctx.key_context_data()->parms().coeff_modulus()) moduli.push_back(m.value());
+    rnd::sample_uniform_host(ctx.engine(), seed, moduli, prime, slot, n, out, ctx.stream());
+}
+std::vector<int> iota_limbs(std::size_t L)
+{
+    std::vector<int> v(L);
+    for (std::size_t i = 0; i < L; i++) v[i] = (int)i;
+    return v;
+}
+const prng_seed_type *seed_of(const SeedMap &seeds, std::size_t index, std::size_t digit)
+{
+    auto it = seeds.find(index);
+    if (it == seeds.end() || digit >= it->second.size()) return nullptr;
+    return &it->second[digit];
+}
+
 // residues of a [polys][limbs][n] block must be canonical (SEAL: is_data_valid_for)
 bool residues_valid(const std::vector<std::uint64_t> &w, const std::vector<Modulus> &cm, std::size_t n)
 {
@@ -214,6 +264,31 @@ std::streamoff Ciphertext::save(seal_byte *out, std::size_t size, compr_mode_typ
     return save_to_buffer(*this, out, size, mode);
 }
 
+std::streamoff Ciphertext::save_size_seeded(const SeedMap &seeds, compr_mode_type mode) const
+{
+    if (!seed_of(seeds, 0, 0)) return save_size(mode);
+    if (size_ != 2) throw std::logic_error("a seeded ciphertext has size 2");
+    return kHeader + 32 + 1 + 8 * 3 + 8 + dynarray_size(coeff_modulus_size_ * poly_modulus_degree_) + kInfo;
+}
+
+std::streamoff Ciphertext::save_seeded(std::ostream &stream, const SeedMap &seeds, compr_mode_type mode) const
+{
+    const prng_seed_type *seed = seed_of(seeds, 0, 0);
+    if (!seed) return save(stream, mode);
+    const std::streamoff total = save_size_seeded(seeds, mode);
+    write_header(stream, (std::uint64_t)total, mode);
+    put(stream, parms_id_);
+    put<std::uint8_t>(stream, is_ntt_form_ ? 1 : 0);
+    put<std::uint64_t>(stream, size_);
+    put<std::uint64_t>(stream, poly_modulus_degree_);
+    put<std::uint64_t>(stream, coeff_modulus_size_);
+    put<double>(stream, scale_);
+    write_dynarray(stream, data(), coeff_modulus_size_ * poly_modulus_degree_); // c0
+    write_info(stream, *seed);
+    if (!stream) throw std::runtime_error("I/O error");
+    return total;
+}
+
 std::streamoff Ciphertext::load(const SEALContext &context, std::istream &stream)
 {
     const auto h = read_header(stream);
@@ -230,8 +305,18 @@ std::streamoff Ciphertext::load(const SEALContext &context, std::istream &stream
         throw std::logic_error("ciphertext data is invalid");
     std::vector<std::uint64_t> w;
     read_dynarray(stream, w, (std::size_t)(size * n * L));
+    std::streamoff expect = kHeader + 32 + 1 + 24 + 8 + dynarray_size(w.size());
+    if (size == 2 && w.size() == n * L)
+    {
+        // seeded: c0 loaded, c1 expanded from the UniformRandomGeneratorInfo that follows
+        const prng_seed_type seed = read_info(stream);
+        w.resize(2 * n * L);
+        expand_uniform(context, seed, iota_limbs((std::size_t)L), iota_limbs((std::size_t)L), (std::size_t)n,
+                       w.data() + n * L);
+        expect += kInfo;
+    }
     if (w.size() != size * n * L || !residues_valid(w, cd->parms().coeff_modulus(), n) ||
-        h.size != (std::uint64_t)(kHeader + 32 + 1 + 24 + 8 + dynarray_size(w.size())))
+        h.size != (std::uint64_t)expect)
         throw std::logic_error("ciphertext data is invalid");
     resize(context, id, (std::size_t)size);
     is_ntt_form_ = ntt != 0;
@@ -251,11 +336,23 @@ std::streamoff Ciphertext::load(const SEALContext &context, const seal_byte *in,
 namespace
 {
 std::streamoff pk_size(std::size_t K, std::size_t n) { return kHeader + 32 + 1 + 24 + 8 + dynarray_size(2 * K * n); }
+// a seeded PublicKey record: c0 only, then the seed
+std::streamoff pk_size_seeded(std::size_t K, std::size_t n)
+{
+    return kHeader + 32 + 1 + 24 + 8 + dynarray_size(K * n) + kInfo;
+}
 } // namespace
 
 // A level-truncated key (KSwitchKeys, digits D < K-1) is written as D PublicKeys of D+1 limbs
 // (primes q_0..q_{D-1}, P): the same record layout, an extension SEAL itself does not read.
-std::streamoff KSwitchKeys::save_size(compr_mode_type) const
+std::streamoff KSwitchKeys::save_size(compr_mode_type mode) const { return save_size_seeded(SeedMap{}, mode); }
+
+std::streamoff KSwitchKeys::save(std::ostream &stream, compr_mode_type mode) const
+{
+    return save_seeded(stream, SeedMap{}, mode);
+}
+
+std::streamoff KSwitchKeys::save_size_seeded(const SeedMap &seeds, compr_mode_type) const
 {
     if (maker_) throw std::logic_error("deferred Galois keys cannot be serialized");
     const std::size_t dim1 = keys_.empty() ? 0 : keys_.rbegin()->first + 1;
@@ -265,14 +362,15 @@ std::streamoff KSwitchKeys::save_size(compr_mode_type) const
         const std::size_t KL = limbs_of(kv.first), words = kv.second.words();
         const std::size_t n = KL > 1 ? words / (2 * KL * (KL - 1)) : 0;
         if (!n || words != (KL - 1) * 2 * KL * n) throw std::logic_error("key data is invalid");
-        total += (std::streamoff)(KL - 1) * pk_size(KL, n);
+        for (std::size_t d = 0; d + 1 < KL; d++)
+            total += seed_of(seeds, kv.first, d) ? pk_size_seeded(KL, n) : pk_size(KL, n);
     }
     return total;
 }
 
-std::streamoff KSwitchKeys::save(std::ostream &stream, compr_mode_type mode) const
+std::streamoff KSwitchKeys::save_seeded(std::ostream &stream, const SeedMap &seeds, compr_mode_type mode) const
 {
-    const std::streamoff total = save_size(mode);
+    const std::streamoff total = save_size_seeded(seeds, mode);
     write_header(stream, (std::uint64_t)total, mode);
     put(stream, parms_id_);
     const std::size_t dim1 = keys_.empty() ? 0 : keys_.rbegin()->first + 1;
@@ -290,14 +388,21 @@ std::streamoff KSwitchKeys::save(std::ostream &stream, compr_mode_type mode) con
         const std::uint64_t *p = it->second.host();
         for (std::size_t d = 0; d < digits; d++)
         {
-            write_header(stream, (std::uint64_t)pk_size(KL, n), compr_mode_type::none);
+            const prng_seed_type *seed = seed_of(seeds, i, d);
+            write_header(stream, (std::uint64_t)(seed ? pk_size_seeded(KL, n) : pk_size(KL, n)), compr_mode_type::none);
             put(stream, parms_id_);
             put<std::uint8_t>(stream, 1);
             put<std::uint64_t>(stream, 2);
             put<std::uint64_t>(stream, n);
             put<std::uint64_t>(stream, KL);
             put<double>(stream, 1.0);
-            write_dynarray(stream, p + d * 2 * KL * n, 2 * KL * n);
+            if (seed)
+            {
+                write_dynarray(stream, p + d * 2 * KL * n, KL * n); // c0; c1 is the seed's
+                write_info(stream, *seed);
+            }
+            else
+                write_dynarray(stream, p + d * 2 * KL * n, 2 * KL * n);
         }
     }
     if (!stream) throw std::runtime_error("I/O error");
@@ -345,7 +450,20 @@ std::streamoff KSwitchKeys::load(const SEALContext &context, std::istream &strea
                 throw std::logic_error("KSwitchKeys data is invalid");
             std::vector<std::uint64_t> w;
             read_dynarray(stream, w, 2 * KL * n);
-            if (w.size() != 2 * KL * n || !residues_valid(w, stored, n) || rh.size != (std::uint64_t)pk_size(KL, n))
+            std::streamoff expect = pk_size(KL, n);
+            if (w.size() == KL * n)
+            {
+                // seeded digit: c1 is SEAL's draw over every key-level prime, restricted to the
+                // stored ones (q_0..q_{digits-1}, P) for a level-truncated key
+                const prng_seed_type seed = read_info(stream);
+                std::vector<int> slot(K, -1);
+                for (std::size_t l = 0; l < digits; l++) slot[l] = (int)l;
+                slot[K - 1] = (int)digits;
+                w.resize(2 * KL * n);
+                expand_uniform(context, seed, iota_limbs(K), slot, n, w.data() + KL * n);
+                expect = pk_size_seeded(KL, n);
+            }
+            if (w.size() != 2 * KL * n || !residues_valid(w, stored, n) || rh.size != (std::uint64_t)expect)
                 throw std::logic_error("KSwitchKeys data is invalid");
             std::memcpy(dst + d * 2 * KL * n, w.data(), 8 * w.size());
             total += (std::streamoff)rh.size;

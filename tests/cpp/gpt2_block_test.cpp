@@ -64,15 +64,38 @@ static std::map<std::string, Mat> load_fixture(const std::string &dir)
 
 static std::vector<double> vec(const Mat &m) { return m.v; }
 
+// "key value" pairs of the fixture's header line (make_fixture.py header())
+static std::map<std::string, double> fixture_header(const std::string &dir)
+{
+    std::ifstream txt(dir + "/block.txt");
+    std::string line, tok;
+    std::getline(txt, line);
+    std::istringstream is(line);
+    std::vector<std::string> w;
+    while (is >> tok) w.push_back(tok);
+    std::map<std::string, double> out;
+    for (std::size_t i = 0; i + 1 < w.size(); i++)
+    {
+        char *end = nullptr;
+        const double v = std::strtod(w[i + 1].c_str(), &end);
+        if (end && *end == 0 && !w[i + 1].empty()) out[w[i]] = v;
+    }
+    return out;
+}
+
 int main(int argc, char **argv)
 {
     std::setvbuf(stdout, nullptr, _IONBF, 0);
     const std::string dir = argc > 1 ? argv[1] : "tests/golden/gpt2_block";
+    // "block": the whole block only (the GPT-2-width fixture, make_fixture.py --full)
+    const bool block_only = argc > 2 && std::string(argv[2]) == "block";
     try
     {
         const auto fx = load_fixture(dir);
+        const auto hdr = fixture_header(dir);
         const Mat &X = fx.at("x");
-        const int T = X.rows, d = X.cols, F = fx.at("fc_w").cols, H = 4, dh = d / H;
+        const int T = X.rows, d = X.cols, F = fx.at("fc_w").cols, H = hdr.count("heads") ? (int)hdr.at("heads") : 4,
+                  dh = d / H;
         const double kTol = 1e-3;
 
         // INIT() of gpt2/util.h:36-74: {49} + 21 x {46} + 14 x {49} + {60}, h = 192, scale 2^46
@@ -157,6 +180,7 @@ int main(int argc, char **argv)
         std::uniform_real_distribution<double> U(-1, 1);
 
         // ------------------------------------------------------------ packing helpers (pack.py)
+        if (!block_only)
         {
             // pack_tight / unpack_tight with rows straddling the ciphertext boundary
             const int rows = 1400, rs = 24, st = 64, c = S / st;
@@ -202,6 +226,7 @@ int main(int argc, char **argv)
             }
             report("unpack_tight restores the stride-64 layout", e < kTol && back.size() == in.size(), e, since(t));
         }
+        if (!block_only)
         {
             // expand_bias / expand_bias_head_row / expand_bias_head_col (pack.py:78-113)
             auto t = std::chrono::steady_clock::now();
@@ -232,6 +257,7 @@ int main(int argc, char **argv)
             }
             report("expand_bias / expand_bias_head_row / expand_bias_head_col vs pack.py", e < kTol, e, since(t));
         }
+        if (!block_only)
         {
             // KV cache (optimize.cpp:4-40): augment_value_row keeps row idx of A, the rest from the
             // cache; augment_value_col clears cache column idx and adds A rotated by idx
@@ -268,6 +294,7 @@ int main(int argc, char **argv)
         for (int r = 0; r < T; r++)
             for (int j = 0; j <= r; j++) keep[r][j] = 1.0;
         AttentionParams ap;
+        if (hdr.count("inv_iters")) ap.inv_iters = (int)hdr.at("inv_iters");
         BlockDims dims;
         dims.rows = T;
         dims.d_model = d;
@@ -286,6 +313,7 @@ int main(int argc, char **argv)
             encrypt_block_weights(pw, bw, dims, encoder, encryptor, decryptor, evaluator, gk, rk, remaining_level + 1);
             std::printf("block weights encrypted and packed: %.2f s\n", since(t));
         }
+        if (!block_only)
         {
             auto t = std::chrono::steady_clock::now();
             auto xin = enc_rows(X);
@@ -296,6 +324,7 @@ int main(int argc, char **argv)
             std::printf("   layer_norm_rows: %zu limbs out\n", out.coeff_modulus_size());
             report("layer_norm_rows(x) vs restated LN1", e < kTol, e, since(t));
         }
+        if (!block_only)
         {
             auto t = std::chrono::steady_clock::now();
             auto a = enc_rows(fx.at("ln1"));
@@ -317,6 +346,7 @@ int main(int argc, char **argv)
             }
             report("attn_proj_heads: Q (row head layout) and V (column head layout), all slots", e < kTol, e, since(t));
         }
+        if (!block_only)
         {
             auto t = std::chrono::steady_clock::now();
             auto hin = enc_rows(fx.at("hidden"));
@@ -326,6 +356,7 @@ int main(int argc, char **argv)
             std::printf("   compute_gelu_block: %zu limbs out\n", g.coeff_modulus_size());
             report("compute_gelu_block(hidden) vs restated GELU", e < kTol, e, since(t));
         }
+        if (!block_only)
         {
             auto t = std::chrono::steady_clock::now();
             auto a = enc_rows(fx.at("ln2"));
@@ -350,7 +381,9 @@ int main(int argc, char **argv)
             std::printf("   stages: ln1 %.3g  attn %.3g  x1 %.3g  ln2 %.3g  ffn %.3g  y %.3g; y %zu limbs; "
                         "vs exact GPT-2 block math %.3g\n",
                         e_ln1, e_attn, e_x1, e_ln2, e_ffn, e_y, y[0].coeff_modulus_size(), e_exact);
-            report("GPT-2 block (T 16, d 64, 4 heads, d_ff 256) vs committed plain restatement",
+            std::printf("block_seconds %.3f\n", secs);
+            report("GPT-2 block (T " + std::to_string(T) + ", d " + std::to_string(d) + ", " + std::to_string(H) +
+                       " heads, d_ff " + std::to_string(F) + ") vs plain restatement",
                    std::max({ e_ln1, e_attn, e_x1, e_ln2, e_ffn, e_y }) < kTol, e_y, secs);
         }
     }

@@ -1,0 +1,178 @@
+// The batched (not SEAL API) evaluator entry points against their one-by-one counterparts, word for
+// word and scale for scale: rotate_vectors (keyed steps, NAF-composed steps, step 0, mixed levels),
+// rescale_to_next_inplace_many, relinearize_inplace_many and multiply_reduced_error_many (equal
+// levels, and unequal levels where the reduced-error adjustment runs).  N = 2^13 and 2^16.
+//   seal_batch_test <log N>
+#include "seal/seal.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+
+using namespace seal;
+
+static int g_fail = 0;
+static bool same(const Ciphertext &a, const Ciphertext &b)
+{
+    if (a.size() != b.size() || a.coeff_modulus_size() != b.coeff_modulus_size() || a.scale() != b.scale() ||
+        a.parms_id() != b.parms_id())
+        return false;
+    const PolyStore &x = a.store(), &y = b.store();
+    return x.words() == y.words() && std::memcmp(x.host(), y.host(), x.words() * 8) == 0;
+}
+static void check(const std::string &what, bool ok)
+{
+    std::printf("[%s] %s\n", ok ? "PASS" : "FAIL", what.c_str());
+    if (!ok) g_fail++;
+}
+
+int main(int argc, char **argv)
+{
+    const int logN = argc > 1 ? std::atoi(argv[1]) : 13;
+    const std::size_t N = (std::size_t)1 << logN;
+    std::vector<int> bits{ 51 };
+    for (int i = 0; i < 6; i++) bits.push_back(46);
+    bits.push_back(51);
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(N);
+    parms.set_coeff_modulus(CoeffModulus::Create(N, bits));
+    parms.set_random_generator(
+        std::make_shared<Blake2xbPRNGFactory>(std::array<std::uint64_t, 8>{ 3, 1, 4, 1, 5, 9, 2, 6 }));
+    SEALContext ctx(parms, true, sec_level_type::none);
+    KeyGenerator keygen(ctx);
+    PublicKey pk;
+    keygen.create_public_key(pk);
+    RelinKeys rlk;
+    keygen.create_relin_keys(rlk);
+    const int slots = (int)N / 2;
+    std::vector<int> steps{ 1, 2, 4, 8, 16, slots - 1, slots - 16 };
+    GaloisKeys glk;
+    keygen.create_galois_keys(steps, glk);
+    CKKSEncoder encoder(ctx);
+    Encryptor encryptor(ctx, pk);
+    Evaluator ev(ctx, encoder);
+    const double scale = std::pow(2.0, 46);
+    std::mt19937_64 g(11);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    auto fresh = [&](int drop) {
+        std::vector<double> v(slots);
+        for (auto &x : v) x = U(g);
+        Plaintext p;
+        Ciphertext c;
+        encoder.encode(v, scale, p);
+        encryptor.encrypt(p, c);
+        for (int i = 0; i < drop; i++) ev.mod_switch_to_next_inplace(c);
+        return c;
+    };
+    try
+    {
+        // rotate_vectors: 11 entries over two levels, keyed, NAF (3, 5, -7) and zero steps
+        std::vector<Ciphertext> in;
+        std::vector<int> st{ 1, 3, 0, 16, slots - 1, 5, 2, -7, 4, 8, 1 };
+        for (std::size_t i = 0; i < st.size(); i++) in.push_back(fresh(i % 3 == 2 ? 1 : 0));
+        std::vector<Ciphertext> out(st.size()), want(st.size());
+        std::vector<const Ciphertext *> pin;
+        std::vector<Ciphertext *> pout;
+        for (std::size_t i = 0; i < st.size(); i++)
+        {
+            pin.push_back(&in[i % 4 == 3 ? 0 : i]); // some entries share an input
+            pout.push_back(&out[i]);
+        }
+        ev.rotate_vectors(pin, st, glk, pout);
+        bool ok = true;
+        for (std::size_t i = 0; i < st.size(); i++)
+        {
+            ev.rotate_vector(*pin[i], st[i], glk, want[i]);
+            ok = ok && same(out[i], want[i]);
+        }
+        check("rotate_vectors == rotate_vector (11 entries, 2 levels, keyed / NAF / zero steps)", ok);
+
+        // rescale_to_next_inplace_many on products (size 3 and relinearized size 2), two levels
+        std::vector<Ciphertext> r1, r2;
+        for (int i = 0; i < 10; i++)
+        {
+            Ciphertext a = fresh(i % 2), b = fresh(i % 2), m;
+            ev.multiply(a, b, m);
+            if (i % 3) ev.relinearize_inplace(m, rlk);
+            r1.push_back(m);
+        }
+        r2 = r1;
+        std::vector<Ciphertext *> pr;
+        for (auto &c : r1) pr.push_back(&c);
+        ev.rescale_to_next_inplace_many(pr);
+        ok = true;
+        for (std::size_t i = 0; i < r2.size(); i++)
+        {
+            ev.rescale_to_next_inplace(r2[i]);
+            ok = ok && same(r1[i], r2[i]);
+        }
+        check("rescale_to_next_inplace_many == rescale_to_next_inplace (10 entries, sizes 2 / 3, 2 levels)", ok);
+
+        // relinearize_inplace_many: 9 size-3 entries over three levels and one size-2 entry
+        std::vector<Ciphertext> l1, l2;
+        for (int i = 0; i < 10; i++)
+        {
+            Ciphertext a = fresh(i % 3), b = fresh(i % 3), m;
+            ev.multiply(a, b, m);
+            if (i == 9) ev.relinearize_inplace(m, rlk);
+            l1.push_back(m);
+        }
+        l2 = l1;
+        std::vector<Ciphertext *> pl;
+        for (auto &c : l1) pl.push_back(&c);
+        ev.relinearize_inplace_many(pl, rlk);
+        ok = true;
+        for (std::size_t i = 0; i < l2.size(); i++)
+        {
+            ev.relinearize_inplace(l2[i], rlk);
+            ok = ok && same(l1[i], l2[i]);
+        }
+        check("relinearize_inplace_many == relinearize_inplace (10 entries, 3 levels, one already size 2)", ok);
+
+        // multiply_reduced_error_many: equal levels and both unequal orders
+        std::vector<Ciphertext> A, B, M(12), W(12);
+        for (int i = 0; i < 12; i++)
+        {
+            A.push_back(fresh(i % 4 == 1 ? 1 : 0));
+            B.push_back(fresh(i % 4 == 2 ? 2 : 0));
+        }
+        std::vector<const Ciphertext *> pa, pb;
+        std::vector<Ciphertext *> pm;
+        for (int i = 0; i < 12; i++)
+        {
+            pa.push_back(&A[i]);
+            pb.push_back(&B[i % 5 == 4 ? 0 : i]);
+            pm.push_back(&M[i]);
+        }
+        ev.multiply_reduced_error_many(pa, pb, rlk, pm);
+        ok = true;
+        for (int i = 0; i < 12; i++)
+        {
+            ev.multiply_reduced_error(*pa[i], *pb[i], rlk, W[i]);
+            ok = ok && same(M[i], W[i]);
+        }
+        check("multiply_reduced_error_many == multiply_reduced_error (12 entries, equal and unequal levels)", ok);
+
+        bool threw = false;
+        try
+        {
+            std::vector<Ciphertext *> bad{ &M[0], &M[0] };
+            ev.multiply_reduced_error_many({ &A[0], &A[1] }, { &B[0], &B[1] }, rlk, bad);
+        }
+        catch (const std::invalid_argument &)
+        {
+            threw = true;
+        }
+        check("multiply_reduced_error_many rejects repeated destinations", threw);
+    }
+    catch (const std::exception &e)
+    {
+        std::printf("exception: %s\nFAILED\n", e.what());
+        return 1;
+    }
+    std::printf(g_fail ? "FAILED (%d)\n" : "ALL PASSED\n", g_fail);
+    return g_fail ? 1 : 0;
+}

@@ -244,6 +244,143 @@ int main(int argc, char **argv)
         kf << kstr;
     }
 
+    // seeded objects (Serializable<T>, SEAL's seeded save: ciphertext.cpp:148-239, keygenerator.h:83-310):
+    // the second polynomial of every symmetric encryption is written as its PRNG seed, and load()
+    // expands it into the words a twin generation wrote.  A fixed-seed factory gives every
+    // generator the same seed, so the Serializable and the plain creators draw identical objects.
+    {
+        EncryptionParameters sp = parms;
+        sp.set_random_generator(
+            std::make_shared<Blake2xbPRNGFactory>(prng_seed_type{ 11, 12, 13, 14, 15, 16, 17, 18 }));
+        SEALContext sctx(sp, true, sec_level_type::none);
+        KeyGenerator kg(sctx);
+        CKKSEncoder senc(sctx);
+        Plaintext spt;
+        senc.encode(x, scale, spt);
+        auto bytes_of = [](const auto &ser) {
+            std::stringstream t;
+            const auto w = ser.save(t);
+            CHECK(w == ser.save_size() && (std::streamoff)t.str().size() == w);
+            return t.str();
+        };
+        // ciphertext: encrypt_symmetric / encrypt_zero_symmetric
+        Encryptor se(sctx, kg.secret_key());
+        Ciphertext full, zfull;
+        se.encrypt_symmetric(spt, full);
+        const std::string sb = bytes_of(se.encrypt_symmetric(spt));
+        const std::size_t Ln = full.coeff_modulus_size() * n;
+        CHECK((std::streamoff)sb.size() == full.save_size() - (std::streamoff)(8 * Ln) + 81);
+        Ciphertext back_s;
+        {
+            std::stringstream t(sb);
+            CHECK(back_s.load(sctx, t) == (std::streamoff)sb.size());
+        }
+        CHECK(back_s.size() == 2 && back_s.scale() == full.scale() && back_s.parms_id() == full.parms_id());
+        CHECK(std::memcmp(back_s.data(), full.data(), 8 * full.dyn_array_size()) == 0);
+        se.encrypt_zero_symmetric(zfull);
+        const std::string zb = bytes_of(se.encrypt_zero_symmetric());
+        Ciphertext zback;
+        {
+            std::stringstream t(zb);
+            zback.load(sctx, t);
+        }
+        CHECK(std::memcmp(zback.data(), zfull.data(), 8 * zfull.dyn_array_size()) == 0);
+        // a lower level: the seed expands over that level's primes only
+        Ciphertext lowfull;
+        Plaintext lowpt;
+        senc.encode(x, sctx.first_context_data()->next_context_data()->parms_id(), scale, lowpt);
+        se.encrypt_symmetric(lowpt, lowfull);
+        const std::string lb = bytes_of(se.encrypt_symmetric(lowpt));
+        Ciphertext lowback;
+        {
+            std::stringstream t(lb);
+            lowback.load(sctx, t);
+        }
+        CHECK(lowback.coeff_modulus_size() == lowfull.coeff_modulus_size() &&
+              std::memcmp(lowback.data(), lowfull.data(), 8 * lowfull.dyn_array_size()) == 0);
+        // decrypts after load
+        Decryptor sdec(sctx, kg.secret_key());
+        Plaintext sp_back;
+        sdec.decrypt(back_s, sp_back);
+        std::vector<double> ys;
+        senc.decode(sp_back, ys);
+        double es = 0;
+        for (std::size_t i = 0; i < x.size(); i++) es = std::max(es, std::fabs(ys[i] - x[i]));
+        std::printf("seeded ciphertext: %zu bytes (full %lld), decrypt error %.3g\n", sb.size(),
+                    (long long)full.save_size(), es);
+        CHECK(es < 1e-6);
+        // public key, relin keys, Galois keys
+        PublicKey pkf;
+        kg.create_public_key(pkf);
+        const std::string pb = bytes_of(kg.create_public_key());
+        PublicKey pkb;
+        {
+            std::stringstream t(pb);
+            pkb.load(sctx, t);
+        }
+        CHECK(std::memcmp(pkb.data().data(), pkf.data().data(), 8 * pkf.data().dyn_array_size()) == 0);
+        RelinKeys rkf;
+        kg.create_relin_keys(rkf);
+        const std::string rb = bytes_of(kg.create_relin_keys());
+        RelinKeys rkb;
+        {
+            std::stringstream t(rb);
+            CHECK(rkb.load(sctx, t) == (std::streamoff)rb.size());
+        }
+        const std::size_t ri = RelinKeys::get_index(2);
+        CHECK(rkb.has_key(2) && rkb.key(ri).words() == rkf.key(ri).words() &&
+              std::memcmp(rkb.key(ri).host(), rkf.key(ri).host(), 8 * rkf.key(ri).words()) == 0);
+        std::printf("seeded relin keys: %zu bytes (full %lld)\n", rb.size(), (long long)rkf.save_size());
+        CHECK((std::streamoff)rb.size() < rkf.save_size() * 6 / 10);
+        GaloisKeys gkf;
+        kg.create_galois_keys(std::vector<int>{ 1, -1 }, gkf);
+        const std::string gb = bytes_of(kg.create_galois_keys(std::vector<int>{ 1, -1 }));
+        GaloisKeys gkb;
+        {
+            std::stringstream t(gb);
+            gkb.load(sctx, t);
+        }
+        bool gsame = gkb.size() == gkf.size() && gkf.size() == 2;
+        for (std::size_t i = 0; i < 2 * n && gsame; i++)
+            if (gkf.has_index(i))
+                gsame = gkb.has_index(i) && gkb.key(i).words() == gkf.key(i).words() &&
+                        std::memcmp(gkb.key(i).host(), gkf.key(i).host(), 8 * gkf.key(i).words()) == 0;
+        CHECK(gsame);
+        // a public-key encryption has no seed: Serializable saves it in full
+        Encryptor pe(sctx, pkf);
+        Ciphertext pfull;
+        pe.encrypt(spt, pfull);
+        CHECK(pe.encrypt(spt).save_size() == pfull.save_size());
+        CHECK(throws([&] { pe.encrypt_symmetric(spt); }));
+        Encryptor both(sctx, pkf, kg.secret_key());
+        CHECK(bytes_of(both.encrypt_symmetric(spt)) == sb);
+        // corrupt seed records are rejected: PRNG type, info header size, truncation
+        auto load_s = [&](const std::string &b) {
+            std::stringstream t(b);
+            Ciphertext c;
+            c.load(sctx, t);
+        };
+        std::string bad = sb;
+        bad[sb.size() - 65] = 2; // shake256 (not supported)
+        CHECK(throws([&] { load_s(bad); }));
+        bad = sb;
+        bad[sb.size() - 65] = 7;
+        CHECK(throws([&] { load_s(bad); }));
+        bad = sb;
+        bad[sb.size() - 81 + 8] ^= 1; // info record size
+        CHECK(throws([&] { load_s(bad); }));
+        CHECK(throws([&] { load_s(sb.substr(0, sb.size() - 10)); }));
+        // for the Python check: the seeded file and its full twin (the oracle expands the seed)
+        std::ofstream f1(dir + "/ct_seeded.bin", std::ios::binary), f2(dir + "/ct_twin.bin", std::ios::binary);
+        f1 << sb;
+        full.save(f2);
+        std::ofstream f3(dir + "/relin_seeded.bin", std::ios::binary), f4(dir + "/relin_twin.bin", std::ios::binary);
+        f3 << rb;
+        rkf.save(f4);
+        std::ofstream f5(dir + "/key_moduli.txt");
+        for (auto &q : sctx.key_context_data()->parms().coeff_modulus()) f5 << q.value() << "\n";
+    }
+
     // files for the Python-side format check
     {
         std::ofstream f(dir + "/ct.bin", std::ios::binary);

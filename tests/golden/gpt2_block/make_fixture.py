@@ -22,6 +22,10 @@ Every matrix product is exact here (the encrypted path's placements only move va
 restated slot by slot because the approximate max depends on the order quickMax combines entries.
 
 Run: python tests/golden/gpt2_block/make_fixture.py  (writes block.bin / block.txt next to itself)
+     python tests/golden/gpt2_block/make_fixture.py --full DIR  (GPT-2 dimensions: T 128, d 768,
+     12 heads, d_ff 3072, 11 Goldschmidt steps; the ~58 MB of weights are regenerated from the seed
+     wherever the test runs, and the committed full/expected.bin -- y and y_exact, with
+     full/expected.txt -- pins the result: tests/test_gpt2.py checks a regenerated fixture against it)
 """
 import math
 import os
@@ -219,13 +223,27 @@ def exact_block(x, w):
     return x1 + g @ w["pj_w"] + w["pj_b"]
 
 
+# at full width the Q / K weights are drawn at 0.7 / sqrt(d) so that every score stays inside the
+# row-max step's domain (computeMax takes sign(0.1 (a - b)), |a - b| <= 10)
+FULL = dict(T=128, D=768, H=12, F=3072, INV_ITERS=11, QK_STD=0.7)
+QK_STD = 1.0
+
+
+def set_dims(T_=16, D_=64, H_=4, F_=256, INV_ITERS_=8, QK_STD_=1.0):
+    """Block dimensions for the functions above (module globals; the small fixture by default)."""
+    global T, D, H, F, DH, INV_ITERS, INV_NORM, QK_STD
+    T, D, H, F, INV_ITERS, QK_STD = T_, D_, H_, F_, INV_ITERS_, QK_STD_
+    DH = D // H
+    INV_NORM = 1.0 / T
+
+
 def make_inputs(seed=SEED):
     rng = np.random.default_rng(seed)
     x = rng.normal(0.0, 1.0, (T, D))
     w = {
         "ln1_g": 1.0 + 0.1 * rng.normal(size=D), "ln1_b": 0.1 * rng.normal(size=D),
-        "qw": rng.normal(0, 1.0 / math.sqrt(D), (D, D)), "qb": 0.05 * rng.normal(size=D),
-        "kw": rng.normal(0, 1.0 / math.sqrt(D), (D, D)), "kb": 0.05 * rng.normal(size=D),
+        "qw": rng.normal(0, QK_STD / math.sqrt(D), (D, D)), "qb": 0.05 * rng.normal(size=D),
+        "kw": rng.normal(0, QK_STD / math.sqrt(D), (D, D)), "kb": 0.05 * rng.normal(size=D),
         "vw": rng.normal(0, 1.0 / math.sqrt(D), (D, D)), "vb": 0.05 * rng.normal(size=D),
         "ow": rng.normal(0, 0.5 / math.sqrt(D), (D, D)), "ob": 0.05 * rng.normal(size=D),
         "ln2_g": 1.0 + 0.1 * rng.normal(size=D), "ln2_b": 0.1 * rng.normal(size=D),
@@ -248,11 +266,17 @@ def arrays(seed=SEED):
     return [(k, np.atleast_2d(np.asarray(allv[k], dtype="<f8"))) for k in ORDER_IN + ORDER_OUT], ranges
 
 
-def write(dst=HERE):
+def header():
+    return (f"# gpt2 block fixture: T {T} d {D} heads {H} d_ff {F} seed {SEED} alpha {GELU_ALPHA} "
+            f"newton {NEWTON_ITERS} inv_iters {INV_ITERS}" + (f" qk_std {QK_STD}" if QK_STD != 1.0 else ""))
+
+
+def write(dst=HERE, names=None):
     items, ranges = arrays()
+    if names is not None:
+        items = [(k, a) for k, a in items if k in names]
     off = 0
-    lines = [f"# gpt2 block fixture: T {T} d {D} heads {H} d_ff {F} seed {SEED} alpha {GELU_ALPHA} "
-             f"newton {NEWTON_ITERS} inv_iters {INV_ITERS}", "# name rows cols offset(doubles)"]
+    lines = [header(), "# name rows cols offset(doubles)"]
     blob = bytearray()
     for name, a in items:
         lines.append(f"{name} {a.shape[0]} {a.shape[1]} {off}")
@@ -266,6 +290,18 @@ def write(dst=HERE):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] in ("--full", "--full-expected"):
+        set_dims(*[FULL[k] for k in ("T", "D", "H", "F", "INV_ITERS", "QK_STD")])
+        dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(HERE, "full")
+        os.makedirs(dst, exist_ok=True)
+        if sys.argv[1] == "--full-expected":  # the committed pin: outputs only
+            r = write(dst, names={"y", "y_exact"})
+            os.replace(os.path.join(dst, "block.bin"), os.path.join(dst, "expected.bin"))
+            os.replace(os.path.join(dst, "block.txt"), os.path.join(dst, "expected.txt"))
+        else:
+            r = write(dst)
+        print("ranges:", r)
+        sys.exit(0)
     r = write()
     items, _ = arrays()
     d = dict(items)

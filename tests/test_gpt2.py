@@ -6,6 +6,7 @@ checks every approximation over all 32768 slots against its plain-double restate
 (tests/cpp/gpt2_test.cpp)."""
 import os
 import subprocess
+import sys
 
 import pytest
 
@@ -110,6 +111,51 @@ def test_gpt2_block_end_to_end():
     _build()
     r = subprocess.run([os.path.join(ROOT, "build", "gpt2_block_test"), BLOCK_DIR], capture_output=True, text=True,
                        timeout=600, cwd=ROOT)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
+
+
+def _read_fixture(d, stem):
+    import numpy as np
+
+    raw = np.fromfile(os.path.join(d, stem + ".bin"), dtype="<f8")
+    out = {}
+    for line in open(os.path.join(d, stem + ".txt")):
+        if line.startswith("#"):
+            continue
+        name, r, c, off = line.split()
+        r, c, off = int(r), int(c), int(off)
+        out[name] = raw[off:off + r * c].reshape(r, c)
+    return out
+
+
+def test_full_width_fixture_pinned(tmp_path):
+    """The GPT-2-width fixture (T 128, d 768, 12 heads, d_ff 3072), regenerated from its seed as the
+    GPU run does (make_fixture.py --full), reproduces the committed outputs full/expected.bin."""
+    import numpy as np
+
+    subprocess.check_call([sys.executable, os.path.join(BLOCK_DIR, "make_fixture.py"), "--full", str(tmp_path)],
+                          stdout=subprocess.DEVNULL)
+    got = _read_fixture(str(tmp_path), "block")
+    want = _read_fixture(os.path.join(BLOCK_DIR, "full"), "expected")
+    assert got["x"].shape == (128, 768) and got["fc_w"].shape == (768, 3072)
+    for k in ("y", "y_exact"):
+        assert np.abs(got[k] - want[k]).max() < 1e-9, k
+    assert "heads 12" in open(os.path.join(str(tmp_path), "block.txt")).readline()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.environ.get("MHE_GPT2_FULL"), reason="GPT-2-width block: minutes; MHE_GPT2_FULL=1 runs it "
+                    "(scripts/gpu_gpt2_full.sh, profiles/r03*_gpt2_full_block.log.txt)")
+def test_gpt2_block_full_width(tmp_path):
+    """GPU: the whole block at GPT-2 dimensions against the regenerated full-width restatement, every
+    stage within 1e-3, s/block printed (block_seconds)."""
+    _build()
+    subprocess.check_call([sys.executable, os.path.join(BLOCK_DIR, "make_fixture.py"), "--full", str(tmp_path)],
+                          stdout=subprocess.DEVNULL)
+    r = subprocess.run([os.path.join(ROOT, "build", "gpt2_block_test"), str(tmp_path), "block"], capture_output=True,
+                       text=True, timeout=1500, cwd=ROOT)
     print(r.stdout)
     print(r.stderr)
     assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr

@@ -118,3 +118,20 @@ def test_batch_errors(small):
         ch.eng.apply_galois_batch([a], [4], [key])
     with pytest.raises(mhe.MheError):
         ch.eng.rescale_batch([a], outs=[a])
+
+
+@pytest.mark.parametrize("log_n", [13, 16])
+def test_seal_surface_batches_equal_one_by_one(log_n):
+    """The seal:: batched entry points (rotate_vectors, rescale_to_next_inplace_many,
+    relinearize_inplace_many, multiply_reduced_error_many) give the words and scales of the
+    one-by-one calls they replace, over mixed levels, shared inputs, NAF-composed and zero steps
+    (tests/cpp/seal_batch_test.cpp)."""
+    import os
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "fhe-gpt-2_amd", "seal"), "../../build/seal_batch_test"])
+    r = subprocess.run([os.path.join(root, "build", "seal_batch_test"), str(log_n)], capture_output=True, text=True,
+                       timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr

@@ -100,3 +100,62 @@ def test_save_load_roundtrip(tmp_path):
         assert (ntt, sz, nn, kl) == (1, 2, n, K)
         off += size
     assert off == len(k)
+
+
+def _parse_ct(b, off=0):
+    """One Ciphertext record at `off`: (end offset, fields, c0/c1 or c0 + seed)."""
+    size = _header(b, off)
+    ntt, sz, nn, L, scale = struct.unpack_from("<BQQQd", b, off + 48)
+    d = off + 16 + 32 + 1 + 24 + 8
+    dsize = _header(b, d)
+    (count,) = struct.unpack_from("<Q", b, d + 16)
+    data = np.frombuffer(b, dtype="<u8", count=count, offset=d + 24).reshape(-1, L, nn)
+    seed = None
+    if count == L * nn:  # seeded: UniformRandomGeneratorInfo follows the DynArray
+        i = d + dsize
+        assert _header(b, i) == 81
+        assert b[i + 16] == 1  # prng_type::blake2xb
+        seed = list(struct.unpack_from("<8Q", b, i + 17))
+        assert i + 81 == off + size
+    else:
+        assert d + dsize == off + size
+    return off + size, dict(ntt=ntt, size=sz, n=nn, L=L, scale=scale), data, seed
+
+
+@pytest.mark.gpu
+def test_seeded_save_expands_with_the_oracle_prng(tmp_path):
+    """SEAL's seeded save (ciphertext.cpp:148-239): a Serializable ciphertext / relin key is written
+    with c0 only plus a Blake2xb UniformRandomGeneratorInfo per encryption, and that seed expanded by
+    the oracle's own restatement of sample_poly_uniform (oracle/seal_random.c, rlwe.cpp:133-162)
+    gives exactly the c1 of the full twin written by the plain creators."""
+    import oracle as O
+
+    _build()
+    r = subprocess.run([EXE, "roundtrip", str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    kmod = [int(x) for x in open(tmp_path / "key_moduli.txt").read().split()]
+    n = 1 << 13
+    ctx = O.Context(13, kmod)
+    b = open(tmp_path / "ct_seeded.bin", "rb").read()
+    end, f, c0, seed = _parse_ct(b)
+    assert end == len(b) and seed is not None and f["size"] == 2
+    t = open(tmp_path / "ct_twin.bin", "rb").read()
+    _, ft, twin, tseed = _parse_ct(t)
+    assert tseed is None and ft == f
+    assert np.array_equal(c0[0], twin[0])
+    assert np.array_equal(ctx.sample(seed, "uniform", f["L"]), twin[1])
+    assert len(b) == len(t) - 8 * f["L"] * n + 81
+    # relin keys: every digit record seeded; digit j's seed expands to the twin's c1 over all K primes
+    kb = open(tmp_path / "relin_seeded.bin", "rb").read()
+    kt = open(tmp_path / "relin_twin.bin", "rb").read()
+    assert _header(kb) == len(kb) and _header(kt) == len(kt)
+    dim1, dim2 = struct.unpack_from("<QQ", kb, 48)
+    assert (dim1, dim2) == (1, len(kmod) - 1) and struct.unpack_from("<QQ", kt, 48) == (dim1, dim2)
+    ob, ot = 64, 64
+    for _ in range(dim2):
+        ob, fb, c0b, sd = _parse_ct(kb, ob)
+        ot, ft, twin, _ = _parse_ct(kt, ot)
+        assert sd is not None and fb["L"] == len(kmod)
+        assert np.array_equal(c0b[0], twin[0])
+        assert np.array_equal(ctx.sample(sd, "uniform", len(kmod)), twin[1])
+    assert ob == len(kb) and ot == len(kt)
