@@ -295,6 +295,9 @@ def main():
     ap.add_argument("--key-format", choices=("prepared", "seal"), default="prepared",
                     help="relin key as the engine's prepared format (mhe_key_prepare, 48-bit planes for "
                          "primes < 2^48; bit-identical results) or SEAL's u64 layout")
+    ap.add_argument("--hmult-group", type=int, default=8,
+                    help="HMults per mhe_hmult_batch call (one batched key switch sharing the relin key "
+                         "stream; 1 = one mhe_hmult call each)")
     ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams the batch is spread over (round robin; 4 = the hardware queues per process)")
     args = ap.parse_args()
@@ -343,6 +346,21 @@ def main():
     b_p = [ptr(b[i]) for i in range(B)]
     o_p = [ptr(out[i]) for i in range(B)]
     k_p = ptr(key)
+    G = max(1, args.hmult_group)
+    # calls of G independent HMults each (mhe_hmult_batch: one batched key switch per call whose
+    # entries share the relin key stream), dealt round robin over the streams
+    arr = lambda ps: (mhe.ctypes.c_void_p * len(ps))(*ps)  # noqa: E731
+    calls = [(min(G, B - i0), arr(a_p[i0:i0 + G]), arr(b_p[i0:i0 + G]), arr(o_p[i0:i0 + G])) for i0 in range(0, B, G)]
+
+    def run_calls(stream_list):
+        for ci, (cnt, ca, cb, co) in enumerate(calls):
+            st = stream_list[ci % len(stream_list)]
+            if G == 1:
+                rc = eng.hmult_raw(ca[0], cb[0], k_p, K, co[0], L, st)
+            else:
+                rc = eng.hmult_batch_raw(cnt, ca, cb, k_p, K, co, L, st)
+            if rc:
+                raise mhe.MheError(rc, mhe.lib().mhe_last_error().decode())
 
     def step():
         if len(streams) > 1:  # the extra streams start after the main stream's prior work
@@ -350,10 +368,7 @@ def main():
             ev.record(stream)
             for s_ in streams[1:]:
                 s_.wait_event(ev)
-        for i in range(B):
-            rc = eng.hmult_raw(a_p[i], b_p[i], k_p, K, o_p[i], L, sps[i % len(sps)])
-            if rc:
-                raise mhe.MheError(rc, mhe.lib().mhe_last_error().decode())
+        run_calls(sps)
         if len(streams) > 1:  # join back so the timing events on the main stream cover all
             for s_ in streams[1:]:
                 ev = torch.cuda.Event()
@@ -395,10 +410,7 @@ def main():
     lib.mhe_kernel_time(eng._h, 1, mhe.ctypes.byref(mc_ms), mhe.ctypes.byref(mc_n))
     if len(sps) > 1:
         for _ in range(min(args.steps, 4)):
-            for i in range(B):
-                rc = eng.hmult_raw(a_p[i], b_p[i], k_p, K, o_p[i], L, sps[0])
-                if rc:
-                    raise mhe.MheError(rc, lib.mhe_last_error().decode())
+            run_calls(sps[:1])
         torch.cuda.synchronize(dev)
         lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))
         lib.mhe_kernel_time(eng._h, 1, mhe.ctypes.byref(mc_ms), mhe.ctypes.byref(mc_n))
@@ -415,7 +427,7 @@ def main():
                 traffic, traffic_src = t["hbm_bytes_per_hmult"], os.path.relpath(f, ROOT)
                 pk = {k.split("<")[0]: v for k, v in t.get("per_kernel_GB_per_hmult", {}).items()}
                 km_traffic = pk.get("k_ks_row_mac")
-                km_traffic = None if km_traffic is None else km_traffic * 1e9  # one launch per HMult
+                km_traffic = None if km_traffic is None else km_traffic * 1e9 * min(G, B)  # G HMults per launch
         except (OSError, ValueError, KeyError):
             pass
 
@@ -434,8 +446,12 @@ def main():
     per_hmult_s = gpu_s / hmults_per_gpu  # HIP-event time per HMult (batch over its streams)
     # algorithmic bytes as SURVEY.md §8(d) defines them (SEAL's u64 key layout); a prepared key
     # streams fewer (streamed_key_bytes_per_launch), which is what the format buys
-    km_bytes = ks_row_mac_key_bytes(L, n)
-    km_streamed = ks_row_mac_key_bytes(L, n, moduli, prepared)
+    # one launch covers G HMults (mhe_hmult_batch): the key slice once, and every entry's target
+    # limbs read ([L][n]) and key inner products written ([2][L+1][n])
+    G_launch = min(G, B)
+    io_bytes = G_launch * (L + 2 * (L + 1)) * n * 8
+    km_bytes = ks_row_mac_key_bytes(L, n) + io_bytes
+    km_streamed = ks_row_mac_key_bytes(L, n, moduli, prepared) + io_bytes
     hm_bytes = hmult_bytes(L)
     achieved = hm_bytes / per_hmult_s / 1e9
     km_achieved = km_bytes / (km_avg_us * 1e-6) / 1e9 if km_avg_us > 0 else 0.0
@@ -457,12 +473,17 @@ def main():
             "log_n": LOG_N,
             "limbs": L,
             "batch_per_gpu": B,
+            "hmults_per_call": G,
+            "call": "mhe_hmult_batch" if G > 1 else "mhe_hmult",
             "streams": args.streams,
             "parallelism": f"replicas{world} (independent ciphertexts per GPU, key broadcast over RCCL)",
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_ks_row_mac (fused ModUp row pass + key inner products; 1 launch per HMult)",
+            "kernel": (f"k_ks_row_mac (fused ModUp row pass + key inner products; one launch per {G_launch} HMults "
+                       "sharing the relin key stream)"),
+            "hmults_per_launch": G_launch,
+            "bytes_model": "relin key slice once per launch + per HMult: target limbs read, key products written",
             "achieved": round(km_achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -487,8 +508,10 @@ def main():
             **v,
             "peak_lane_ops_per_s": FP64_LANE_OPS_PEAK,
             "peak_source": "v_fma_f64 microbenchmark, profiles/r01_ubench_valu.txt (spec 39.3e12)",
-            "floor_us": round(v["fp64_lane_ops"] / FP64_LANE_OPS_PEAK * 1e6, 2),
-            "frac": round(v["fp64_lane_ops"] / FP64_LANE_OPS_PEAK / (km_avg_us * 1e-6), 4) if km_avg_us > 0 else None,
+            "floor_us": round(G_launch * v["fp64_lane_ops"] / FP64_LANE_OPS_PEAK * 1e6, 2),
+            "frac": (round(G_launch * v["fp64_lane_ops"] / FP64_LANE_OPS_PEAK / (km_avg_us * 1e-6), 4)
+                     if km_avg_us > 0 else None),
+            "hmults_per_launch": G_launch,
             "sq_insts_valu_per_launch": sq_valu,
             "issued_lane_ops_frac": (round(sq_valu * 64 / FP64_LANE_OPS_PEAK / (km_avg_us * 1e-6), 4)
                                      if sq_valu and km_avg_us > 0 else None),

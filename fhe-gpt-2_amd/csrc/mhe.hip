@@ -169,6 +169,7 @@ struct WsEntry
     u64 *coeff = nullptr; // [L][n]        INTT(target); the rescale's / ModDown's INTT'd last limbs
     u64 *modup = nullptr; // [L+1][L][n]   lifted + NTT'd digits; reused by mod-down/rescale
     u64 *acc = nullptr;   // [2][L+1][n]   key inner products
+    u64 *ct3 = nullptr;   // [3][L][n]     tensor output of a batched HMult
 };
 
 struct Workspace
@@ -214,6 +215,7 @@ struct mhe_ctx
     int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
     int timing = 0;      // record HIP events around the key-switch kernels (mhe_ctx_set_timing)
     int hmult_fused = 1; // HMult: ModDown fused with the rescale (MHE_HMULT_FUSED=0: separate)
+    int ks_share = 1;    // batched key switches sharing one key: XCD-grouped entries (MHE_KS_SHARE=0: off)
     int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
@@ -280,8 +282,8 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int en
         const int E = std::max(entries, w.entries);
         const size_t n = c->n, L = std::max(limbs, w.max_limbs);
         const size_t Lc = L < 3 ? 3 : L;
-        const size_t per = Lc * n + (L + 1) * L * n + 2 * (L + 1) * n;
-        size_t words = (size_t)E * per + L * n + 3 * L * n;
+        const size_t per = Lc * n + (L + 1) * L * n + 2 * (L + 1) * n + 3 * L * n;
+        size_t words = (size_t)E * per + L * n;
         HIP_TRY(hipSetDevice(c->device));
         if (hipMalloc(&w.base, words * sizeof(u64)) != hipSuccess)
         {
@@ -294,12 +296,13 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int en
             w.e[i].coeff = w.base + (size_t)i * per;
             w.e[i].modup = w.e[i].coeff + Lc * n;
             w.e[i].acc = w.e[i].modup + (L + 1) * L * n;
+            w.e[i].ct3 = w.e[i].acc + 2 * (L + 1) * n;
         }
         w.coeff = w.e[0].coeff;
         w.modup = w.e[0].modup;
         w.acc = w.e[0].acc;
         w.tmp = w.base + (size_t)E * per;
-        w.ct3 = w.tmp + L * n;
+        w.ct3 = w.e[0].ct3;
         w.max_limbs = (int)L;
         w.entries = E;
     }
@@ -1401,6 +1404,10 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
         // 48-bit intermediate (ntt.h tile16): only k_modup_col writes it, so only with column groups
         const int pack = (c->ks_pack && c->ks_colgroups > 0) ? 1 : 0;
         KsPtrs kp{};
+        int share = B > 1 ? 1 : 0; // one key for every entry: XCD-grouped entries (k_ks_row_mac)
+        for (int e = 0; e < B; e++)
+            if (jobs[e].key != jobs[0].key || jobs[e].key_limbs != jobs[0].key_limbs) share = 0;
+        if (!c->ks_share) share = 0;
         for (int e = 0; e < B; e++)
         {
             kp.coeff[e] = w->e[e].coeff;
@@ -1428,7 +1435,7 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
             }
             timing_end(tc, st);
             hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
-            ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, pack, kpack, st);
+            ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, pack, kpack, share, st);
             timing_end(tm, st);
         }
     }
@@ -1694,6 +1701,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_KS_CHUNK")) c->ks_chunk = atoi(f);
     if (const char *f = getenv("MHE_KS_FCHUNK")) c->ks_fchunk = atoi(f);
     if (const char *f = getenv("MHE_HMULT_FUSED")) c->hmult_fused = atoi(f);
+    if (const char *f = getenv("MHE_KS_SHARE")) c->ks_share = atoi(f);
     if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
     if (const char *f = getenv("MHE_KS_PACK")) c->ks_pack = atoi(f);
     if (const char *f = getenv("MHE_GALOIS_FUSED")) c->galois_fused = atoi(f);
@@ -2573,6 +2581,53 @@ MHE_EXPORT int mhe_mod_switch_drop(mhe_ctx *c, const uint64_t *in, uint64_t *out
         for (int l = 0; l + 1 < limbs; l++)
             HIP_TRY(mhe_internal_copy_d2d((char *)out + p * dst_pitch + l * limb_bytes,
                                           (const char *)in + p * src_pitch + l * limb_bytes, limb_bytes, S(s)));
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_hmult_batch(mhe_ctx *c, int count, const uint64_t *const *a, const uint64_t *const *b,
+                               const uint64_t *key, int key_limbs, uint64_t *const *out, int limbs, void *s)
+{
+    // mhe_hmult of every entry, MHE_MAXB per key switch: the tensor products into per-entry
+    // scratch, then one batched key switch (all entries share the relinearization key, so
+    // k_ks_row_mac reads it once per XCD) with the fused rescale tail -- bit-identical to count
+    // mhe_hmult calls
+    int r = check_limbs(c, limbs, 2);
+    if (r) return r;
+    if (count < 0 || (count && (!a || !b || !out)) || !key) return fail(MHE_ERR_ARG, "invalid argument");
+    for (int i = 0; i < count; i++)
+    {
+        if (!a[i] || !b[i] || !out[i]) return fail(MHE_ERR_ARG, "invalid argument");
+        for (int j = 0; j < count; j++)
+            if (j != i && out[j] == out[i]) return fail(MHE_ERR_ARG, "outputs must be distinct");
+    }
+    hipStream_t st = S(s);
+    const size_t n = c->n;
+    for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
+    {
+        const int B = std::min(MHE_MAXB, count - i0);
+        Workspace *w;
+        if ((r = get_ws(c, st, c->K - 1, &w, B))) return r;
+        KsJob jobs[MHE_MAXB];
+        for (int e = 0; e < B; e++)
+        {
+            const int i = i0 + e;
+            if ((r = launch_tensor(c, a[i], b[i], w->e[e].ct3, limbs, a[i] == b[i], st))) return r;
+            jobs[e] = KsJob{ w->e[e].ct3, w->e[e].ct3 + ((size_t)2 * limbs * n), key, key_limbs,
+                             c->hmult_fused ? out[i] : nullptr };
+        }
+        if ((r = run_switch_key_batch(c, jobs, B, limbs, st))) return r;
+        if (!c->hmult_fused)
+        {
+            const u64 *in[MHE_MAXB];
+            u64 *o[MHE_MAXB];
+            for (int e = 0; e < B; e++)
+            {
+                in[e] = w->e[e].ct3;
+                o[e] = out[i0 + e];
+            }
+            if ((r = run_rescale_batch(c, in, o, B, 2, limbs, st))) return r;
+        }
+    }
     return MHE_OK;
 }
 

@@ -884,15 +884,31 @@ template <int LOGR, bool FP, bool KPF>
 #endif
 __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int log_n,
-                                                       long long twd, int I0, int pack, int kpack)
+                                                       long long twd, int I0, int pack, int kpack, int share)
 {
-    // batch entry blockIdx.z: inter [cnt][L][n] column-pass output, target [L][n] NTT form,
+    // tile (bx = column block group, by = output prime) and batch entry bz.  With `share` (every
+    // entry reads the same key, gridDim.x * gridDim.y a multiple of 8) the linear workgroup ids are
+    // dealt so that the gridDim.z entries of one tile are ids 8 apart and adjacent in dispatch
+    // order: workgroups go to the 8 XCDs round robin, so all entries of a tile run on one XCD at
+    // the same time and the key stream is fetched from HBM once and hit in that XCD's L2 by the
+    // others.
+    u32 bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (share)
+    {
+        const u32 X = gridDim.x, Y = gridDim.y, Bn = gridDim.z;
+        const u32 id = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+        const u32 r = id % (8 * Bn), tile = (id / (8 * Bn)) * 8 + r % 8;
+        bz = r / 8;
+        bx = tile % X;
+        by = tile / X;
+    }
+    // batch entry bz: inter [cnt][L][n] column-pass output, target [L][n] NTT form,
     // key [digits][2][key_limbs][n], acc [2][L+1][n]
-    const u64 *__restrict__ inter = P.inter[blockIdx.z];
-    const u64 *__restrict__ target = P.target[blockIdx.z];
-    const u64 *__restrict__ key = P.key[blockIdx.z];
-    u64 *__restrict__ acc = P.acc[blockIdx.z];
-    const int key_limbs = P.key_limbs[blockIdx.z];
+    const u64 *__restrict__ inter = P.inter[bz];
+    const u64 *__restrict__ target = P.target[bz];
+    const u64 *__restrict__ key = P.key[bz];
+    u64 *__restrict__ acc = P.acc[bz];
+    const int key_limbs = P.key_limbs[bz];
     using SH = RowMacShape<LOGR>;
     using A = NttArith<FP>;
     using T = typename A::T;
@@ -906,10 +922,10 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
     __shared__ TW twl[S * (R + 1)];
     const int j0 = 0, j1 = L;
     const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
-    const u32 b = blockIdx.x * S + sl;
+    const u32 b = bx * S + sl;
     const u32 base = b << LOGR;
     const u32 R1 = 1u << (log_n - LOGR);
-    const int I = I0 + blockIdx.y; // inter holds output primes I0 .. I0 + gridDim.y - 1
+    const int I = I0 + (int)by; // inter holds output primes I0 .. I0 + gridDim.y - 1
     const int pi = (I == L) ? K - 1 : I;
     const int ki = (I == L) ? key_limbs - 1 : I;
     const PrimeDev p = primes[pi];
@@ -925,7 +941,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             const u32 blk = idx / R, k = idx % R;
             if (k == 0) continue;
             const int s = 31 - __builtin_clz(k);
-            twl[blk * (R + 1) + k] = tw[(((R1 + blockIdx.x * S + blk) << s)) + (k - (1u << s))];
+            twl[blk * (R + 1) + k] = tw[(((R1 + bx * S + blk) << s)) + (k - (1u << s))];
         }
     }
     const TW *mytw = &twl[sl * (R + 1)];
@@ -1144,6 +1160,264 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
         run(ar0);
 }
 
+// k_ks_row_mac with E = 2^EB residues per lane (EB = 2: half the live registers of the E = 8
+// kernel, so 4 waves per SIMD instead of 2 hide the digit and key loads), the 2^LOGR-point row
+// transform in ceil(LOGR / EB) register phases with swizzled LDS transposes inside one wave, and
+// the key inner products in the last phase's layout: every lane holds E consecutive residues, so
+// the key streams and the accumulator stores are 8- / 16-byte vector accesses and no transpose
+// back to a coalesced layout is needed.  Same arithmetic, same words (MHE_KS_EB selects).
+template <int LOGR, int EB>
+struct RowMacShapeE
+{
+    static constexpr int R = 1 << LOGR;
+    static constexpr int E = 1 << EB;
+    static constexpr int TPS = R / E;
+    static_assert(TPS <= 64, "a block's transposes must stay inside one wave");
+    static constexpr int S = 256 / TPS;
+    static constexpr int NP = (LOGR + EB - 1) / EB; // register phases
+};
+
+template <int EB>
+__device__ __forceinline__ u32 laye(u32 t, int e, int b_lo)
+{
+    return ((t >> b_lo) << (b_lo + EB)) | ((u32)e << b_lo) | (t & ((1u << b_lo) - 1));
+}
+
+template <int LOGR, bool FP, int EB, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_ks_row_mac_e(
+    KsPtrs P, const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all, int L, int K, int log_n,
+    long long twd, int I0, int pack, int kpack, int share)
+{
+    u32 bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+    if (share)
+    {
+        // entries reading one key: a tile's entries are ids 8 apart (one XCD), adjacent in dispatch
+        const u32 X = gridDim.x, Y = gridDim.y, Bn = gridDim.z;
+        const u32 id = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+        const u32 r = id % (8 * Bn), tile = (id / (8 * Bn)) * 8 + r % 8;
+        bz = r / 8;
+        bx = tile % X;
+        by = tile / X;
+    }
+    const u64 *__restrict__ inter = P.inter[bz];
+    const u64 *__restrict__ target = P.target[bz];
+    const u64 *__restrict__ key = P.key[bz];
+    u64 *__restrict__ acc = P.acc[bz];
+    const int key_limbs = P.key_limbs[bz];
+    using SH = RowMacShapeE<LOGR, EB>;
+    using A = NttArith<FP>;
+    using T = typename A::T;
+    using TW = typename A::TW;
+    constexpr int R = SH::R, E = SH::E, TPS = SH::TPS, S = SH::S, NP = SH::NP;
+    constexpr int B_A = LOGR - EB; // the first phase's in-lane bits (the ModUp intermediate's load layout)
+    __shared__ T xch[2][S * R];
+    __shared__ TW twl[S * (R + 1)];
+    const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
+    const u32 b = bx * S + sl;
+    const u32 base = b << LOGR;
+    const u32 R1 = 1u << (log_n - LOGR);
+    const int I = I0 + (int)by;
+    const int pi = (I == L) ? K - 1 : I;
+    const int ki = (I == L) ? key_limbs - 1 : I;
+    const PrimeDev p = primes[pi];
+    const size_t n = (size_t)1 << log_n;
+    const size_t kstride = (size_t)key_limbs * n;
+    const A ar0(p, tw_all + ((size_t)pi << log_n), twd);
+    {
+        const TW *tw = ar0.tw;
+        for (u32 idx = tid; idx < (u32)(S * R); idx += 256)
+        {
+            const u32 blk = idx / R, k = idx % R;
+            if (k == 0) continue;
+            const int s = 31 - __builtin_clz(k);
+            twl[blk * (R + 1) + k] = tw[(((R1 + bx * S + blk) << s)) + (k - (1u << s))];
+        }
+    }
+    const TW *mytw = &twl[sl * (R + 1)];
+    T *xb0 = &xch[0][sl * R], *xb1 = &xch[1][sl * R];
+
+    auto run = [&](const auto &ar) {
+        constexpr bool LZ = std::is_same<typename std::decay<decltype(ar)>::type, NttArithF<true>>::value;
+        using AccT = typename std::conditional<FP, double, Acc128>::type;
+        AccT a0[E], a1[E];
+#pragma unroll
+        for (int e = 0; e < E; e++)
+        {
+            if constexpr (FP)
+                a0[e] = a1[e] = 0.0;
+            else
+                a0[e] = a1[e] = Acc128{ 0, 0 };
+        }
+        const bool pk = inter_packed(pack, p.q);
+        // digit J: the column-pass output in the first phase's layout, or (J == I) the input limb,
+        // already in NTT form, straight into the MAC layout
+        auto load_digit = [&](int J, u64 (&v)[E]) {
+            if (J == I)
+            {
+                const u64 *src = target + (size_t)J * n + base;
+#pragma unroll
+                for (int e = 0; e < E; e++) v[e] = ld_nt<2>(&src[laye<EB>(t, e, 0)]);
+            }
+            else if (pk)
+            {
+                const u32 *lo = reinterpret_cast<const u32 *>(inter + ((size_t)(I - I0) * L + J) * n);
+                const unsigned short *hi = reinterpret_cast<const unsigned short *>(lo + n);
+#pragma unroll
+                for (int e = 0; e < E; e++)
+                {
+                    const u32 idx = base + laye<EB>(t, e, B_A);
+                    v[e] = (u64)ld_nt<2>(&lo[tile16(idx)]) | ((u64)ld_nt<2>(&hi[tile16h(idx)]) << 32);
+                }
+            }
+            else
+            {
+                const u64 *src = inter + ((size_t)(I - I0) * L + J) * n + base;
+#pragma unroll
+                for (int e = 0; e < E; e++) v[e] = ld_nt<2>(&src[laye<EB>(t, e, B_A)]);
+            }
+        };
+        u64 vin[E];
+        load_digit(0, vin);
+        lds_barrier(); // twiddles visible
+        const bool kpk = kpack && p.q < (1ull << 48) && key[(size_t)ki * n + n - 1] == KEY_PACK_TAG;
+        auto load_key = [&](int J, u64 (&ka)[E], u64 (&kb)[E]) {
+            const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
+            const u64 *k1 = k0 + kstride;
+            const u32 r0 = base + laye<EB>(t, 0, 0); // E consecutive residues per lane
+            if (kpk)
+            {
+                const u32 *l0 = reinterpret_cast<const u32 *>(k0) + r0;
+                const u32 *l1 = reinterpret_cast<const u32 *>(k1) + r0;
+                const unsigned short *h0 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k0) + n) + r0;
+                const unsigned short *h1 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k1) + n) + r0;
+#pragma unroll
+                for (int e = 0; e < E; e++)
+                {
+                    ka[e] = (u64)ld_nt<1>(&l0[e]) | ((u64)ld_nt<1>(&h0[e]) << 32);
+                    kb[e] = (u64)ld_nt<1>(&l1[e]) | ((u64)ld_nt<1>(&h1[e]) << 32);
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++)
+                {
+                    ka[e] = ld_nt<1>(&k0[r0 + e]);
+                    kb[e] = ld_nt<1>(&k1[r0 + e]);
+                }
+            }
+        };
+        for (int J = 0; J < L; J++)
+        {
+            u64 kk0[E], kk1[E], vnext[E];
+            load_key(J, kk0, kk1);
+            if (J + 1 < L) load_digit(J + 1, vnext);
+            T d[E];
+            if (J != I)
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++) d[e] = ar.in52(vin[e]);
+                int bp = B_A;
+#pragma unroll
+                for (int ph = 0; ph < NP; ph++)
+                {
+                    const int s0 = ph * EB, s1 = (s0 + EB < LOGR) ? s0 + EB : LOGR;
+                    const int bl = (LOGR - s0 - EB > 0) ? LOGR - s0 - EB : 0;
+                    if (ph > 0)
+                    {
+                        T *x = (ph & 1) ? xb1 : xb0;
+                        wave_lds_fence();
+#pragma unroll
+                        for (int e = 0; e < E; e++) x[swz(laye<EB>(t, e, bp))] = d[e];
+                        wave_lds_fence();
+#pragma unroll
+                        for (int e = 0; e < E; e++) d[e] = x[swz(laye<EB>(t, e, bl))];
+                    }
+#pragma unroll
+                    for (int s = s0; s < s1; s++)
+                        ar.template fwd_tab<E>(d, 1 << (LOGR - 1 - s - bl), mytw,
+                                               [&](int e) { return (1 << s) + (laye<EB>(t, e, bl) >> (LOGR - s)); });
+                    bp = bl;
+                }
+                if constexpr (!FP)
+                {
+#pragma unroll
+                    for (int e = 0; e < E; e++) d[e] = ar.canon(d[e]);
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++) d[e] = ar.in52(vin[e]);
+            }
+            if constexpr (FP)
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++)
+                {
+                    const double dv = LZ ? d[e] : fp_reduce(d[e], ar.q, ar.qinv);
+                    a0[e] += fp_mulmod_gen(dv, fp_from_u52(kk0[e]), ar.q, ar.qinv);
+                    a1[e] += fp_mulmod_gen(dv, fp_from_u52(kk1[e]), ar.q, ar.qinv);
+                    if (!LZ && (J & 1))
+                    {
+                        a0[e] = fp_reduce(a0[e], ar.q, ar.qinv);
+                        a1[e] = fp_reduce(a1[e], ar.q, ar.qinv);
+                    }
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++)
+                {
+                    mac128(a0[e], d[e], kk0[e]);
+                    mac128(a1[e], d[e], kk1[e]);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) vin[e] = vnext[e];
+        }
+        u64 *o0 = acc + (size_t)I * n + base;
+        u64 *o1 = o0 + (size_t)(L + 1) * n;
+#pragma unroll
+        for (int e = 0; e < E; e++)
+        {
+            const u32 r = laye<EB>(t, e, 0);
+            if constexpr (FP)
+            {
+                o0[r] = fp_canon(a0[e], ar.q, ar.qinv);
+                o1[r] = fp_canon(a1[e], ar.q, ar.qinv);
+            }
+            else
+            {
+                o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
+                o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
+            }
+        }
+    };
+    if constexpr (FP)
+    {
+        if (p.q < (1ull << 47) && (double)L * 1.25 * (double)p.q < 9007199254740992.0)
+            run(NttArithF<true>(p, tw_all + ((size_t)pi << log_n), twd));
+        else
+            run(ar0);
+    }
+    else
+        run(ar0);
+}
+
+// Row-MAC kernel variant (MHE_KS_EB): 0 = k_ks_row_mac (E = 8, MAC after a transpose back);
+// k_ks_row_mac_e with 2 = E 4 at 3 waves/SIMD (148 VGPRs), 4 = E 4 at 4 waves/SIMD (128 VGPRs,
+// spills), 3 = E 8 at 2 waves/SIMD
+static inline int ks_row_eb()
+{
+    static const int v = [] {
+        const char *f = getenv("MHE_KS_EB");
+        return f ? atoi(f) : 0;
+    }();
+    return v;
+}
+
 // Key prefetch distance of the fused kernel: none (default; measured equal, fewer VGPRs) or one digit ahead (MHE_KS_KPF=1).
 static inline bool ks_key_prefetch()
 {
@@ -1158,37 +1432,57 @@ static inline bool ks_key_prefetch()
 // removed); ResNet-20 (L <= 31): G=1 0.865-0.873 images/s vs 0.832-0.839 with G=2
 template <int LOGR, bool FP>
 static inline void ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
-                                long long twd, int I0, int cnt, int pack, int kpack, hipStream_t st)
+                                long long twd, int I0, int cnt, int pack, int kpack, int share, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
+    const int eb = ks_row_eb();
+    if (eb == 2 || eb == 3 || eb == 4)
+    {
+        const dim3 g(blocks / (eb == 3 ? RowMacShapeE<LOGR, 3>::S : RowMacShapeE<LOGR, 2>::S), cnt, B);
+        share = (share && B > 1 && (g.x * g.y) % 8 == 0) ? 1 : 0;
+        if (eb == 2)
+            hipLaunchKernelGGL((k_ks_row_mac_e<LOGR, FP, 2, 3>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
+                               I0, pack, kpack, share);
+        else if (eb == 4)
+            hipLaunchKernelGGL((k_ks_row_mac_e<LOGR, FP, 2, 4>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
+                               I0, pack, kpack, share);
+        else
+            hipLaunchKernelGGL((k_ks_row_mac_e<LOGR, FP, 3, 2>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
+                               I0, pack, kpack, share);
+        return;
+    }
     const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, B);
+    share = (share && B > 1 && (grid.x * grid.y) % 8 == 0) ? 1 : 0;
     if (ks_key_prefetch())
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
-                           pack, kpack);
+                           pack, kpack, share);
     else
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
-                           pack, kpack);
+                           pack, kpack, share);
 }
 
 template <int LOGR>
 static inline void ks_row_mac_m(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
-                                const NttMode &m, int I0, int cnt, int pack, int kpack, hipStream_t st)
+                                const NttMode &m, int I0, int cnt, int pack, int kpack, int share, hipStream_t st)
 {
     if (m.fp)
-        ks_row_mac_a<LOGR, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, st);
+        ks_row_mac_a<LOGR, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, share, st);
     else
-        ks_row_mac_a<LOGR, false>(P, B, primes, tw, L, K, log_n, 0, I0, cnt, pack, kpack, st);
+        ks_row_mac_a<LOGR, false>(P, B, primes, tw, L, K, log_n, 0, I0, cnt, pack, kpack, share, st);
 }
 
 // Fused row pass + MAC for output primes I0 .. I0+cnt-1 (each entry's inter holds exactly those),
-// over B batch entries.
+// over B batch entries; share: every entry's key pointer is the same (XCD-grouped entries)
 static inline void ks_row_mac_chunk(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K,
-                                    int log_n, const NttMode &m, int I0, int cnt, int pack, int kpack, hipStream_t st)
+                                    int log_n, const NttMode &m, int I0, int cnt, int pack, int kpack, int share,
+                                    hipStream_t st)
 {
     switch (log_n / 2)
     {
-    case 6: ks_row_mac_m<6>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, st); break;
-    case 7: ks_row_mac_m<7>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, st); break;
-    case 8: ks_row_mac_m<8>(P, B, primes, tw, L, K, log_n, m, I0, cnt, (pack && log_n == 16) ? 1 : 0, kpack, st); break;
+    case 6: ks_row_mac_m<6>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, share, st); break;
+    case 7: ks_row_mac_m<7>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, share, st); break;
+    case 8:
+        ks_row_mac_m<8>(P, B, primes, tw, L, K, log_n, m, I0, cnt, (pack && log_n == 16) ? 1 : 0, kpack, share, st);
+        break;
     }
 }

@@ -72,6 +72,7 @@ SIGNATURES = {
     "mhe_mod_switch_drop": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_modraise": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_hmult": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]),
+    "mhe_hmult_batch": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]),
     "mhe_encoder_create": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int]),
     "mhe_encoder_destroy": (ctypes.c_int, [vp]),
     "mhe_ckks_encode": (ctypes.c_int, [vp, vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -392,6 +393,18 @@ class Engine:
         _check(lib().mhe_hmult(self._h, _ptr(a), _ptr(b), _ptr(key), self._key_limbs(key), _ptr(out), L,
                                self.stream()))
         return out
+
+    def hmult_batch(self, a_list, b_list, key, outs=None):
+        """mhe_hmult_batch: len(a_list) independent HMults sharing the relinearization key."""
+        L = a_list[0].shape[1]
+        outs = [self.empty(2, L - 1, self.n) for _ in a_list] if outs is None else outs
+        _check(lib().mhe_hmult_batch(self._h, len(a_list), self._ptrs(a_list), self._ptrs(b_list), _ptr(key),
+                                     self._key_limbs(key), self._ptrs(outs), L, self.stream()))
+        return outs
+
+    def hmult_batch_raw(self, count, a_ptrs, b_ptrs, key_ptr, key_limbs, out_ptrs, L, stream):
+        """Pointer-level batched HMult for the benchmark loop (ctypes pointer arrays)."""
+        return lib().mhe_hmult_batch(self._h, count, a_ptrs, b_ptrs, key_ptr, key_limbs, out_ptrs, L, stream)
 
     def encode(self, values, scale, limbs, out=None, bound_limbs=None):
         """CKKSEncoder::encode -> NTT-form plaintext [limbs][n] on the device.  `bound_limbs`

@@ -15,7 +15,10 @@
 // and one rotation per output element (MatrixMul.cpp:118-188); products whose row or column falls
 // outside the matrices contribute zeros and are skipped.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -314,6 +317,19 @@ void ensure_levels(Ciphertext &c, int levels, Bootstrapper &bt, Evaluator &ev)
         bootstrap(c, r, bt, ev);
         c = r;
     }
+}
+
+// MHE_BLOCK_VERBOSE=1: elapsed seconds since the first call, per block sub-stage
+void block_progress(const char *what)
+{
+    static const bool on = [] {
+        const char *e = std::getenv("MHE_BLOCK_VERBOSE");
+        return e && std::atoi(e) != 0;
+    }();
+    static const auto t0 = std::chrono::steady_clock::now();
+    if (on)
+        std::printf("    %-16s %.2f s\n", what,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
 }
 
 std::vector<double> tiled(const std::vector<double> &v, int rows, int stride, int first_row = 0)
@@ -859,6 +875,7 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
     attn_proj_heads(A, qw, qb, Q, rows, cols, heads, false, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     attn_proj_heads(A, kw, kb, K, rows, cols, heads, false, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     attn_proj_heads(A, vw, vb, V, rows, cols, heads, true, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    block_progress("qkv projections");
     if (!kv_cache.empty())
     {
         if (kv_cache.size() < 2) throw std::invalid_argument("attentionLayer: kv_cache holds K and V");
@@ -870,6 +887,7 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
     for (auto &c : Q) ensure_levels(c, 3, bootstrapper, evaluator);
     for (auto &c : K) ensure_levels(c, 3, bootstrapper, evaluator);
     qk_heads(Q, K, S, rows, dh, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    block_progress("q.k^t");
     std::vector<double> keep_slots(kSlots, 0.0), pin(kSlots, 0.0);
     for (int r = 0; r < rows; r++)
     {
@@ -892,9 +910,11 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
         compute_softmax_rows(s, rows, keep_slots, params.inv_norm > 0 ? params.inv_norm : 1.0 / rows, params.inv_iters,
                              bootstrapper, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     }
+    block_progress("softmax");
     for (auto &c : V) ensure_levels(c, 3, bootstrapper, evaluator);
     for (auto &c : S) ensure_levels(c, 3, bootstrapper, evaluator);
     sv_heads(S, V, pre_out, rows, dh, cols, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    block_progress("s.v");
     for (auto &c : pre_out) ensure_levels(c, 3, bootstrapper, evaluator);
     std::vector<Ciphertext> bias{ b_out };
     row_matmul(pre_out, w_out, bias, outputs, rows, cols, cols, encoder, encryptor, decryptor, evaluator, gal_keys,
@@ -911,6 +931,7 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, C
     for (auto &c : A) ensure_levels(c, 3, bootstrapper, evaluator);
     std::vector<Ciphertext> hidden, bias1{ b1 }, bias2{ b2 };
     row_matmul(A, W1, bias1, hidden, rows, cols, d_ff, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    block_progress("fc");
     for (auto &h : hidden)
     {
         ensure_levels(h, 20, bootstrapper, evaluator);
@@ -919,6 +940,7 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, C
         h = g;
         ensure_levels(h, 3, bootstrapper, evaluator);
     }
+    block_progress("gelu");
     row_matmul(hidden, W2, bias2, outputs, rows, d_ff, cols, encoder, encryptor, decryptor, evaluator, gal_keys,
                relin_keys);
 }
@@ -931,6 +953,17 @@ void transformer_block(std::vector<Ciphertext> &x, BlockWeights &w, const std::v
 {
     // full_gpt2.py:94-147: LN1 -> attention -> residual -> LN2 -> MLP -> residual
     const int T = dims.rows, d = dims.d_model;
+    // MHE_BLOCK_VERBOSE=1: the elapsed time after each stage on stdout
+    static const bool verbose = [] {
+        const char *e = std::getenv("MHE_BLOCK_VERBOSE");
+        return e && std::atoi(e) != 0;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto stage = [&](const char *name) {
+        if (verbose)
+            std::printf("  block stage %-10s done at %.2f s\n", name,
+                        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    };
     const int c = kSlots / (2 * round_to_2(d));
     auto ln = [&](std::vector<Ciphertext> &in, const std::vector<double> &g, const std::vector<double> &b) {
         std::vector<Ciphertext> out(in.size());
@@ -944,19 +977,23 @@ void transformer_block(std::vector<Ciphertext> &x, BlockWeights &w, const std::v
     };
     std::vector<std::vector<Ciphertext>> no_cache;
     std::vector<Ciphertext> ln1 = ln(x, w.ln1_g, w.ln1_b);
+    stage("ln1");
     if (trace) trace->ln1 = ln1;
     std::vector<Ciphertext> attn;
     attentionLayer(ln1, w.qw, w.qb, w.kw, w.kb, w.vw, w.vb, w.ow, w.ob, keep, no_cache, attn, T, d, dims.heads, 0,
                    params, bootstrapper, keygen, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    stage("attention");
     if (trace) trace->attn = attn;
     std::vector<Ciphertext> x1(x.size());
     for (std::size_t i = 0; i < x.size(); i++) evaluator.add_reduced_error(attn[i], x[i], x1[i]);
     if (trace) trace->x1 = x1;
     std::vector<Ciphertext> ln2 = ln(x1, w.ln2_g, w.ln2_b);
+    stage("ln2");
     if (trace) trace->ln2 = ln2;
     std::vector<Ciphertext> ffn;
     FeedForwardLayer(ln2, w.fc_w, w.fc_b, w.pj_w, w.pj_b, ffn, T, d, dims.d_ff, params.gelu_alpha, bootstrapper,
                      encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    stage("ffn");
     if (trace) trace->ffn = ffn;
     y.assign(x.size(), Ciphertext());
     for (std::size_t i = 0; i < x.size(); i++) evaluator.add_reduced_error(ffn[i], x1[i], y[i]);
@@ -995,9 +1032,11 @@ void encrypt_block_weights(const PlainBlockWeights &p, BlockWeights &w, const Bl
     expand_bias_head_row(qb, w.qb, H, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, T);
     expand_bias_head_row(kb, w.kb, H, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, T);
     expand_bias_head_col(vb, w.vb, H, T, dh, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
-    expand_bias(ob, w.ob, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, T);
-    expand_bias(fb, w.fc_b, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, T);
-    expand_bias(pb, w.pj_b, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, T);
+    // one row-packed bias ciphertext serves every output ciphertext: the rows one ciphertext holds
+    auto rows_per_ct = [&](int len) { return std::min(T, kSlots / (2 * round_to_2(len))); };
+    expand_bias(ob, w.ob, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, rows_per_ct(d));
+    expand_bias(fb, w.fc_b, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, rows_per_ct(F));
+    expand_bias(pb, w.pj_b, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, rows_per_ct(d));
     for (auto *v : { &w.qb, &w.kb, &w.vb })
         for (auto &c : *v) drop(c);
     drop(w.ob);

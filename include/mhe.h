@@ -196,6 +196,13 @@ int mhe_modraise(mhe_ctx *ctx, const uint64_t *in, uint64_t *out, int size, int 
  * a, b: [2][L][n] -> out: [2][L-1][n]. */
 int mhe_hmult(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, const uint64_t *relin_key, int key_limbs,
               uint64_t *out, int limbs, void *stream);
+/* mhe_hmult for each i of `count` independent HMults sharing relin_key: out[i] = HMult(a[i], b[i]),
+ * bit-identical to count mhe_hmult calls.  Up to 8 run per key switch, whose key stream is read
+ * once per XCD for all of them (the independent multiply_inplace + relinearize_inplace +
+ * rescale_to_next_inplace calls of the reference's callers, e.g. cnn_seal.cpp:423-430 products
+ * of one layer, or the C2 microbenchmark's loop).  Outputs distinct; a[i] == b[i] squares. */
+int mhe_hmult_batch(mhe_ctx *ctx, int count, const uint64_t *const *a, const uint64_t *const *b,
+                    const uint64_t *relin_key, int key_limbs, uint64_t *const *out, int limbs, void *stream);
 
 /* ---- CKKS encoding (SEAL/ckks.cpp:10-200, SEAL/ckks.h:457-640) ---------------------------
  * An encoder holds CKKSEncoder's constructor tables (index map 5^i, complex roots).  Encoding

@@ -19,8 +19,9 @@ export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o $TAG --output-format csv -- python3 "$R/bench.py" --no-cpu --resnet-images 0 --streams 1 --steps 3 --warmup 1 > gpurun_out/prof.log 2>&1 || exit $?
 find gpurun_out/prof -name "*kernel_trace*" -delete
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "^(k_|void k_)" -d "$R/gpurun_out/pmc/$c" -o pmc --output-format csv -- python3 "$R/bench.py" --no-cpu --resnet-images 0 --streams 1 --steps 1 --warmup 0 --batch 2 > "gpurun_out/pmc/$c.log" 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "^(k_|void k_)" -d "$R/gpurun_out/pmc/$c" -o pmc --output-format csv -- python3 "$R/bench.py" --no-cpu --resnet-images 0 --streams 1 --steps 1 --warmup 0 --batch 8 > "gpurun_out/pmc/$c.log" 2>&1 || exit $?
 done
-python3 scripts/traffic.py gpurun_out/pmc auto gpurun_out/pmc/traffic.json > gpurun_out/pmc/traffic.log 2>&1
+# 8 HMults in the run (one mhe_hmult_batch call, the bench's default launch shape)
+python3 scripts/traffic.py gpurun_out/pmc 8 gpurun_out/pmc/traffic.json > gpurun_out/pmc/traffic.log 2>&1
 find gpurun_out/pmc -name "*.csv" -delete
 exit $rc

@@ -10,6 +10,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <fstream>
 #include <map>
 #include <random>
@@ -86,6 +88,29 @@ static std::map<std::string, double> fixture_header(const std::string &dir)
 int main(int argc, char **argv)
 {
     std::setvbuf(stdout, nullptr, _IONBF, 0);
+    // heartbeat: a line every 30 s so a long block run is never mistaken for a hang
+    const auto t_start = std::chrono::steady_clock::now();
+    std::atomic<bool> done{ false };
+    std::thread beat([&] {
+        int k = 0;
+        while (!done.load())
+        {
+            std::this_thread::sleep_for(std::chrono::milliseconds(200));
+            if (++k % 150 == 0)
+                std::printf("  ... %.0f s\n",
+                            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+        }
+    });
+    struct Join
+    {
+        std::atomic<bool> &d;
+        std::thread &t;
+        ~Join()
+        {
+            d = true;
+            t.join();
+        }
+    } join{ done, beat };
     const std::string dir = argc > 1 ? argv[1] : "tests/golden/gpt2_block";
     // "block": the whole block only (the GPT-2-width fixture, make_fixture.py --full)
     const bool block_only = argc > 2 && std::string(argv[2]) == "block";

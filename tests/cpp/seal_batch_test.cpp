@@ -48,7 +48,13 @@ int main(int argc, char **argv)
     RelinKeys rlk;
     keygen.create_relin_keys(rlk);
     const int slots = (int)N / 2;
-    std::vector<int> steps{ 1, 2, 4, 8, 16, slots - 1, slots - 16 };
+    // +-2^i for i < 5: steps 3, 5 and -7 below have no key of their own (SEAL's NAF path)
+    std::vector<int> steps;
+    for (int i = 0; i < 5; i++)
+    {
+        steps.push_back(1 << i);
+        steps.push_back(slots - (1 << i));
+    }
     GaloisKeys glk;
     keygen.create_galois_keys(steps, glk);
     CKKSEncoder encoder(ctx);

@@ -103,6 +103,53 @@ def test_switch_key_batch(small, L):
         assert np.array_equal(ch.down(dct[i]), ch.oc.switch_key(cts[i], tgs[i], keys[i]))
 
 
+@pytest.mark.parametrize("count", [1, 3, 8, 11])
+def test_hmult_batch(small, count):
+    """mhe_hmult_batch: independent HMults sharing the relinearization key (the XCD-grouped key
+    stream of k_ks_row_mac) equal the oracle's HMult entry for entry, squares included."""
+    ch = small
+    L = ch.K - 1
+    key = ch.rand_key()
+    a = [ch.rand(2, L, ch.n) for _ in range(count)]
+    b = [ch.rand(2, L, ch.n) for _ in range(count)]
+    da = [ch.up(x) for x in a]
+    db = [da[i] if i % 4 == 3 else ch.up(b[i]) for i in range(count)]  # every 4th entry a square
+    outs = ch.eng.hmult_batch(da, db, ch.up(key))
+    for i in range(count):
+        want = ch.oc.hmult(a[i], a[i] if i % 4 == 3 else b[i], key)
+        assert np.array_equal(ch.down(outs[i]), want), i
+
+
+@pytest.mark.parametrize("prepared", [False, True])
+def test_hmult_batch_resnet_size(resnet, prepared):
+    """N = 2^16 (the grid where every tile count is a multiple of 8): 9 HMults in one call (8 + 1)
+    equal one-by-one mhe_hmult, with SEAL's key layout and the prepared 48-bit key."""
+    ch = resnet
+    L = 6
+    key = ch.up(truncated(ch.rand_key(), L))
+    if prepared:
+        key = ch.eng.key_prepare(key)
+    a = [ch.up(ch.rand(2, L, ch.n)) for _ in range(9)]
+    b = [ch.up(ch.rand(2, L, ch.n)) for _ in range(9)]
+    outs = ch.eng.hmult_batch(a, b, key)
+    for i in range(9):
+        assert np.array_equal(ch.down(outs[i]), ch.down(ch.eng.hmult(a[i], b[i], key))), i
+
+
+def test_switch_key_batch_shared_key(small):
+    """A batched key switch whose entries all read one key (XCD-grouped entries) equals the oracle."""
+    ch = small
+    L = 3
+    key = ch.rand_key()
+    dkey = ch.up(key)
+    cts = [ch.rand(2, L, ch.n) for _ in range(8)]
+    tgs = [ch.rand(L, ch.n) for _ in range(8)]
+    dct = [ch.up(c) for c in cts]
+    ch.eng.switch_key_batch(dct, [ch.up(t) for t in tgs], [dkey] * 8)
+    for i in range(8):
+        assert np.array_equal(ch.down(dct[i]), ch.oc.switch_key(cts[i], tgs[i], key))
+
+
 def test_batch_errors(small):
     ch = small
     L = 3
@@ -118,6 +165,8 @@ def test_batch_errors(small):
         ch.eng.apply_galois_batch([a], [4], [key])
     with pytest.raises(mhe.MheError):
         ch.eng.rescale_batch([a], outs=[a])
+    with pytest.raises(mhe.MheError, match="distinct"):
+        ch.eng.hmult_batch([a, a], [a, a], key, outs=[o, o])
 
 
 @pytest.mark.parametrize("log_n", [13, 16])
