@@ -712,6 +712,43 @@ private:
     SecretKey sk_;
 };
 
+// (not SEAL API) Lockstep: threads that evaluate the same operation sequence on different data (the
+// images of a batch) join one group.  While joined, every top-level rotation (rotate_vector[s],
+// rotate_vector_inplace), relinearization (relinearize_inplace, and the one inside
+// multiply_[inplace_]reduced_error) and rescale_to_next_inplace of a member waits for the
+// same-numbered call of every other member, and all of them run as one batched launch sequence on
+// one stream: entries of one rotation key together, so k_ks_row_mac reads each key once for all
+// members, and at low levels one launch fills the chip that one image's could not.  Results are
+// word for word those of the unbatched calls.  A member that leaves (scope end, exception) is no
+// longer waited for; calls whose kinds differ within a round run one by one.
+struct LsOp;
+class Lockstep
+{
+public:
+    explicit Lockstep(std::size_t members);
+    ~Lockstep();
+    Lockstep(const Lockstep &) = delete;
+    Lockstep &operator=(const Lockstep &) = delete;
+    // RAII membership of the calling thread
+    class Member
+    {
+    public:
+        explicit Member(Lockstep &group);
+        ~Member();
+        Member(const Member &) = delete;
+        Member &operator=(const Member &) = delete;
+
+    private:
+        Lockstep &g_;
+    };
+    std::size_t rounds() const;        // batched rounds run so far
+    std::size_t merged_calls() const;  // member calls that ran inside a merged round
+    struct Impl;
+
+private:
+    std::unique_ptr<Impl> impl_;
+};
+
 class Evaluator
 {
 public:
@@ -877,6 +914,10 @@ private:
     void switch_key(Ciphertext &encrypted, const std::uint64_t *target_dev, const KSwitchKeys &keys,
                     std::size_t index) const;
     void rotate_internal(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys) const;
+    // Lockstep: hand `op` to the calling thread's group (false: no group, run it directly)
+    bool lockstep_submit(LsOp &op) const;
+    friend struct Lockstep::Impl;
+    void lockstep_execute(std::vector<LsOp *> &ops) const;
     std::size_t limbs_of(const parms_id_type &id) const;
     SEALContext context_;
     CKKSEncoder &encoder_;

@@ -51,6 +51,22 @@ struct Ops
     RelinKeys &relin_keys;
 };
 
+// The limbs a matrix product's operands are dropped to before it runs: the product and the mask
+// take two levels, and two limbs stay so the next bootstrap can prescale (gpt2.cpp).  Key
+// switches cost ~L^2, so a product on a freshly bootstrapped (22-limb) operand is ~15x the cost
+// at 5 limbs; dropping limbs does not change the values.  The second operand (weights, K, V) is
+// kept one level above the first, so every product takes multiply_reduced_error's unequal-level
+// path, which rescales it to the first operand's scale (evaluator.cpp:312-362) -- at equal levels
+// the reduced-error product would overwrite that scale instead.
+constexpr int kMatmulLimbs = 5;
+
+Ciphertext dropped(const Ciphertext &c, int limbs, Evaluator &ev)
+{
+    Ciphertext r = c;
+    while ((int)r.coeff_modulus_size() > limbs) ev.mod_switch_to_next_inplace(r);
+    return r;
+}
+
 constexpr std::size_t kBatch = 8; // independent ciphertexts per batched launch (MHE_MAXB)
 
 struct Accum
@@ -246,8 +262,17 @@ void packed_matmul(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, int A
     if ((long)A.size() * c < A_rows) throw std::invalid_argument("packed_matmul: too few input ciphertexts");
     if ((long)W.size() * c < W_cols) throw std::invalid_argument("packed_matmul: too few weight ciphertexts");
     Placer pl(o);
-    Ciphertext rolled;
+    Ciphertext rolled, Wj;
     std::vector<Ciphertext> prods;
+    // operands at the fewest limbs the product needs (kMatmulLimbs), W one level above A
+    std::vector<Ciphertext> Ad(A.size());
+    int la = kMatmulLimbs;
+    for (std::size_t i = 0; i < A.size(); i++)
+    {
+        Ad[i] = dropped(A[i], kMatmulLimbs, o.evaluator);
+        la = std::min(la, (int)Ad[i].coeff_modulus_size());
+    }
+    std::size_t wj = W.size();
     for (std::size_t j = 0; j < W.size(); j++)
         for (int rots = 0; rots < c; rots++)
         {
@@ -260,15 +285,20 @@ void packed_matmul(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, int A
                 if (any) is.push_back(i);
             }
             if (is.empty()) continue;
+            if (wj != j)
+            {
+                Wj = dropped(W[j], la + 1, o.evaluator);
+                wj = j;
+            }
             if (rots)
-                o.evaluator.rotate_vector(W[j], rots * SA, o.gal_keys, rolled);
+                o.evaluator.rotate_vector(Wj, rots * SA, o.gal_keys, rolled);
             else
-                rolled = W[j];
+                rolled = Wj;
             for (std::size_t b0 = 0; b0 < is.size(); b0 += kBatch)
             {
                 const std::size_t nb = std::min(kBatch, is.size() - b0);
                 std::vector<const Ciphertext *> a(nb), w(nb, &rolled);
-                for (std::size_t b = 0; b < nb; b++) a[b] = &A[is[b0 + b]];
+                for (std::size_t b = 0; b < nb; b++) a[b] = &Ad[is[b0 + b]];
                 products(a, w, prods, o);
                 fold_many(prods, R, R, o);
                 for (std::size_t b = 0; b < nb; b++)
@@ -622,7 +652,8 @@ void qk_heads(std::vector<Ciphertext> &Q, std::vector<Ciphertext> &K, std::vecto
     std::vector<Ciphertext> rolled, prods;
     for (std::size_t h = 0; h < Q.size(); h++)
     {
-        dup = K[h];
+        const Ciphertext q = dropped(Q[h], kMatmulLimbs, o.evaluator);
+        dup = dropped(K[h], (int)q.coeff_modulus_size() + 1, o.evaluator);
         replicate(dup, P, o);
         Placer pl(o);
         for (int r0 = 0; r0 < rows; r0 += (int)kBatch)
@@ -631,7 +662,7 @@ void qk_heads(std::vector<Ciphertext> &Q, std::vector<Ciphertext> &K, std::vecto
             std::vector<int> steps(nb);
             for (int b = 0; b < nb; b++) steps[b] = (r0 + b) * 2 * dh;
             rotations_of(dup, steps, rolled, o);
-            std::vector<const Ciphertext *> a(nb, &Q[h]), w(nb);
+            std::vector<const Ciphertext *> a(nb, &q), w(nb);
             for (int b = 0; b < nb; b++) w[b] = &rolled[b];
             products(a, w, prods, o);
             fold_many(prods, dh, dh, o);
@@ -667,7 +698,8 @@ void sv_heads(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vecto
     std::vector<Ciphertext> rolled, prods;
     for (std::size_t h = 0; h < S.size(); h++)
     {
-        dup = V[h];
+        const Ciphertext sc = dropped(S[h], kMatmulLimbs, o.evaluator);
+        dup = dropped(V[h], (int)sc.coeff_modulus_size() + 1, o.evaluator);
         replicate(dup, P, o);
         for (int r0 = 0; r0 < dh; r0 += (int)kBatch)
         {
@@ -675,7 +707,7 @@ void sv_heads(std::vector<Ciphertext> &S, std::vector<Ciphertext> &V, std::vecto
             std::vector<int> steps(nb);
             for (int b = 0; b < nb; b++) steps[b] = (r0 + b) * 2 * rows;
             rotations_of(dup, steps, rolled, o);
-            std::vector<const Ciphertext *> a(nb, &S[h]), w(nb);
+            std::vector<const Ciphertext *> a(nb, &sc), w(nb);
             for (int b = 0; b < nb; b++) w[b] = &rolled[b];
             products(a, w, prods, o);
             fold_many(prods, rows, rows, o);

@@ -726,7 +726,18 @@ std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vecto
     std::atomic<std::size_t> next{ 0 };
     std::exception_ptr err;
     std::mutex err_mu;
+    // MHE_RESNET_LOCKSTEP=1: the images in flight run their key switches and rescales as one
+    // batched launch per operation (seal::Lockstep)
+    static const bool lockstep = [] {
+        const char *e = std::getenv("MHE_RESNET_LOCKSTEP");
+        return e && std::atoi(e) != 0;
+    }();
+    const int nthreads = std::max(1, threads);
+    std::unique_ptr<seal::Lockstep> group;
+    if (lockstep && nthreads > 1) group = std::make_unique<seal::Lockstep>((std::size_t)nthreads);
     auto work = [&] {
+        std::unique_ptr<seal::Lockstep::Member> member;
+        if (group) member = std::make_unique<seal::Lockstep::Member>(*group);
         try
         {
             for (std::size_t i; (i = next.fetch_add(1)) < images.size();) out[i] = infer(images[i]);
@@ -738,8 +749,10 @@ std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vecto
         }
     };
     std::vector<std::thread> pool;
-    for (int t = 0; t < std::max(1, threads); t++) pool.emplace_back(work);
+    for (int t = 0; t < nthreads; t++) pool.emplace_back(work);
     for (auto &t : pool) t.join();
+    if (group && std::getenv("MHE_RESNET_LOCKSTEP_STATS"))
+        std::fprintf(stderr, "lockstep: %zu rounds, %zu member calls merged\n", group->rounds(), group->merged_calls());
     if (err) std::rethrow_exception(err);
     return out;
 }

@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <exception>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -65,6 +67,37 @@ private:
     if (trace_op_.top()) trace_op_.extra = (S)
 
 const parms_id_type parms_id_zero = { 0, 0, 0, 0 };
+
+struct LsOp
+{
+    enum Kind
+    {
+        ROT,
+        RESC,
+        RELIN,
+        MULRE
+    } kind = ROT;
+    std::vector<const Ciphertext *> in, in2;
+    std::vector<int> steps;
+    std::vector<Ciphertext *> out;
+    const GaloisKeys *gk = nullptr;
+    const RelinKeys *rk = nullptr;
+    const Evaluator *ev = nullptr;
+    std::exception_ptr err;
+};
+
+namespace
+{
+thread_local Lockstep::Impl *tl_ls = nullptr; // the calling thread's group
+thread_local int tl_ls_direct = 0;            // > 0 inside a round's execution: calls run directly
+struct LsDirect
+{
+    LsDirect() { ++tl_ls_direct; }
+    ~LsDirect() { --tl_ls_direct; }
+};
+} // namespace
+
+
 
 namespace
 {
@@ -1781,6 +1814,14 @@ void Evaluator::switch_key(Ciphertext &encrypted, const std::uint64_t *target, c
 
 void Evaluator::relinearize_inplace(Ciphertext &encrypted, const RelinKeys &relin_keys, MemoryPoolHandle) const
 {
+    if (tl_ls)
+    {
+        LsOp op;
+        op.kind = LsOp::RELIN;
+        op.out = { &encrypted };
+        op.rk = &relin_keys;
+        if (lockstep_submit(op)) return;
+    }
     TRACE_OP("relinearize", trace::ct(encrypted), trace::ct(encrypted));
     // relinearize_internal (evaluator.cpp:1061-1116)
     Level lv = check_ct(context_, encrypted, "encrypted");
@@ -1938,6 +1979,13 @@ void Evaluator::rescale_to_next(const Ciphertext &encrypted, Ciphertext &destina
 
 void Evaluator::rescale_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
 {
+    if (tl_ls)
+    {
+        LsOp op;
+        op.kind = LsOp::RESC;
+        op.out = { &encrypted };
+        if (lockstep_submit(op)) return;
+    }
     rescale_to_next(encrypted, encrypted);
 }
 
@@ -2110,6 +2158,16 @@ void Evaluator::rotate_internal(Ciphertext &encrypted, int steps, const GaloisKe
 void Evaluator::rotate_vector_inplace(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                                       MemoryPoolHandle) const
 {
+    if (tl_ls)
+    {
+        LsOp op;
+        op.kind = LsOp::ROT;
+        op.in = { &encrypted };
+        op.steps = { steps };
+        op.out = { &encrypted };
+        op.gk = &galois_keys;
+        if (lockstep_submit(op)) return;
+    }
     TRACE_OP("rotate", trace::ct(encrypted), trace::ct(encrypted));
     TRACE_EXTRA("\"step\": " + std::to_string(steps));
     rotate_internal(encrypted, steps, galois_keys);
@@ -2139,6 +2197,16 @@ void Evaluator::apply_galois_to(const Ciphertext &encrypted, std::uint32_t galoi
 void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                               Ciphertext &destination, MemoryPoolHandle) const
 {
+    if (tl_ls)
+    {
+        LsOp op;
+        op.kind = LsOp::ROT;
+        op.in = { &encrypted };
+        op.steps = { steps };
+        op.out = { &destination };
+        op.gk = &galois_keys;
+        if (lockstep_submit(op)) return;
+    }
     TRACE_OP("rotate", trace::ct(destination), trace::ct(encrypted));
     TRACE_EXTRA("\"step\": " + std::to_string(steps));
     if (&encrypted != &destination && steps != 0)
@@ -2154,9 +2222,176 @@ void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const Galo
     rotate_vector_inplace(destination, steps, galois_keys);
 }
 
+// ------------------------------------------------------------------------------ Lockstep
+struct Lockstep::Impl
+{
+    std::mutex mu;
+    std::condition_variable cv;
+    std::size_t active;
+    std::size_t arrived = 0;
+    std::uint64_t round = 0;
+    std::size_t rounds_run = 0, merged = 0;
+    std::vector<LsOp *> reqs;
+    explicit Impl(std::size_t m) : active(m) {}
+    // called with mu held once every active member has arrived: runs the round, wakes the members
+    void run_round(std::unique_lock<std::mutex> &lk)
+    {
+        std::vector<LsOp *> batch;
+        batch.swap(reqs);
+        lk.unlock();
+        {
+            LsDirect d;
+            batch[0]->ev->lockstep_execute(batch);
+        }
+        lk.lock();
+        arrived = 0;
+        round++;
+        rounds_run++;
+        if (batch.size() > 1) merged += batch.size();
+        cv.notify_all();
+    }
+};
+
+Lockstep::Lockstep(std::size_t members) : impl_(std::make_unique<Impl>(members)) {}
+Lockstep::~Lockstep() = default;
+std::size_t Lockstep::rounds() const
+{
+    std::lock_guard<std::mutex> g(impl_->mu);
+    return impl_->rounds_run;
+}
+std::size_t Lockstep::merged_calls() const
+{
+    std::lock_guard<std::mutex> g(impl_->mu);
+    return impl_->merged;
+}
+
+Lockstep::Member::Member(Lockstep &group) : g_(group) { tl_ls = group.impl_.get(); }
+
+Lockstep::Member::~Member()
+{
+    tl_ls = nullptr;
+    Impl *g = g_.impl_.get();
+    std::unique_lock<std::mutex> lk(g->mu);
+    if (g->active) g->active--;
+    if (g->arrived > 0 && g->arrived >= g->active) g->run_round(lk);
+}
+
+bool Evaluator::lockstep_submit(LsOp &op) const
+{
+    Lockstep::Impl *g = tl_ls;
+    if (!g || tl_ls_direct > 0 || trace::enabled()) return false;
+    op.ev = this;
+    std::unique_lock<std::mutex> lk(g->mu);
+    const std::uint64_t r = g->round;
+    g->reqs.push_back(&op);
+    if (++g->arrived >= g->active)
+        g->run_round(lk);
+    else
+        g->cv.wait(lk, [&] { return g->round != r; });
+    lk.unlock();
+    if (op.err) std::rethrow_exception(op.err);
+    return true;
+}
+
+void Evaluator::lockstep_execute(std::vector<LsOp *> &ops) const
+{
+    // one member's call as it would have run alone
+    auto run_one = [&](LsOp &o) {
+        try
+        {
+            switch (o.kind)
+            {
+            case LsOp::ROT:
+                if (o.in.size() == 1 && o.out[0] == o.in[0])
+                    rotate_vector_inplace(*o.out[0], o.steps[0], *o.gk);
+                else if (o.in.size() == 1)
+                    rotate_vector(*o.in[0], o.steps[0], *o.gk, *o.out[0]);
+                else
+                    rotate_vectors(o.in, o.steps, *o.gk, o.out);
+                break;
+            case LsOp::RESC: rescale_to_next_inplace_many(o.out); break;
+            case LsOp::RELIN: relinearize_inplace_many(o.out, *o.rk); break;
+            case LsOp::MULRE:
+                if (o.out[0] == o.in[0])
+                    multiply_inplace_reduced_error(*o.out[0], *o.in2[0], *o.rk);
+                else
+                    multiply_reduced_error(*o.in[0], *o.in2[0], *o.rk, *o.out[0]);
+                break;
+            }
+        }
+        catch (...)
+        {
+            o.err = std::current_exception();
+        }
+    };
+    bool same = ops.size() > 1;
+    for (LsOp *o : ops) same = same && o->kind == ops[0]->kind && o->gk == ops[0]->gk && o->rk == ops[0]->rk;
+    if (!same)
+    {
+        for (LsOp *o : ops) run_one(*o);
+        return;
+    }
+    try
+    {
+        // the members' entries as one batch; an output that is also an input (in place) or repeated
+        // goes through a temporary
+        std::vector<const Ciphertext *> in, in2;
+        std::vector<int> steps;
+        std::vector<Ciphertext *> out, dst;
+        for (LsOp *o : ops)
+        {
+            in.insert(in.end(), o->in.begin(), o->in.end());
+            in2.insert(in2.end(), o->in2.begin(), o->in2.end());
+            steps.insert(steps.end(), o->steps.begin(), o->steps.end());
+            dst.insert(dst.end(), o->out.begin(), o->out.end());
+        }
+        const LsOp::Kind kind = ops[0]->kind;
+        if (kind == LsOp::RESC)
+        {
+            rescale_to_next_inplace_many(dst);
+            return;
+        }
+        if (kind == LsOp::RELIN)
+        {
+            relinearize_inplace_many(dst, *ops[0]->rk);
+            return;
+        }
+        std::vector<Ciphertext> tmp(dst.size());
+        out = dst;
+        for (std::size_t i = 0; i < dst.size(); i++)
+        {
+            bool alias = false;
+            for (std::size_t j = 0; j < dst.size() && !alias; j++)
+                alias = dst[i] == in[j] || (kind == LsOp::MULRE && dst[i] == in2[j]) || (j != i && dst[i] == dst[j]);
+            if (alias) out[i] = &tmp[i];
+        }
+        if (kind == LsOp::ROT)
+            rotate_vectors(in, steps, *ops[0]->gk, out);
+        else
+            multiply_reduced_error_many(in, in2, *ops[0]->rk, out);
+        for (std::size_t i = 0; i < dst.size(); i++)
+            if (out[i] != dst[i]) *dst[i] = std::move(tmp[i]);
+    }
+    catch (...)
+    {
+        const std::exception_ptr e = std::current_exception();
+        for (LsOp *o : ops) o->err = e;
+    }
+}
+
 void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted, const std::vector<int> &steps,
                                const GaloisKeys &galois_keys, const std::vector<Ciphertext *> &destinations) const
 {
+    if (tl_ls)
+    {
+        LsOp op;
+        op.kind = LsOp::ROT;
+        op.in = encrypted;
+        op.steps = steps;
+        op.out = destinations;
+        op.gk = &galois_keys;
+        if (lockstep_submit(op)) return;
+    }
     if (encrypted.size() != steps.size() || encrypted.size() != destinations.size())
         throw std::invalid_argument("encrypted, steps and destinations must have the same size");
     for (std::size_t i = 0; i < destinations.size(); i++)
@@ -2188,11 +2423,7 @@ void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted,
     }
     void *s = context_.stream();
     std::vector<bool> done(encrypted.size(), false);
-    for (auto &g : groups)
-    {
-        const std::vector<std::size_t> &idx = g.second;
-        if (idx.size() < 2) continue;
-        const std::size_t L = g.first;
+    auto launch = [&](const std::vector<std::size_t> &idx, std::size_t L) {
         std::vector<const std::uint64_t *> in, keys;
         std::vector<std::uint64_t *> out;
         std::vector<std::uint32_t> elts;
@@ -2218,6 +2449,22 @@ void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted,
         chk(mhe_apply_galois_batch(context_.engine(), (int)idx.size(), in.data(), out.data(), elts.data(), keys.data(),
                                    kls.data(), (int)L, s));
         for (std::size_t i : idx) done[i] = true;
+    };
+    for (auto &g : groups)
+    {
+        std::vector<std::size_t> idx = g.second;
+        if (idx.size() < 2) continue;
+        // entries of one key side by side; when every key has several entries (the members of a
+        // Lockstep group), one launch per key, so its entries share the key stream (k_ks_row_mac)
+        std::stable_sort(idx.begin(), idx.end(), [&](std::size_t a, std::size_t b) { return elt[a] < elt[b]; });
+        std::map<std::uint32_t, std::vector<std::size_t>> by_elt;
+        for (std::size_t i : idx) by_elt[elt[i]].push_back(i);
+        bool shared = by_elt.size() > 1;
+        for (auto &e : by_elt) shared = shared && e.second.size() >= 2;
+        if (shared)
+            for (auto &e : by_elt) launch(e.second, g.first);
+        else
+            launch(idx, g.first);
     }
     for (std::size_t i = 0; i < encrypted.size(); i++)
         if (!done[i]) rotate_vector(*encrypted[i], steps[i], galois_keys, *destinations[i]);
@@ -2625,6 +2872,16 @@ void Evaluator::reduced_error_op(Ciphertext &encrypted1, const Ciphertext &encry
 void Evaluator::reduced_error_out(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination,
                                   Rmode mode, const RelinKeys *relin_keys) const
 {
+    if (tl_ls && mode == Rmode::mul)
+    {
+        LsOp op;
+        op.kind = LsOp::MULRE;
+        op.in = { &encrypted1 };
+        op.in2 = { &encrypted2 };
+        op.out = { &destination };
+        op.rk = relin_keys;
+        if (lockstep_submit(op)) return;
+    }
     TRACE_OP(mode == Rmode::add ? "add_re" : mode == Rmode::sub ? "sub_re" : "mul_re", trace::ct(destination),
              trace::ct(encrypted1), trace::ct(encrypted2));
     // equal levels: encrypted1 takes encrypted2's scale, then the op (reduced_error_op); written
@@ -2677,6 +2934,16 @@ void Evaluator::sub_inplace_reduced_error(Ciphertext &encrypted1, const Cipherte
 void Evaluator::multiply_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2,
                                                const RelinKeys &relin_keys) const
 {
+    if (tl_ls)
+    {
+        LsOp op;
+        op.kind = LsOp::MULRE;
+        op.in = { &encrypted1 };
+        op.in2 = { &encrypted2 };
+        op.out = { &encrypted1 };
+        op.rk = &relin_keys;
+        if (lockstep_submit(op)) return;
+    }
     TRACE_OP("mul_re", trace::ct(encrypted1), trace::ct(encrypted1), trace::ct(encrypted2));
     reduced_error_op(encrypted1, encrypted2, Rmode::mul);
     relinearize_inplace(encrypted1, relin_keys);

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 
 using namespace seal;
 
@@ -161,6 +162,61 @@ int main(int argc, char **argv)
             ok = ok && same(M[i], W[i]);
         }
         check("multiply_reduced_error_many == multiply_reduced_error (12 entries, equal and unequal levels)", ok);
+
+        // Lockstep group: 4 threads run one operation sequence on their own inputs; the group
+        // merges their rotations, relinearizations, reduced-error products and rescales into
+        // batched launches.  Every result equals the sequence run alone, including a member with
+        // an extra operation (misaligned rounds) and one that leaves after half the sequence.
+        {
+            constexpr int M = 4;
+            std::vector<Ciphertext> x0, y0;
+            for (int m = 0; m < M; m++)
+            {
+                x0.push_back(fresh(0));
+                y0.push_back(fresh(0));
+            }
+            auto sequence = [&](int m, std::vector<Ciphertext> &res) {
+                Ciphertext x = x0[m], y = y0[m], r1, r2, t;
+                ev.rotate_vector(x, 1, glk, r1);                 // keyed
+                ev.rotate_vector_inplace(y, 3, glk);             // NAF-composed
+                std::vector<Ciphertext> rr(2);
+                ev.rotate_vectors({ &x, &y }, { 2, slots - 1 }, glk, { &rr[0], &rr[1] });
+                ev.multiply_reduced_error(r1, rr[0], rlk, t);    // product + relinearization
+                ev.rescale_to_next_inplace(t);
+                if (m == 1) ev.rotate_vector_inplace(t, 4, glk); // misaligns this member's rounds
+                ev.multiply_inplace_reduced_error(y, rr[1], rlk);
+                ev.rescale_to_next_inplace(y);
+                res = { r1, y, rr[0], rr[1], t };
+                if (m == 3) return;                              // leaves early
+                Ciphertext sq;
+                ev.square(t, sq);
+                ev.relinearize_inplace(sq, rlk);
+                ev.rescale_to_next_inplace(sq);
+                ev.rotate_vector_inplace(sq, slots - 16, glk);
+                res.push_back(sq);
+            };
+            std::vector<std::vector<Ciphertext>> alone(M), grouped(M);
+            for (int m = 0; m < M; m++) sequence(m, alone[m]);
+            Lockstep group(M);
+            {
+                std::vector<std::thread> th;
+                for (int m = 0; m < M; m++)
+                    th.emplace_back([&, m] {
+                        Lockstep::Member member(group);
+                        sequence(m, grouped[m]);
+                    });
+                for (auto &t : th) t.join();
+            }
+            bool ok = true;
+            for (int m = 0; m < M; m++)
+            {
+                ok = ok && alone[m].size() == grouped[m].size();
+                for (std::size_t i = 0; ok && i < alone[m].size(); i++) ok = same(alone[m][i], grouped[m][i]);
+            }
+            std::printf("lockstep: %zu rounds, %zu member calls merged\n", group.rounds(), group.merged_calls());
+            check("Lockstep group (4 threads; rotations, relinearizations, products, rescales merged) == each alone",
+                  ok && group.merged_calls() > 0);
+        }
 
         bool threw = false;
         try
