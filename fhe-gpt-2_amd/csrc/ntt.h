@@ -545,7 +545,10 @@ struct KsPtrs
 };
 
 template <int LOGR, int LOGT, bool FP>
-__global__ __launch_bounds__(256, 3) void k_modup_col(KsPtrs P, const PrimeDev *__restrict__ primes,
+#ifndef MHE_MODUP_OCC
+#define MHE_MODUP_OCC 3 // waves per SIMD the ModUp column pass is compiled for (168 VGPRs)
+#endif
+__global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                    const Tw *__restrict__ tw_all, int L, int K, int log_n,
                                                    long long twd, int I0, int Icnt, int pack, int X, int IG, int xcd)
 {

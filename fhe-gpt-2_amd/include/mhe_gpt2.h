@@ -216,10 +216,13 @@ struct PlainBlockWeights
     // row-major [in][out] as GPT-2's Conv1D (x W + b)
     std::vector<double> ln1_g, ln1_b, qw, qb, kw, kb, vw, vb, ow, ob, ln2_g, ln2_b, fc_w, fc_b, pj_w, pj_b;
 };
+// The FFN hidden state is held in d_model-wide column chunks, each row-packed like the block's input
+// (FeedForwardLayer): fc_b holds one bias ciphertext per chunk, pj_w the packed W2 rows of chunk 0,
+// then chunk 1, ...
 struct BlockWeights
 {
-    std::vector<Ciphertext> qw, qb, kw, kb, vw, vb, ow, fc_w, pj_w;
-    Ciphertext ob, fc_b, pj_b;
+    std::vector<Ciphertext> qw, qb, kw, kb, vw, vb, ow, fc_w, fc_b, pj_w;
+    Ciphertext ob, pj_b;
     std::vector<double> ln1_g, ln1_b, ln2_g, ln2_b;
 };
 struct BlockTrace
@@ -300,7 +303,7 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
                     const AttentionParams &params, Bootstrapper &bootstrapper, seal::KeyGenerator &keygen,
                     CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator,
                     GaloisKeys &gal_keys, RelinKeys &relin_keys);
-void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, Ciphertext b1,
+void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, std::vector<Ciphertext> &b1,
                       std::vector<Ciphertext> &W2, Ciphertext b2, std::vector<Ciphertext> &outputs, int rows, int cols,
                       int d_ff, double gelu_alpha, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
                       Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,

@@ -725,15 +725,18 @@ struct LsOp;
 class Lockstep
 {
 public:
+    struct Impl;
     explicit Lockstep(std::size_t members);
     ~Lockstep();
     Lockstep(const Lockstep &) = delete;
     Lockstep &operator=(const Lockstep &) = delete;
-    // RAII membership of the calling thread
+    // RAII membership of the calling thread; an inactive member's calls run directly except inside
+    // an Active scope (all members must open and close their Active scopes at the same points of
+    // their operation sequences)
     class Member
     {
     public:
-        explicit Member(Lockstep &group);
+        explicit Member(Lockstep &group, bool active = true);
         ~Member();
         Member(const Member &) = delete;
         Member &operator=(const Member &) = delete;
@@ -741,9 +744,20 @@ public:
     private:
         Lockstep &g_;
     };
+    // merge the calling member's operations for this scope (no-op outside a group)
+    class Active
+    {
+    public:
+        Active();
+        ~Active();
+        Active(const Active &) = delete;
+        Active &operator=(const Active &) = delete;
+
+    private:
+        Impl *saved_;
+    };
     std::size_t rounds() const;        // batched rounds run so far
     std::size_t merged_calls() const;  // member calls that ran inside a merged round
-    struct Impl;
 
 private:
     std::unique_ptr<Impl> impl_;

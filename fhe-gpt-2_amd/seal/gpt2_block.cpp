@@ -254,14 +254,13 @@ struct Target
     double factor;
 };
 template <class Sink>
-void packed_matmul(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, int A_rows, int A_cols, int W_cols,
-                   std::size_t n_out, std::vector<Ciphertext> &outputs, Sink sink, Ops &o)
+void packed_matmul_into(Placer &pl, const std::vector<Ciphertext> &A, const std::vector<Ciphertext> &W, int A_rows,
+                        int A_cols, int W_cols, std::size_t n_out, Sink sink, Ops &o)
 {
     const int R = round_to_2(A_cols), SA = 2 * R, c = kSlots / SA;
     if (A_cols < 1 || SA > kSlots) throw std::invalid_argument("packed_matmul: A_cols out of range");
     if ((long)A.size() * c < A_rows) throw std::invalid_argument("packed_matmul: too few input ciphertexts");
     if ((long)W.size() * c < W_cols) throw std::invalid_argument("packed_matmul: too few weight ciphertexts");
-    Placer pl(o);
     Ciphertext rolled, Wj;
     std::vector<Ciphertext> prods;
     // operands at the fewest limbs the product needs (kMatmulLimbs), W one level above A
@@ -317,6 +316,14 @@ void packed_matmul(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, int A
                 }
             }
         }
+}
+
+template <class Sink>
+void packed_matmul(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W, int A_rows, int A_cols, int W_cols,
+                   std::size_t n_out, std::vector<Ciphertext> &outputs, Sink sink, Ops &o)
+{
+    Placer pl(o);
+    packed_matmul_into(pl, A, W, A_rows, A_cols, W_cols, n_out, sink, o);
     pl.finish(outputs, n_out);
 }
 
@@ -953,16 +960,32 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
                relin_keys);
 }
 
-void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, Ciphertext b1,
+void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, std::vector<Ciphertext> &b1,
                       std::vector<Ciphertext> &W2, Ciphertext b2, std::vector<Ciphertext> &outputs, int rows, int cols,
                       int d_ff, double gelu_alpha, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
                       Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
                       RelinKeys &relin_keys)
 {
-    // layers.cpp:3-24 (layers.py:93-116): dense to d_ff, GELU, dense back, biases after each
-    for (auto &c : A) ensure_levels(c, 3, bootstrapper, evaluator);
-    std::vector<Ciphertext> hidden, bias1{ b1 }, bias2{ b2 };
-    row_matmul(A, W1, bias1, hidden, rows, cols, d_ff, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+    // layers.cpp:3-24 (layers.py:93-116): dense to d_ff, GELU, dense back, biases after each.  The
+    // hidden state is held in `cols`-wide column chunks, each row-packed like the input: FC1 then
+    // places every element inside its own row's window (one mask per folded product instead of one
+    // per output row; the reference's stride-2*d_ff layout would need a rotation group per row), GELU
+    // is elementwise, and FC2 sums the chunks' products (chunk k times rows k*cols.. of W2) into one
+    // placement.  W2 / b1 come chunked from encrypt_block_weights.
+    Ops o{ encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys };
+    const int SA = 2 * round_to_2(cols), c = kSlots / SA, cpc = (rows + c - 1) / c;
+    const int nchunk = (d_ff + cols - 1) / cols, wpc = (cols + c - 1) / c;
+    if ((int)b1.size() != nchunk) throw std::invalid_argument("FeedForwardLayer: one FC1 bias per hidden chunk");
+    if ((int)W2.size() != nchunk * wpc) throw std::invalid_argument("FeedForwardLayer: W2 must be packed per chunk");
+    for (auto &x : A) ensure_levels(x, 3, bootstrapper, evaluator);
+    std::vector<Ciphertext> hidden;
+    packed_matmul(A, W1, rows, cols, d_ff, (std::size_t)(nchunk * cpc), hidden,
+                  [&](int row, int col) {
+                      return Target{ (col / cols) * cpc + row / c, (row % c) * SA + col % cols, 1.0 };
+                  },
+                  o);
+    for (int k = 0; k < nchunk; k++)
+        for (int i = 0; i < cpc; i++) evaluator.add_inplace_reduced_error(hidden[(std::size_t)(k * cpc + i)], b1[k]);
     block_progress("fc");
     for (auto &h : hidden)
     {
@@ -973,8 +996,17 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, C
         ensure_levels(h, 3, bootstrapper, evaluator);
     }
     block_progress("gelu");
-    row_matmul(hidden, W2, bias2, outputs, rows, d_ff, cols, encoder, encryptor, decryptor, evaluator, gal_keys,
-               relin_keys);
+    Placer pl(o);
+    for (int k = 0; k < nchunk; k++)
+    {
+        std::vector<Ciphertext> hk(hidden.begin() + k * cpc, hidden.begin() + (k + 1) * cpc);
+        std::vector<Ciphertext> wk(W2.begin() + k * wpc, W2.begin() + (k + 1) * wpc);
+        packed_matmul_into(pl, hk, wk, rows, cols, cols, (std::size_t)cpc,
+                           [&](int row, int col) { return Target{ row / c, (row % c) * SA + col, 1.0 }; }, o);
+    }
+    pl.finish(outputs, (std::size_t)cpc);
+    std::vector<Ciphertext> bias2{ b2 };
+    add_bias(outputs, bias2, evaluator);
 }
 
 void transformer_block(std::vector<Ciphertext> &x, BlockWeights &w, const std::vector<std::vector<double>> &keep,
@@ -1056,7 +1088,18 @@ void encrypt_block_weights(const PlainBlockWeights &p, BlockWeights &w, const Bl
     pack_w(p.vw, d, d, w.vw);
     pack_w(p.ow, d, d, w.ow);
     pack_w(p.fc_w, d, F, w.fc_w);
-    pack_w(p.pj_w, F, d, w.pj_w);
+    // W2 (F x d) by d-row chunks (FeedForwardLayer's hidden chunks), the last one zero-padded to d rows
+    const int nchunk = (F + d - 1) / d;
+    w.pj_w.clear();
+    for (int k = 0; k < nchunk; k++)
+    {
+        std::vector<double> wk((std::size_t)d * d, 0.0);
+        for (int r = 0; r < d && k * d + r < F; r++)
+            for (int j = 0; j < d; j++) wk[(std::size_t)r * d + j] = p.pj_w[(std::size_t)(k * d + r) * d + j];
+        std::vector<Ciphertext> part;
+        pack_w(wk, d, d, part);
+        w.pj_w.insert(w.pj_w.end(), part.begin(), part.end());
+    }
     std::vector<double> qb = p.qb, kb = p.kb, vb = p.vb, ob = p.ob, fb = p.fc_b, pb = p.pj_b;
     w.qb.clear();
     w.kb.clear();
@@ -1067,12 +1110,20 @@ void encrypt_block_weights(const PlainBlockWeights &p, BlockWeights &w, const Bl
     // one row-packed bias ciphertext serves every output ciphertext: the rows one ciphertext holds
     auto rows_per_ct = [&](int len) { return std::min(T, kSlots / (2 * round_to_2(len))); };
     expand_bias(ob, w.ob, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, rows_per_ct(d));
-    expand_bias(fb, w.fc_b, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, rows_per_ct(F));
+    w.fc_b.clear();
+    for (int k = 0; k < nchunk; k++)
+    {
+        std::vector<double> bk(d, 0.0);
+        for (int j = 0; j < d && k * d + j < F; j++) bk[j] = fb[(std::size_t)(k * d + j)];
+        Ciphertext cb;
+        expand_bias(bk, cb, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, rows_per_ct(d));
+        w.fc_b.push_back(cb);
+    }
     expand_bias(pb, w.pj_b, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, rows_per_ct(d));
     for (auto *v : { &w.qb, &w.kb, &w.vb })
         for (auto &c : *v) drop(c);
     drop(w.ob);
-    drop(w.fc_b);
+    for (auto &cb : w.fc_b) drop(cb);
     drop(w.pj_b);
     w.ln1_g = p.ln1_g;
     w.ln1_b = p.ln1_b;

@@ -630,7 +630,10 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
         const auto a = clk::now();
         op_begin();
         Ciphertext c = cnn.cipher(), rtn;
-        m.boot[j]->bootstrap_real_3(rtn, c);
+        {
+            seal::Lockstep::Active merge; // MHE_RESNET_LOCKSTEP=2 (a no-op outside a group)
+            m.boot[j]->bootstrap_real_3(rtn, c);
+        }
         cnn.set_ciphertext(rtn);
         sync();
         t_boot += std::chrono::duration<double>(clk::now() - a).count();
@@ -727,17 +730,18 @@ std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vecto
     std::exception_ptr err;
     std::mutex err_mu;
     // MHE_RESNET_LOCKSTEP=1: the images in flight run their key switches and rescales as one
-    // batched launch per operation (seal::Lockstep)
-    static const bool lockstep = [] {
+    // batched launch per operation (seal::Lockstep); 2: only inside bootstrapping, where the
+    // rotations run at high levels with one key per step shared by all images
+    static const int lockstep = [] {
         const char *e = std::getenv("MHE_RESNET_LOCKSTEP");
-        return e && std::atoi(e) != 0;
+        return e ? std::atoi(e) : 0;
     }();
     const int nthreads = std::max(1, threads);
     std::unique_ptr<seal::Lockstep> group;
     if (lockstep && nthreads > 1) group = std::make_unique<seal::Lockstep>((std::size_t)nthreads);
     auto work = [&] {
         std::unique_ptr<seal::Lockstep::Member> member;
-        if (group) member = std::make_unique<seal::Lockstep::Member>(*group);
+        if (group) member = std::make_unique<seal::Lockstep::Member>(*group, lockstep == 1);
         try
         {
             for (std::size_t i; (i = next.fetch_add(1)) < images.size();) out[i] = infer(images[i]);

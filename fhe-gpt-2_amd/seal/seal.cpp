@@ -88,7 +88,8 @@ struct LsOp
 
 namespace
 {
-thread_local Lockstep::Impl *tl_ls = nullptr; // the calling thread's group
+thread_local Lockstep::Impl *tl_ls = nullptr;        // the calling thread's group, while merging
+thread_local Lockstep::Impl *tl_ls_member = nullptr; // the group the thread is a member of
 thread_local int tl_ls_direct = 0;            // > 0 inside a round's execution: calls run directly
 struct LsDirect
 {
@@ -2265,11 +2266,19 @@ std::size_t Lockstep::merged_calls() const
     return impl_->merged;
 }
 
-Lockstep::Member::Member(Lockstep &group) : g_(group) { tl_ls = group.impl_.get(); }
+Lockstep::Member::Member(Lockstep &group, bool active) : g_(group)
+{
+    tl_ls_member = group.impl_.get();
+    tl_ls = active ? tl_ls_member : nullptr;
+}
+
+Lockstep::Active::Active() : saved_(tl_ls) { tl_ls = tl_ls_member; }
+Lockstep::Active::~Active() { tl_ls = saved_; }
 
 Lockstep::Member::~Member()
 {
     tl_ls = nullptr;
+    tl_ls_member = nullptr;
     Impl *g = g_.impl_.get();
     std::unique_lock<std::mutex> lk(g->mu);
     if (g->active) g->active--;

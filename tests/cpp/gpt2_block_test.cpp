@@ -385,7 +385,13 @@ int main(int argc, char **argv)
         {
             auto t = std::chrono::steady_clock::now();
             auto a = enc_rows(fx.at("ln2"));
-            std::vector<Ciphertext> hid, bias{ bw.fc_b };
+            // the row-packed FC1 bias of the reference layout (the block itself holds the hidden
+            // state in d-wide chunks with one bias ciphertext each)
+            std::vector<double> fb = pw.fc_b;
+            Ciphertext fcb;
+            expand_bias(fb, fcb, encoder, encryptor, decryptor, evaluator, gk, rk,
+                        std::min(T, S / (2 * round_to_2(F))));
+            std::vector<Ciphertext> hid, bias{ fcb };
             row_matmul(a, bw.fc_w, bias, hid, T, d, F, encoder, encryptor, decryptor, evaluator, gk, rk);
             const double e = err_rows(hid, fx.at("hidden"));
             report("row_matmul ln2 x W_fc + b (16 x 64 . 64 x 256)", e < kTol, e, since(t));
