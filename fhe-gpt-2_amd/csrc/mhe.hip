@@ -211,6 +211,9 @@ struct mhe_ctx
     Tw *invq = nullptr;
     TwF *twf = nullptr; // FP64 twiddles (w, w/q), [K][n] forward then [K][n] inverse
     NttMode nm;         // FP64 butterflies when every prime is < 2^51 (MHE_FP=0 forces integer)
+    // the two ModUp key-switch kernels when only the special prime is >= 2^51 (the GPT-2 chain's
+    // 60-bit P): FP64 per output prime below 2^51, integer for P (fp = 2: mixed; MHE_KS_MIX=0: off)
+    NttMode nm_ks;
     int ks_fused = 1; // fused row-pass + key-MAC kernel (MHE_KS_FUSED=0: separate row pass + MAC)
     int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
     int timing = 0;      // record HIP events around the key-switch kernels (mhe_ctx_set_timing)
@@ -1424,7 +1427,7 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
             if (c->ks_colgroups > 0)
             {
                 const int IG = c->ks_colgroups < cnt ? c->ks_colgroups : cnt;
-                modup_col(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, IG, pack, st);
+                modup_col(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm_ks, I0, cnt, IG, pack, st);
             }
             else
             {
@@ -1435,7 +1438,7 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
             }
             timing_end(tc, st);
             hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
-            ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm, I0, cnt, pack, kpack, share, st);
+            ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm_ks, I0, cnt, pack, kpack, share, st);
             timing_end(tm, st);
         }
     }
@@ -1768,11 +1771,16 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (e == hipSuccess) e = hipMemcpy(c->tw, tw.data(), sizeof(Tw) * tw.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->itw, itw.data(), sizeof(Tw) * itw.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(c->invq, invq.data(), sizeof(Tw) * invq.size(), hipMemcpyHostToDevice);
-    // FP64 arithmetic (fparith.h) needs q < 2^51 for every prime of the chain
-    bool fp = true;
+    // FP64 arithmetic (fparith.h) needs q < 2^51 for every prime of the chain; with only the last
+    // (special) prime above, the ModUp kernels still run FP64 for every other output prime
+    bool fp = true, fp_data = true;
     for (int k = 0; k < count; k++) fp = fp && moduli[k] < ((u64)1 << 51);
-    if (const char *f = getenv("MHE_FP")) fp = fp && atoi(f) != 0;
-    if (e == hipSuccess && fp)
+    for (int k = 0; k + 1 < count; k++) fp_data = fp_data && moduli[k] < ((u64)1 << 51);
+    if (const char *f = getenv("MHE_FP"))
+        if (atoi(f) == 0) fp = fp_data = false;
+    bool mix = !fp && fp_data && count > 1;
+    if (const char *f = getenv("MHE_KS_MIX")) mix = mix && atoi(f) != 0;
+    if (e == hipSuccess && (fp || mix))
     {
         std::vector<TwF> twf((size_t)2 * count * n);
         for (int k = 0; k < count; k++)
@@ -1789,9 +1797,12 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
         if (e == hipSuccess) e = hipMemcpy(c->twf, twf.data(), sizeof(TwF) * twf.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess)
         {
-            c->nm.fp = 1;
-            c->nm.dfwd = (long long)((const char *)c->twf - (const char *)c->tw);
-            c->nm.dinv = (long long)((const char *)(c->twf + (size_t)count * n) - (const char *)c->itw);
+            NttMode m;
+            m.fp = fp ? 1 : 2;
+            m.dfwd = (long long)((const char *)c->twf - (const char *)c->tw);
+            m.dinv = (long long)((const char *)(c->twf + (size_t)count * n) - (const char *)c->itw);
+            if (fp) c->nm = m;
+            c->nm_ks = m;
         }
     }
     if (e != hipSuccess)

@@ -544,10 +544,11 @@ struct KsPtrs
     int key_limbs[MHE_MAXB];
 };
 
-template <int LOGR, int LOGT, bool FP>
 #ifndef MHE_MODUP_OCC
 #define MHE_MODUP_OCC 3 // waves per SIMD the ModUp column pass is compiled for (168 VGPRs)
 #endif
+// MIX (with FP): output primes >= 2^51 (the GPT-2 chain's special prime) take the integer sweep
+template <int LOGR, int LOGT, bool FP, bool MIX = false>
 __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                    const Tw *__restrict__ tw_all, int L, int K, int log_n,
                                                    long long twd, int I0, int Icnt, int pack, int X, int IG, int xcd)
@@ -602,15 +603,18 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
     auto sweep = [&](auto mode) {
         constexpr int M = decltype(mode)::value; // 0 integer, 1 FP lazy, 2 FP full
         using AA = std::conditional_t<M == 0, NttArith<false>, std::conditional_t<M == 1, NttArithF<true>, NttArithF<false>>>;
+        using VT = typename AA::T;
+        VT *const lds_v = reinterpret_cast<VT *>(lds); // same 8-byte elements either way
         for (int I = i_lo; I < i_hi; I++)
         {
             if (I == J) continue; // uniform per workgroup
             const int pi = (I == L) ? K - 1 : I;
             const PrimeDev p = primes[pi];
             if (M == 1 && !(p.q < (1ull << 47))) continue;
-            if (M == 2 && p.q < (1ull << 47)) continue;
+            if (M == 2 && (p.q < (1ull << 47) || !(p.q < (1ull << 51)))) continue;
+            if (M == 0 && FP && p.q < (1ull << 51)) continue; // mixed: the FP sweeps took it
             const AA ar(p, tw_all + ((size_t)pi << log_n), twd);
-            T v[E];
+            VT v[E];
             if constexpr (M != 0)
             {
 #pragma unroll
@@ -620,16 +624,20 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
             {
                 const bool red = qJ > p.q; // key_modulus[J] <= key_modulus[I] -> plain copy
 #pragma unroll
-                for (int e = 0; e < E; e++) v[e] = red ? barrett64(x[e], p) : x[e];
+                for (int e = 0; e < E; e++)
+                {
+                    const u64 xe = FP ? (u64)xd[e] : x[e]; // FP: the digit held as an exact double
+                    v[e] = red ? barrett64(xe, p) : xe;
+                }
             }
 #pragma unroll
             for (int s = 0; s < LOGE; s++)
                 ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
 #pragma unroll
-            for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+            for (int e = 0; e < E; e++) lds_v[sl * LD + t + TPS * e] = v[e];
             lds_barrier(); // LDS only: the previous output prime's stores stay in flight
 #pragma unroll
-            for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+            for (int e = 0; e < E; e++) v[e] = lds_v[sl * LD + E * t + e];
 #pragma unroll
             for (int s = LOGE; s < LOGR; s++)
                 ar.template fwd<E>(v, 1 << (LOGR - 1 - s),
@@ -669,12 +677,13 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
     {
         sweep(std::integral_constant<int, 1>{});
         sweep(std::integral_constant<int, 2>{});
+        if constexpr (MIX) sweep(std::integral_constant<int, 0>{});
     }
     else
         sweep(std::integral_constant<int, 0>{});
 }
 
-template <int LOGR, bool FP>
+template <int LOGR, bool FP, bool MIX = false>
 static inline void modup_col_a(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K,
                                int log_n, long long twd, int I0, int Icnt, int IG, int pack, hipStream_t st)
 {
@@ -690,8 +699,8 @@ static inline void modup_col_a(const KsPtrs &P, int B, const PrimeDev *primes, c
     }();
     const int X = subs / SH::S;
     const int xcd = (xcd_env && (X * L) % 8 == 0) ? 1 : 0;
-    hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP>), dim3((unsigned)(X * L * IG), (unsigned)B), dim3(256), 0, st, P,
-                       primes, tw, L, K, log_n, twd, I0, Icnt, pack, X, IG, xcd);
+    hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP, MIX>), dim3((unsigned)(X * L * IG), (unsigned)B), dim3(256), 0, st,
+                       P, primes, tw, L, K, log_n, twd, I0, Icnt, pack, X, IG, xcd);
 }
 
 // ModUp column pass for output primes I0 .. I0+Icnt-1 (each entry's inter holds exactly those), in
@@ -704,16 +713,19 @@ static inline void modup_col(const KsPtrs &P, int B, const PrimeDev *primes, con
     switch ((log_n + 1) / 2)
     {
     case 6:
-        if (m.fp) modup_col_a<6, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        if (m.fp == 2) modup_col_a<6, true, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        else if (m.fp) modup_col_a<6, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
         else modup_col_a<6, false>(P, B, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
         break;
     case 7:
-        if (m.fp) modup_col_a<7, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        if (m.fp == 2) modup_col_a<7, true, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
+        else if (m.fp) modup_col_a<7, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, 0, st);
         else modup_col_a<7, false>(P, B, primes, tw, L, K, log_n, 0, I0, Icnt, IG, 0, st);
         break;
     case 8:
         pack = (pack && log_n == 16) ? 1 : 0;
-        if (m.fp) modup_col_a<8, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, pack, st);
+        if (m.fp == 2) modup_col_a<8, true, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, pack, st);
+        else if (m.fp) modup_col_a<8, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, Icnt, IG, pack, st);
         else modup_col_a<8, false>(P, B, primes, tw, L, K, log_n, 0, I0, Icnt, IG, pack, st);
         break;
     }
@@ -875,7 +887,7 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
                                [&](int e) { return (1 << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
 }
 
-template <int LOGR, bool FP, bool KPF>
+template <int LOGR, bool FP, bool KPF, bool MIX = false>
 #ifndef MHE_KS_OCC
 #define MHE_KS_OCC 2 // waves per SIMD the fused MAC is compiled for
 #endif
@@ -883,7 +895,7 @@ template <int LOGR, bool FP, bool KPF>
 #define MHE_KS_XCH 2 // LDS transpose buffers of the fused MAC (1 or 2)
 #endif
 #ifndef MHE_KS_DPF
-#define MHE_KS_DPF 1 // fused MAC: load the next digit one digit ahead (1) or at the top of the digit (0)
+#define MHE_KS_DPF 1 // fused MAC: load the next digit one digit ahead (1), two ahead (2) or at the top of the digit (0)
 #endif
 __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int log_n,
@@ -936,33 +948,39 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
     const size_t kstride = (size_t)key_limbs * n;
     const A ar0(p, tw_all + ((size_t)pi << log_n), twd);
 
-    // stage this workgroup's row-pass twiddles (all digits share them)
-    {
-        const TW *tw = ar0.tw;
-        for (u32 idx = tid; idx < (u32)(S * R); idx += 256)
-        {
-            const u32 blk = idx / R, k = idx % R;
-            if (k == 0) continue;
-            const int s = 31 - __builtin_clz(k);
-            twl[blk * (R + 1) + k] = tw[(((R1 + bx * S + blk) << s)) + (k - (1u << s))];
-        }
-    }
-    const TW *mytw = &twl[sl * (R + 1)];
-    T *x0 = &xch[0][sl * R], *x1 = &xch[MHE_KS_XCH - 1][sl * R];
-
     auto run = [&](const auto &ar) {
+        // the arithmetic of this workgroup's prime: FP64, or (MIX, a prime >= 2^51) integer, with the
+        // LDS buffers reinterpreted (8-byte residues, 16-byte twiddles either way)
+        using AR = typename std::decay<decltype(ar)>::type;
+        using T = typename AR::T;
+        using TW = typename AR::TW;
+        constexpr bool FPA = !std::is_same<T, u64>::value;
+        TW *const twl_a = reinterpret_cast<TW *>(twl);
+        // stage this workgroup's row-pass twiddles (all digits share them)
+        {
+            const TW *tw = ar.tw;
+            for (u32 idx = tid; idx < (u32)(S * R); idx += 256)
+            {
+                const u32 blk = idx / R, k = idx % R;
+                if (k == 0) continue;
+                const int s = 31 - __builtin_clz(k);
+                twl_a[blk * (R + 1) + k] = tw[(((R1 + bx * S + blk) << s)) + (k - (1u << s))];
+            }
+        }
+        const TW *mytw = &twl_a[sl * (R + 1)];
+        T *x0 = reinterpret_cast<T *>(&xch[0][sl * R]), *x1 = reinterpret_cast<T *>(&xch[MHE_KS_XCH - 1][sl * R]);
         // FP: the key inner products run in FP64 as well (fp_mulmod_gen); with q < 2^47 and
         // 1.25 (j1 - j0) q < 2^53 (LZ, chosen below) the digits stay unreduced and the products
         // (|.| < 1.25q each) sum exactly, otherwise digits are reduced and the sums every second
         // digit.  Integer: 128-bit
         // accumulation, one Barrett reduction at the end (evaluator.cpp:2412-2462).
-        constexpr bool LZ = std::is_same<typename std::decay<decltype(ar)>::type, NttArithF<true>>::value;
-        using AccT = typename std::conditional<FP, double, Acc128>::type;
+        constexpr bool LZ = std::is_same<AR, NttArithF<true>>::value;
+        using AccT = typename std::conditional<FPA, double, Acc128>::type;
         AccT a0[8], a1[8];
 #pragma unroll
         for (int e = 0; e < 8; e++)
         {
-            if constexpr (FP)
+            if constexpr (FPA)
                 a0[e] = a1[e] = 0.0;
             else
                 a0[e] = a1[e] = Acc128{ 0, 0 };
@@ -997,7 +1015,9 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             }
         };
         u64 vin[8];
+        u64 vin2[8]; // MHE_KS_DPF == 2: the digit after next, two loads in flight
         if (MHE_KS_DPF) load_digit(j0, vin);
+        if (MHE_KS_DPF == 2 && j0 + 1 < j1) load_digit(j0 + 1, vin2);
         lds_barrier(); // twiddles visible
 
         // key limbs of a digit: issued one digit ahead (KPF) or at the top of the digit (the
@@ -1043,6 +1063,10 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
                 load_key(J + 1, kn0, kn1);
             if (!MHE_KS_DPF)
                 load_digit(J, vin); // no prefetch: occupancy hides the latency instead
+            else if (MHE_KS_DPF == 2)
+            {
+                if (J + 2 < j1) load_digit(J + 2, vnext);
+            }
             else if (J + 1 < j1)
                 load_digit(J + 1, vnext);
             T d[8]; // the digit in the coalesced layout, NTT form
@@ -1079,7 +1103,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
 #pragma unroll
                 for (int e = 0; e < 8; e++)
                 {
-                    if constexpr (FP)
+                    if constexpr (FPA)
                         xl[swz(lay(t, e, bl))] = w[e];
                     else
                         xl[swz(lay(t, e, bl))] = ar.canon(w[e]);
@@ -1093,7 +1117,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
 #pragma unroll
                 for (int e = 0; e < 8; e++) d[e] = ar.in52(vin[e]); // the target: a canonical ciphertext limb
             }
-            if constexpr (FP)
+            if constexpr (FPA)
             {
 #pragma unroll
                 for (int e = 0; e < 8; e++)
@@ -1117,7 +1141,16 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
                     mac128(a1[e], d[e], kk1[e]);
                 }
             }
-            if (MHE_KS_DPF)
+            if (MHE_KS_DPF == 2)
+            {
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    vin[e] = vin2[e];
+                    vin2[e] = vnext[e];
+                }
+            }
+            else if (MHE_KS_DPF)
             {
 #pragma unroll
                 for (int e = 0; e < 8; e++) vin[e] = vnext[e];
@@ -1138,7 +1171,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
         for (int e = 0; e < 8; e++)
         {
             const u32 r = lay(t, e, B_A);
-            if constexpr (FP)
+            if constexpr (FPA)
             {
                 o0[r] = fp_canon(a0[e], ar.q, ar.qinv);
                 o1[r] = fp_canon(a1[e], ar.q, ar.qinv);
@@ -1154,7 +1187,9 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
     {
         // lazy digits and sums only while this group's j1 - j0 products (|.| < 1.25q each) sum
         // exactly: 1.25 (j1 - j0) q < 2^53 (q < 2^47 allows up to 51 digits per group)
-        if (p.q < (1ull << 47) && (double)(j1 - j0) * 1.25 * (double)p.q < 9007199254740992.0)
+        if (MIX && !(p.q < (1ull << 51)))
+            run(NttArith<false>(p, tw_all + ((size_t)pi << log_n), 0));
+        else if (p.q < (1ull << 47) && (double)(j1 - j0) * 1.25 * (double)p.q < 9007199254740992.0)
             run(NttArithF<true>(p, tw_all + ((size_t)pi << log_n), twd));
         else
             run(ar0);
@@ -1433,12 +1468,20 @@ static inline bool ks_key_prefetch()
 
 // measured at L=44: G=1 763, 2 738, 4 700 HMult/s (digit groups with a partial-sum reduction, since
 // removed); ResNet-20 (L <= 31): G=1 0.865-0.873 images/s vs 0.832-0.839 with G=2
-template <int LOGR, bool FP>
+template <int LOGR, bool FP, bool MIX = false>
 static inline void ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
                                 long long twd, int I0, int cnt, int pack, int kpack, int share, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
     const int eb = ks_row_eb();
+    if constexpr (MIX)
+    {
+        const dim3 g(blocks / RowMacShape<LOGR>::S, cnt, B);
+        share = (share && B > 1 && (g.x * g.y) % 8 == 0) ? 1 : 0;
+        hipLaunchKernelGGL((k_ks_row_mac<LOGR, true, false, true>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
+                           I0, pack, kpack, share);
+        return;
+    }
     if (eb == 2 || eb == 3 || eb == 4)
     {
         const dim3 g(blocks / (eb == 3 ? RowMacShapeE<LOGR, 3>::S : RowMacShapeE<LOGR, 2>::S), cnt, B);
@@ -1468,7 +1511,9 @@ template <int LOGR>
 static inline void ks_row_mac_m(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
                                 const NttMode &m, int I0, int cnt, int pack, int kpack, int share, hipStream_t st)
 {
-    if (m.fp)
+    if (m.fp == 2)
+        ks_row_mac_a<LOGR, true, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, share, st);
+    else if (m.fp)
         ks_row_mac_a<LOGR, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, share, st);
     else
         ks_row_mac_a<LOGR, false>(P, B, primes, tw, L, K, log_n, 0, I0, cnt, pack, kpack, share, st);

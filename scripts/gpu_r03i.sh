@@ -6,11 +6,12 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r03i
 mkdir -p $O
 timeout -k 10 300 ./build/seal_batch_test 13 > $O/seal_batch13.log 2>&1 || exit $?
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "mixed or reference_chains or variants or hmult_small" > $O/pytest_mixed.log 2>&1 || exit $?
 timeout -k 10 300 ./build/gpt2_block_test tests/golden/gpt2_block > $O/gpt2_small.log 2>&1 || exit $?
 for v in 2 0 2; do
   MHE_RESNET_LOCKSTEP=$v MHE_RESNET_LOCKSTEP_STATS=1 timeout -k 10 600 ./build/resnet_test tests/golden/resnet/resnet20_params.bin tests/golden/comp 4 20 4 > $O/resnet_ls${v}_$(date +%s).log 2>&1 || exit $?
 done
-for lib in mocc2 cur mocc2 cur; do
+for lib in mocc2 dpf2 cur mocc2 dpf2 cur; do
   if [ $lib = cur ]; then unset MHE_LIB_PATH; else export MHE_LIB_PATH="$PWD/build/var/$lib/libmhe.so"; fi
   timeout -k 10 300 python bench.py --no-cpu --resnet-images 0 --steps 5 --warmup 2 > $O/hm_${lib}_$(date +%s).json 2> /dev/null || exit $?
 done

@@ -744,3 +744,27 @@ def test_extreme_residues_bit_exact(bits, fill):
     assert np.array_equal(ch.down(ch.eng.apply_galois_to(ch.up(a), elt, dkey)), ch.oc.apply_galois(a, elt, key))
     assert np.array_equal(ch.down(ch.eng.rescale_to_next(ch.up(a))), ch.oc.rescale(a))
     assert np.array_equal(ch.down(ch.eng.ntt_forward(ch.up(a))), ch.oc.ntt(a, O.NTT_FWD))
+
+
+MIXED_BITS = [49, 46, 46, 46, 49, 60]  # GPT-2-shaped: data primes < 2^51, a 60-bit special prime
+
+
+@pytest.mark.parametrize("log_n", [12, 16])
+def test_mixed_fp_integer_key_switch(log_n):
+    """GPT-2-shaped chain (every data prime < 2^51, special prime 60-bit): the ModUp column pass and
+    the fused row-pass MAC run FP64 per output prime below 2^51 and integer for the special prime
+    (NttMode fp = 2, MHE_KS_MIX); key switch, HMult and a rotation equal the oracle at every level."""
+    ch = Chain(log_n, MIXED_BITS, seed=70 + log_n)
+    key = ch.rand_key()
+    for L in (1, 3, ch.K - 1):
+        ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
+        got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
+        assert np.array_equal(got, ch.oc.switch_key(ct, target, key)), L
+    L = ch.K - 1
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.hmult(ch.up(a), ch.up(b), ch.up(key)))
+    assert np.array_equal(got, ch.oc.hmult(a, b, key))
+    elt = mhe.galois_elt_from_step(log_n, 3)
+    x = ch.rand(2, L, ch.n)
+    got = ch.down(ch.eng.apply_galois(ch.up(x), elt, ch.up(key)))
+    assert np.array_equal(got, ch.oc.apply_galois(x, elt, key))
