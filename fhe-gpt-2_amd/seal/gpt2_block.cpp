@@ -15,7 +15,11 @@
 // and one rotation per output element (MatrixMul.cpp:118-188); products whose row or column falls
 // outside the matrices contribute zeros and are skipped.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <exception>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -367,6 +371,49 @@ void block_progress(const char *what)
     if (on)
         std::printf("    %-16s %.2f s\n", what,
                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+}
+
+// f(i) for i in [0, n) on up to MHE_GPT2_THREADS threads (default 4; 1 = in order on the calling
+// thread) whose evaluator calls merge into batched launches (seal::Lockstep): the heads / hidden
+// ciphertexts / row groups of one block stage run the same operation sequence on different data
+template <class F>
+void lockstep_for(std::size_t n, F f)
+{
+    static const int threads = [] {
+        const char *e = std::getenv("MHE_GPT2_THREADS");
+        return e ? std::max(1, std::atoi(e)) : 4;
+    }();
+    if (threads <= 1 || n <= 1)
+    {
+        for (std::size_t i = 0; i < n; i++) f(i);
+        return;
+    }
+    const std::size_t nt = std::min<std::size_t>((std::size_t)threads, n);
+    seal::Lockstep group(nt);
+    std::atomic<std::size_t> next{ 0 };
+    std::exception_ptr err;
+    std::mutex mu;
+    std::vector<std::thread> pool;
+    for (std::size_t t = 0; t < nt; t++)
+        pool.emplace_back([&] {
+            seal::Lockstep::Member member(group);
+            try
+            {
+                for (std::size_t i; (i = next.fetch_add(1)) < n;) f(i);
+            }
+            catch (...)
+            {
+                std::lock_guard<std::mutex> g(mu);
+                if (!err) err = std::current_exception();
+            }
+        });
+    for (auto &t : pool) t.join();
+    if (err) std::rethrow_exception(err);
+}
+
+void ensure_levels_all(std::vector<Ciphertext> &cs, int levels, Bootstrapper &bt, Evaluator &ev)
+{
+    lockstep_for(cs.size(), [&](std::size_t i) { ensure_levels(cs[i], levels, bt, ev); });
 }
 
 std::vector<double> tiled(const std::vector<double> &v, int rows, int stride, int first_row = 0)
@@ -909,7 +956,7 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
     if (heads < 1 || cols % heads) throw std::invalid_argument("attentionLayer: heads must divide cols");
     if ((int)keep.size() != rows) throw std::invalid_argument("attentionLayer: keep must be rows x rows");
     const int dh = cols / heads;
-    for (auto &c : A) ensure_levels(c, 4, bootstrapper, evaluator);
+    ensure_levels_all(A, 4, bootstrapper, evaluator);
     std::vector<Ciphertext> Q, K, V, S, pre_out;
     attn_proj_heads(A, qw, qb, Q, rows, cols, heads, false, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     attn_proj_heads(A, kw, kb, K, rows, cols, heads, false, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
@@ -923,8 +970,8 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
         kv_cache[0] = K;
         kv_cache[1] = V;
     }
-    for (auto &c : Q) ensure_levels(c, 3, bootstrapper, evaluator);
-    for (auto &c : K) ensure_levels(c, 3, bootstrapper, evaluator);
+    ensure_levels_all(Q, 3, bootstrapper, evaluator);
+    ensure_levels_all(K, 3, bootstrapper, evaluator);
     qk_heads(Q, K, S, rows, dh, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     block_progress("q.k^t");
     std::vector<double> keep_slots(kSlots, 0.0), pin(kSlots, 0.0);
@@ -937,9 +984,9 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
             pin[(std::size_t)r * 2 * rows + j] = keep[r][j] != 0.0 ? 0.0 : params.masked_score;
         }
     }
-    Plaintext plain;
-    for (auto &s : S)
-    {
+    lockstep_for(S.size(), [&](std::size_t h) {
+        Ciphertext &s = S[h];
+        Plaintext plain;
         ensure_levels(s, 1, bootstrapper, evaluator);
         evaluator.multiply_vector_inplace_reduced_error(s, keep_slots);
         evaluator.rescale_to_next_inplace(s);
@@ -948,13 +995,13 @@ void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std
         evaluator.add_plain_inplace(s, plain);
         compute_softmax_rows(s, rows, keep_slots, params.inv_norm > 0 ? params.inv_norm : 1.0 / rows, params.inv_iters,
                              bootstrapper, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
-    }
+    });
     block_progress("softmax");
-    for (auto &c : V) ensure_levels(c, 3, bootstrapper, evaluator);
-    for (auto &c : S) ensure_levels(c, 3, bootstrapper, evaluator);
+    ensure_levels_all(V, 3, bootstrapper, evaluator);
+    ensure_levels_all(S, 3, bootstrapper, evaluator);
     sv_heads(S, V, pre_out, rows, dh, cols, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     block_progress("s.v");
-    for (auto &c : pre_out) ensure_levels(c, 3, bootstrapper, evaluator);
+    ensure_levels_all(pre_out, 3, bootstrapper, evaluator);
     std::vector<Ciphertext> bias{ b_out };
     row_matmul(pre_out, w_out, bias, outputs, rows, cols, cols, encoder, encryptor, decryptor, evaluator, gal_keys,
                relin_keys);
@@ -977,7 +1024,7 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, s
     const int nchunk = (d_ff + cols - 1) / cols, wpc = (cols + c - 1) / c;
     if ((int)b1.size() != nchunk) throw std::invalid_argument("FeedForwardLayer: one FC1 bias per hidden chunk");
     if ((int)W2.size() != nchunk * wpc) throw std::invalid_argument("FeedForwardLayer: W2 must be packed per chunk");
-    for (auto &x : A) ensure_levels(x, 3, bootstrapper, evaluator);
+    ensure_levels_all(A, 3, bootstrapper, evaluator);
     std::vector<Ciphertext> hidden;
     packed_matmul(A, W1, rows, cols, d_ff, (std::size_t)(nchunk * cpc), hidden,
                   [&](int row, int col) {
@@ -987,14 +1034,14 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, s
     for (int k = 0; k < nchunk; k++)
         for (int i = 0; i < cpc; i++) evaluator.add_inplace_reduced_error(hidden[(std::size_t)(k * cpc + i)], b1[k]);
     block_progress("fc");
-    for (auto &h : hidden)
-    {
+    lockstep_for(hidden.size(), [&](std::size_t i) {
+        Ciphertext &h = hidden[i];
         ensure_levels(h, 20, bootstrapper, evaluator);
         Ciphertext g;
         compute_gelu_block(h, g, gelu_alpha, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
         h = g;
         ensure_levels(h, 3, bootstrapper, evaluator);
-    }
+    });
     block_progress("gelu");
     Placer pl(o);
     for (int k = 0; k < nchunk; k++)
@@ -1031,12 +1078,11 @@ void transformer_block(std::vector<Ciphertext> &x, BlockWeights &w, const std::v
     const int c = kSlots / (2 * round_to_2(d));
     auto ln = [&](std::vector<Ciphertext> &in, const std::vector<double> &g, const std::vector<double> &b) {
         std::vector<Ciphertext> out(in.size());
-        for (std::size_t i = 0; i < in.size(); i++)
-        {
+        lockstep_for(in.size(), [&](std::size_t i) {
             const int r = std::min(c, T - (int)i * c);
             layer_norm_rows(in[i], out[i], g, b, r, d, params.newton_iters, bootstrapper, encoder, encryptor,
                             decryptor, evaluator, gal_keys, relin_keys);
-        }
+        });
         return out;
     };
     std::vector<std::vector<Ciphertext>> no_cache;

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 timeout -k 10 300 ./build/gpt2_block_test tests/golden/gpt2_block > gpurun_out/gpt2_small.log 2>&1 || exit $?
 FX=$(mktemp -d /tmp/gpt2fx.XXXXXX)
 python3 tests/golden/gpt2_block/make_fixture.py --full "$FX" > gpurun_out/gpt2_full_fixture.log 2>&1 || exit $?
-MHE_VEC_CACHE_GB=${VEC_CACHE_GB:-160} MHE_BLOCK_VERBOSE=1 timeout -k 10 ${FULL_LIMIT:-1000} ./build/gpt2_block_test "$FX" block > gpurun_out/gpt2_full.log 2>&1
+MHE_VEC_CACHE_GB=${VEC_CACHE_GB:-100} MHE_BLOCK_VERBOSE=1 timeout -k 10 ${FULL_LIMIT:-1000} ./build/gpt2_block_test "$FX" block > gpurun_out/gpt2_full.log 2>&1
 rc=$?
 rm -rf "$FX"
 exit $rc

@@ -5,6 +5,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r03i
 mkdir -p $O
+bash scripts/gpu_sq.sh || exit $?
 timeout -k 10 300 ./build/seal_batch_test 13 > $O/seal_batch13.log 2>&1 || exit $?
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "mixed or reference_chains or variants or hmult_small" > $O/pytest_mixed.log 2>&1 || exit $?
 timeout -k 10 300 ./build/gpt2_block_test tests/golden/gpt2_block > $O/gpt2_small.log 2>&1 || exit $?
@@ -18,7 +19,7 @@ done
 unset MHE_LIB_PATH
 FX=$(mktemp -d /tmp/gpt2fx.XXXXXX)
 python3 tests/golden/gpt2_block/make_fixture.py --full "$FX" > $O/gpt2_full_fixture.log 2>&1 || exit $?
-MHE_VEC_CACHE_GB=160 MHE_BLOCK_VERBOSE=1 timeout -k 10 600 ./build/gpt2_block_test "$FX" block > $O/gpt2_full.log 2>&1
+MHE_VEC_CACHE_GB=100 MHE_BLOCK_VERBOSE=1 timeout -k 10 500 ./build/gpt2_block_test "$FX" block > $O/gpt2_full.log 2>&1
 rc=$?
 rm -rf "$FX"
 exit $rc
