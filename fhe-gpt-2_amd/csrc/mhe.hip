@@ -519,19 +519,25 @@ struct JobModDownRow
         bool fp;
         double pd, pi, invd;
         __device__ u64 load(u32 x) const { return buf[x]; }
-        __device__ void store(u32 x, u64 t) const
+        struct Pre
+        {
+            u64 a, c;
+        };
+        __device__ Pre pre(u32 x) const { return Pre{ accp[x], replace ? 0 : ctp[x] }; }
+        __device__ void store(u32 x, u64 t, Pre o) const
         {
             if (fp)
             {
                 // acc and t canonical: (acc - t) P^-1 in (-1.25p, 1.25p), plus c < p, one
                 // canonicalisation (|.| < 2^53): the residue of the integer form
-                const double v = fp_mulmod_gen(fp_from_u52(accp[x]) - fp_from_u52(t), invd, pd, pi);
-                ctp[x] = fp_canon(replace ? v : v + fp_from_u52(ctp[x]), pd, pi);
+                const double v = fp_mulmod_gen(fp_from_u52(o.a) - fp_from_u52(t), invd, pd, pi);
+                ctp[x] = fp_canon(replace ? v : v + fp_from_u52(o.c), pd, pi);
                 return;
             }
-            u64 v = mul_shoup(accp[x] + p.four_q - t, inv.x, inv.y, p.q);
-            ctp[x] = replace ? v : addmod(v, ctp[x], p.q); // 0 + v = v: the same word
+            u64 v = mul_shoup(o.a + p.four_q - t, inv.x, inv.y, p.q);
+            ctp[x] = replace ? v : addmod(v, o.c, p.q); // 0 + v = v: the same word
         }
+        __device__ void store(u32 x, u64 t) const { store(x, t, pre(x)); }
     };
     __device__ View view(int y) const
     {
@@ -619,13 +625,16 @@ struct JobRescaleRow
         bool skip, fp;
         double pd, pi, invd;
         __device__ u64 load(u32 x) const { return buf[x]; }
-        __device__ void store(u32 x, u64 t) const
+        using Pre = u64;
+        __device__ Pre pre(u32 x) const { return inp[x]; }
+        __device__ void store(u32 x, u64 t, u64 in) const
         {
             if (fp) // in and t canonical: (in - t) q_last^-1 in (-1.25p, 1.25p), canonicalised
-                outp[x] = fp_canon(fp_mulmod_gen(fp_from_u52(inp[x]) - fp_from_u52(t), invd, pd, pi), pd, pi);
+                outp[x] = fp_canon(fp_mulmod_gen(fp_from_u52(in) - fp_from_u52(t), invd, pd, pi), pd, pi);
             else
-                outp[x] = mul_shoup(inp[x] + p.four_q - t, inv.x, inv.y, p.q);
+                outp[x] = mul_shoup(in + p.four_q - t, inv.x, inv.y, p.q);
         }
+        __device__ void store(u32 x, u64 t) const { store(x, t, pre(x)); }
     };
     __device__ View view(int y) const
     {
@@ -746,21 +755,27 @@ struct JobMDRRow
         bool skip, fp;
         double pd, pi, pinvd, qlinvd;
         __device__ u64 load(u32 x) const { return buf[x]; }
-        __device__ void store(u32 x, u64 U) const
+        struct Pre
+        {
+            u64 a, c;
+        };
+        __device__ Pre pre(u32 x) const { return Pre{ accp[x], ctp[x] }; }
+        __device__ void store(u32 x, u64 U, Pre o) const
         {
             if (fp)
             {
                 // acc_i P^-1 in (-1.25p, 1.25p); c + a - U is an exact integer below 2^53; its
                 // centered residue times q_{L-1}^-1, canonicalised: the residue of the integer form
-                const double a = fp_mulmod_gen(fp_from_u52(accp[x]), pinvd, pd, pi);
-                const double v = fp_reduce(fp_from_u52(ctp[x]) + a - fp_from_u52(U), pd, pi);
+                const double a = fp_mulmod_gen(fp_from_u52(o.a), pinvd, pd, pi);
+                const double v = fp_reduce(fp_from_u52(o.c) + a - fp_from_u52(U), pd, pi);
                 outp[x] = fp_canon(fp_mulmod_gen(v, qlinvd, pd, pi), pd, pi);
                 return;
             }
-            const u64 a = mul_shoup(accp[x], pinv.x, pinv.y, p.q);  // acc_i P^-1
-            const u64 v = ctp[x] + a + p.four_q - U;                // < 6q
+            const u64 a = mul_shoup(o.a, pinv.x, pinv.y, p.q); // acc_i P^-1
+            const u64 v = o.c + a + p.four_q - U;              // < 6q
             outp[x] = mul_shoup(v, qlinv.x, qlinv.y, p.q);
         }
+        __device__ void store(u32 x, u64 U) const { store(x, U, pre(x)); }
     };
     __device__ View view(int y) const
     {

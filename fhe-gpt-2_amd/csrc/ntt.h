@@ -315,6 +315,48 @@ __global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n, long long t
     for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
 }
 
+// Row-pass epilogue operands.  A View whose store() reads other buffers (the ModDown / rescale
+// epilogues read acc and ct at the stored index) declares `Pre` and pre(x): the pass loads those
+// operands for all its E indices right after its own loads, so their latency hides behind the
+// butterflies, and hands them to store(x, v, pre).  Without it each store's loads wait for the
+// previous store (the compiler cannot move a load above a store that may alias it): E serialised
+// HBM round trips per lane at the end of the kernel.
+#ifndef MHE_ROW_PRE
+#define MHE_ROW_PRE 1
+#endif
+template <class V, class = void>
+struct PreOf
+{
+    using type = char;
+    static constexpr bool value = false;
+};
+template <class V>
+struct PreOf<V, std::void_t<typename V::Pre>>
+{
+    using type = typename V::Pre;
+    static constexpr bool value = MHE_ROW_PRE != 0;
+};
+
+// LDS image of a row pass's transposes.  The in-lane phase writes position t + TPS e and the
+// cross-lane phase reads E t + e (and back); with a plain padded row the second pattern puts the
+// 16 lanes of a sub-transform on a stride of E 8-byte words, an 8-way bank conflict at LOGR = 8
+// (SQ_LDS_BANK_CONFLICT 6.5x the LDS busy cycles, profiles/r03k).  XOR-ing the low LOGE bits with
+// the high ones and a row pitch of R + TPS words makes both patterns conflict-free for every row
+// shape (bank model of MI355X_MICROARCH.md §LDS: 64 banks, 32-lane groups for ds_*_b64).
+#ifndef MHE_ROW_SWZ
+#define MHE_ROW_SWZ 1
+#endif
+template <int LOGR, int LOGT>
+struct RowLds
+{
+    static constexpr int R = 1 << LOGR, TPS = 1 << LOGT, LOGE = LOGR - LOGT, E = 1 << LOGE;
+    static constexpr int LD = MHE_ROW_SWZ ? R + TPS : R + 1;
+    __device__ static __forceinline__ int at(int sl, int p)
+    {
+        return sl * LD + (MHE_ROW_SWZ ? (p ^ ((p >> LOGE) & (E - 1))) : p);
+    }
+};
+
 // --------------------------------------------------------------------- forward, row pass
 template <int LOGR, int LOGT, class Job, bool FP>
 __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long twd)
@@ -322,35 +364,51 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long t
     using SH = Shape<LOGR, LOGT>;
     using A = NttArith<FP>;
     using T = typename A::T;
-    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
-    __shared__ T lds[S * LD];
+    using RL = RowLds<LOGR, LOGT>;
+    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S;
+    __shared__ T lds[S * RL::LD];
     const int tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
     const u32 b = blockIdx.x * S + sl;
     const u32 base = b << LOGR;
     const u32 rb = (1u << (log_n - LOGR)) + b; // 2^k1 + b
     const auto V = job.view(blockIdx.y);
     if (V.skip) return; // uniform per workgroup, before any barrier
+    using VW = std::remove_cv_t<decltype(V)>;
+    constexpr bool PRE = PreOf<VW>::value;
     const A ar(V.p, V.tw, twd);
     T v[E];
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = ar.in(V.load(base + t + TPS * e));
+    [[maybe_unused]] typename PreOf<VW>::type pr[E];
+    if constexpr (PRE)
+    {
+#pragma unroll
+        for (int e = 0; e < E; e++) pr[e] = V.pre(base + t + TPS * e);
+    }
 #pragma unroll
     for (int s = 0; s < LOGE; s++)
         ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (rb << s) + (e >> (LOGE - s)); });
 #pragma unroll
-    for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+    for (int e = 0; e < E; e++) lds[RL::at(sl, t + TPS * e)] = v[e];
     wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
-    for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+    for (int e = 0; e < E; e++) v[e] = lds[RL::at(sl, E * t + e)];
 #pragma unroll
     for (int s = LOGE; s < LOGR; s++)
         ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
     // transpose back so stores (and epilogue reads) are coalesced
 #pragma unroll
-    for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
+    for (int e = 0; e < E; e++) lds[RL::at(sl, E * t + e)] = v[e];
     wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
-    for (int e = 0; e < E; e++) V.store(base + t + TPS * e, ar.out(lds[sl * LD + t + TPS * e]));
+    for (int e = 0; e < E; e++)
+    {
+        const u64 o = ar.out(lds[RL::at(sl, t + TPS * e)]);
+        if constexpr (PRE)
+            V.store(base + t + TPS * e, o, pr[e]);
+        else
+            V.store(base + t + TPS * e, o);
+    }
 }
 
 // --------------------------------------------------------------------- inverse, row pass
@@ -360,8 +418,9 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long t
     using SH = Shape<LOGR, LOGT>;
     using A = NttArith<FP>;
     using T = typename A::T;
-    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
-    __shared__ T lds[S * LD];
+    using RL = RowLds<LOGR, LOGT>;
+    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S;
+    __shared__ T lds[S * RL::LD];
     const int tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
     const u32 b = blockIdx.x * S + sl;
     const u32 base = b << LOGR;
@@ -371,18 +430,18 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long t
     const A ar(V.p, V.tw, twd);
     T v[E];
 #pragma unroll
-    for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = ar.in(V.load(base + t + TPS * e));
+    for (int e = 0; e < E; e++) lds[RL::at(sl, t + TPS * e)] = ar.in(V.load(base + t + TPS * e));
     wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
-    for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+    for (int e = 0; e < E; e++) v[e] = lds[RL::at(sl, E * t + e)];
 #pragma unroll
     for (int s = LOGR - 1; s >= LOGE; s--)
         ar.template inv<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
 #pragma unroll
-    for (int e = 0; e < E; e++) lds[sl * LD + E * t + e] = v[e];
+    for (int e = 0; e < E; e++) lds[RL::at(sl, E * t + e)] = v[e];
     wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
 #pragma unroll
-    for (int e = 0; e < E; e++) v[e] = lds[sl * LD + t + TPS * e];
+    for (int e = 0; e < E; e++) v[e] = lds[RL::at(sl, t + TPS * e)];
 #pragma unroll
     for (int s = LOGE - 1; s >= 0; s--)
         ar.template inv<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (rb << s) + (e >> (LOGE - s)); });
@@ -875,8 +934,17 @@ __device__ __forceinline__ u32 lay(u32 t, int e, int b_lo)
 
 
 
+// Slot of twiddle entry k in a block's LDS row.  The last stages read entries 4 apart across the
+// lanes (16-byte entries: a 64-byte stride), a 4-way conflict for ds_read_b128's 16-lane groups;
+// XOR-ing bits 4-5 into bits 0-1 with an unpadded row makes every stage's reads conflict-free
+// (bank model of MI355X_MICROARCH.md §LDS; SQ_LDS_BANK_CONFLICT was 0.55x the LDS busy cycles).
+__device__ __forceinline__ u32 twz(u32 k)
+{
+    return k ^ ((k >> 4) & 3);
+}
+
 // Forward stages [s0, s1) of the local 2^LOGR transform, twiddles from the block's LDS row
-// (entry (1 << s) + g holds tw[((2^k1 + b) << s) + g]).
+// (entry (1 << s) + g, at slot twz(.), holds tw[((2^k1 + b) << s) + g]).
 template <int LOGR, class A>
 __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_lo, int s0, int s1,
                                            const typename A::TW *twl, const A &ar, int /*deduce*/ = 0)
@@ -884,7 +952,7 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
 #pragma unroll
     for (int s = s0; s < s1; s++)
         ar.template fwd_tab<8>(v, 1 << (LOGR - 1 - s - b_lo), twl, // gap in slot units
-                               [&](int e) { return (1 << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
+                               [&](int e) { return twz((1u << s) + (lay(t, e, b_lo) >> (LOGR - s))); });
 }
 
 template <int LOGR, bool FP, bool KPF, bool MIX = false>
@@ -934,7 +1002,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
     // operations complete in order; the fences only stop the compiler from reordering them):
     // 49 KB per workgroup fits 3 workgroups per CU, two buffers (65.6 KB) only 2
     __shared__ T xch[MHE_KS_XCH][S * R];
-    __shared__ TW twl[S * (R + 1)];
+    __shared__ TW twl[S * R];
     const int j0 = 0, j1 = L;
     const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
     const u32 b = bx * S + sl;
@@ -964,10 +1032,10 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
                 const u32 blk = idx / R, k = idx % R;
                 if (k == 0) continue;
                 const int s = 31 - __builtin_clz(k);
-                twl_a[blk * (R + 1) + k] = tw[(((R1 + bx * S + blk) << s)) + (k - (1u << s))];
+                twl_a[blk * R + twz(k)] = tw[(((R1 + bx * S + blk) << s)) + (k - (1u << s))];
             }
         }
-        const TW *mytw = &twl_a[sl * (R + 1)];
+        const TW *mytw = &twl_a[sl * R];
         T *x0 = reinterpret_cast<T *>(&xch[0][sl * R]), *x1 = reinterpret_cast<T *>(&xch[MHE_KS_XCH - 1][sl * R]);
         // FP: the key inner products run in FP64 as well (fp_mulmod_gen); with q < 2^47 and
         // 1.25 (j1 - j0) q < 2^53 (LZ, chosen below) the digits stay unreduced and the products

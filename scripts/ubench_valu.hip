@@ -40,6 +40,9 @@ __global__ __launch_bounds__(256) void k_bench(uint64_t *out, uint64_t seed)
             if (KIND == 5) a[c] = a[c] * (wq + c) - __umul64hi(a[c], wq) * q;                   // Shoup lazy mulmod
             if (KIND == 6) d[c] = d[c] * dm;                                                    // v_mul_f64
             if (KIND == 7) a[c] = (uint64_t)((uint32_t)a[c] * 2654435761u) ^ a[c];              // lo-mul + xor
+            if (KIND == 8) d[c] = __builtin_rint(d[c] * dm);                                    // v_mul_f64 + v_rndne_f64
+            if (KIND == 9) d[c] = __builtin_fma(d[c], dm, 6755399441055744.0) - 6755399441055744.0; // fma + add (magic rounding)
+            if (KIND == 10) d[c] = d[c] + da;                                                   // v_add_f64
         }
     }
     uint64_t s = 0;
@@ -78,6 +81,9 @@ int main()
     run<5>("shoup_lazy mulmod (64b)", out);
     run<6>("v_mul_f64", out);
     run<7>("mul_lo+xor", out);
+    run<8>("v_mul_f64 + v_rndne_f64", out);
+    run<9>("v_fma_f64 + v_add_f64 (magic)", out);
+    run<10>("v_add_f64", out);
     (void)hipFree(out);
     return 0;
 }
