@@ -712,6 +712,11 @@ private:
     SecretKey sk_;
 };
 
+// (not SEAL API) Batched launches of the *_many / rotate_vectors calls, on by default.  Off, every
+// entry runs as its own call (the words are the same either way: tests compare the two).
+void set_batched_launches(bool on);
+bool batched_launches();
+
 // (not SEAL API) Lockstep: threads that evaluate the same operation sequence on different data (the
 // images of a batch) join one group.  While joined, every top-level rotation (rotate_vector[s],
 // rotate_vector_inplace), relinearization (relinearize_inplace, and the one inside

@@ -351,9 +351,37 @@ void Polynomial::homomorphic_poly_evaluation(SEALContext &, CKKSEncoder &, Encry
         evaluator.add_const(baby[i], -1.0, baby[i]);
         babybool[i] = true;
     }
+    // T_i for 2^a < i < 2^(a+1) needs only T's below 2^a (res, diff < 2^a): each band's products
+    // and rescales run as one batch (each T_i's operations are the reference's, in its order)
+    for (long lo = 2; lo < heap_k; lo *= 2)
+    {
+        std::vector<long> band;
+        for (long i = lo + 1; i < std::min(2 * lo, heap_k); i++)
+            if (!babybool[i]) band.push_back(i);
+        if (band.empty()) continue;
+        std::vector<const Ciphertext *> m1, m2;
+        std::vector<Ciphertext *> mo;
+        for (long i : band)
+        {
+            const long lpow2 = 1L << (int)std::floor(std::log(i) / std::log(2));
+            m1.push_back(&baby[lpow2]);
+            m2.push_back(&baby[i - lpow2]);
+            mo.push_back(&baby[i]);
+        }
+        evaluator.multiply_reduced_error_many(m1, m2, relin_keys, mo);
+        evaluator.rescale_to_next_inplace_many(mo);
+        for (long i : band)
+        {
+            const long lpow2 = 1L << (int)std::floor(std::log(i) / std::log(2));
+            const long res = i - lpow2, diff = std::labs(lpow2 - res);
+            evaluator.double_inplace(baby[i]);
+            evaluator.sub_reduced_error(baby[i], baby[diff], baby[i]);
+            babybool[i] = true;
+        }
+    }
     for (long i = 1; i < heap_k; i++)
     {
-        if (babybool[i]) continue;
+        if (babybool[i]) continue; // (every i is covered by a band above)
         const long lpow2 = 1L << (int)std::floor(std::log(i) / std::log(2));
         const long res = i - lpow2, diff = std::labs(lpow2 - res);
         evaluator.multiply_reduced_error(baby[lpow2], baby[res], relin_keys, baby[i]);
@@ -395,34 +423,52 @@ void Polynomial::homomorphic_poly_evaluation(SEALContext &, CKKSEncoder &, Encry
         evaluator.add_const_inplace(giant[i], -1.0);
     }
 
-    // leaves: sum_j c_j T_j by multiply_const + rescale
+    // leaves: sum_j c_j T_j by multiply_const + rescale.  Every term of every leaf is made first
+    // and all of them are rescaled as one batch; each leaf is then summed in the reference's order.
     std::vector<Ciphertext> cipherheap(heaplen);
     std::vector<bool> cipherheapbool(heaplen, false);
-    Ciphertext tmp;
     long heapfirst = (1L << heap_m) - 1, heaplast = (1L << (heap_m + 1)) - 1;
-    for (long i = heapfirst; i < heaplast; i++)
     {
-        if (!poly_heap[i]) continue;
-        const Polynomial &p = *poly_heap[i];
-        cipherheapbool[i] = true;
-        evaluator.multiply_const(baby[1], p.chebcoeff[1], cipherheap[i]);
-        evaluator.rescale_to_next_inplace(cipherheap[i]);
-        if (!(std::abs(p.chebcoeff[1]) <= zero)) evaluator.add_const_inplace(cipherheap[i], p.chebcoeff[0]);
-        for (long j = 2; j <= p.deg; j++)
+        std::vector<std::vector<Ciphertext>> terms(heaplen);
+        std::vector<Ciphertext *> resc;
+        for (long i = heapfirst; i < heaplast; i++)
         {
-            if (std::abs(p.chebcoeff[j]) <= zero) continue;
-            evaluator.multiply_const(j < heap_k ? baby[j] : giant[0], p.chebcoeff[j], tmp);
-            evaluator.rescale_to_next_inplace(tmp);
-            evaluator.add_reduced_error(cipherheap[i], tmp, cipherheap[i]);
+            if (!poly_heap[i]) continue;
+            const Polynomial &p = *poly_heap[i];
+            cipherheapbool[i] = true;
+            evaluator.multiply_const(baby[1], p.chebcoeff[1], cipherheap[i]);
+            resc.push_back(&cipherheap[i]);
+            long cnt = 0;
+            for (long j = 2; j <= p.deg; j++)
+                if (!(std::abs(p.chebcoeff[j]) <= zero)) cnt++;
+            terms[i].resize(cnt);
+            long t = 0;
+            for (long j = 2; j <= p.deg; j++)
+            {
+                if (std::abs(p.chebcoeff[j]) <= zero) continue;
+                evaluator.multiply_const(j < heap_k ? baby[j] : giant[0], p.chebcoeff[j], terms[i][t]);
+                resc.push_back(&terms[i][t++]);
+            }
+        }
+        evaluator.rescale_to_next_inplace_many(resc);
+        for (long i = heapfirst; i < heaplast; i++)
+        {
+            if (!poly_heap[i]) continue;
+            const Polynomial &p = *poly_heap[i];
+            if (!(std::abs(p.chebcoeff[1]) <= zero)) evaluator.add_const_inplace(cipherheap[i], p.chebcoeff[0]);
+            for (Ciphertext &tm : terms[i]) evaluator.add_reduced_error(cipherheap[i], tm, cipherheap[i]);
         }
     }
-    // combine: node = quotient * T_{k 2^g} + remainder
+    // combine: node = quotient * T_{k 2^g} + remainder; the nodes of one depth as one batch
     long depth = heap_m, gindex = 0;
     while (depth != 0)
     {
         depth--;
         heapfirst = (1L << depth) - 1;
         heaplast = (1L << (depth + 1)) - 1;
+        std::vector<long> prod;
+        std::vector<const Ciphertext *> m1, m2;
+        std::vector<Ciphertext *> mo;
         for (long i = heapfirst; i < heaplast; i++)
         {
             if (!poly_heap[i]) continue;
@@ -431,12 +477,15 @@ void Polynomial::homomorphic_poly_evaluation(SEALContext &, CKKSEncoder &, Encry
                 cipherheap[i] = cipherheap[2 * (i + 1)];
             else
             {
-                evaluator.multiply_reduced_error(cipherheap[2 * (i + 1) - 1], giant[gindex], relin_keys,
-                                                 cipherheap[i]);
-                evaluator.rescale_to_next_inplace(cipherheap[i]);
-                evaluator.add_reduced_error(cipherheap[i], cipherheap[2 * (i + 1)], cipherheap[i]);
+                prod.push_back(i);
+                m1.push_back(&cipherheap[2 * (i + 1) - 1]);
+                m2.push_back(&giant[gindex]);
+                mo.push_back(&cipherheap[i]);
             }
         }
+        evaluator.multiply_reduced_error_many(m1, m2, relin_keys, mo);
+        evaluator.rescale_to_next_inplace_many(mo);
+        for (long i : prod) evaluator.add_reduced_error(cipherheap[i], cipherheap[2 * (i + 1)], cipherheap[i]);
         gindex++;
     }
     rtn = cipherheap[0];

@@ -265,9 +265,16 @@ void eval_polynomial_integrate(Encryptor &encryptor, Evaluator &evaluator, Decry
 
     if (tree.type == evaltype::oddbaby)
     {
+        // The reference's operation sequence per node, with the independent work of one depth
+        // issued together: the leaves' rescales as one batch, and every product of the depth (the
+        // internal nodes' spines, the giant step and the odd baby steps, all relinearized with one
+        // key) as one multiply_reduced_error_many, then their rescales as one batch.  Each
+        // ciphertext sees the same operations in the same order as in SEALfunc.cpp:60-313, so the
+        // words are the same; only the launches are shared.
         for (long i = 1; i <= total_depth; i++)
         {
             // leaves finishing at depth i: odd polynomials in T_1, T_3, ...
+            std::vector<Ciphertext *> resc;
             for (long j = 1; j < nodes; j++)
             {
                 if (tree.tree[j] != 0 || total_depth + 1 - minicomp::num_one(j) != i) continue;
@@ -281,42 +288,82 @@ void eval_polynomial_integrate(Encryptor &encryptor, Evaluator &evaluator, Decry
                     evaluator.add_inplace_reduced_error(*pt[j], temp1);
                     idx += 2;
                 }
-                evaluator.rescale_to_next_inplace(*pt[j]);
+                resc.push_back(pt[j].get());
             }
+            evaluator.rescale_to_next_inplace_many(resc);
+
+            // every product of this depth
+            std::vector<const Ciphertext *> m1, m2;
+            std::vector<Ciphertext *> mo;
+            std::vector<std::unique_ptr<Ciphertext>> extra; // spine products after a node's first
+            struct Spine
+            {
+                long j, kend;
+                std::vector<Ciphertext *> terms;
+            };
+            std::vector<Spine> spines;
             // internal nodes finishing at depth i (odd index: the start of a right spine)
             for (long j = 1; j < nodes; j++)
             {
                 if (tree.tree[j] <= 0 || total_depth + 1 - minicomp::num_one(j) != i || j % 2 != 1) continue;
+                Spine sp{ j, j, {} };
                 long k = j;
                 pt[j] = std::make_unique<Ciphertext>();
-                evaluator.multiply_reduced_error(need(T[tree.tree[k]], "T[tree.tree[k]]"), need(pt[2 * k + 1], "pt"),
-                                                 relin_keys, *pt[j]);
+                m1.push_back(&need(T[tree.tree[k]], "T[tree.tree[k]]"));
+                m2.push_back(&need(pt[2 * k + 1], "pt"));
+                mo.push_back(pt[j].get());
                 k *= 2;
                 while (tree.tree[k] != 0)
                 {
-                    evaluator.multiply_reduced_error(need(T[tree.tree[k]], "T[tree.tree[k]]"),
-                                                     need(pt[2 * k + 1], "pt"), relin_keys, temp1);
-                    evaluator.add_inplace_reduced_error(*pt[j], temp1);
+                    extra.push_back(std::make_unique<Ciphertext>());
+                    m1.push_back(&need(T[tree.tree[k]], "T[tree.tree[k]]"));
+                    m2.push_back(&need(pt[2 * k + 1], "pt"));
+                    mo.push_back(extra.back().get());
+                    sp.terms.push_back(extra.back().get());
                     k *= 2;
                 }
-                evaluator.rescale_to_next_inplace(*pt[j]);
-                evaluator.add_inplace_reduced_error(*pt[j], need(pt[k], "pt[k]"));
+                sp.kend = k;
+                spines.push_back(std::move(sp));
             }
-            // giant steps T_{2^i} and odd baby steps T_j, 2^{i-1} < j < 2^i
-            if (i <= tree.m - 1)
+            // giant step T_{2^i} and odd baby steps T_j, 2^{i-1} < j < 2^i (evalT: T_{m+n} =
+            // 2 T_m T_n - T_{|m-n|})
+            struct Step
             {
-                const long g = pow2(i);
-                T[g] = std::make_unique<Ciphertext>();
-                evalT(evaluator, relin_keys, *T[g], need(T[pow2(i - 1)], "T"), need(T[pow2(i - 1)], "T"),
-                      need(T[0], "T[0]"));
-            }
+                long g;
+                const Ciphertext *minus;
+                std::unique_ptr<Ciphertext> prod;
+            };
+            std::vector<Step> steps;
+            auto add_step = [&](long g, long m, long nn, long mn) {
+                Step st{ g, &need(T[mn], "T"), std::make_unique<Ciphertext>() };
+                m1.push_back(&need(T[m], "T"));
+                m2.push_back(&need(T[nn], "T"));
+                mo.push_back(st.prod.get());
+                steps.push_back(std::move(st));
+            };
+            if (i <= tree.m - 1) add_step(pow2(i), pow2(i - 1), pow2(i - 1), 0);
             if (i <= tree.l)
-                for (long j = pow2(i - 1) + 1; j <= pow2(i) - 1; j += 2)
-                {
-                    T[j] = std::make_unique<Ciphertext>();
-                    evalT(evaluator, relin_keys, *T[j], need(T[pow2(i - 1)], "T"), need(T[j - pow2(i - 1)], "T"),
-                          need(T[pow2(i) - j], "T"));
-                }
+                for (long j = pow2(i - 1) + 1; j <= pow2(i) - 1; j += 2) add_step(j, pow2(i - 1), j - pow2(i - 1), pow2(i) - j);
+            evaluator.multiply_reduced_error_many(m1, m2, relin_keys, mo);
+
+            resc.clear();
+            for (Spine &sp : spines)
+            {
+                for (Ciphertext *t : sp.terms) evaluator.add_inplace_reduced_error(*pt[sp.j], *t);
+                resc.push_back(pt[sp.j].get());
+            }
+            for (Step &st : steps)
+            {
+                evaluator.add_inplace_reduced_error(*st.prod, *st.prod);
+                resc.push_back(st.prod.get());
+            }
+            evaluator.rescale_to_next_inplace_many(resc);
+            for (Spine &sp : spines) evaluator.add_inplace_reduced_error(*pt[sp.j], need(pt[sp.kend], "pt[k]"));
+            for (Step &st : steps)
+            {
+                T[st.g] = std::make_unique<Ciphertext>();
+                evaluator.sub_reduced_error(*st.prod, *st.minus, *T[st.g]);
+            }
         }
         res = need(pt[1], "pt[1]");
         return;

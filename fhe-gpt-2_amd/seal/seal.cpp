@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <atomic>
 #include <condition_variable>
 #include <exception>
 #include <cstdlib>
@@ -2223,6 +2224,20 @@ void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const Galo
     rotate_vector_inplace(destination, steps, galois_keys);
 }
 
+// ------------------------------------------------------------------------------ batching switch
+namespace
+{
+std::atomic<bool> g_batched{ true };
+}
+void set_batched_launches(bool on)
+{
+    g_batched.store(on);
+}
+bool batched_launches()
+{
+    return g_batched.load();
+}
+
 // ------------------------------------------------------------------------------ Lockstep
 struct Lockstep::Impl
 {
@@ -2403,6 +2418,11 @@ void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted,
     }
     if (encrypted.size() != steps.size() || encrypted.size() != destinations.size())
         throw std::invalid_argument("encrypted, steps and destinations must have the same size");
+    if (!batched_launches())
+    {
+        for (std::size_t i = 0; i < destinations.size(); i++) rotate_vector(*encrypted[i], steps[i], galois_keys, *destinations[i]);
+        return;
+    }
     for (std::size_t i = 0; i < destinations.size(); i++)
     {
         if (!encrypted[i] || !destinations[i]) throw std::invalid_argument("null ciphertext");
@@ -2484,6 +2504,12 @@ void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted,
 
 void Evaluator::relinearize_inplace_many(const std::vector<Ciphertext *> &encrypted, const RelinKeys &relin_keys) const
 {
+    if (!batched_launches())
+    {
+        for (Ciphertext *c : encrypted)
+            if (c && c->size() > 2) relinearize_inplace(*c, relin_keys);
+        return;
+    }
     // relinearize_inplace of every entry; size-3 entries of one level share one batched key switch
     trace::Scope tsc; // traced as one "relinearize" record per entry
     std::vector<std::string> tin;
@@ -2537,6 +2563,12 @@ void Evaluator::multiply_reduced_error_many(const std::vector<const Ciphertext *
 {
     if (encrypted1.size() != encrypted2.size() || encrypted1.size() != destinations.size())
         throw std::invalid_argument("encrypted1, encrypted2 and destinations must have the same size");
+    if (!batched_launches())
+    {
+        for (std::size_t i = 0; i < destinations.size(); i++)
+            multiply_reduced_error(*encrypted1[i], *encrypted2[i], relin_keys, *destinations[i]);
+        return;
+    }
     for (std::size_t i = 0; i < destinations.size(); i++)
     {
         if (!encrypted1[i] || !encrypted2[i] || !destinations[i]) throw std::invalid_argument("null ciphertext");
@@ -2584,6 +2616,11 @@ void Evaluator::multiply_reduced_error_many(const std::vector<const Ciphertext *
 
 void Evaluator::rescale_to_next_inplace_many(const std::vector<Ciphertext *> &encrypted) const
 {
+    if (!batched_launches())
+    {
+        for (Ciphertext *c : encrypted) rescale_to_next_inplace(*c);
+        return;
+    }
     // rescale_to_next of every entry; entries of one level and size run as one batched launch
     trace::Scope tsc; // traced as one "rescale" record per entry
     std::vector<std::string> tin;

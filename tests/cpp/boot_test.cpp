@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -215,6 +216,20 @@ int main(int argc, char **argv)
                     std::log2(out.scale()), err, std::log2(err), bt.cached_plaintexts());
         if (!(err < 1e-3)) fail++;
         if (out.coeff_modulus_size() < 3) fail++;
+    }
+    {
+        // batched launches (BSGS rotations, EvalMod products and rescales of one depth) give the
+        // same words as every operation run alone
+        Ciphertext in0 = ct, in1 = ct, o0, o1;
+        set_batched_launches(false);
+        bt.bootstrap_real_3(o0, in0);
+        set_batched_launches(true);
+        bt.bootstrap_real_3(o1, in1);
+        const PolyStore &x = o0.store(), &y = o1.store();
+        const bool same = o0.parms_id() == o1.parms_id() && o0.scale() == o1.scale() && x.words() == y.words() &&
+                          std::memcmp(x.host(), y.host(), x.words() * 8) == 0;
+        std::printf("batched vs one-by-one bootstrap: %s (%zu words)\n", same ? "identical" : "DIFFERENT", x.words());
+        if (!same) fail++;
     }
     std::printf("galois key memory: %.2f GB\n", gal_keys.device_bytes() / 1e9);
     std::printf("%s\n", fail ? "FAILED" : "ok");
