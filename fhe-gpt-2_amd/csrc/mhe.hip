@@ -221,6 +221,7 @@ struct mhe_ctx
     int ks_share = 1;    // batched key switches sharing one key: XCD-grouped entries (MHE_KS_SHARE=0: off)
     int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
+    int ks_inv_fused = 1; // the fused MAC runs the special limbs' inverse row pass (MHE_KS_INV_FUSED)
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
     int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
@@ -1400,6 +1401,7 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
     if (r) return r;
     const int log_n = c->log_n;
     const size_t n = c->n;
+    int special_inv_done = 0; // the fused MAC ran the special limbs' inverse row pass
     // 1. t_target = INTT(target), canonical (evaluator.cpp:2351-2354)
     {
         JobB<JobStrided> j;
@@ -1453,7 +1455,9 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
             }
             timing_end(tc, st);
             hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
-            ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm_ks, I0, cnt, pack, kpack, share, st);
+            const int has_special = (I0 <= L && L < I0 + cnt && c->ks_inv_fused) ? 1 : 0;
+            special_inv_done |= ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm_ks, I0, cnt, pack, kpack,
+                                                 share, c->itw, has_special, st);
             timing_end(tm, st);
         }
     }
@@ -1486,7 +1490,7 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
         for (int e = 0; e < B; e++)
             j.j[e] = JobStrided{ w->e[e].acc + (size_t)L * n, w->e[e].acc + (size_t)L * n, (size_t)(L + 1) * n,
                                  (size_t)(L + 1) * n, c->K - 1, 0, c->primes, c->itw, log_n, 0 };
-        inv_row(j, log_n, 2 * B, c->nm, st);
+        if (!special_inv_done) inv_row(j, log_n, 2 * B, c->nm, st);
         // the special limbs' inverse column pass runs inside the lift column pass (k_icol_lift)
         // (not in the HMult tail: JobMDRCol reads the fully inverse-transformed special limbs)
         ColSrc cs{};
@@ -1721,6 +1725,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_HMULT_FUSED")) c->hmult_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_SHARE")) c->ks_share = atoi(f);
     if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
+    if (const char *f = getenv("MHE_KS_INV_FUSED")) c->ks_inv_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_PACK")) c->ks_pack = atoi(f);
     if (const char *f = getenv("MHE_GALOIS_FUSED")) c->galois_fused = atoi(f);
     if (const char *f = getenv("MHE_ICOL_FUSED")) c->icol_fused = atoi(f);

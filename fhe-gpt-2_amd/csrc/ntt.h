@@ -967,7 +967,8 @@ template <int LOGR, bool FP, bool KPF, bool MIX = false>
 #endif
 __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int log_n,
-                                                       long long twd, int I0, int pack, int kpack, int share)
+                                                       long long twd, int I0, int pack, int kpack, int share,
+                                                       const Tw *__restrict__ itw_all, long long tinv, int inv_special)
 {
     // tile (bx = column block group, by = output prime) and batch entry bz.  With `share` (every
     // entry reads the same key, gridDim.x * gridDim.y a multiple of 8) the linear workgroup ids are
@@ -1235,6 +1236,67 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
         }
         u64 *o0 = acc + (size_t)I * n + base;
         u64 *o1 = o0 + (size_t)(L + 1) * n;
+        if (inv_special && I == L) // uniform per workgroup
+        {
+            // The ModDown's first step, the inverse row pass of the special limbs (k_inv_row with
+            // JobStrided, evaluator.cpp:2466-2475), on this workgroup's rows: its accumulators are
+            // whole 2^LOGR-blocks, so the Gentleman-Sande stages LOGR-1 .. 0 run here -- in-lane
+            // position bits 0-2, then 3-5, then the rest, with the same swizzled in-wave transposes
+            // -- and the separate launch (and its HBM round trip) disappears.  Canonical output.
+            using AI = NttArith<FPA>;
+            const AI ai(p, itw_all + ((size_t)pi << log_n), tinv);
+            const u32 rbi = R1 + b;
+            auto tr = [&](T (&w)[8], int from, int to) {
+                wave_lds_fence();
+#pragma unroll
+                for (int e = 0; e < 8; e++) x0[swz(lay(t, e, from))] = w[e];
+                wave_lds_fence();
+#pragma unroll
+                for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, to))];
+            };
+            auto stages = [&](T (&w)[8], int b_lo, int s_hi, int s_lo) {
+#pragma unroll
+                for (int s = s_hi; s >= s_lo; s--)
+                    ai.template inv<8>(w, 1 << (LOGR - 1 - s - b_lo),
+                                       [&](int e) { return (rbi << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
+            };
+            auto inv_rows = [&](T (&w)[8]) {
+                tr(w, B_A, 0);
+                stages(w, 0, LOGR - 1, LOGR - 3);
+                tr(w, 0, 3);
+                stages(w, 3, LOGR - 4, LOGR > 6 ? LOGR - 6 : 0);
+                if (LOGR > 6)
+                {
+                    tr(w, 3, B_A);
+                    stages(w, B_A, LOGR - 7, 0);
+                }
+            };
+            T w0[8], w1[8];
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+            {
+                if constexpr (FPA)
+                {
+                    w0[e] = fp_reduce(a0[e], ar.q, ar.qinv);
+                    w1[e] = fp_reduce(a1[e], ar.q, ar.qinv);
+                }
+                else
+                {
+                    w0[e] = barrett128(a0[e].lo, a0[e].hi, p);
+                    w1[e] = barrett128(a1[e].lo, a1[e].hi, p);
+                }
+            }
+            inv_rows(w0);
+            inv_rows(w1);
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+            {
+                const u32 r = lay(t, e, B_A);
+                o0[r] = ai.canon(w0[e]);
+                o1[r] = ai.canon(w1[e]);
+            }
+            return;
+        }
 #pragma unroll
         for (int e = 0; e < 8; e++)
         {
@@ -1537,8 +1599,9 @@ static inline bool ks_key_prefetch()
 // measured at L=44: G=1 763, 2 738, 4 700 HMult/s (digit groups with a partial-sum reduction, since
 // removed); ResNet-20 (L <= 31): G=1 0.865-0.873 images/s vs 0.832-0.839 with G=2
 template <int LOGR, bool FP, bool MIX = false>
-static inline void ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
-                                long long twd, int I0, int cnt, int pack, int kpack, int share, hipStream_t st)
+static inline int ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
+                               long long twd, int I0, int cnt, int pack, int kpack, int share, const Tw *itw,
+                               long long tinv, int inv_special, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
     const int eb = ks_row_eb();
@@ -1547,8 +1610,8 @@ static inline void ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, 
         const dim3 g(blocks / RowMacShape<LOGR>::S, cnt, B);
         share = (share && B > 1 && (g.x * g.y) % 8 == 0) ? 1 : 0;
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, true, false, true>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
-                           I0, pack, kpack, share);
-        return;
+                           I0, pack, kpack, share, itw, tinv, inv_special);
+        return inv_special;
     }
     if (eb == 2 || eb == 3 || eb == 4)
     {
@@ -1563,42 +1626,49 @@ static inline void ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, 
         else
             hipLaunchKernelGGL((k_ks_row_mac_e<LOGR, FP, 3, 2>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
                                I0, pack, kpack, share);
-        return;
+        return 0; // the E-variants leave the special limbs' inverse row pass to k_inv_row
     }
     const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, B);
     share = (share && B > 1 && (grid.x * grid.y) % 8 == 0) ? 1 : 0;
     if (ks_key_prefetch())
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
-                           pack, kpack, share);
+                           pack, kpack, share, itw, tinv, inv_special);
     else
         hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
-                           pack, kpack, share);
+                           pack, kpack, share, itw, tinv, inv_special);
+    return inv_special;
 }
 
 template <int LOGR>
-static inline void ks_row_mac_m(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
-                                const NttMode &m, int I0, int cnt, int pack, int kpack, int share, hipStream_t st)
+static inline int ks_row_mac_m(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K, int log_n,
+                               const NttMode &m, int I0, int cnt, int pack, int kpack, int share, const Tw *itw,
+                               int inv_special, hipStream_t st)
 {
     if (m.fp == 2)
-        ks_row_mac_a<LOGR, true, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, share, st);
-    else if (m.fp)
-        ks_row_mac_a<LOGR, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, share, st);
-    else
-        ks_row_mac_a<LOGR, false>(P, B, primes, tw, L, K, log_n, 0, I0, cnt, pack, kpack, share, st);
+        return ks_row_mac_a<LOGR, true, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, share, itw,
+                                              m.dinv, inv_special, st);
+    if (m.fp)
+        return ks_row_mac_a<LOGR, true>(P, B, primes, tw, L, K, log_n, m.dfwd, I0, cnt, pack, kpack, share, itw, m.dinv,
+                                        inv_special, st);
+    return ks_row_mac_a<LOGR, false>(P, B, primes, tw, L, K, log_n, 0, I0, cnt, pack, kpack, share, itw, 0, inv_special,
+                                     st);
 }
 
 // Fused row pass + MAC for output primes I0 .. I0+cnt-1 (each entry's inter holds exactly those),
 // over B batch entries; share: every entry's key pointer is the same (XCD-grouped entries)
-static inline void ks_row_mac_chunk(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K,
-                                    int log_n, const NttMode &m, int I0, int cnt, int pack, int kpack, int share,
-                                    hipStream_t st)
+// inv_special: the launch covers the special prime (I = L) and may finish the special limbs' inverse
+// row pass itself (itw: inverse twiddles); returns 1 when it did, 0 when k_inv_row must still run.
+static inline int ks_row_mac_chunk(const KsPtrs &P, int B, const PrimeDev *primes, const Tw *tw, int L, int K,
+                                   int log_n, const NttMode &m, int I0, int cnt, int pack, int kpack, int share,
+                                   const Tw *itw, int inv_special, hipStream_t st)
 {
     switch (log_n / 2)
     {
-    case 6: ks_row_mac_m<6>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, share, st); break;
-    case 7: ks_row_mac_m<7>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, share, st); break;
+    case 6: return ks_row_mac_m<6>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, share, itw, inv_special, st);
+    case 7: return ks_row_mac_m<7>(P, B, primes, tw, L, K, log_n, m, I0, cnt, 0, kpack, share, itw, inv_special, st);
     case 8:
-        ks_row_mac_m<8>(P, B, primes, tw, L, K, log_n, m, I0, cnt, (pack && log_n == 16) ? 1 : 0, kpack, share, st);
-        break;
+        return ks_row_mac_m<8>(P, B, primes, tw, L, K, log_n, m, I0, cnt, (pack && log_n == 16) ? 1 : 0, kpack, share,
+                               itw, inv_special, st);
     }
+    return 0;
 }

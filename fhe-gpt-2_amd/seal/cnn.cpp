@@ -286,7 +286,7 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
     };
 
     if (cipher_pool.size() < static_cast<size_t>(6 + fh * fw - 1)) cipher_pool.resize(6 + fh * fw - 1);
-    Ciphertext &ctxt_in = cipher_pool[0], &ct_zero = cipher_pool[1], &temp = cipher_pool[2], &sum = cipher_pool[3],
+    Ciphertext &ctxt_in = cipher_pool[0], &ct_zero = cipher_pool[1], &sum = cipher_pool[3],
                &total_sum = cipher_pool[4], &var = cipher_pool[5];
     ctxt_in = cnn_in.cipher();
 
@@ -322,8 +322,21 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         { ko, ho, wo, to, n });
 
     const int d = static_cast<int>(log2_long(ki)), c = static_cast<int>(log2_long(ti));
+    // The q output-channel blocks i9 are independent until they are summed into total_sum, and
+    // each runs the same operation sequence (cnn_seal.cpp:435-493): they advance together, so each
+    // step -- the rescale of the tap sum, every channel-fold rotation (one key for all blocks), the
+    // gathering rotations -- is one batched launch over the blocks.  Every ciphertext sees the
+    // reference's operations in the reference's order, and total_sum is accumulated in (i9, i8)
+    // order, so the words are those of the block-by-block loop.
+    std::vector<Ciphertext> sums(q), vars(q), tmps(q);
+    std::vector<Ciphertext *> sp(q), vp(q), tp(q);
+    std::vector<const Ciphertext *> vc(q);
     for (int i9 = 0; i9 < q; i9++)
     {
+        sp[i9] = &sums[i9];
+        vp[i9] = &vars[i9];
+        tp[i9] = &tmps[i9];
+        vc[i9] = &vars[i9];
         // filter taps: multiply_vector_reduced_error + add_inplace_reduced_error, the product and the
         // add fused into one pass (bit-identical; every tap is at the input's level)
         for (int i1 = 0; i1 < fh; i1++)
@@ -336,55 +349,68 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
                 const Plaintext &wp = evaluator.cached_vector_plain(
                     tap, id.a, id.b, [&] { return weight_vec(i1, i2, i9); }, scratch);
                 if (i1 == 0 && i2 == 0)
-                    evaluator.multiply_plain(tap, wp, sum);
+                    evaluator.multiply_plain(tap, wp, sums[i9]);
                 else
-                    evaluator.multiply_plain_add_reduced_error(sum, tap, wp);
+                    evaluator.multiply_plain_add_reduced_error(sums[i9], tap, wp);
             }
-        evaluator.rescale_to_next_inplace(sum);
-        var = sum;
+    }
+    evaluator.rescale_to_next_inplace_many(sp);
+    for (int i9 = 0; i9 < q; i9++) vars[i9] = std::move(sums[i9]);
 
-        // sum over the input channels held in one replica
-        auto fold = [&](long step) {
-            rotate_copy(var, temp, static_cast<int>(step), evaluator, gal_keys);
-            evaluator.add_inplace_reduced_error(var, temp);
-        };
-        for (int x = 0; x < d; x++) fold(pow2(x));
-        for (int x = 0; x < d; x++) fold(pow2(x) * ki * wi);
-        if (c == -1)
-        {
-            sum = ct_zero;
-            std::vector<Ciphertext> parts(ti);
-            std::vector<Ciphertext *> pp;
-            std::vector<int> steps;
+    // sum over the input channels held in one replica
+    auto fold = [&](long step) {
+        rotate_copies(vc, std::vector<int>(q, static_cast<int>(step)), tp, evaluator, gal_keys);
+        for (int i9 = 0; i9 < q; i9++) evaluator.add_inplace_reduced_error(vars[i9], tmps[i9]);
+    };
+    for (int x = 0; x < d; x++) fold(pow2(x));
+    for (int x = 0; x < d; x++) fold(pow2(x) * ki * wi);
+    if (c == -1)
+    {
+        std::vector<std::vector<Ciphertext>> parts(q, std::vector<Ciphertext>(ti));
+        std::vector<const Ciphertext *> pin;
+        std::vector<Ciphertext *> pout;
+        std::vector<int> steps;
+        for (int i9 = 0; i9 < q; i9++)
             for (int x = 0; x < ti; x++)
             {
-                pp.push_back(&parts[x]);
+                pin.push_back(&vars[i9]);
+                pout.push_back(&parts[i9][x]);
                 steps.push_back(ki * ki * hi * wi * x);
             }
-            rotate_copies(var, steps, pp, evaluator, gal_keys);
-            for (int x = 0; x < ti; x++) evaluator.add_inplace_reduced_error(sum, parts[x]);
-            var = sum;
+        rotate_copies(pin, steps, pout, evaluator, gal_keys);
+        for (int i9 = 0; i9 < q; i9++)
+        {
+            sum = ct_zero;
+            for (int x = 0; x < ti; x++) evaluator.add_inplace_reduced_error(sum, parts[i9][x]);
+            vars[i9] = sum;
         }
-        else
-            for (int x = 0; x < c; x++) fold(pow2(x) * ki * ki * hi * wi);
+    }
+    else
+        for (int x = 0; x < c; x++) fold(pow2(x) * ki * ki * hi * wi);
 
-        // gather each output channel into its slots of the output layout (the rotations of var
-        // are independent: batched launches, then the products and sums in the reference's order)
-        std::vector<Ciphertext> gathered(pi);
+    // gather each output channel into its slots of the output layout (the rotations of every block
+    // are independent: batched launches, then the products and sums in the reference's order)
+    std::vector<std::vector<Ciphertext>> gathered(q, std::vector<Ciphertext>(pi));
+    {
+        std::vector<const Ciphertext *> gin;
         std::vector<Ciphertext *> gp;
         std::vector<int> gsteps;
+        for (int i9 = 0; i9 < q; i9++)
+            for (int i8 = 0; i8 < pi && pi * i9 + i8 < co; i8++)
+            {
+                const int j4 = pi * i9 + i8;
+                gin.push_back(&vars[i9]);
+                gp.push_back(&gathered[i9][i8]);
+                gsteps.push_back((int)((n / pi) * (j4 % pi) - j4 % ko - (j4 / (ko * ko)) * ko * ko * ho * wo -
+                                       ((j4 % (ko * ko)) / ko) * ko * wo));
+            }
+        rotate_copies(gin, gsteps, gp, evaluator, gal_keys);
+    }
+    for (int i9 = 0; i9 < q; i9++)
         for (int i8 = 0; i8 < pi && pi * i9 + i8 < co; i8++)
         {
             const int j4 = pi * i9 + i8;
-            gp.push_back(&gathered[i8]);
-            gsteps.push_back((int)((n / pi) * (j4 % pi) - j4 % ko - (j4 / (ko * ko)) * ko * ko * ho * wo -
-                                   ((j4 % (ko * ko)) / ko) * ko * wo));
-        }
-        rotate_copies(var, gsteps, gp, evaluator, gal_keys);
-        for (int i8 = 0; i8 < pi && pi * i9 + i8 < co; i8++)
-        {
-            const int j4 = pi * i9 + i8;
-            Ciphertext &g = gathered[i8];
+            Ciphertext &g = gathered[i9][i8];
             Recipe id = sel_id;
             id.ints({ j4 });
             multiply_static_vector(evaluator, g, id, [&] { return select_vec(j4); });
@@ -393,7 +419,7 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
             else
                 evaluator.add_inplace_reduced_error(total_sum, g);
         }
-    }
+    gathered.clear();
     evaluator.rescale_to_next_inplace(total_sum);
     var = total_sum;
 
