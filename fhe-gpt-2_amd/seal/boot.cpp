@@ -474,7 +474,7 @@ void Polynomial::homomorphic_poly_evaluation(SEALContext &, CKKSEncoder &, Encry
             if (!poly_heap[i]) continue;
             cipherheapbool[i] = true;
             if (!cipherheapbool[2 * (i + 1) - 1])
-                cipherheap[i] = cipherheap[2 * (i + 1)];
+                cipherheap[i] = std::move(cipherheap[2 * (i + 1)]); // the child is not read again
             else
             {
                 prod.push_back(i);
@@ -488,7 +488,7 @@ void Polynomial::homomorphic_poly_evaluation(SEALContext &, CKKSEncoder &, Encry
         for (long i : prod) evaluator.add_reduced_error(cipherheap[i], cipherheap[2 * (i + 1)], cipherheap[i]);
         gindex++;
     }
-    rtn = cipherheap[0];
+    rtn = std::move(cipherheap[0]);
 }
 } // namespace boot
 
@@ -1590,13 +1590,13 @@ void Bootstrapper::giant_rotate_sum(std::vector<Ciphertext> &giantct, std::vecto
     Ciphertext tmpct;
     for (std::size_t k = 0; k < giantct.size(); k++)
     {
-        const Ciphertext &term = (first + (int)k != 0) ? rotct[k] : giantct[k];
+        Ciphertext &term = (first + (int)k != 0) ? rotct[k] : giantct[k];
         if (k == 0)
-            tmpct = term;
+            tmpct = std::move(term); // the terms are dead after the sum: no device copies
         else
             evaluator.add_inplace_reduced_error(tmpct, term);
     }
-    rtncipher = tmpct;
+    rtncipher = std::move(tmpct);
 }
 
 void Bootstrapper::rotated_bsgs_linear_transform(Ciphertext &rtncipher, Ciphertext &cipher, int totlen,

@@ -380,9 +380,9 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         rotate_copies(pin, steps, pout, evaluator, gal_keys);
         for (int i9 = 0; i9 < q; i9++)
         {
-            sum = ct_zero;
-            for (int x = 0; x < ti; x++) evaluator.add_inplace_reduced_error(sum, parts[i9][x]);
-            vars[i9] = sum;
+            Ciphertext acc = ct_zero;
+            for (int x = 0; x < ti; x++) evaluator.add_inplace_reduced_error(acc, parts[i9][x]);
+            vars[i9] = std::move(acc);
         }
     }
     else
@@ -415,13 +415,13 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
             id.ints({ j4 });
             multiply_static_vector(evaluator, g, id, [&] { return select_vec(j4); });
             if (i8 == 0 && i9 == 0)
-                total_sum = g;
+                total_sum = std::move(g);
             else
                 evaluator.add_inplace_reduced_error(total_sum, g);
         }
     gathered.clear();
     evaluator.rescale_to_next_inplace(total_sum);
-    var = total_sum;
+    var = std::move(total_sum);
 
     // po replicas of the output
     if (!end)
@@ -437,9 +437,9 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         }
         rotate_copies(var, rsteps, rp, evaluator, gal_keys);
         for (int u6 = 0; u6 < po; u6++) evaluator.add_inplace_reduced_error(sum, reps[u6]);
-        var = sum;
+        var = std::move(sum);
     }
-    cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, var);
+    cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, std::move(var));
 }
 
 // ------------------------------------------------------------------------ batch norm
@@ -474,7 +474,7 @@ void multiplexed_parallel_batch_norm_seal(const TensorCipher &cnn_in, TensorCiph
     encoder.encode(g, temp.scale(), plain);
     encryptor.encrypt(plain, cipher_g);
     evaluator.sub_inplace_reduced_error(temp, cipher_g);
-    cnn_out = TensorCipher(logn, ki, hi, wi, ci, ti, pi, temp);
+    cnn_out = TensorCipher(logn, ki, hi, wi, ci, ti, pi, std::move(temp));
 }
 
 // ------------------------------------------------------------------------ ReLU
@@ -489,7 +489,7 @@ void ReLU_seal(const TensorCipher &cnn_in, TensorCipher &cnn_out, long comp_no, 
     Ciphertext temp = cnn_in.cipher();
     minimax_ReLU_seal(comp_no, deg, alpha, tree, scaled_val, scalingfactor, encryptor, evaluator, decryptor, encoder,
                       public_key, secret_key, relin_keys, temp, temp);
-    cnn_out = TensorCipher(cnn_in.logn(), cnn_in.k(), cnn_in.h(), cnn_in.w(), cnn_in.c(), cnn_in.t(), cnn_in.p(), temp);
+    cnn_out = TensorCipher(cnn_in.logn(), cnn_in.k(), cnn_in.h(), cnn_in.w(), cnn_in.c(), cnn_in.t(), cnn_in.p(), std::move(temp));
 }
 
 // ------------------------------------------------------------------------ residual add
@@ -502,7 +502,7 @@ void cnn_add_seal(const TensorCipher &cnn1, const TensorCipher &cnn2, TensorCiph
     Ciphertext a = cnn1.cipher();
     const Ciphertext b = cnn2.cipher();
     evaluator.add_inplace_reduced_error(a, b);
-    destination = TensorCipher(cnn1.logn(), cnn1.k(), cnn1.h(), cnn1.w(), cnn1.c(), cnn1.t(), cnn1.p(), a);
+    destination = TensorCipher(cnn1.logn(), cnn1.k(), cnn1.h(), cnn1.w(), cnn1.c(), cnn1.t(), cnn1.p(), std::move(a));
 }
 
 // ------------------------------------------------------------------------ downsampling
@@ -573,7 +573,7 @@ void multiplexed_parallel_downsampling_seal(const TensorCipher &cnn_in, TensorCi
         rotate_copies(packed, rsteps, rp, evaluator, gal_keys);
         for (auto &r : reps) evaluator.add_inplace_reduced_error(sum, r);
     }
-    cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, sum);
+    cnn_out = TensorCipher(logn, ko, ho, wo, co, to, po, std::move(sum));
 }
 
 // ------------------------------------------------------------------------ average pooling
@@ -626,7 +626,7 @@ void averagepooling_seal_scale(const TensorCipher &cnn_in, TensorCipher &cnn_out
                 evaluator.add_inplace_reduced_error(sum, temp);
         }
     evaluator.rescale_to_next_inplace(sum);
-    cnn_out = TensorCipher(logn, 1, 1, 1, ci, ti, 1, sum);
+    cnn_out = TensorCipher(logn, 1, 1, 1, ci, ti, 1, std::move(sum));
 }
 
 // ------------------------------------------------------------------------ fully connected
@@ -673,5 +673,5 @@ void matrix_multiplication_seal(const TensorCipher &cnn_in, TensorCipher &cnn_ou
             evaluator.add_inplace_reduced_error(sum, temp);
     }
     evaluator.rescale_to_next_inplace(sum);
-    cnn_out = TensorCipher(cnn_in.logn(), cnn_in.k(), cnn_in.h(), cnn_in.w(), cnn_in.c(), cnn_in.t(), cnn_in.p(), sum);
+    cnn_out = TensorCipher(cnn_in.logn(), cnn_in.k(), cnn_in.h(), cnn_in.w(), cnn_in.c(), cnn_in.t(), cnn_in.p(), std::move(sum));
 }

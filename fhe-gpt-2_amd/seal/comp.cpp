@@ -365,7 +365,7 @@ void eval_polynomial_integrate(Encryptor &encryptor, Evaluator &evaluator, Decry
                 evaluator.sub_reduced_error(*st.prod, *st.minus, *T[st.g]);
             }
         }
-        res = need(pt[1], "pt[1]");
+        res = std::move(need(pt[1], "pt[1]"));
         return;
     }
 

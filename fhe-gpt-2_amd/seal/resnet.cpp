@@ -586,7 +586,7 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
 
     Ciphertext ctxt = cnn.cipher();
     for (int i = 0; i < m.boot_level - 3; i++) evaluator.mod_switch_to_next_inplace(ctxt);
-    cnn.set_ciphertext(ctxt);
+    cnn.set_ciphertext(std::move(ctxt));
 
     // layer 0
     if (log) *log << "layer 0" << std::endl;
@@ -608,7 +608,7 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
         evaluator.multiply_plain_inplace(ctxt, scaler);
         evaluator.rescale_to_next_inplace(ctxt);
         ctxt.scale() = std::pow(2.0, 46);
-        cnn.set_ciphertext(ctxt);
+        cnn.set_ciphertext(std::move(ctxt));
     }
     multiplexed_parallel_batch_norm_seal(cnn, cnn, prm.bn_bias[stage], prm.bn_running_mean[stage],
                                          prm.bn_running_var[stage], prm.bn_weight[stage], epsilon, encoder, encryptor,
@@ -634,7 +634,7 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
             seal::Lockstep::Active merge; // MHE_RESNET_LOCKSTEP=2 (a no-op outside a group)
             m.boot[j]->bootstrap_real_3(rtn, c);
         }
-        cnn.set_ciphertext(rtn);
+        cnn.set_ciphertext(std::move(rtn));
         sync();
         t_boot += std::chrono::duration<double>(clk::now() - a).count();
         res.bootstraps++;
