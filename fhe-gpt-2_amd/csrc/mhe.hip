@@ -935,6 +935,34 @@ __global__ void k_mulplain_add(const u64 *a, const u64 *b, u64 *acc, const Prime
     *(ulonglong2 *)(acc + i) = r;
 }
 
+// acc = (accumulate ? acc : 0) + sum_k a_k * b_k, up to 16 terms per launch (pointers in the kernel
+// arguments); each thread's 2 * cnt loads are independent, so they are all in flight together
+#define MHE_SUM_TERMS 16
+struct SumPtrs
+{
+    const u64 *a[MHE_SUM_TERMS];
+    const u64 *b[MHE_SUM_TERMS];
+};
+__global__ void k_mulplain_sum(SumPtrs P, int cnt, u64 *acc, int accumulate, const PrimeDev *primes, int limbs,
+                               int log_n, size_t total2)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 >= total2) return;
+    const size_t i = i2 * 2;
+    const size_t limb_words = (size_t)limbs << log_n;
+    const int l = (int)((i >> log_n) % limbs);
+    const PrimeDev p = primes[l];
+    ulonglong2 z = accumulate ? *(const ulonglong2 *)(acc + i) : ulonglong2{ 0, 0 };
+    for (int k = 0; k < cnt; k++)
+    {
+        const ulonglong2 x = *(const ulonglong2 *)(P.a[k] + i);
+        const ulonglong2 y = *(const ulonglong2 *)(P.b[k] + i % limb_words);
+        z.x = addmod(z.x, mulmod(x.x, y.x, p), p.q);
+        z.y = addmod(z.y, mulmod(x.y, y.y, p), p.q);
+    }
+    *(ulonglong2 *)(acc + i) = z;
+}
+
 struct ScalarTab
 {
     u64 v[64];
@@ -2305,6 +2333,33 @@ MHE_EXPORT int mhe_multiply_plain_add(mhe_ctx *c, const uint64_t *a, const uint6
     hipLaunchKernelGGL(k_mulplain_add, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, acc, c->primes, limbs, c->log_n,
                        total2);
     HIP_LAUNCH_CHECK();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_multiply_plain_sum(mhe_ctx *c, int count, const uint64_t *const *a, const uint64_t *const *b,
+                                      uint64_t *out, int accumulate, int polys, int limbs, void *s)
+{
+    if (count < 1 || !a || !b || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    for (int k = 0; k < count; k++)
+    {
+        int r = check_poly_args(c, a[k], polys, limbs);
+        if (r) return r;
+        if (!b[k]) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    }
+    const size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
+    for (int k0 = 0; k0 < count; k0 += MHE_SUM_TERMS)
+    {
+        const int cnt = std::min(MHE_SUM_TERMS, count - k0);
+        SumPtrs P{};
+        for (int k = 0; k < cnt; k++)
+        {
+            P.a[k] = a[k0 + k];
+            P.b[k] = b[k0 + k];
+        }
+        hipLaunchKernelGGL(k_mulplain_sum, ELEM_GRID(total2), dim3(256), 0, S(s), P, cnt, out,
+                           (accumulate || k0 > 0) ? 1 : 0, c->primes, limbs, c->log_n, total2);
+        HIP_LAUNCH_CHECK();
+    }
     return MHE_OK;
 }
 

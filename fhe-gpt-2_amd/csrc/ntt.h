@@ -358,7 +358,7 @@ struct RowLds
 };
 
 // --------------------------------------------------------------------- forward, row pass
-template <int LOGR, int LOGT, class Job, bool FP>
+template <int LOGR, int LOGT, class Job, bool FP, bool PRE_ON = true>
 __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long twd)
 {
     using SH = Shape<LOGR, LOGT>;
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long t
     const auto V = job.view(blockIdx.y);
     if (V.skip) return; // uniform per workgroup, before any barrier
     using VW = std::remove_cv_t<decltype(V)>;
-    constexpr bool PRE = PreOf<VW>::value;
+    constexpr bool PRE = PreOf<VW>::value && PRE_ON;
     const A ar(V.p, V.tw, twd);
     T v[E];
 #pragma unroll
@@ -800,6 +800,19 @@ enum PassKind
     INV_COL
 };
 
+// Launches of at most this many workgroups prefetch a row pass's epilogue operands (PreOf): with
+// the operands in registers the kernel runs at 3 instead of 4 waves/SIMD, which pays for latency-bound
+// launches of a few rounds (ResNet's rescales and ModDowns) but not for the HMult tail's ~11k
+// workgroups (MHE_ROW_PRE_MAX_WG).
+static inline long row_pre_max_wg()
+{
+    static const long v = [] {
+        const char *e = getenv("MHE_ROW_PRE_MAX_WG");
+        return e ? atol(e) : 8192L;
+    }();
+    return v;
+}
+
 template <int PASS, int LOGR, class Job, bool FP>
 static inline void launch_pass_a(const Job &job, int log_n, int jobs, long long twd, hipStream_t st)
 {
@@ -808,7 +821,13 @@ static inline void launch_pass_a(const Job &job, int log_n, int jobs, long long 
     const int subs = 1 << (log_n - LOGR);
     dim3 grid(subs / SH::S, jobs);
     if (PASS == FWD_COL) hipLaunchKernelGGL((k_fwd_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
-    if (PASS == FWD_ROW) hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if (PASS == FWD_ROW)
+    {
+        if ((long)grid.x * grid.y <= row_pre_max_wg())
+            hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP, true>), grid, dim3(256), 0, st, job, log_n, twd);
+        else
+            hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP, false>), grid, dim3(256), 0, st, job, log_n, twd);
+    }
     if (PASS == INV_ROW) hipLaunchKernelGGL((k_inv_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
     if (PASS == INV_COL) hipLaunchKernelGGL((k_inv_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
 }

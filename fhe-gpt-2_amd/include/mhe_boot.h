@@ -230,6 +230,12 @@ private:
                           int gs, int basicstep, seal::Ciphertext &rtncipher);
     void multiply_diag(seal::Ciphertext &ct, const std::vector<std::complex<double>> &diag, int coeff_logn,
                        int shift, seal::Ciphertext &dest, double coeff_scale = 1.0, bool accumulate = false);
+    // the encoded, rotated diagonal multiply_diag multiplies by (cached, or built into `local`)
+    const seal::Plaintext &diag_plain(seal::Ciphertext &ct, const std::vector<std::complex<double>> &diag, int coeff_logn,
+                                      int shift, double coeff_scale, seal::Plaintext &local);
+    // one giant step's inner sum: sum_j diag_j(babyct[j]) * babyct[j] into dest (multiply_plain_sum)
+    void diag_sum(const std::vector<seal::Ciphertext *> &cts, const std::vector<const std::vector<std::complex<double>> *> &diags,
+                  int coeff_logn, int shift, double coeff_scale, seal::Ciphertext &dest);
     struct PtKey
     {
         const void *diag;

@@ -864,6 +864,11 @@ public:
     // (not SEAL API) multiply_plain(encrypted, plain, t) + add_inplace_reduced_error(acc, t) for acc at
     // encrypted's level, fused into one pass with bit-identical output
     void multiply_plain_add_reduced_error(Ciphertext &acc, const Ciphertext &encrypted, const Plaintext &plain) const;
+    // (not SEAL API) multiply_plain(encrypted[0], plain[0], destination), then
+    // multiply_plain_add_reduced_error(destination, encrypted[k], plain[k]) for k = 1, 2, ... (all at one
+    // level and size): the same words and scale, one pass per 16 terms (mhe_multiply_plain_sum)
+    void multiply_plain_sum(const std::vector<const Ciphertext *> &encrypted, const std::vector<const Plaintext *> &plain,
+                            Ciphertext &destination) const;
     void add_reduced_error(const Ciphertext &encrypted1, const Ciphertext &encrypted2, Ciphertext &destination) const
     {
         // evaluator.h: operands swap when destination aliases encrypted2

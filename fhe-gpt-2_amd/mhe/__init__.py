@@ -40,6 +40,8 @@ SIGNATURES = {
     "mhe_stream_sync": (ctypes.c_int, [vp, vp]),
     "mhe_stream_wait": (ctypes.c_int, [vp, vp, vp]),
     "mhe_multiply_plain_add": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_multiply_plain_sum": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              vp]),
     "mhe_key_traffic": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_key_prepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_unprepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
@@ -267,6 +269,14 @@ class Engine:
         out = self.empty(*a.shape) if out is None else out
         p, l = self._pl(a)
         _check(lib().mhe_multiply_plain(self._h, _ptr(a), _ptr(pt), _ptr(out), p, l, self.stream()))
+        return out
+
+    def multiply_plain_sum(self, cts, pts, out=None, accumulate=False):
+        """mhe_multiply_plain_sum: out (+)= sum_k cts[k] * pts[k] in one pass per 16 terms."""
+        out = self.empty(*cts[0].shape) if out is None else out
+        p, l = self._pl(cts[0])
+        _check(lib().mhe_multiply_plain_sum(self._h, len(cts), self._ptrs(cts), self._ptrs(pts), _ptr(out),
+                                            1 if accumulate else 0, p, l, self.stream()))
         return out
 
     def _scalar(self, fn, a, scalars, out):

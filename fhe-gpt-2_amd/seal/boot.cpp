@@ -1455,11 +1455,38 @@ bool pt_cache_on()
 void Bootstrapper::multiply_diag(Ciphertext &ct, const std::vector<cd> &diag, int coeff_logn, int shift,
                                  Ciphertext &dest, double coeff_scale, bool accumulate)
 {
+    Plaintext local;
+    const Plaintext &pt = diag_plain(ct, diag, coeff_logn, shift, coeff_scale, local);
+    // accumulate: dest += ct * pt (the loop's add_inplace_reduced_error fused into the product)
+    if (accumulate)
+        evaluator.multiply_plain_add_reduced_error(dest, ct, pt);
+    else
+        evaluator.multiply_plain(ct, pt, dest);
+}
+
+void Bootstrapper::diag_sum(const std::vector<Ciphertext *> &cts, const std::vector<const std::vector<cd> *> &diags,
+                            int coeff_logn, int shift, double coeff_scale, Ciphertext &dest)
+{
+    // multiply_diag(cts[0], ..., dest) then multiply_diag(cts[j], ..., dest, accumulate) for j > 0:
+    // the products and their sum in one pass (Evaluator::multiply_plain_sum), the same words
+    std::vector<Plaintext> locals(cts.size());
+    std::vector<const Ciphertext *> cs;
+    std::vector<const Plaintext *> ps;
+    for (std::size_t j = 0; j < cts.size(); j++)
+    {
+        ps.push_back(&diag_plain(*cts[j], *diags[j], coeff_logn, shift, coeff_scale, locals[j]));
+        cs.push_back(cts[j]);
+    }
+    evaluator.multiply_plain_sum(cs, ps, dest);
+}
+
+const Plaintext &Bootstrapper::diag_plain(Ciphertext &ct, const std::vector<cd> &diag, int coeff_logn, int shift,
+                                          double coeff_scale, Plaintext &local)
+{
     // rotation(coeff_logn, Nh, shift, diag) + multiply_vector_reduced_error (Bootstrapper.cpp:1983-1984):
     // the diagonal is encoded at ct.scale() on the first level and kept at ct's level
     const PtKey key{ &diag, shift, ct.coeff_modulus_size(), ct.scale(), coeff_scale, coeff_logn };
     const Plaintext *pt = nullptr;
-    Plaintext local;
     if (pt_cache_on())
     {
         std::lock_guard<std::mutex> lk(g_pt_mu);
@@ -1481,11 +1508,7 @@ void Bootstrapper::multiply_diag(Ciphertext &ct, const std::vector<cd> &diag, in
         else
             pt = &local;
     }
-    // accumulate: dest += ct * pt (the loop's add_inplace_reduced_error fused into the product)
-    if (accumulate)
-        evaluator.multiply_plain_add_reduced_error(dest, ct, *pt);
-    else
-        evaluator.multiply_plain(ct, *pt, dest);
+    return *pt;
 }
 
 std::size_t Bootstrapper::verify_cache()
@@ -1557,14 +1580,15 @@ void Bootstrapper::bsgs_linear_transform(Ciphertext &rtncipher, Ciphertext &ciph
     std::vector<Ciphertext> giantct(ng), rotct(ng);
     for (int i = giantfirst1; i <= giantlast1; i++)
     {
-        bool giantbool = false;
         const int jlast = i != giantlast1 ? basicstart1 + gs1 - 1 : totlen - i * gs1;
+        std::vector<Ciphertext *> cts;
+        std::vector<const std::vector<cd> *> diags;
         for (int j = basicstart1; j <= jlast; j++)
         {
-            multiply_diag(babyct[j - basicstart1], fftcoeff[(i * gs1 + j) + totlen], coeff_logn,
-                          (-i) * gs1 * basicstep, giantct[i - giantfirst1], coeff_scale, giantbool);
-            giantbool = true;
+            cts.push_back(&babyct[j - basicstart1]);
+            diags.push_back(&fftcoeff[(i * gs1 + j) + totlen]);
         }
+        if (!cts.empty()) diag_sum(cts, diags, coeff_logn, (-i) * gs1 * basicstep, coeff_scale, giantct[i - giantfirst1]);
     }
     giant_rotate_sum(giantct, rotct, giantfirst1, gs1, basicstep, rtncipher);
 }
@@ -1628,14 +1652,15 @@ void Bootstrapper::rotated_bsgs_linear_transform(Ciphertext &rtncipher, Cipherte
     std::vector<Ciphertext> giantct(giantlast2 + 1), rotct(giantlast2 + 1);
     for (int i = 0; i <= giantlast2; i++)
     {
-        bool giantbool = false;
         const int jlast = i != giantlast2 ? gs2 - 1 : totlen - i * gs2;
+        std::vector<Ciphertext *> cts;
+        std::vector<const std::vector<cd> *> diags;
         for (int j = 0; j <= jlast; j++)
         {
-            multiply_diag(babyct[j], fftcoeff[i * gs2 + j], coeff_logn, (-i) * gs2 * basicstep, giantct[i],
-                          coeff_scale, giantbool);
-            giantbool = true;
+            cts.push_back(&babyct[j]);
+            diags.push_back(&fftcoeff[i * gs2 + j]);
         }
+        if (!cts.empty()) diag_sum(cts, diags, coeff_logn, (-i) * gs2 * basicstep, coeff_scale, giantct[i]);
     }
     giant_rotate_sum(giantct, rotct, 0, gs2, basicstep, rtncipher);
 }

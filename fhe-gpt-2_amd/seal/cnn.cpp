@@ -337,22 +337,23 @@ void multiplexed_parallel_convolution_seal(const TensorCipher &cnn_in, TensorCip
         vp[i9] = &vars[i9];
         tp[i9] = &tmps[i9];
         vc[i9] = &vars[i9];
-        // filter taps: multiply_vector_reduced_error + add_inplace_reduced_error, the product and the
-        // add fused into one pass (bit-identical; every tap is at the input's level)
+        // filter taps: multiply_vector_reduced_error + add_inplace_reduced_error over the fh x fw taps,
+        // every product and the sum in one pass (Evaluator::multiply_plain_sum; bit-identical, every
+        // tap is at the input's level)
+        std::vector<Plaintext> scratch((size_t)fh * fw);
+        std::vector<const Ciphertext *> taps;
+        std::vector<const Plaintext *> wps;
         for (int i1 = 0; i1 < fh; i1++)
             for (int i2 = 0; i2 < fw; i2++)
             {
-                Ciphertext &tap = *rot[fw * i1 + i2];
-                Plaintext scratch;
+                const Ciphertext &tap = *rot[fw * i1 + i2];
                 Recipe id = conv_id;
                 id.ints({ i1, i2, i9 });
-                const Plaintext &wp = evaluator.cached_vector_plain(
-                    tap, id.a, id.b, [&] { return weight_vec(i1, i2, i9); }, scratch);
-                if (i1 == 0 && i2 == 0)
-                    evaluator.multiply_plain(tap, wp, sums[i9]);
-                else
-                    evaluator.multiply_plain_add_reduced_error(sums[i9], tap, wp);
+                wps.push_back(&evaluator.cached_vector_plain(tap, id.a, id.b, [&] { return weight_vec(i1, i2, i9); },
+                                                              scratch[(size_t)fw * i1 + i2]));
+                taps.push_back(&tap);
             }
+        evaluator.multiply_plain_sum(taps, wps, sums[i9]);
     }
     evaluator.rescale_to_next_inplace_many(sp);
     for (int i9 = 0; i9 < q; i9++) vars[i9] = std::move(sums[i9]);

@@ -2793,6 +2793,50 @@ void Evaluator::multiply_plain_add_reduced_error(Ciphertext &acc, const Cipherte
     acc.scale() = new_scale;
 }
 
+void Evaluator::multiply_plain_sum(const std::vector<const Ciphertext *> &encrypted,
+                                   const std::vector<const Plaintext *> &plain, Ciphertext &destination) const
+{
+    if (encrypted.empty() || encrypted.size() != plain.size())
+        throw std::invalid_argument("encrypted and plain must be non-empty and of the same size");
+    for (std::size_t k = 0; k < encrypted.size(); k++)
+        if (!encrypted[k] || !plain[k] || encrypted[k] == &destination)
+            throw std::invalid_argument("multiply_plain_sum: null operand or destination among the inputs");
+    // term by term under the evaluator trace (one record per operation) or with batching off
+    if (trace::enabled() || !batched_launches())
+    {
+        multiply_plain(*encrypted[0], *plain[0], destination);
+        for (std::size_t k = 1; k < encrypted.size(); k++)
+            multiply_plain_add_reduced_error(destination, *encrypted[k], *plain[k]);
+        return;
+    }
+    const Ciphertext &e0 = *encrypted[0];
+    Level lv = check_ct(context_, e0, "encrypted");
+    double new_scale = 0;
+    for (std::size_t k = 0; k < encrypted.size(); k++)
+    {
+        const Ciphertext &e = *encrypted[k];
+        const Plaintext &p = *plain[k];
+        Level lk = check_ct(context_, e, "encrypted");
+        if (lk.L != lv.L || e.size() != e0.size())
+            throw std::invalid_argument("multiply_plain_add: acc and encrypted must share level and size");
+        if (!e.is_ntt_form() || !p.is_ntt_form()) throw std::invalid_argument("NTT form mismatch");
+        if (e.parms_id() != p.parms_id()) throw std::invalid_argument("encrypted_ntt and plain_ntt parameter mismatch");
+        new_scale = e.scale() * p.scale();
+        check_scale(new_scale, lv);
+    }
+    void *s = context_.stream();
+    std::vector<const std::uint64_t *> a, b;
+    for (std::size_t k = 0; k < encrypted.size(); k++)
+    {
+        a.push_back(encrypted[k]->store().dev_read(s));
+        b.push_back(plain[k]->store().dev_read(s));
+    }
+    fresh_dest(context_, e0, destination, e0.size());
+    chk(mhe_multiply_plain_sum(context_.engine(), (int)a.size(), a.data(), b.data(), destination.store().dev_write(s, true),
+                               0, (int)e0.size(), (int)lv.L, s));
+    destination.scale() = new_scale; // the last term's product scale, as the reduced-error adds leave it
+}
+
 namespace
 {
 template <typename T>

@@ -113,6 +113,14 @@ int mhe_multiply_plain(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint6
  * pass, bit-identical to the two (evaluator.cpp:1891-1930, 78-120) */
 int mhe_multiply_plain_add(mhe_ctx *ctx, const uint64_t *a, const uint64_t *b, uint64_t *acc, int polys, int limbs,
                            void *stream);
+/* out = (accumulate ? out : 0) + sum_k a[k] * b[k] over `count` terms (each b[k] broadcast over the
+ * polys of a[k]): one multiply_plain_ntt followed by count - 1 fused multiply_plain + add_inplace
+ * steps of the same level, in one pass per 16 terms; the residues are those of the term-by-term
+ * sequence (every partial sum is reduced mod q, and modular addition does not depend on order).
+ * Used by the convolution's filter taps (cnn_seal.cpp:435-453) and the BSGS inner sums
+ * (Bootstrapper.cpp:1975-1988). */
+int mhe_multiply_plain_sum(mhe_ctx *ctx, int count, const uint64_t *const *a, const uint64_t *const *b, uint64_t *out,
+                           int accumulate, int polys, int limbs, void *stream);
 /* multiply_poly_scalar_coeffmod with one scalar per limb (scalars[l] < q_l), host array;
  * used by multiply_const (evaluator.cpp:287-301). */
 int mhe_multiply_scalar(mhe_ctx *ctx, const uint64_t *a, const uint64_t *scalars, uint64_t *out, int polys,

@@ -136,6 +136,25 @@ def test_multiply_plain_ntt(small):
     assert np.array_equal(got, ch.oc.multiply_plain(ct, pt))
 
 
+@pytest.mark.parametrize("terms", [1, 9, 17])
+def test_multiply_plain_sum(small, terms):
+    """mhe_multiply_plain_sum == multiply_plain of the first term + add of each later product
+    (the conv taps / BSGS inner sums), also past the 16 terms of one launch and accumulating."""
+    ch = small
+    L = ch.K - 1
+    cts = [ch.rand(2, L, ch.n) for _ in range(terms)]
+    pts = [ch.rand(L, ch.n) for _ in range(terms)]
+    want = ch.oc.multiply_plain(cts[0], pts[0])
+    for c, p in zip(cts[1:], pts[1:]):
+        want = ch.oc.add(want, ch.oc.multiply_plain(c, p))
+    dc, dp = [ch.up(c) for c in cts], [ch.up(p) for p in pts]
+    got = ch.down(ch.eng.multiply_plain_sum(dc, dp))
+    assert np.array_equal(got, want)
+    acc = ch.rand(2, L, ch.n)
+    got2 = ch.down(ch.eng.multiply_plain_sum(dc, dp, out=ch.up(acc), accumulate=True))
+    assert np.array_equal(got2, ch.oc.add(acc, want))
+
+
 def test_multiply_add_scalar(small):
     ch = small
     L = ch.K - 1
