@@ -498,6 +498,10 @@ def main():
             "modup_col_avg_launch_us": round(mc_avg_us, 2),
             "launches_timed": km_n.value,
             "timing": "HIP events around each launch on its stream; single-stream pass when --streams > 1",
+            # with one key stream shared by G_launch HMults the kernel moves few bytes per HMult and is
+            # bound by FP64 VALU issue instead: valu_roofline (model lane-ops; SQ_INSTS_VALU when
+            # committed) is the binding fraction, this HBM fraction only the bytes it moves
+            "binding_resource": "valu" if G_launch > 1 else "hbm",
         },
         # the same kernel against the FP64 VALU issue rate ("also report the int-VALU
         # bound"; the engine's modular arithmetic runs on the FP64 pipe, csrc/fparith.h)

@@ -874,13 +874,16 @@ static inline void icol_lift_a(const ColSrc &cs, const Job &job, int polys, int 
     constexpr int LOGT = LOGR <= 7 ? 3 : 4;
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
-    // one output prime per group (MHE_ICOL_GROUP primes per group): the grid stays as wide as the
-    // separate forward column pass's, and each workgroup redoes the cheap inverse stages of its
-    // columns from L2
-    static const int per = [] {
+    // output primes per workgroup: each workgroup redoes the inverse column stages of its columns
+    // (from L2) once per group, so small launches keep one prime per workgroup (the widest grid) and
+    // batched ones share the inverse stages over 2-3 primes (ubench at 31 / 20 limbs, profiles/r03v:
+    // 4 rescales 207 -> 185 us); MHE_ICOL_GROUP fixes the count
+    static const int fixed = [] {
         const char *e = getenv("MHE_ICOL_GROUP");
-        return e && atoi(e) > 0 ? atoi(e) : 1;
+        return e && atoi(e) > 0 ? atoi(e) : 0;
     }();
+    const int jobs = polys * cnt;
+    const int per = fixed ? fixed : jobs >= 128 ? 3 : jobs >= 56 ? 2 : 1;
     const int IG = (cnt + per - 1) / per;
     hipLaunchKernelGGL((k_icol_lift<LOGR, LOGT, Job, FP>), dim3(subs / SH::S, polys, IG), dim3(256), 0, st, cs, job,
                        cnt, log_n, dinv, dfwd);
