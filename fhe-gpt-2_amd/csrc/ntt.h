@@ -28,7 +28,9 @@
 // Batched launches: one launch of a key-switch / rescale kernel serves up to MHE_MAXB independent
 // ciphertexts of the same level (per-entry pointers in the kernel arguments, entry = a grid
 // dimension), so small-level work from independent rotations or images fills the chip.
+#ifndef MHE_MAXB
 #define MHE_MAXB 8
+#endif
 
 
 // Streaming (non-temporal) access for the key-switch streams, selected at build time (MHE_NT bit 0:
