@@ -608,6 +608,9 @@ struct KsPtrs
 #ifndef MHE_MODUP_OCC
 #define MHE_MODUP_OCC 3 // waves per SIMD the ModUp column pass is compiled for (168 VGPRs)
 #endif
+#ifndef MHE_MODUP_TWG
+#define MHE_MODUP_TWG 5 // output primes per group whose twiddles the ModUp column pass stages in LDS
+#endif
 // MIX (with FP): output primes >= 2^51 (the GPT-2 chain's special prime) take the integer sweep
 template <int LOGR, int LOGT, bool FP, bool MIX = false>
 __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, const PrimeDev *__restrict__ primes,
@@ -620,7 +623,13 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
     using A = NttArith<FP>;
     using T = typename A::T;
     constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
+    constexpr int R = SH::R;
     __shared__ T lds[S * LD];
+    // The column-pass twiddles of the group's output primes (entries 1 .. R-1 of each prime's table,
+    // the same for every column), staged once per workgroup.  Read from global memory stage by stage
+    // instead, each twiddle load's s_waitcnt also waited for the previous prime's stores (one
+    // counter for loads and stores), so compute and stores of consecutive primes never overlapped.
+    __shared__ Tw twc[MHE_MODUP_TWG > 0 ? MHE_MODUP_TWG * R : 1];
     const int tid = threadIdx.x, sl = tid % S, t = tid / S;
     const int logC = log_n - LOGR;
     // 1-D grid of X column blocks x L digits x IG output-prime groups.  xcd: the IG groups of one
@@ -651,6 +660,23 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
 #pragma unroll
     for (int e = 0; e < E; e++) x[e] = src[c + ((u32)(t + TPS * e) << logC)];
     const u64 qJ = primes[J].q;
+    // twiddles of the group's primes into LDS (16 B each: the FP table (w, w/q) or the integer one
+    // (w, Shoup), whichever the prime's sweep uses); groups wider than MHE_MODUP_TWG read global
+    const bool twl_on = MHE_MODUP_TWG > 0 && i_hi - i_lo <= MHE_MODUP_TWG; // uniform per workgroup
+    if (twl_on)
+    {
+        const int ng = i_hi - i_lo;
+        for (int k = tid; k < ng * R; k += 256)
+        {
+            const int g = k / R, idx = k % R;
+            const int I = i_lo + g;
+            const int pi = (I == L) ? K - 1 : I;
+            const bool fpt = FP && primes[pi].q < (1ull << 51);
+            const char *base = reinterpret_cast<const char *>(tw_all + ((size_t)pi << log_n)) + (fpt ? twd : 0);
+            twc[k] = reinterpret_cast<const Tw *>(base)[idx];
+        }
+        lds_barrier(); // twiddles visible
+    }
     // FP: the digit residues (< 2^51, exact in a double) are converted once, not once per output
     // prime (u64 -> f64 is several VALU instructions)
     double xd[E];
@@ -675,6 +701,8 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
             if (M == 2 && (p.q < (1ull << 47) || !(p.q < (1ull << 51)))) continue;
             if (M == 0 && FP && p.q < (1ull << 51)) continue; // mixed: the FP sweeps took it
             const AA ar(p, tw_all + ((size_t)pi << log_n), twd);
+            using TWA = typename AA::TW;
+            const TWA *tl = reinterpret_cast<const TWA *>(&twc[(I - i_lo) * R]);
             VT v[E];
             if constexpr (M != 0)
             {
@@ -691,18 +719,37 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
                     v[e] = red ? barrett64(xe, p) : xe;
                 }
             }
+            if (twl_on)
+            {
 #pragma unroll
-            for (int s = 0; s < LOGE; s++)
-                ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+                for (int s = 0; s < LOGE; s++)
+                    ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - s), tl, [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+            }
+            else
+            {
+#pragma unroll
+                for (int s = 0; s < LOGE; s++)
+                    ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+            }
 #pragma unroll
             for (int e = 0; e < E; e++) lds_v[sl * LD + t + TPS * e] = v[e];
             lds_barrier(); // LDS only: the previous output prime's stores stay in flight
 #pragma unroll
             for (int e = 0; e < E; e++) v[e] = lds_v[sl * LD + E * t + e];
+            if (twl_on)
+            {
 #pragma unroll
-            for (int s = LOGE; s < LOGR; s++)
-                ar.template fwd<E>(v, 1 << (LOGR - 1 - s),
-                                   [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
+                for (int s = LOGE; s < LOGR; s++)
+                    ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - s), tl,
+                                           [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
+            }
+            else
+            {
+#pragma unroll
+                for (int s = LOGE; s < LOGR; s++)
+                    ar.template fwd<E>(v, 1 << (LOGR - 1 - s),
+                                       [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
+            }
             u64 *dst = modup + (((size_t)(I - I0) * L + J) << log_n);
             if (inter_packed(pack, p.q)) // uniform per workgroup
             {
@@ -728,8 +775,12 @@ __global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, cons
             }
             else
             {
+                // one base pointer per lane and a uniform stride: no per-element 64-bit offsets to
+                // keep (they were spilled to scratch and reloaded with a vmcnt(0) wait per store)
+                const size_t stride = (size_t)1 << logC;
+                u64 *d0 = dst + c + ((size_t)(E * t) << logC);
 #pragma unroll
-                for (int e = 0; e < E; e++) st_nt<0>(&dst[c + ((u32)(E * t + e) << logC)], ar.out(v[e]));
+                for (int e = 0; e < E; e++) st_nt<0>(d0 + (size_t)e * stride, ar.out(v[e]));
             }
             lds_barrier(); // lds is rewritten by the next output prime (its stores need not land)
         }
