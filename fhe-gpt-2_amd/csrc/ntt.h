@@ -611,9 +611,14 @@ struct KsPtrs
 #ifndef MHE_MODUP_TWG
 #define MHE_MODUP_TWG 5 // output primes per group whose twiddles the ModUp column pass stages in LDS
 #endif
-// MIX (with FP): output primes >= 2^51 (the GPT-2 chain's special prime) take the integer sweep
+// MIX (with FP): output primes >= 2^51 (the GPT-2 chain's special prime) take the integer sweep.
+// The integer and MIX variants get 2 waves/SIMD: at 3 (168 VGPRs) they spilled 116-124 bytes per
+// lane, and each scratch reload waits for every store in flight (one vmcnt for loads and stores)
+#ifndef MHE_MODUP_OCC_INT
+#define MHE_MODUP_OCC_INT 2
+#endif
 template <int LOGR, int LOGT, bool FP, bool MIX = false>
-__global__ __launch_bounds__(256, MHE_MODUP_OCC) void k_modup_col(KsPtrs P, const PrimeDev *__restrict__ primes,
+__global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_INT) void k_modup_col(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                    const Tw *__restrict__ tw_all, int L, int K, int log_n,
                                                    long long twd, int I0, int Icnt, int pack, int X, int IG, int xcd)
 {
