@@ -183,7 +183,7 @@ def resnet_leg(device, images, streams, layers=20):
     """Second half of BASELINE.json's metric: seconds per image of encrypted ResNet-20 CIFAR-10
     (config C3: multiplexed conv + approximate ReLU + 18 bootstraps at N=2^16; config C4's network
     with layers=110), through the runner's C ABI (include/mhe_resnet_capi.h) in this process, with
-    the reference's pretrained parameters on seeded synthetic images: one image alone (latency), then
+    the reference's pretrained parameters on seeded synthetic images: single-stream images (latency), then
     `images` images on `streams` host threads (one HIP stream each).
     One key set for the whole job: rank 0 generates it (planning inference + SEAL
     keys truncated to their levels), every buffer is broadcast over RCCL/xGMI and imported by the
@@ -208,9 +208,16 @@ def resnet_leg(device, images, streams, layers=20):
     info = runner.info()
     rng = np.random.default_rng(1000 + rank)
     imgs = rng.uniform(-2.5, 2.5, size=(images, 3072))
+    # latency: `lat` images one after another on one stream; the first also fills the runner's
+    # static-operand encode cache, so the median of >= 3 is the warm per-image time (one image for
+    # the deeper networks, where the batch below already is that single image)
+    lat = 3 if layers <= 20 else 1
+    lat_imgs = rng.uniform(-2.5, 2.5, size=(lat, 3072))
     runner.key_traffic(reset=True)
-    one = runner.infer_batch(imgs[:1], 1)
-    key_bytes = runner.key_traffic(reset=True)  # key-switching key bytes of one image
+    one = runner.infer_batch(lat_imgs, 1)
+    key_bytes = runner.key_traffic(reset=True) / lat  # key-switching key bytes of one image
+    k_med = int(np.argsort(one["seconds"])[lat // 2])
+    sec_one = float(one["seconds"][k_med])
     if world > 1:
         dist.barrier()
     t2 = time.perf_counter()
@@ -219,16 +226,18 @@ def resnet_leg(device, images, streams, layers=20):
     # every image's decrypted logits against the plain network (exact ReLU), on every rank -- the
     # keys there may have arrived over RCCL; a miss fails the leg
     tol = 0.05 if layers <= 20 else 0.08
-    errs = runner.check_logits(imgs[:1], one["logits"], tol) + runner.check_logits(imgs, batch["logits"], tol)
+    errs = runner.check_logits(lat_imgs, one["logits"], tol) + runner.check_logits(imgs, batch["logits"], tol)
     prepared = runner.keys_prepared()
     runner.close()
     return {
         "workload": ("C3" if layers == 20 else "C4" if layers == 110 else "ResNet")
         + f": ResNet-{layers} CIFAR-10, N=2^16, 31+1 primes, sparse bootstrapping (logn 14/13/12)",
         "data": "reference pretrained parameters (tests/golden/resnet), seeded synthetic images",
-        "sec_per_image_1stream": round(float(one["seconds"][0]), 4),
-        "bootstrap_s_per_image": round(float(one["boot"][0]), 4),
-        "relu_s_per_image": round(float(one["relu"][0]), 4),
+        "sec_per_image_1stream": round(sec_one, 4),
+        "sec_per_image_1stream_samples": [round(float(x), 4) for x in one["seconds"]],
+        "latency_stat": f"median of {lat} images, one stream" if lat > 1 else "one image, one stream",
+        "bootstrap_s_per_image": round(float(one["boot"][k_med]), 4),
+        "relu_s_per_image": round(float(one["relu"][k_med]), 4),
         "batch_wall_s": round(batch_wall, 4),
         "batch_images": images,
         "streams": streams,
@@ -248,10 +257,10 @@ def resnet_leg(device, images, streams, layers=20):
         "roofline": {
             "bound": "hbm",
             "key_bytes_per_image": key_bytes,
-            "achieved": round(key_bytes / float(one["seconds"][0]) / 1e9, 1),
+            "achieved": round(key_bytes / sec_one / 1e9, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(key_bytes / float(one["seconds"][0]) / 1e9 / HBM_PEAK_GBS, 4),
+            "frac": round(key_bytes / sec_one / 1e9 / HBM_PEAK_GBS, 4),
         },
         "key_sharing": shared if shared else "single GPU: keys generated here",
         "labels": [int(x) for x in batch["labels"]],
@@ -276,6 +285,153 @@ def max_over_ranks(seconds, device):
     return seconds
 
 
+class HMultWorkload:
+    """The timed workload of the HMult leg, built exactly once and shared with
+    tests/test_bench_path.py (which checks every output of these calls against the oracle):
+    `batch` independent HMults at L limbs on the C2 chain, one relin key drawn on rank 0 (seeded) and
+    broadcast, the engine's prepared key format (or SEAL's), calls of `group` HMults each
+    (mhe_hmult_batch) dealt round robin over `streams` HIP streams."""
+
+    def __init__(self, dev, rank=0, limbs=44, batch=32, group=8, streams=4, key_format="prepared", keep_host=False):
+        self.dev, self.L, self.B = dev, limbs, batch
+        self.moduli = mhe.coeff_modulus_create(1 << LOG_N, C2_BITS)
+        K = self.K = len(self.moduli)
+        L = limbs
+        assert 2 <= L <= K - 1
+        self.eng = eng = mhe.Engine(LOG_N, self.moduli, device=dev.index or 0)
+        n = self.n = eng.n
+        q_t = torch.tensor(self.moduli, dtype=torch.int64, device=dev)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(20261015 + rank)
+        # relin key: rank 0 draws it, RCCL broadcast to every GPU (SURVEY.md §8(e))
+        self.key = key = torch.empty((K - 1, 2, K, n), dtype=torch.int64, device=dev)
+        if rank == 0:
+            g0 = torch.Generator(device=dev)
+            g0.manual_seed(7)
+            key.copy_(rand_residues((K - 1, 2, K, n), q_t, g0))
+        broadcast_key(key, src=0)
+        # SEAL-layout host copy of the key for the oracle check (taken before the in-place prepare)
+        self.key_host = key.cpu().numpy().view(np.uint64) if keep_host else None
+        self.prepared = key_format == "prepared"
+        if self.prepared:  # one-time conversion to the engine's key format, outside the timed region
+            eng.key_prepare(key)
+            torch.cuda.synchronize(dev)
+        self.a = rand_residues((batch, 2, L, n), q_t[:L], gen)
+        self.b = rand_residues((batch, 2, L, n), q_t[:L], gen)
+        self.out = torch.empty((batch, 2, L - 1, n), dtype=torch.int64, device=dev)
+        self.stream = torch.cuda.current_stream(dev)
+        self.streams = [self.stream] + [torch.cuda.Stream(dev) for _ in range(streams - 1)]
+        self.sps = [mhe.ctypes.c_void_p(s_.cuda_stream) for s_ in self.streams]
+        for s_ in self.sps:
+            mhe.lib().mhe_ctx_reserve(eng._h, K - 1, s_)
+        ptr = lambda t: mhe.ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        a_p = [ptr(self.a[i]) for i in range(batch)]
+        b_p = [ptr(self.b[i]) for i in range(batch)]
+        o_p = [ptr(self.out[i]) for i in range(batch)]
+        self.k_p = ptr(key)
+        self.G = G = max(1, group)
+        # calls of G independent HMults each (mhe_hmult_batch: one batched key switch per call whose
+        # entries share the relin key stream), dealt round robin over the streams
+        arr = lambda ps: (mhe.ctypes.c_void_p * len(ps))(*ps)  # noqa: E731
+        self.calls = [(i0, min(G, batch - i0), arr(a_p[i0:i0 + G]), arr(b_p[i0:i0 + G]), arr(o_p[i0:i0 + G]))
+                      for i0 in range(0, batch, G)]
+
+    def call_streams(self):
+        """[(first entry, count, stream index)] of the calls one step issues."""
+        return [(i0, cnt, ci % len(self.sps)) for ci, (i0, cnt, _, _, _) in enumerate(self.calls)]
+
+    def run_calls(self, stream_list=None):
+        stream_list = stream_list or self.sps
+        for ci, (_, cnt, ca, cb, co) in enumerate(self.calls):
+            st = stream_list[ci % len(stream_list)]
+            if self.G == 1:
+                rc = self.eng.hmult_raw(ca[0], cb[0], self.k_p, self.K, co[0], self.L, st)
+            else:
+                rc = self.eng.hmult_batch_raw(cnt, ca, cb, self.k_p, self.K, co, self.L, st)
+            if rc:
+                raise mhe.MheError(rc, mhe.lib().mhe_last_error().decode())
+
+    def step(self):
+        stream, streams = self.stream, self.streams
+        if len(streams) > 1:  # the extra streams start after the main stream's prior work
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            for s_ in streams[1:]:
+                s_.wait_event(ev)
+        self.run_calls()
+        if len(streams) > 1:  # join back so the timing events on the main stream cover all
+            for s_ in streams[1:]:
+                ev = torch.cuda.Event()
+                ev.record(s_)
+                stream.wait_event(ev)
+
+    def host(self, t):
+        return t.cpu().numpy().view(np.uint64)
+
+
+def check_timed_outputs(w, entries, threads):
+    """Recompute `entries` of the timed HMults with the oracle (test infrastructure, used here only as
+    the checker) on the same inputs and the SEAL-layout key, and require identical words."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    oc = O.Context(LOG_N, w.moduli)
+    idx = list(entries)
+    a = np.ascontiguousarray(w.host(w.a[idx]))
+    b = np.ascontiguousarray(w.host(w.b[idx]))
+    got = w.host(w.out[idx])
+    t0 = time.perf_counter()
+    want, _ = oc.hmult_batch(a, b, w.key_host, threads=min(threads, len(idx)))
+    dt = time.perf_counter() - t0
+    bad = [i for j, i in enumerate(idx) if not np.array_equal(got[j], want[j])]
+    if bad:
+        raise AssertionError(f"timed HMult outputs {bad} differ from the oracle")
+    return {"entries": idx, "calls_streams": [c for c in w.call_streams() if any(c[0] <= i < c[0] + c[1] for i in idx)],
+            "vs": "oracle/mhe_oracle.c hmult (SEAL evaluator restatement), SEAL-layout key", "oracle_s": round(dt, 2)}
+
+
+def launch_ranks(args):
+    """`--gpus N` without a launcher: start N worker processes of this script (one per GPU, RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set) and exit with the first failing child's code.  This
+    process touches no GPU (import torch does not; no device is counted or opened here), so the
+    workers own the devices."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        p.wait()
+        if p.returncode and not rc:
+            rc = p.returncode
+    if rc:  # a failed rank can leave the others waiting in a collective
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def stub_worker(args, world, rank):
+    """--stub: the launcher's rank plumbing without a GPU (gloo): every rank checks WORLD_SIZE
+    against --gpus and joins one all-reduce; rank 0 prints the ranks seen (tests/test_dist.py)."""
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+    t = torch.tensor([1.0 + rank])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "backend": dist.get_backend(), "ranks_seen": dist.get_world_size(),
+                          "rank_sum": float(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -292,6 +448,8 @@ def main():
                     help="20: config C3 (ResNet-20); 110: config C4's network (ResNet-110, one image per GPU "
                          "with --resnet-images 1 --resnet-streams 1)")
     ap.add_argument("--resnet-streams", type=int, default=4, help="images in flight per GPU (one stream each)")
+    ap.add_argument("--c4", choices=("auto", "on", "off"), default="auto",
+                    help="config C4 leg (ResNet-110, one image per GPU on the shared key set); auto = when N > 1")
     ap.add_argument("--key-format", choices=("prepared", "seal"), default="prepared",
                     help="relin key as the engine's prepared format (mhe_key_prepare, 48-bit planes for "
                          "primes < 2^48; bit-identical results) or SEAL's u64 layout")
@@ -300,85 +458,34 @@ def main():
                          "stream; 1 = one mhe_hmult call each)")
     ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams the batch is spread over (round robin; 4 = the hardware queues per process)")
+    ap.add_argument("--stub", action="store_true", help="rank plumbing only, on gloo without a GPU (tests)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.stub:
+        return stub_worker(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     L = args.limbs
-    moduli = mhe.coeff_modulus_create(1 << LOG_N, C2_BITS)
-    K = len(moduli)
-    assert 2 <= L <= K - 1
-    eng = mhe.Engine(LOG_N, moduli, device=local)
-    n = eng.n
-    q_t = torch.tensor(moduli, dtype=torch.int64, device=dev)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(20261015 + rank)
-
-    # relin key: rank 0 draws it, RCCL broadcast to every GPU
-    key = torch.empty((K - 1, 2, K, n), dtype=torch.int64, device=dev)
-    if rank == 0:
-        g0 = torch.Generator(device=dev)
-        g0.manual_seed(7)
-        key.copy_(rand_residues((K - 1, 2, K, n), q_t, g0))
-    broadcast_key(key, src=0)
-    prepared = args.key_format == "prepared"
-    if prepared:  # one-time conversion to the engine's key format, outside the timed region
-        eng.key_prepare(key)
-        torch.cuda.synchronize(dev)
-    B = args.batch
-    a = rand_residues((B, 2, L, n), q_t[:L], gen)
-    b = rand_residues((B, 2, L, n), q_t[:L], gen)
-    out = torch.empty((B, 2, L - 1, n), dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
-    sps = [mhe.ctypes.c_void_p(s_.cuda_stream) for s_ in streams]
-    for s_ in sps:
-        mhe.lib().mhe_ctx_reserve(eng._h, K - 1, s_)
-    ptr = lambda t: mhe.ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    a_p = [ptr(a[i]) for i in range(B)]
-    b_p = [ptr(b[i]) for i in range(B)]
-    o_p = [ptr(out[i]) for i in range(B)]
-    k_p = ptr(key)
-    G = max(1, args.hmult_group)
-    # calls of G independent HMults each (mhe_hmult_batch: one batched key switch per call whose
-    # entries share the relin key stream), dealt round robin over the streams
-    arr = lambda ps: (mhe.ctypes.c_void_p * len(ps))(*ps)  # noqa: E731
-    calls = [(min(G, B - i0), arr(a_p[i0:i0 + G]), arr(b_p[i0:i0 + G]), arr(o_p[i0:i0 + G])) for i0 in range(0, B, G)]
-
-    def run_calls(stream_list):
-        for ci, (cnt, ca, cb, co) in enumerate(calls):
-            st = stream_list[ci % len(stream_list)]
-            if G == 1:
-                rc = eng.hmult_raw(ca[0], cb[0], k_p, K, co[0], L, st)
-            else:
-                rc = eng.hmult_batch_raw(cnt, ca, cb, k_p, K, co, L, st)
-            if rc:
-                raise mhe.MheError(rc, mhe.lib().mhe_last_error().decode())
-
-    def step():
-        if len(streams) > 1:  # the extra streams start after the main stream's prior work
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            for s_ in streams[1:]:
-                s_.wait_event(ev)
-        run_calls(sps)
-        if len(streams) > 1:  # join back so the timing events on the main stream cover all
-            for s_ in streams[1:]:
-                ev = torch.cuda.Event()
-                ev.record(s_)
-                stream.wait_event(ev)
-
+    check = rank == 0 and not args.no_cpu  # keep the SEAL-layout key on the host for the output check
+    w = HMultWorkload(dev, rank, L, args.batch, args.hmult_group, args.streams, args.key_format, keep_host=check)
+    eng, n, moduli, B, G = w.eng, w.n, w.moduli, w.B, w.G
+    stream, sps = w.stream, w.sps
     lib = mhe.lib()
     lib.mhe_ctx_set_timing(eng._h, 1)
     for _ in range(args.warmup):
-        step()
+        w.step()
     torch.cuda.synchronize(dev)
     km_ms, km_n = mhe.ctypes.c_double(), mhe.ctypes.c_int()
     mc_ms, mc_n = mhe.ctypes.c_double(), mhe.ctypes.c_int()  # k_modup_col, the second key-switch kernel
@@ -392,7 +499,7 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        step()
+        w.step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -401,6 +508,12 @@ def main():
     torch.cuda.synchronize(dev)
     gpu_s = ev0.elapsed_time(ev1) / 1e3
     elapsed = max_over_ranks(max(wall, gpu_s), dev)
+    # the timed calls' outputs, checked against the oracle on rank 0 (one entry per call, so every
+    # stream and batch position class is covered), before the single-stream pass below rewrites them
+    timed_check = None
+    if check:
+        entries = sorted({i0 + (ci * 3) % cnt for ci, (i0, cnt, _) in enumerate(w.call_streams())})
+        timed_check = check_timed_outputs(w, entries, args.cpu_threads)
     # HIP-event time of the dominant kernel, recorded by the engine on the stream each launch
     # ran on (mhe_ctx_set_timing / mhe_kernel_time).  With several streams the launches of
     # different HMults overlap, so the kernel's own duration is taken from a short
@@ -410,7 +523,7 @@ def main():
     lib.mhe_kernel_time(eng._h, 1, mhe.ctypes.byref(mc_ms), mhe.ctypes.byref(mc_n))
     if len(sps) > 1:
         for _ in range(min(args.steps, 4)):
-            run_calls(sps[:1])
+            w.run_calls(sps[:1])
         torch.cuda.synchronize(dev)
         lib.mhe_kernel_time(eng._h, 0, mhe.ctypes.byref(km_ms), mhe.ctypes.byref(km_n))
         lib.mhe_kernel_time(eng._h, 1, mhe.ctypes.byref(mc_ms), mhe.ctypes.byref(mc_n))
@@ -451,7 +564,7 @@ def main():
     G_launch = min(G, B)
     io_bytes = G_launch * (L + 2 * (L + 1)) * n * 8
     km_bytes = ks_row_mac_key_bytes(L, n) + io_bytes
-    km_streamed = ks_row_mac_key_bytes(L, n, moduli, prepared) + io_bytes
+    km_streamed = ks_row_mac_key_bytes(L, n, moduli, w.prepared) + io_bytes
     hm_bytes = hmult_bytes(L)
     achieved = hm_bytes / per_hmult_s / 1e9
     km_achieved = km_bytes / (km_avg_us * 1e-6) / 1e9 if km_avg_us > 0 else 0.0
@@ -477,7 +590,13 @@ def main():
             "call": "mhe_hmult_batch" if G > 1 else "mhe_hmult",
             "streams": args.streams,
             "parallelism": f"replicas{world} (independent ciphertexts per GPU, key broadcast over RCCL)",
+            "ranks": (dist.get_world_size() if world > 1 else 1),
+            "backend": (dist.get_backend() if world > 1 else None),
         },
+        # rank 0 recomputed entries of the timed calls (the last step's outputs, one entry per
+        # mhe_hmult_batch call / stream) with the oracle on the same inputs: identical words
+        "timed_output_checked": timed_check is not None,
+        "timed_output_check": timed_check,
         "roofline": {
             "bound": "hbm",
             "kernel": (f"k_ks_row_mac (fused ModUp row pass + key inner products; one launch per {G_launch} HMults "
@@ -534,17 +653,24 @@ def main():
             "us_per_hmult": round(per_hmult_s * 1e6, 2),
         },
     }
+    del w  # the HMult leg's buffers (relin key, inputs) are not needed by the ResNet legs
+    torch.cuda.empty_cache()
+    legs = []
     if args.resnet_images > 0:
-        r = resnet_leg(local, args.resnet_images, args.resnet_streams, args.resnet_layers)
+        legs.append((args.resnet_layers, args.resnet_images, args.resnet_streams))
+    if args.c4 == "on" or (args.c4 == "auto" and world > 1):
+        legs.append((110, 1, 1))  # config C4: ResNet-110, one image per GPU, shared key set
+    for layers, images, streams in legs:
+        r = resnet_leg(local, images, streams, layers)
         t = torch.tensor([r["batch_wall_s"], r["sec_per_image_1stream"]], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         r["batch_wall_s"], r["sec_per_image_1stream"] = float(t[0]), float(t[1])
-        r["images_per_s"] = round(world * args.resnet_images / r["batch_wall_s"], 4)
+        r["images_per_s"] = round(world * images / r["batch_wall_s"], 4)
         r["n_gpus"] = world
-        if args.resnet_layers == 20:
+        if layers == 20:
             r["vs_reference_cpu"] = round(RESNET20_CPU_S / r["sec_per_image_1stream"], 1)
-        result[f"resnet{args.resnet_layers}"] = r
+        result[f"resnet{layers}"] = r
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(moduli, L, args.cpu_threads)
     if rank == 0:

@@ -1325,6 +1325,14 @@ static int check_limbs(mhe_ctx *c, int limbs, int lo)
     return MHE_OK;
 }
 
+// Do the word ranges [a, a + aw) and [b, b + bw) share a word?  The batched entry points run every
+// entry inside the same kernels, so an output that overlaps another entry's operand would be read
+// and written by one launch in an order that depends on the grid (not the order of count calls).
+static bool ranges_overlap(const u64 *a, size_t aw, const u64 *b, size_t bw)
+{
+    return a < b + bw && b < a + aw;
+}
+
 // Forward NTT of [polys][limbs] (limb l on prime l).
 static int run_ntt_fwd(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limbs, int full, hipStream_t st)
 {
@@ -2541,12 +2549,15 @@ MHE_EXPORT int mhe_apply_galois_batch(mhe_ctx *c, int count, const uint64_t *con
     {
         if (!in[i] || !out[i] || !keys[i]) return fail(MHE_ERR_ARG, "Galois key not present");
         if (!(elts[i] & 1) || elts[i] >= 2 * c->n) return fail(MHE_ERR_ARG, "Galois element is not valid");
+        // every key is checked before the first launch, so a bad key leaves no output half-written
+        if (key_limbs[i] < limbs + 1 || key_limbs[i] > c->K)
+            return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
         // outputs must be disjoint from every input and from each other (all are written before the
         // first key switch reads its input's permutation back from its own output)
         for (int j = 0; j < count; j++)
         {
-            const bool ov_in = out[i] < in[j] + 2 * ps && in[j] < out[i] + 2 * ps;
-            const bool ov_out = j != i && out[i] < out[j] + 2 * ps && out[j] < out[i] + 2 * ps;
+            const bool ov_in = ranges_overlap(out[i], 2 * ps, in[j], 2 * ps);
+            const bool ov_out = j != i && ranges_overlap(out[i], 2 * ps, out[j], 2 * ps);
             if (ov_in || ov_out) return fail(MHE_ERR_ARG, "result cannot point to the same value as operand");
         }
     }
@@ -2586,10 +2597,15 @@ MHE_EXPORT int mhe_rescale_batch(mhe_ctx *c, int count, const uint64_t *const *i
     if (limbs < 2) return fail(MHE_ERR_RANGE, "end of modulus switching chain reached");
     if (limbs > c->K || size < 1 || size > 3 || count < 0 || (count && (!in || !out)))
         return fail(MHE_ERR_ARG, "encrypted is not valid for encryption parameters");
+    const size_t iw = ((size_t)size * limbs) << c->log_n, ow = ((size_t)size * (limbs - 1)) << c->log_n;
     for (int i = 0; i < count; i++)
     {
         if (!in[i] || !out[i]) return fail(MHE_ERR_ARG, "encrypted is not valid for encryption parameters");
-        if (in[i] == out[i]) return fail(MHE_ERR_ARG, "rescale output must not alias its input");
+        // an output may share no word with any entry's input or with another output: the last pass
+        // writes out[i] while other workgroups of the same launch still read their inputs
+        for (int j = 0; j < count; j++)
+            if (ranges_overlap(out[i], ow, in[j], iw) || (j != i && ranges_overlap(out[i], ow, out[j], ow)))
+                return fail(MHE_ERR_ARG, "rescale output must not alias its input");
     }
     for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
     {
@@ -2680,11 +2696,21 @@ MHE_EXPORT int mhe_hmult_batch(mhe_ctx *c, int count, const uint64_t *const *a, 
     int r = check_limbs(c, limbs, 2);
     if (r) return r;
     if (count < 0 || (count && (!a || !b || !out)) || !key) return fail(MHE_ERR_ARG, "invalid argument");
+    if (key_limbs < limbs + 1 || key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
+    const size_t iw = (size_t)2 * limbs * c->n, ow = (size_t)2 * (limbs - 1) * c->n;
     for (int i = 0; i < count; i++)
     {
         if (!a[i] || !b[i] || !out[i]) return fail(MHE_ERR_ARG, "invalid argument");
+        // out[i] may overlap its own operands (they are consumed by the tensor product before the
+        // tail writes out[i]) but no other entry's operands (a later chunk reads them after this
+        // chunk's tail) and no other output
         for (int j = 0; j < count; j++)
-            if (j != i && out[j] == out[i]) return fail(MHE_ERR_ARG, "outputs must be distinct");
+        {
+            if (j == i) continue;
+            if (ranges_overlap(out[i], ow, out[j], ow)) return fail(MHE_ERR_ARG, "outputs must be distinct");
+            if (ranges_overlap(out[i], ow, a[j], iw) || ranges_overlap(out[i], ow, b[j], iw))
+                return fail(MHE_ERR_ARG, "result cannot point to the same value as another entry's operand");
+        }
     }
     hipStream_t st = S(s);
     const size_t n = c->n;

@@ -1335,7 +1335,9 @@ void Encryptor::zero_at(parms_id_type parms_id, Ciphertext &destination, bool sy
 
 void Encryptor::encrypt_zero(parms_id_type parms_id, Ciphertext &destination, MemoryPoolHandle) const
 {
-    zero_at(parms_id, destination, !asymmetric_, nullptr);
+    // SEAL's encrypt_zero / encrypt are public-key encryptions (encryptor.h:158-164, encryptor.cpp:
+    // 177-181): without a public key they throw, even when a secret key is set
+    zero_at(parms_id, destination, false, nullptr);
 }
 
 void Encryptor::encrypt_zero(Ciphertext &destination, MemoryPoolHandle pool) const
@@ -1368,16 +1370,15 @@ Serializable<Ciphertext> Encryptor::encrypt_zero_symmetric(MemoryPoolHandle pool
 
 void Encryptor::encrypt(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle) const
 {
-    encrypt_plain(plain, destination, !asymmetric_, nullptr);
+    encrypt_plain(plain, destination, false, nullptr);
 }
 
 Serializable<Ciphertext> Encryptor::encrypt(const Plaintext &plain, MemoryPoolHandle) const
 {
-    // a public-key encryption has no seed to save; a secret-key-only Encryptor saves it seeded
+    // a public-key encryption has no seed to save (encrypt_symmetric is the seeded form)
     Ciphertext c;
-    prng_seed_type seed{};
-    encrypt_plain(plain, c, !asymmetric_, &seed);
-    return Serializable<Ciphertext>(std::move(c), asymmetric_ ? SeedMap{} : SeedMap{ { 0, { seed } } });
+    encrypt_plain(plain, c, false, nullptr);
+    return Serializable<Ciphertext>(std::move(c), SeedMap{});
 }
 
 void Encryptor::encrypt_symmetric(const Plaintext &plain, Ciphertext &destination, MemoryPoolHandle) const
@@ -2398,8 +2399,11 @@ void Evaluator::lockstep_execute(std::vector<LsOp *> &ops) const
     }
     catch (...)
     {
-        const std::exception_ptr e = std::current_exception();
-        for (LsOp *o : ops) o->err = e;
+        // The merged call validates every entry before its first launch (rescale / relinearize), or
+        // wrote only outputs that are not inputs (rotations, products through temporaries), so the
+        // members' operands are unchanged here: each member's call runs again on its own and gets
+        // its own result or its own error, as without the group.
+        for (LsOp *o : ops) run_one(*o);
     }
 }
 
@@ -2627,10 +2631,17 @@ void Evaluator::rescale_to_next_inplace_many(const std::vector<Ciphertext *> &en
     if (tsc.top())
         for (const Ciphertext *c : encrypted) tin.push_back(c ? trace::ct(*c) : std::string());
     std::map<std::pair<std::size_t, std::size_t>, std::vector<Ciphertext *>> groups;
+    // every entry is validated before the first group launches, so a bad entry throws with every
+    // ciphertext unchanged (as the first failing one-by-one call would leave the rest)
     for (Ciphertext *c : encrypted)
     {
         if (!c) throw std::invalid_argument("null ciphertext");
         Level lv = check_ct(context_, *c, "encrypted");
+        if (context_.last_parms_id() == c->parms_id()) throw std::invalid_argument("end of modulus switching chain reached");
+        if (!c->is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
+        auto next = lv.cd->next_context_data();
+        check_scale(c->scale() / (double)lv.cd->parms().coeff_modulus().back().value(),
+                    level_of(context_, next->parms_id(), "parms_id"));
         groups[{ lv.L, c->size() }].push_back(c);
     }
     void *s = context_.stream();

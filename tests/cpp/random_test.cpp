@@ -68,7 +68,7 @@ int main(int argc, char **argv)
     dump(dir + "/asym_l2.bin", ct2.data(), 2 * 2 * n);
     Encryptor sym(ctx, keygen.secret_key());
     Ciphertext ct3;
-    sym.encrypt_zero(ct3);
+    sym.encrypt_zero_symmetric(ct3);
     dump(dir + "/sym_first.bin", ct3.data(), 2 * (K - 1) * n);
     std::printf("random_test ok: n=%zu K=%zu hw=%zu\n", n, K, hw);
     return 0;

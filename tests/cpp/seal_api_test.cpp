@@ -166,8 +166,19 @@ static void test_encrypt_zero_and_decrypt()
     Plaintext p;
     e.encoder->encode(v, std::pow(2.0, 40), p);
     Ciphertext c;
-    sym.encrypt(p, c);
+    sym.encrypt_symmetric(p, c);
     CHECK(max_err(e.dec(c), v) < 1e-4);
+    // encrypt() is a public-key encryption in SEAL and throws without a public key
+    bool threw = false;
+    try
+    {
+        sym.encrypt(p, c);
+    }
+    catch (const std::logic_error &ex)
+    {
+        threw = std::string(ex.what()) == "public key is not set";
+    }
+    CHECK(threw);
 }
 
 static void test_add_sub_negate()

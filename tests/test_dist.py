@@ -181,3 +181,39 @@ def test_key_sharing_serialized_keys_gloo_world2():
     assert r0[4] == r1[4] == {0: (3, 2, 4, 64), 1: (2, 2, 3, 64), 4: (1, 2, 2, 64)}
     assert r1[5] and not r0[5]                                   # the receiver finished its import
     assert r0[6] == r1[6] == [0, 1]                              # results gathered from every rank
+
+
+# ----------------------------------------------------------------------------- bench.py --gpus N
+def _bench_env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE"):
+        env.pop(k, None)
+    return env
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_launcher_spawns_n_ranks(n):
+    """`python bench.py --gpus N` without a launcher starts N ranks itself (the driver's command shape
+    for the scaling run); --stub runs the rank plumbing on gloo: every rank checks WORLD_SIZE against
+    --gpus and joins an all-reduce, and rank 0 reports the world it saw."""
+    import json
+    import subprocess
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--stub"], env=_bench_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 alone prints
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == n and out["ranks_seen"] == n and out["backend"] == "gloo"
+    assert out["rank_sum"] == sum(1.0 + k for k in range(n))
+
+
+def test_bench_rejects_world_mismatch():
+    """A launcher-provided WORLD_SIZE that disagrees with --gpus is an error, not a silent 1-rank run."""
+    import subprocess
+
+    env = dict(_bench_env(), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stub"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

@@ -169,6 +169,46 @@ def test_batch_errors(small):
         ch.eng.hmult_batch([a, a], [a, a], key, outs=[o, o])
 
 
+def test_batch_overlap_errors(small):
+    """Entries of one batch run inside the same kernels, so an output may share no word with another
+    entry's operand or output (partial overlaps, not just equal pointers, are refused
+    before any launch); an output over its own operands stays allowed where one call allows it."""
+    ch = small
+    L = 4
+    n = ch.n
+    key = ch.up(ch.rand_key())
+    big = ch.eng.empty(6, L, n)  # one allocation, sliced so that ranges overlap partially
+    x = ch.up(ch.rand(2, L, n))
+    y = ch.up(ch.rand(2, L, n))
+    # rescale: out[0] overlaps the second half of in[1]
+    in1 = big[0:2]
+    out0 = big.view(-1)[(2 * L - 1) * n:(2 * L - 1) * n + 2 * (L - 1) * n].view(2, L - 1, n)
+    with pytest.raises(mhe.MheError, match="alias"):
+        ch.eng.rescale_batch([x, in1], outs=[out0, ch.eng.empty(2, L - 1, n)])
+    # rescale: two outputs overlapping by one limb
+    o_a = big.view(-1)[0:2 * (L - 1) * n].view(2, L - 1, n)
+    o_b = big.view(-1)[(2 * (L - 1) - 1) * n:(4 * (L - 1) - 1) * n].view(2, L - 1, n)
+    with pytest.raises(mhe.MheError, match="alias"):
+        ch.eng.rescale_batch([x, y], outs=[o_a, o_b])
+    # hmult: out[0] over b[1]
+    b1 = big[2:4]
+    o0 = big.view(-1)[2 * L * n + n:2 * L * n + n + 2 * (L - 1) * n].view(2, L - 1, n)
+    with pytest.raises(mhe.MheError, match="another entry"):
+        ch.eng.hmult_batch([x, y], [x, b1], key, outs=[o0, ch.eng.empty(2, L - 1, n)])
+    # hmult: out[i] over its own a[i] is fine and gives the oracle's words
+    a_host = ch.rand(2, L, n)
+    own = ch.up(a_host)
+    outs = ch.eng.hmult_batch([own], [own], key, outs=[own.view(-1)[:2 * (L - 1) * n].view(2, L - 1, n)])
+    assert np.array_equal(ch.down(outs[0]), ch.oc.hmult(a_host, a_host, ch.down(key)))
+    # Galois batch: a bad key level is refused before anything is written
+    o = ch.eng.empty(2, L, n)
+    o.fill_(7)
+    elt = mhe.galois_elt_from_step(ch.log_n, 1)
+    with pytest.raises(mhe.MheError, match="kswitch_keys"):
+        ch.eng.apply_galois_batch([x, y], [elt, elt], [key, key[:, :, :L]], outs=[o, ch.eng.empty(2, L, n)])
+    assert bool((o == 7).all())
+
+
 @pytest.mark.parametrize("log_n", [13, 16])
 def test_seal_surface_batches_equal_one_by_one(log_n):
     """The seal:: batched entry points (rotate_vectors, rescale_to_next_inplace_many,
