@@ -9,12 +9,13 @@
 // three-level BSGS CoeffToSlot / SlotToCoeff (sflinv_3 / sfl_half_3), modraise, the Chebyshev
 // cosine + double-angle modular reduction and the scaled linear arcsine (inverse_deg = 1).
 //
-// Host-side coefficient generation is this build's own: the reference finds the cosine and
-// arcsine polynomials with NTL's RR Remez (common/Remez.cpp, not available here) and merges the
-// special-FFT butterfly stages with index loops (Bootstrapper.cpp:512-1908).  Here the cosine
-// is fitted in __float128 on the same union of intervals (least squares on Chebyshev nodes of
-// every interval), the linear arcsine is the exact equioscillation solution, and the merged
-// diagonals are products of the same butterfly stages written as sparse diagonal matrices.
+// Host-side coefficient generation restates the reference's: the cosine and arcsine polynomials
+// come from its multi-interval Remez exchange (common/Remez.cpp, NTL RR there) run in __float128
+// (pinned by the reference's cosine.txt to every printed digit), and the linear-transform
+// diagonals from genorigcoeff / genfftcoeff_3 / geninvfftcoeff_3 (Bootstrapper.cpp:512-592,
+// 1116-1383, 1516-1776) with the reference's loops and operation order (lt_coefficients_3), so the
+// encoded diagonals are the reference's doubles.  lt_coefficients_3_merged derives the same
+// diagonals independently (products of sparse stage matrices) as the check.
 // The evaluation trees, rotation steps, levels and scales are the reference's.
 #pragma once
 
@@ -68,6 +69,8 @@ public:
 using LTDiags = std::vector<std::vector<std::complex<double>>>;
 void lt_coefficients_3(int logn, long logNh, long boundary_K, LTDiags &f1, LTDiags &f2, LTDiags &f3, LTDiags &i1,
                        LTDiags &i2, LTDiags &i3);
+void lt_coefficients_3_merged(int logn, long logNh, long boundary_K, LTDiags &f1, LTDiags &f2, LTDiags &f3,
+                              LTDiags &i1, LTDiags &i2, LTDiags &i3);
 
 // target = quotient * T_chebdeg + remainder, all in the Chebyshev basis (Polynomial.cpp:890-916).
 void divide_poly(Polynomial &quotient, Polynomial &remainder, const Polynomial &target, long chebdeg);

@@ -291,9 +291,17 @@ void layer_norm_rows(Ciphertext &input, Ciphertext &output, const std::vector<do
                      const std::vector<double> &beta, int rows, int row_size, int newton_iters,
                      Bootstrapper &bootstrapper, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
                      Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
+// The weight of GELU's last piece (x for x >= 3): `reference` is b3 = 0.5 s2 as PolyApprox.cpp:484-485
+// and plain_approx/poly.py:33 write it (+-x/4 outside the middle pieces); `indicator` (the block's
+// default, a deliberate departure) is s2 + 1/2, the indicator of x >= 3 that GELU needs.
+enum class GeluLastPiece
+{
+    indicator,
+    reference
+};
 void compute_gelu_block(Ciphertext &inputs, Ciphertext &outputs, double alpha, CKKSEncoder &encoder,
                         Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
-                        RelinKeys &relin_keys);
+                        RelinKeys &relin_keys, GeluLastPiece last = GeluLastPiece::indicator);
 // layers.cpp
 void attentionLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &qw, std::vector<Ciphertext> &qb,
                     std::vector<Ciphertext> &kw, std::vector<Ciphertext> &kb, std::vector<Ciphertext> &vw,

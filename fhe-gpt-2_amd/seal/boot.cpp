@@ -2,12 +2,13 @@
 //
 // Ciphertext-operation sequences follow cnn_ckks/cpu-ckks/single-key/ckks_bootstrapping/
 // Bootstrapper.cpp and ModularReducer.cpp and cnn_ckks/common/Polynomial.cpp (cited per
-// function); the host-side coefficient generation is this build's own (see the header).
+// function); the host-side coefficient generation restates the reference's (see the header).
 #include "mhe_boot.h"
 
 #include <quadmath.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -1332,11 +1333,13 @@ std::vector<std::vector<cd>> layout(const Diags &M, int n, int step, int totlen,
 
 namespace boot
 {
-void lt_coefficients_3(int ln, long logNh, long boundary_K, LTDiags &f1, LTDiags &f2, LTDiags &f3, LTDiags &i1,
-                       LTDiags &i2, LTDiags &i3)
+void lt_coefficients_3_merged(int ln, long logNh, long boundary_K, LTDiags &f1, LTDiags &f2, LTDiags &f3,
+                              LTDiags &i1, LTDiags &i2, LTDiags &i3)
 {
-    // genorigcoeff + genfftcoeff_3 + geninvfftcoeff_3 (Bootstrapper.cpp:512-590, 1116-1908), sparse
-    // slots: three merged groups each way, with the reference's scalings and 2n-slot extensions.
+    // The same diagonals derived independently: each group of butterfly stages as a product of
+    // sparse diagonal matrices (compose / layout above), with the reference's scalings and 2n-slot
+    // extensions.  Equal to lt_coefficients_3 up to rounding (a few ULPs, boot_host_test); kept as
+    // the check of the reference-order restatement below.
     const int cn = 1 << ln;
     if (ln > logNh) throw std::logic_error("slot count above N/2");
     const cd I(0, 1);
@@ -1405,6 +1408,198 @@ void lt_coefficients_3(int ln, long logNh, long boundary_K, LTDiags &f1, LTDiags
                 v[j + cn] = -I * v[j];
             }
         }
+    }
+}
+} // namespace boot
+
+// ------------------------------------------------------------------ reference operation order
+// genorigcoeff + genfftcoeff_3 + geninvfftcoeff_3 (Bootstrapper.cpp:512-592, 1116-1383, 1516-1776)
+// restated with the reference's loops, so every double is produced by the same operations in the
+// same order: the butterfly stages (orig_coeffvec / orig_invcoeffvec) from std::polar, each merged
+// diagonal as the running product of 3^div stage entries, summed into its BSGS slot case by case.
+// The reference's CNN target is built at -O0 (cnn_ckks/CMakeLists.txt), so std::polar's cos() and
+// sin() are two libm calls (never merged into sincos(), whose last bit differs for some angles), and
+// a complex product is (ac - bd) + (ad + bc) i without FMA contraction.
+namespace
+{
+// one butterfly stage: entries [3][n] (index 0, 1, 2 = offsets -w, 0, +w of the reference's tmpcount)
+using StageCoeff = std::array<std::vector<cd>, 3>;
+
+__attribute__((noinline)) cd polar_o0(double theta)
+{
+    double t = theta;
+    const double c = std::cos(t);
+    asm volatile("" : "+x"(t)); // a separate sin() call, as at -O0
+    const double sn = std::sin(t);
+    return cd(1.0 * c, 1.0 * sn);
+}
+
+// (a + bi)(c + di) = (ac - bd) + (ad + bc) i, each product rounded, no FMA (libgcc __muldc3 / GCC's
+// inline expansion for finite operands)
+__attribute__((optimize("fp-contract=off"))) inline cd cmul(const cd &x, const cd &y)
+{
+    const double a = x.real(), b = x.imag(), c = y.real(), d = y.imag();
+    const double ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    return cd(ac - bd, ad + bc);
+}
+
+__attribute__((optimize("fp-contract=off"))) void genorigcoeff_one(int ln, std::vector<StageCoeff> &fwd,
+                                                                      std::vector<StageCoeff> &inv)
+{
+    // Bootstrapper.cpp:512-592 for one slot count (u fixed)
+    const int n = 1 << ln;
+    fwd.assign(ln, StageCoeff{});
+    inv.assign(ln, StageCoeff{});
+    for (auto &st : fwd)
+        for (auto &v : st) v.assign(n, cd(0.0, 0.0));
+    for (auto &st : inv)
+        for (auto &v : st) v.assign(n, cd(0.0, 0.0));
+    double theta_0 = M_PI / (double)(2L * n);
+    int blocklen = 1, blockcount = n;
+    for (int i = 0; i < ln; i++)
+    {
+        blocklen <<= 1;
+        blockcount >>= 1;
+        const double theta = theta_0 * (double)(1 << (ln - 1 - i));
+        int power = 1;
+        cd zeta = polar_o0(theta * (double)power);
+        for (int j = 0; j < blocklen / 2; j++)
+        {
+            for (int k = 0; k < blockcount; k++)
+            {
+                const int a = k * blocklen + j, b = a + blocklen / 2;
+                fwd[i][1][a] = 1.0;
+                fwd[i][1][b] = -zeta;
+                fwd[i][0][a] = 0.0;
+                fwd[i][0][b] = 1.0;
+                fwd[i][2][a] = zeta;
+                fwd[i][2][b] = 0.0;
+            }
+            power = (5 * power) % (1 << (i + 3));
+            zeta = polar_o0(theta * (double)power);
+        }
+    }
+    theta_0 = -M_PI / (double)(2L * n);
+    blocklen = n;
+    blockcount = 1;
+    for (int i = 0; i < ln; i++)
+    {
+        const double theta = theta_0 * (double)(1 << i);
+        int power = 1;
+        cd zeta = polar_o0(theta * (double)power);
+        for (int j = 0; j < blocklen / 2; j++)
+        {
+            for (int k = 0; k < blockcount; k++)
+            {
+                const int a = k * blocklen + j, b = a + blocklen / 2;
+                inv[i][1][a] = 0.5;
+                inv[i][1][b] = cd(-0.5 * zeta.real(), -0.5 * zeta.imag());
+                inv[i][0][a] = 0.0;
+                inv[i][0][b] = cd(0.5 * zeta.real(), 0.5 * zeta.imag());
+                inv[i][2][a] = 0.5;
+                inv[i][2][b] = 0.0;
+            }
+            power = (5 * power) % (1 << ((ln - 1 - i) + 3));
+            zeta = polar_o0(theta * (double)power);
+        }
+        blocklen >>= 1;
+        blockcount <<= 1;
+    }
+}
+
+// One merged group: the reference's loop over the 3^div stage-entry choices (genfftcoeff_3's j loop).
+// Case j picks entry tmpcount[p] of stage p0 + p; its offset weight is 2^p (forward, `rev` false) or
+// 2^(div-1-p) (inverse); the running product is read at (k + step (n + current_pos)) mod n and added
+// into out[slot(pos)][k] for k < n.
+template <class Slot>
+__attribute__((optimize("fp-contract=off"))) void merge_group(const std::vector<StageCoeff> &orig, int p0, int div,
+                                                              bool rev, int step, int n, Slot slot, boot::LTDiags &out)
+{
+    std::vector<int> tmpcount(div);
+    std::vector<cd> tmpvec(n);
+    const int all_case_count = (int)std::pow(3, div);
+    auto wt = [&](int p) { return rev ? 1 << (div - 1 - p) : 1 << p; };
+    for (int j = 0; j < all_case_count; j++)
+    {
+        int ind = j, pos = 0;
+        for (int p = 0; p < div; p++)
+        {
+            const int ind_res = ind % 3;
+            pos += (ind_res - 1) * wt(p);
+            tmpcount[p] = ind_res;
+            ind = (ind - ind_res) / 3;
+        }
+        int current_pos = pos;
+        for (int k = 0; k < n; k++) tmpvec[k] = cd(1.0, 0.0);
+        for (int p = 0; p < div; p++)
+        {
+            current_pos = current_pos - (tmpcount[p] - 1) * wt(p);
+            const std::vector<cd> &st = orig[p0 + p][tmpcount[p]];
+            for (int k = 0; k < n; k++) tmpvec[k] = cmul(tmpvec[k], st[(k + step * (n + current_pos)) % n]);
+        }
+        std::vector<cd> &dst = out[slot(pos)];
+        for (int k = 0; k < n; k++) dst[k] += tmpvec[k];
+    }
+}
+} // namespace
+
+namespace boot
+{
+__attribute__((optimize("fp-contract=off"))) void lt_coefficients_3(int ln, long logNh, long boundary_K, LTDiags &f1,
+                                                                       LTDiags &f2, LTDiags &f3, LTDiags &i1,
+                                                                       LTDiags &i2, LTDiags &i3)
+{
+    if (ln > logNh) throw std::logic_error("slot count above N/2");
+    const int n = 1 << ln;
+    const bool full = ln == logNh;
+    std::vector<StageCoeff> of, oi;
+    genorigcoeff_one(ln, of, oi);
+    const int ext = full ? 1 : 2; // the sparse branch's diagonals are 2n long (second half filled below)
+    auto sized = [&](LTDiags &g, int count, int len) { g.assign(count, std::vector<cd>(len, cd(0.0, 0.0))); };
+    {
+        // genfftcoeff_3 (Bootstrapper.cpp:1116-1383)
+        const int d3 = (int)std::floor(ln / 3.0), d2 = (int)std::floor((ln - d3) / 2.0), d1 = ln - d3 - d2;
+        const int t1 = (1 << d1) - 1, t2 = (1 << d2) - 1, t3 = (1 << d3) - 1;
+        const int s1 = 1, s2 = 1 << d1, s3 = 1 << (d1 + d2);
+        sized(f1, 2 * t1 + 1, ext * n);
+        sized(f2, 2 * t2 + 1, ext * n);
+        sized(f3, full ? t3 + 1 : 2 * t3 + 1, ext * n);
+        merge_group(of, 0, d1, false, s1, n, [&](int pos) { return pos + t1; }, f1);
+        merge_group(of, d1, d2, false, s2, n, [&](int pos) { return pos + t2; }, f2);
+        if (full)
+            merge_group(of, d1 + d2, d3, false, s3, n, [&](int pos) { return (pos + t3 + 1) % (t3 + 1); }, f3);
+        else
+            merge_group(of, d1 + d2, d3, false, s3, n, [&](int pos) { return pos + t3; }, f3);
+        if (!full)
+        {
+            for (auto *g : { &f1, &f2 })
+                for (auto &v : *g)
+                    for (int j = 0; j < n; j++) v[j + n] = v[j];
+            for (auto &v : f3)
+                for (int j = 0; j < n; j++) v[j + n] = cmul(cd(0.0, 1.0), v[j]);
+        }
+    }
+    {
+        // geninvfftcoeff_3 (Bootstrapper.cpp:1516-1776)
+        const int d1 = (int)std::floor(ln / 3.0), d2 = (int)std::floor((ln - d1) / 2.0), d3 = ln - d1 - d2;
+        const int t1 = (1 << d1) - 1, t2 = (1 << d2) - 1, t3 = (1 << d3) - 1;
+        const int s1 = 1 << (ln - d1), s2 = 1 << (ln - d1 - d2), s3 = 1;
+        sized(i1, t1 + 1, n);
+        sized(i2, 2 * t2 + 1, n);
+        sized(i3, 2 * t3 + 1, full ? n : 2 * n);
+        merge_group(oi, 0, d1, true, s1, n, [&](int pos) { return (pos + t1 + 1) % (t1 + 1); }, i1);
+        merge_group(oi, d1, d2, true, s2, n, [&](int pos) { return pos + t2; }, i2);
+        merge_group(oi, d1 + d2, d3, true, s3, n, [&](int pos) { return pos + t3; }, i3);
+        // complex<double> *= double scales both parts by the same double
+        const double sc1 = full ? 1.0 / (double)boundary_K : 1.0 / (double)(boundary_K * (1L << (logNh - ln)));
+        for (auto &v : i1)
+            for (int j = 0; j < n; j++) v[j] = cd(v[j].real() * sc1, v[j].imag() * sc1);
+        for (auto &v : i3)
+            for (int j = 0; j < n; j++)
+            {
+                v[j] = cd(v[j].real() * 0.5, v[j].imag() * 0.5);
+                if (!full) v[j + n] = cmul(cd(0.0, -1.0), v[j]);
+            }
     }
 }
 } // namespace boot

@@ -905,11 +905,13 @@ void layer_norm_rows(Ciphertext &input, Ciphertext &output, const std::vector<do
 
 void compute_gelu_block(Ciphertext &inputs, Ciphertext &outputs, double alpha, CKKSEncoder &encoder,
                         Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
-                        RelinKeys &relin_keys)
+                        RelinKeys &relin_keys, GeluLastPiece last)
 {
     // compute_gelu (PolyApprox.cpp:443-504, poly.py:30-35) with the signs taken of alpha (x + shift)
-    // so they stay inside the composite sign's [-1, 1], and the x piece weighted by s2 + 1/2 (the
-    // indicator of x >= 3; the reference's 0.5 s2 leaves +-x/4 there)
+    // so they stay inside the composite sign's [-1, 1] (the reference feeds x - 3, x + 1.95, x + 4
+    // unscaled, where the composite sign diverges), and the x piece weighted by s2 + 1/2 (the
+    // indicator of x >= 3) or, with GeluLastPiece::reference, by 0.5 s2 as the reference writes it
+    // (multiply_const + rescale, PolyApprox.cpp:484-485)
     Ciphertext y, s0, s1, s2, tc, b1, b2, b3, p, q;
     evaluator.multiply_const(inputs, alpha, y);
     evaluator.rescale_to_next_inplace(y);
@@ -924,7 +926,13 @@ void compute_gelu_block(Ciphertext &inputs, Ciphertext &outputs, double alpha, C
     half_sign(4.0, s0);
     evaluator.sub_reduced_error(s0, s1, b1);
     evaluator.sub_reduced_error(s1, s2, b2);
-    evaluator.add_const(s2, 0.5, b3);
+    if (last == GeluLastPiece::reference)
+    {
+        evaluator.multiply_const(s2, 0.5, b3);
+        evaluator.rescale_to_next_inplace(b3);
+    }
+    else
+        evaluator.add_const(s2, 0.5, b3);
     compute_gelu_p(inputs, p, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     compute_gelu_q(inputs, q, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
     evaluator.multiply_reduced_error(b1, p, relin_keys, outputs);

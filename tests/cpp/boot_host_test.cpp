@@ -8,6 +8,7 @@
 #include "mhe_boot.h"
 
 #include <cmath>
+#include <cstring>
 #include <cstdio>
 #include <random>
 
@@ -99,9 +100,63 @@ static void check_lt(int logn, int logNh, int K)
     CHECK(i1.size() == (size_t)(1 << c1));
 }
 
+// ULPs between two doubles of the same sign (0 when equal)
+static long ulps(double a, double b)
+{
+    if (a == b) return 0;
+    if ((a < 0) != (b < 0)) return 1L << 62;
+    long ia, ib;
+    std::memcpy(&ia, &a, 8);
+    std::memcpy(&ib, &b, 8);
+    return std::labs(ia - ib);
+}
+
+// The reference-order diagonals (lt_coefficients_3: genfftcoeff_3 / geninvfftcoeff_3's loops) against
+// the independent sparse-matrix derivation (lt_coefficients_3_merged): same shapes, and every double
+// within a few ULPs of the other relative to the diagonal's scale -- the two sum the same products in
+// different orders.  Reports how many doubles differ at all.
+static void check_lt_orders(int logn, int logNh, int K)
+{
+    boot::LTDiags a[6], b[6];
+    boot::lt_coefficients_3(logn, logNh, K, a[0], a[1], a[2], a[3], a[4], a[5]);
+    boot::lt_coefficients_3_merged(logn, logNh, K, b[0], b[1], b[2], b[3], b[4], b[5]);
+    long total = 0, differ = 0, max_ulp = 0;
+    double max_rel = 0;
+    for (int g = 0; g < 6; g++)
+    {
+        CHECK(a[g].size() == b[g].size());
+        for (std::size_t i = 0; i < std::min(a[g].size(), b[g].size()); i++)
+        {
+            CHECK(a[g][i].size() == b[g][i].size());
+            double scale = 0;
+            for (const cd &z : a[g][i]) scale = std::max(scale, std::abs(z));
+            for (std::size_t x = 0; x < std::min(a[g][i].size(), b[g][i].size()); x++)
+                for (int part = 0; part < 2; part++)
+                {
+                    const double u = part ? a[g][i][x].imag() : a[g][i][x].real();
+                    const double v = part ? b[g][i][x].imag() : b[g][i][x].real();
+                    total++;
+                    if (u != v)
+                    {
+                        differ++;
+                        if (std::abs(u) > 1e-3 * scale) max_ulp = std::max(max_ulp, ulps(u, v));
+                        max_rel = std::max(max_rel, std::abs(u - v) / (scale > 0 ? scale : 1.0));
+                    }
+                }
+        }
+    }
+    std::printf("logn %d (logNh %d): reference-order vs merged diagonals: %ld of %ld doubles differ, max %ld ULP "
+                "(entries above 1e-3 of their diagonal), max |diff| / scale %.3g\n",
+                logn, logNh, differ, total, max_ulp, max_rel);
+    CHECK(max_rel < 1e-14);
+}
+
 int main()
 {
     for (int logn : { 3, 5, 6, 8 }) check_lt(logn, 10, 25);
+    for (int logn : { 3, 5, 6, 8, 10 }) check_lt_orders(logn, 10, 25);
+    check_lt_orders(14, 15, 25); // the ResNet bootstrapper_1 shape (logn 14, N = 2^16)
+    check_lt_orders(12, 15, 25);
 
     // cosine approximation of the ResNet setting (cnn/infer_seal.cpp:289-296): K = 25, deg 59,
     // log width 10, two double-angle steps (cos(2 pi (x - 1/4) / 4))

@@ -39,9 +39,9 @@ struct Mat
     double at(int r, int c) const { return v[(std::size_t)r * cols + c]; }
 };
 
-static std::map<std::string, Mat> load_fixture(const std::string &dir)
+static std::map<std::string, Mat> load_fixture(const std::string &dir, const std::string &stem = "block")
 {
-    std::ifstream txt(dir + "/block.txt"), bin(dir + "/block.bin", std::ios::binary);
+    std::ifstream txt(dir + "/" + stem + ".txt"), bin(dir + "/" + stem + ".bin", std::ios::binary);
     if (!txt || !bin) throw std::runtime_error("fixture not found under " + dir);
     std::vector<char> raw((std::istreambuf_iterator<char>(bin)), std::istreambuf_iterator<char>());
     std::map<std::string, Mat> out;
@@ -380,6 +380,33 @@ int main(int argc, char **argv)
             const double e = err_rows({ g }, fx.at("gelu"));
             std::printf("   compute_gelu_block: %zu limbs out\n", g.coeff_modulus_size());
             report("compute_gelu_block(hidden) vs restated GELU", e < kTol, e, since(t));
+        }
+        if (!block_only && std::ifstream(dir + "/gelu_ref.txt"))
+        {
+            // the GELU piece against the reference's own plain formula: plain_approx/poly.py:30-35
+            // restated in numpy (make_gelu_ref.py, np.sign, b3 = 0.5 s2) vs compute_gelu_block with
+            // GeluLastPiece::reference; and the block's default (indicator s2 + 1/2, a departure)
+            // vs its restatement, on the same 4096 inputs >= 0.5 from each breakpoint
+            const auto gx = load_fixture(dir, "gelu_ref");
+            const Mat &gxin = gx.at("x"), &gref = gx.at("poly_gelu"), &gblk = gx.at("gelu_block");
+            std::vector<double> v(S, 0.0);
+            for (int i = 0; i < gxin.cols; i++) v[i] = gxin.v[i];
+            for (int variant = 0; variant < 2; variant++)
+            {
+                auto t = std::chrono::steady_clock::now();
+                Ciphertext in = enc_slots(v), g;
+                const bool ref = variant == 0;
+                compute_gelu_block(in, g, ap.gelu_alpha, encoder, encryptor, decryptor, evaluator, gk, rk,
+                                   ref ? GeluLastPiece::reference : GeluLastPiece::indicator);
+                const auto got = dec_slots(g);
+                double e = 0;
+                for (int i = 0; i < gxin.cols; i++) e = std::max(e, std::fabs(got[i] - (ref ? gref : gblk).v[i]));
+                report(ref ? "compute_gelu_block(GeluLastPiece::reference) vs plain_approx/poly.py gelu (b3 = 0.5 s2), "
+                             "4096 inputs"
+                           : "compute_gelu_block (block default: indicator s2 + 1/2, departure from poly.py's 0.5 s2) "
+                             "vs its restatement",
+                       e < kTol, e, since(t));
+            }
         }
         if (!block_only)
         {
