@@ -176,6 +176,73 @@ def cpu_baseline(moduli, L_main, threads):
     }
 
 
+RESNET_BITS = [51] + [46] * 16 + [51] * 14 + [51]  # cnn/infer_seal.cpp:288-316: 31 data limbs + special
+
+
+def resnet_cpu_estimate(ops, threads):
+    """Estimated CPU seconds per ResNet image on this host: the image's engine operations by kind
+    and level (ops_per_image from the runner, mhe_op_counts) priced with the oracle's single-thread
+    per-operation times (oracle/mhe_oracle.c, the CPU restatement of SEAL's evaluator, -O3 -march=native,
+    built in this run) measured at L in {3, 10, 17, 24, 31} on the ResNet chain and interpolated (key
+    switch: quadratic in L, the rest linear).  An estimate, not a run of the reference: it prices the
+    same operations the GPU ran, one thread per image as the reference's OpenMP loop runs them."""
+    import oracle as O  # test infrastructure: the cpu_baseline leg times it
+
+    n = 1 << LOG_N
+    moduli = mhe.coeff_modulus_create(n, RESNET_BITS)
+    K = len(moduli)
+    oc = O.Context(LOG_N, moduli)
+    rng = np.random.default_rng(20261019)
+    qs = np.array(moduli, np.uint64)
+    levels = (3, 10, 17, 24, 31)
+    Lmax = max(levels)
+    key = rng.integers(0, 2**62, size=(Lmax, 2, K, n), dtype=np.uint64) % qs[None, None, :, None]
+    ct = rng.integers(0, 2**62, size=(2, Lmax, n), dtype=np.uint64) % qs[None, :Lmax, None]
+    ct2 = rng.integers(0, 2**62, size=(2, Lmax, n), dtype=np.uint64) % qs[None, :Lmax, None]
+    elt = O.galois_elt_from_step(n, 5)
+
+    def timed(f, reps=1):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f()
+        return (time.perf_counter() - t0) / reps
+
+    per = {k: [] for k in ("keyswitch", "rescale", "tensor", "mulplain", "addsub", "ntt", "galois")}
+    for L in levels:
+        a = np.ascontiguousarray(ct[:, :L])
+        b = np.ascontiguousarray(ct2[:, :L])
+        kL = np.ascontiguousarray(key[:L])
+        tg = np.ascontiguousarray(b[1])
+        pt = np.ascontiguousarray(b[0])
+        reps = 1 if L >= 17 else 3
+        per["keyswitch"].append(timed(lambda: oc.switch_key(a, tg, kL), reps))
+        per["rescale"].append(timed(lambda: oc.rescale(a), 3) / 2)  # per polynomial
+        per["tensor"].append(timed(lambda: oc.multiply(a, b), 3))
+        per["mulplain"].append(timed(lambda: oc.multiply_plain(a, pt), 3) / 2)
+        per["addsub"].append(timed(lambda: oc.add(a, b), 3) / 2)
+        per["ntt"].append(timed(lambda: oc.ntt(a), 3) / 2)
+        per["galois"].append(timed(lambda: O.apply_galois_ntt(a, LOG_N, elt), 3) / 2)
+    fits = {k: np.polyfit(levels, v, 2 if k == "keyswitch" else 1) for k, v in per.items()}
+    price = dict(fits, scalar=fits["mulplain"])
+    total, by_kind = 0.0, {}
+    for kind, lv in ops.items():
+        f = price.get(kind)
+        if f is None:
+            continue
+        s_ = sum(c * max(0.0, float(np.polyval(f, int(L)))) for L, c in lv.items())
+        by_kind[kind] = round(s_, 2)
+        total += s_
+    return {
+        "estimated_cpu_s_per_image": round(total, 1),
+        "threads_per_image": 1,
+        "throughput_images_per_s_on_host": round(threads / total, 5) if total > 0 else None,
+        "host_cores": threads,
+        "by_kind_s": by_kind,
+        "per_op_s_at_levels": {k: dict(zip(map(str, levels), [round(x, 5) for x in v])) for k, v in per.items()},
+        "kind": "estimate: oracle port (oracle/mhe_oracle.c) per-op CPU times x the GPU run's per-image op counts",
+    }
+
+
 RESNET20_CPU_S = 2188.8  # reference CPU SEAL, s/image, 1 thread per image (BASELINE.md / SURVEY.md §6)
 
 
@@ -214,8 +281,12 @@ def resnet_leg(device, images, streams, layers=20):
     lat = 3 if layers <= 20 else 1
     lat_imgs = rng.uniform(-2.5, 2.5, size=(lat, 3072))
     runner.key_traffic(reset=True)
+    runner.op_counts(reset=True)
     one = runner.infer_batch(lat_imgs, 1)
     key_bytes = runner.key_traffic(reset=True) / lat  # key-switching key bytes of one image
+    # the engine operations of one image, by kind and level (mhe_op_counts): the op mix the CPU
+    # estimate of the cpu_baseline leg prices
+    ops = {k: {str(l): c / lat for l, c in enumerate(v) if c} for k, v in runner.op_counts(reset=True).items()}
     k_med = int(np.argsort(one["seconds"])[lat // 2])
     sec_one = float(one["seconds"][k_med])
     if world > 1:
@@ -263,6 +334,7 @@ def resnet_leg(device, images, streams, layers=20):
             "frac": round(key_bytes / sec_one / 1e9 / HBM_PEAK_GBS, 4),
         },
         "key_sharing": shared if shared else "single GPU: keys generated here",
+        "ops_per_image": ops,
         "labels": [int(x) for x in batch["labels"]],
         "reference_cpu_sec_per_image": RESNET20_CPU_S if layers == 20 else None,
     }
@@ -673,6 +745,12 @@ def main():
         result[f"resnet{layers}"] = r
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(moduli, L, args.cpu_threads)
+        for layers in (20, 110):
+            r = result.get(f"resnet{layers}")
+            if r and r.get("ops_per_image"):
+                est = resnet_cpu_estimate(r["ops_per_image"], result["cpu_baseline"]["cores"])
+                est["vs_gpu_1stream"] = round(est["estimated_cpu_s_per_image"] / r["sec_per_image_1stream"], 1)
+                r["cpu_estimate"] = est
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

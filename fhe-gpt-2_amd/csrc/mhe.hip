@@ -195,8 +195,14 @@ enum TimedKernel
     TK_MODUP_COL = 1   // k_modup_col / ModUp column pass
 };
 
+// Per-level operation counts (mhe_op_counts, include/mhe.h MHE_OPK_*): what a workload asked of the
+// engine, by kind and level -- the op mix a CPU cost model multiplies by per-op CPU timings.
+#define MHE_OPK_KINDS 8
+#define MHE_OPK_LEVELS 64
+
 struct mhe_ctx
 {
+    std::atomic<unsigned long long> opc[MHE_OPK_KINDS][MHE_OPK_LEVELS] = {};
     std::atomic<unsigned long long> key_bytes{ 0 }; // key-switching key bytes read since reset (mhe_key_traffic)
     std::atomic<unsigned long long> key_bytes_prep{ 0 }; // the same slices' bytes in the prepared key format
     int device = 0;
@@ -215,11 +221,9 @@ struct mhe_ctx
     // 60-bit P): FP64 per output prime below 2^51, integer for P (fp = 2: mixed; MHE_KS_MIX=0: off)
     NttMode nm_ks;
     int ks_fused = 1; // fused row-pass + key-MAC kernel (MHE_KS_FUSED=0: separate row pass + MAC)
-    int ks_chunk = 8; // output primes per ModUp chunk (MHE_KS_CHUNK; <= 0 = all at once)
     int timing = 0;      // record HIP events around the key-switch kernels (mhe_ctx_set_timing)
     int hmult_fused = 1; // HMult: ModDown fused with the rescale (MHE_HMULT_FUSED=0: separate)
     int ks_share = 1;    // batched key switches sharing one key: XCD-grouped entries (MHE_KS_SHARE=0: off)
-    int ks_fchunk = 0; // fused path: output primes per chunk (MHE_KS_FCHUNK; <= 0 = all)
     int ks_colgroups = 9; // ModUp column pass: output-prime groups per digit (MHE_KS_COLGROUPS; 0 = one job per (I, J))
     int ks_inv_fused = 1; // the fused MAC runs the special limbs' inverse row pass (MHE_KS_INV_FUSED)
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
@@ -1333,9 +1337,15 @@ static bool ranges_overlap(const u64 *a, size_t aw, const u64 *b, size_t bw)
     return a < b + bw && b < a + aw;
 }
 
+static void count_op(mhe_ctx *c, int kind, int L, unsigned long long k)
+{
+    if (kind >= 0 && kind < MHE_OPK_KINDS && L >= 0 && L < MHE_OPK_LEVELS) c->opc[kind][L].fetch_add(k, std::memory_order_relaxed);
+}
+
 // Forward NTT of [polys][limbs] (limb l on prime l).
 static int run_ntt_fwd(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limbs, int full, hipStream_t st)
 {
+    count_op(c, MHE_OPK_NTT, limbs, (unsigned long long)polys);
     JobFwdPlain j;
     j.src = src;
     j.dst = dst;
@@ -1354,6 +1364,7 @@ static int run_ntt_fwd(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limb
 
 static int run_ntt_inv(mhe_ctx *c, const u64 *src, u64 *dst, int polys, int limbs, int full, hipStream_t st)
 {
+    count_op(c, MHE_OPK_NTT, limbs, (unsigned long long)polys);
     JobInvPlain j;
     j.src = src;
     j.dst = dst;
@@ -1432,6 +1443,8 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
         int r = ks_check_key(c, jobs[e], L, st, &kpack);
         if (r) return r;
     }
+    count_op(c, MHE_OPK_KEYSWITCH, L, (unsigned long long)B);
+    if (hm) count_op(c, MHE_OPK_RESCALE, L, 2ull * B); // the fused HMult tail rescales both polys
     Workspace *w;
     int r = get_ws(c, st, c->K - 1, &w, B);
     if (r) return r;
@@ -1454,9 +1467,9 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
     if (c->ks_fused)
     {
         // 2+3. ModUp column pass, then its row pass fused with the key MAC so NTT'd digits
-        //      never leave registers; optionally in chunks of output primes so a chunk's
-        //      column-pass output can stay in the Infinity Cache (MHE_KS_FCHUNK).
-        const int P = c->ks_fchunk > 0 ? c->ks_fchunk : L + 1;
+        //      never leave registers (chunks of output primes sized for the Infinity Cache
+        //      measured slower at every size).
+        const int P = L + 1;
         // 48-bit intermediate (ntt.h tile16): only k_modup_col writes it, so only with column groups
         const int pack = (c->ks_pack && c->ks_colgroups > 0) ? 1 : 0;
         KsPtrs kp{};
@@ -1499,13 +1512,11 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
     }
     else
     {
-        // 2+3. ModUp + key inner products in chunks of output primes: lift digit J to prime
-        //      I and NTT it (evaluator.cpp:2386-2408; I == J skipped), then
-        //      acc[k][I] = sum_J digit * key[J][k][I] (evaluator.cpp:2410-2463).  The chunk
-        //      scratch is reused, so the column-pass output and the NTT'd digits of a chunk
-        //      stay in the Infinity Cache between the three kernels instead of round-tripping
-        //      through HBM; only the key streams from HBM.  (One entry: B == 1 here.)
-        const int P = c->ks_chunk > 0 ? c->ks_chunk : L + 1;
+        // 2+3. (MHE_KS_FUSED=0, the independent debugging path) ModUp + key inner products in
+        //      three kernels: lift digit J to prime I and NTT it (evaluator.cpp:2386-2408; I == J
+        //      skipped), then acc[k][I] = sum_J digit * key[J][k][I] (evaluator.cpp:2410-2463).
+        //      (One entry: B == 1 here.)
+        const int P = L + 1;
         for (int I0 = 0; I0 <= L; I0 += P)
         {
             const int cnt = (I0 + P <= L + 1) ? P : L + 1 - I0;
@@ -1612,6 +1623,7 @@ static int run_rescale_batch(mhe_ctx *c, const u64 *const *in, u64 *const *out, 
     Workspace *w;
     int r = get_ws(c, st, c->K - 1, &w, B);
     if (r) return r;
+    count_op(c, MHE_OPK_RESCALE, L, (unsigned long long)B * size);
     const int log_n = c->log_n;
     // last[s] = INTT(in[s][L-1]) canonical -> the entry's coeff (size <= 3 polys)
     JobB<JobLastInv> li;
@@ -1756,8 +1768,6 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     c->K = count;
     c->q.assign(moduli, moduli + count);
     if (const char *f = getenv("MHE_KS_FUSED")) c->ks_fused = atoi(f);
-    if (const char *f = getenv("MHE_KS_CHUNK")) c->ks_chunk = atoi(f);
-    if (const char *f = getenv("MHE_KS_FCHUNK")) c->ks_fchunk = atoi(f);
     if (const char *f = getenv("MHE_HMULT_FUSED")) c->hmult_fused = atoi(f);
     if (const char *f = getenv("MHE_KS_SHARE")) c->ks_share = atoi(f);
     if (const char *f = getenv("MHE_KS_COLGROUPS")) c->ks_colgroups = atoi(f);
@@ -2138,6 +2148,17 @@ MHE_EXPORT int mhe_stream_sync(mhe_ctx *c, void *stream)
     return MHE_OK;
 }
 
+MHE_EXPORT int mhe_op_counts(mhe_ctx *c, int kind, uint64_t *counts, int levels, int reset)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (kind < 0 || kind >= MHE_OPK_KINDS || !counts || levels < 1) return fail(MHE_ERR_ARG, "invalid argument");
+    for (int l = 0; l < levels; l++)
+        counts[l] = l < MHE_OPK_LEVELS ? (reset ? c->opc[kind][l].exchange(0) : c->opc[kind][l].load()) : 0;
+    if (reset)
+        for (int l = levels; l < MHE_OPK_LEVELS; l++) c->opc[kind][l].store(0);
+    return MHE_OK;
+}
+
 MHE_EXPORT int mhe_key_traffic(mhe_ctx *c, uint64_t *bytes, int reset)
 {
     if (!valid_ctx(c) || !bytes) return fail(MHE_ERR_ARG, "invalid argument");
@@ -2288,6 +2309,7 @@ static int launch_addsub(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out, int p
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!out || (op < 2 && !b)) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    count_op(c, MHE_OPK_ADDSUB, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_addsub, ELEM_GRID(total2), dim3(256), 0, S(st), a, b, out, c->primes, limbs, c->log_n,
                        total2, op);
@@ -2324,6 +2346,7 @@ MHE_EXPORT int mhe_multiply_plain(mhe_ctx *c, const uint64_t *a, const uint64_t 
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!b || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    count_op(c, MHE_OPK_MULPLAIN, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_mulplain, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, out, c->primes, limbs, c->log_n,
                        total2);
@@ -2337,6 +2360,8 @@ MHE_EXPORT int mhe_multiply_plain_add(mhe_ctx *c, const uint64_t *a, const uint6
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!b || !acc) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    count_op(c, MHE_OPK_MULPLAIN, limbs, (unsigned long long)polys);
+    count_op(c, MHE_OPK_ADDSUB, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_mulplain_add, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, acc, c->primes, limbs, c->log_n,
                        total2);
@@ -2354,6 +2379,8 @@ MHE_EXPORT int mhe_multiply_plain_sum(mhe_ctx *c, int count, const uint64_t *con
         if (r) return r;
         if (!b[k]) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
     }
+    count_op(c, MHE_OPK_MULPLAIN, limbs, (unsigned long long)polys * count);
+    count_op(c, MHE_OPK_ADDSUB, limbs, (unsigned long long)polys * (count - 1 + (accumulate ? 1 : 0)));
     const size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     for (int k0 = 0; k0 < count; k0 += MHE_SUM_TERMS)
     {
@@ -2377,6 +2404,7 @@ static int launch_scalar(mhe_ctx *c, const u64 *a, const u64 *scalars, u64 *out,
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!scalars || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    count_op(c, MHE_OPK_SCALAR, limbs, (unsigned long long)polys);
     ScalarTab t;
     for (int l = 0; l < limbs; l++)
     {
@@ -2414,6 +2442,7 @@ MHE_EXPORT int mhe_set_scalar(mhe_ctx *c, const uint64_t *scalars, uint64_t *out
 
 static int launch_tensor(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out3, int L, int square, hipStream_t st)
 {
+    count_op(c, MHE_OPK_TENSOR, L, 1);
     size_t total2 = ((size_t)L << c->log_n) / 2;
     hipLaunchKernelGGL(k_tensor, ELEM_GRID(total2), dim3(256), 0, st, a, b, out3, c->primes, L, c->log_n, total2,
                        square);
@@ -2465,6 +2494,7 @@ MHE_EXPORT int mhe_relinearize(mhe_ctx *c, uint64_t *ct3, const uint64_t *key, i
 static int launch_galois(mhe_ctx *c, const u64 *in, u32 elt, u64 *out, int polys, int limbs, hipStream_t st)
 {
     if (!(elt & 1) || elt >= 2 * c->n) return fail(MHE_ERR_ARG, "Galois element is not valid");
+    count_op(c, MHE_OPK_GALOIS, limbs, (unsigned long long)polys);
     size_t total = (size_t)polys * limbs << c->log_n;
     hipLaunchKernelGGL(k_galois, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, in, out, elt, c->log_n,
                        total);
@@ -2582,6 +2612,7 @@ MHE_EXPORT int mhe_apply_galois_batch(mhe_ctx *c, int count, const uint64_t *con
             jobs[e] = KsJob{ out[i0 + e], out[i0 + e] + ps, keys[i0 + e], key_limbs[i0 + e], nullptr };
         }
         const size_t total = 2 * ps;
+        count_op(c, MHE_OPK_GALOIS, limbs, 2ull * B);
         hipLaunchKernelGGL(k_galois_b, dim3((unsigned)((total + 255) / 256), (unsigned)B), dim3(256), 0, st, gp, c->log_n,
                            total);
         HIP_LAUNCH_CHECK();

@@ -810,12 +810,8 @@ static inline void modup_col_a(const KsPtrs &P, int B, const PrimeDev *primes, c
     constexpr int LOGT = LOGR <= 7 ? 3 : MHE_MODUP_LOGT8;
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
-    static const int xcd_env = [] {
-        const char *e = getenv("MHE_MODUP_XCD");
-        return e ? atoi(e) : 1;
-    }();
     const int X = subs / SH::S;
-    const int xcd = (xcd_env && (X * L) % 8 == 0) ? 1 : 0;
+    const int xcd = (X * L) % 8 == 0 ? 1 : 0; // XCD-grouped output-prime groups (profiles/r02k_modup_xcd_ab.txt)
     hipLaunchKernelGGL((k_modup_col<LOGR, LOGT, FP, MIX>), dim3((unsigned)(X * L * IG), (unsigned)B), dim3(256), 0, st,
                        P, primes, tw, L, K, log_n, twd, I0, Icnt, pack, X, IG, xcd);
 }
@@ -861,14 +857,10 @@ enum PassKind
 // Launches of at most this many workgroups prefetch a row pass's epilogue operands (PreOf): with
 // the operands in registers the kernel runs at 3 instead of 4 waves/SIMD, which pays for latency-bound
 // launches of a few rounds (ResNet's rescales and ModDowns) but not for the HMult tail's ~11k
-// workgroups (MHE_ROW_PRE_MAX_WG).
+// workgroups.
 static inline long row_pre_max_wg()
 {
-    static const long v = [] {
-        const char *e = getenv("MHE_ROW_PRE_MAX_WG");
-        return e ? atol(e) : 8192L;
-    }();
-    return v;
+    return 8192L;
 }
 
 template <int PASS, int LOGR, class Job, bool FP>
@@ -935,13 +927,9 @@ static inline void icol_lift_a(const ColSrc &cs, const Job &job, int polys, int 
     // output primes per workgroup: each workgroup redoes the inverse column stages of its columns
     // (from L2) once per group, so small launches keep one prime per workgroup (the widest grid) and
     // batched ones share the inverse stages over 2-3 primes (ubench at 31 / 20 limbs, profiles/r03v:
-    // 4 rescales 207 -> 185 us); MHE_ICOL_GROUP fixes the count
-    static const int fixed = [] {
-        const char *e = getenv("MHE_ICOL_GROUP");
-        return e && atoi(e) > 0 ? atoi(e) : 0;
-    }();
+    // 4 rescales 207 -> 185 us)
     const int jobs = polys * cnt;
-    const int per = fixed ? fixed : jobs >= 128 ? 3 : jobs >= 56 ? 2 : 1;
+    const int per = jobs >= 128 ? 3 : jobs >= 56 ? 2 : 1;
     const int IG = (cnt + per - 1) / per;
     hipLaunchKernelGGL((k_icol_lift<LOGR, LOGT, Job, FP>), dim3(subs / SH::S, polys, IG), dim3(256), 0, st, cs, job,
                        cnt, log_n, dinv, dfwd);
@@ -1035,7 +1023,7 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
                                [&](int e) { return twz((1u << s) + (lay(t, e, b_lo) >> (LOGR - s))); });
 }
 
-template <int LOGR, bool FP, bool KPF, bool MIX = false>
+template <int LOGR, bool FP, bool MIX = false>
 #ifndef MHE_KS_OCC
 #define MHE_KS_OCC 2 // waves per SIMD the fused MAC is compiled for
 #endif
@@ -1169,8 +1157,8 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
         if (MHE_KS_DPF == 2 && j0 + 1 < j1) load_digit(j0 + 1, vin2);
         lds_barrier(); // twiddles visible
 
-        // key limbs of a digit: issued one digit ahead (KPF) or at the top of the digit (the
-        // fewer-VGPR variant), consumed after the digit's NTT
+        // key limbs of a digit: issued at the top of the digit, consumed after the digit's NTT (a
+        // one-digit-ahead key prefetch measured equal and costs 32 VGPRs)
         // a prepared key (mhe_key_prepare) holds the limbs of primes below 2^48 as a 32-bit plane
         // [n] and a 16-bit plane [n] in natural order (6 of the slot's 8 bytes per residue)
         const bool kpk = kpack && p.q < (1ull << 48) && key[(size_t)ki * n + n - 1] == KEY_PACK_TAG; // uniform
@@ -1202,14 +1190,10 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             }
         };
         u64 kk0[8], kk1[8];
-        if (KPF) load_key(j0, kk0, kk1);
         for (int J = j0; J < j1; J++)
         {
-            u64 kn0[8], kn1[8], vnext[8];
-            if (!KPF)
-                load_key(J, kk0, kk1);
-            else if (J + 1 < j1)
-                load_key(J + 1, kn0, kn1);
+            u64 vnext[8];
+            load_key(J, kk0, kk1);
             if (!MHE_KS_DPF)
                 load_digit(J, vin); // no prefetch: occupancy hides the latency instead
             else if (MHE_KS_DPF == 2)
@@ -1303,15 +1287,6 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             {
 #pragma unroll
                 for (int e = 0; e < 8; e++) vin[e] = vnext[e];
-            }
-            if (KPF)
-            {
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                {
-                    kk0[e] = kn0[e];
-                    kk1[e] = kn1[e];
-                }
             }
         }
         u64 *o0 = acc + (size_t)I * n + base;
@@ -1408,274 +1383,6 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
         run(ar0);
 }
 
-// k_ks_row_mac with E = 2^EB residues per lane (EB = 2: half the live registers of the E = 8
-// kernel, so 4 waves per SIMD instead of 2 hide the digit and key loads), the 2^LOGR-point row
-// transform in ceil(LOGR / EB) register phases with swizzled LDS transposes inside one wave, and
-// the key inner products in the last phase's layout: every lane holds E consecutive residues, so
-// the key streams and the accumulator stores are 8- / 16-byte vector accesses and no transpose
-// back to a coalesced layout is needed.  Same arithmetic, same words (MHE_KS_EB selects).
-template <int LOGR, int EB>
-struct RowMacShapeE
-{
-    static constexpr int R = 1 << LOGR;
-    static constexpr int E = 1 << EB;
-    static constexpr int TPS = R / E;
-    static_assert(TPS <= 64, "a block's transposes must stay inside one wave");
-    static constexpr int S = 256 / TPS;
-    static constexpr int NP = (LOGR + EB - 1) / EB; // register phases
-};
-
-template <int EB>
-__device__ __forceinline__ u32 laye(u32 t, int e, int b_lo)
-{
-    return ((t >> b_lo) << (b_lo + EB)) | ((u32)e << b_lo) | (t & ((1u << b_lo) - 1));
-}
-
-template <int LOGR, bool FP, int EB, int OCC>
-__global__ __launch_bounds__(256, OCC) void k_ks_row_mac_e(
-    KsPtrs P, const PrimeDev *__restrict__ primes, const Tw *__restrict__ tw_all, int L, int K, int log_n,
-    long long twd, int I0, int pack, int kpack, int share)
-{
-    u32 bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (share)
-    {
-        // entries reading one key: a tile's entries are ids 8 apart (one XCD), adjacent in dispatch
-        const u32 X = gridDim.x, Y = gridDim.y, Bn = gridDim.z;
-        const u32 id = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
-        const u32 r = id % (8 * Bn), tile = (id / (8 * Bn)) * 8 + r % 8;
-        bz = r / 8;
-        bx = tile % X;
-        by = tile / X;
-    }
-    const u64 *__restrict__ inter = P.inter[bz];
-    const u64 *__restrict__ target = P.target[bz];
-    const u64 *__restrict__ key = P.key[bz];
-    u64 *__restrict__ acc = P.acc[bz];
-    const int key_limbs = P.key_limbs[bz];
-    using SH = RowMacShapeE<LOGR, EB>;
-    using A = NttArith<FP>;
-    using T = typename A::T;
-    using TW = typename A::TW;
-    constexpr int R = SH::R, E = SH::E, TPS = SH::TPS, S = SH::S, NP = SH::NP;
-    constexpr int B_A = LOGR - EB; // the first phase's in-lane bits (the ModUp intermediate's load layout)
-    __shared__ T xch[2][S * R];
-    __shared__ TW twl[S * (R + 1)];
-    const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
-    const u32 b = bx * S + sl;
-    const u32 base = b << LOGR;
-    const u32 R1 = 1u << (log_n - LOGR);
-    const int I = I0 + (int)by;
-    const int pi = (I == L) ? K - 1 : I;
-    const int ki = (I == L) ? key_limbs - 1 : I;
-    const PrimeDev p = primes[pi];
-    const size_t n = (size_t)1 << log_n;
-    const size_t kstride = (size_t)key_limbs * n;
-    const A ar0(p, tw_all + ((size_t)pi << log_n), twd);
-    {
-        const TW *tw = ar0.tw;
-        for (u32 idx = tid; idx < (u32)(S * R); idx += 256)
-        {
-            const u32 blk = idx / R, k = idx % R;
-            if (k == 0) continue;
-            const int s = 31 - __builtin_clz(k);
-            twl[blk * (R + 1) + k] = tw[(((R1 + bx * S + blk) << s)) + (k - (1u << s))];
-        }
-    }
-    const TW *mytw = &twl[sl * (R + 1)];
-    T *xb0 = &xch[0][sl * R], *xb1 = &xch[1][sl * R];
-
-    auto run = [&](const auto &ar) {
-        constexpr bool LZ = std::is_same<typename std::decay<decltype(ar)>::type, NttArithF<true>>::value;
-        using AccT = typename std::conditional<FP, double, Acc128>::type;
-        AccT a0[E], a1[E];
-#pragma unroll
-        for (int e = 0; e < E; e++)
-        {
-            if constexpr (FP)
-                a0[e] = a1[e] = 0.0;
-            else
-                a0[e] = a1[e] = Acc128{ 0, 0 };
-        }
-        const bool pk = inter_packed(pack, p.q);
-        // digit J: the column-pass output in the first phase's layout, or (J == I) the input limb,
-        // already in NTT form, straight into the MAC layout
-        auto load_digit = [&](int J, u64 (&v)[E]) {
-            if (J == I)
-            {
-                const u64 *src = target + (size_t)J * n + base;
-#pragma unroll
-                for (int e = 0; e < E; e++) v[e] = ld_nt<2>(&src[laye<EB>(t, e, 0)]);
-            }
-            else if (pk)
-            {
-                const u32 *lo = reinterpret_cast<const u32 *>(inter + ((size_t)(I - I0) * L + J) * n);
-                const unsigned short *hi = reinterpret_cast<const unsigned short *>(lo + n);
-#pragma unroll
-                for (int e = 0; e < E; e++)
-                {
-                    const u32 idx = base + laye<EB>(t, e, B_A);
-                    v[e] = (u64)ld_nt<2>(&lo[tile16(idx)]) | ((u64)ld_nt<2>(&hi[tile16h(idx)]) << 32);
-                }
-            }
-            else
-            {
-                const u64 *src = inter + ((size_t)(I - I0) * L + J) * n + base;
-#pragma unroll
-                for (int e = 0; e < E; e++) v[e] = ld_nt<2>(&src[laye<EB>(t, e, B_A)]);
-            }
-        };
-        u64 vin[E];
-        load_digit(0, vin);
-        lds_barrier(); // twiddles visible
-        const bool kpk = kpack && p.q < (1ull << 48) && key[(size_t)ki * n + n - 1] == KEY_PACK_TAG;
-        auto load_key = [&](int J, u64 (&ka)[E], u64 (&kb)[E]) {
-            const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
-            const u64 *k1 = k0 + kstride;
-            const u32 r0 = base + laye<EB>(t, 0, 0); // E consecutive residues per lane
-            if (kpk)
-            {
-                const u32 *l0 = reinterpret_cast<const u32 *>(k0) + r0;
-                const u32 *l1 = reinterpret_cast<const u32 *>(k1) + r0;
-                const unsigned short *h0 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k0) + n) + r0;
-                const unsigned short *h1 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k1) + n) + r0;
-#pragma unroll
-                for (int e = 0; e < E; e++)
-                {
-                    ka[e] = (u64)ld_nt<1>(&l0[e]) | ((u64)ld_nt<1>(&h0[e]) << 32);
-                    kb[e] = (u64)ld_nt<1>(&l1[e]) | ((u64)ld_nt<1>(&h1[e]) << 32);
-                }
-            }
-            else
-            {
-#pragma unroll
-                for (int e = 0; e < E; e++)
-                {
-                    ka[e] = ld_nt<1>(&k0[r0 + e]);
-                    kb[e] = ld_nt<1>(&k1[r0 + e]);
-                }
-            }
-        };
-        for (int J = 0; J < L; J++)
-        {
-            u64 kk0[E], kk1[E], vnext[E];
-            load_key(J, kk0, kk1);
-            if (J + 1 < L) load_digit(J + 1, vnext);
-            T d[E];
-            if (J != I)
-            {
-#pragma unroll
-                for (int e = 0; e < E; e++) d[e] = ar.in52(vin[e]);
-                int bp = B_A;
-#pragma unroll
-                for (int ph = 0; ph < NP; ph++)
-                {
-                    const int s0 = ph * EB, s1 = (s0 + EB < LOGR) ? s0 + EB : LOGR;
-                    const int bl = (LOGR - s0 - EB > 0) ? LOGR - s0 - EB : 0;
-                    if (ph > 0)
-                    {
-                        T *x = (ph & 1) ? xb1 : xb0;
-                        wave_lds_fence();
-#pragma unroll
-                        for (int e = 0; e < E; e++) x[swz(laye<EB>(t, e, bp))] = d[e];
-                        wave_lds_fence();
-#pragma unroll
-                        for (int e = 0; e < E; e++) d[e] = x[swz(laye<EB>(t, e, bl))];
-                    }
-#pragma unroll
-                    for (int s = s0; s < s1; s++)
-                        ar.template fwd_tab<E>(d, 1 << (LOGR - 1 - s - bl), mytw,
-                                               [&](int e) { return (1 << s) + (laye<EB>(t, e, bl) >> (LOGR - s)); });
-                    bp = bl;
-                }
-                if constexpr (!FP)
-                {
-#pragma unroll
-                    for (int e = 0; e < E; e++) d[e] = ar.canon(d[e]);
-                }
-            }
-            else
-            {
-#pragma unroll
-                for (int e = 0; e < E; e++) d[e] = ar.in52(vin[e]);
-            }
-            if constexpr (FP)
-            {
-#pragma unroll
-                for (int e = 0; e < E; e++)
-                {
-                    const double dv = LZ ? d[e] : fp_reduce(d[e], ar.q, ar.qinv);
-                    a0[e] += fp_mulmod_gen(dv, fp_from_u52(kk0[e]), ar.q, ar.qinv);
-                    a1[e] += fp_mulmod_gen(dv, fp_from_u52(kk1[e]), ar.q, ar.qinv);
-                    if (!LZ && (J & 1))
-                    {
-                        a0[e] = fp_reduce(a0[e], ar.q, ar.qinv);
-                        a1[e] = fp_reduce(a1[e], ar.q, ar.qinv);
-                    }
-                }
-            }
-            else
-            {
-#pragma unroll
-                for (int e = 0; e < E; e++)
-                {
-                    mac128(a0[e], d[e], kk0[e]);
-                    mac128(a1[e], d[e], kk1[e]);
-                }
-            }
-#pragma unroll
-            for (int e = 0; e < E; e++) vin[e] = vnext[e];
-        }
-        u64 *o0 = acc + (size_t)I * n + base;
-        u64 *o1 = o0 + (size_t)(L + 1) * n;
-#pragma unroll
-        for (int e = 0; e < E; e++)
-        {
-            const u32 r = laye<EB>(t, e, 0);
-            if constexpr (FP)
-            {
-                o0[r] = fp_canon(a0[e], ar.q, ar.qinv);
-                o1[r] = fp_canon(a1[e], ar.q, ar.qinv);
-            }
-            else
-            {
-                o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
-                o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
-            }
-        }
-    };
-    if constexpr (FP)
-    {
-        if (p.q < (1ull << 47) && (double)L * 1.25 * (double)p.q < 9007199254740992.0)
-            run(NttArithF<true>(p, tw_all + ((size_t)pi << log_n), twd));
-        else
-            run(ar0);
-    }
-    else
-        run(ar0);
-}
-
-// Row-MAC kernel variant (MHE_KS_EB): 0 = k_ks_row_mac (E = 8, MAC after a transpose back);
-// k_ks_row_mac_e with 2 = E 4 at 3 waves/SIMD (148 VGPRs), 4 = E 4 at 4 waves/SIMD (128 VGPRs,
-// spills), 3 = E 8 at 2 waves/SIMD
-static inline int ks_row_eb()
-{
-    static const int v = [] {
-        const char *f = getenv("MHE_KS_EB");
-        return f ? atoi(f) : 0;
-    }();
-    return v;
-}
-
-// Key prefetch distance of the fused kernel: none (default; measured equal, fewer VGPRs) or one digit ahead (MHE_KS_KPF=1).
-static inline bool ks_key_prefetch()
-{
-    static const bool v = [] {
-        const char *f = getenv("MHE_KS_KPF");
-        return f && atoi(f) != 0;
-    }();
-    return v;
-}
-
 // measured at L=44: G=1 763, 2 738, 4 700 HMult/s (digit groups with a partial-sum reduction, since
 // removed); ResNet-20 (L <= 31): G=1 0.865-0.873 images/s vs 0.832-0.839 with G=2
 template <int LOGR, bool FP, bool MIX = false>
@@ -1684,38 +1391,18 @@ static inline int ks_row_mac_a(const KsPtrs &P, int B, const PrimeDev *primes, c
                                long long tinv, int inv_special, hipStream_t st)
 {
     const int blocks = 1 << (log_n - LOGR);
-    const int eb = ks_row_eb();
     if constexpr (MIX)
     {
         const dim3 g(blocks / RowMacShape<LOGR>::S, cnt, B);
         share = (share && B > 1 && (g.x * g.y) % 8 == 0) ? 1 : 0;
-        hipLaunchKernelGGL((k_ks_row_mac<LOGR, true, false, true>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
+        hipLaunchKernelGGL((k_ks_row_mac<LOGR, true, true>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
                            I0, pack, kpack, share, itw, tinv, inv_special);
         return inv_special;
     }
-    if (eb == 2 || eb == 3 || eb == 4)
-    {
-        const dim3 g(blocks / (eb == 3 ? RowMacShapeE<LOGR, 3>::S : RowMacShapeE<LOGR, 2>::S), cnt, B);
-        share = (share && B > 1 && (g.x * g.y) % 8 == 0) ? 1 : 0;
-        if (eb == 2)
-            hipLaunchKernelGGL((k_ks_row_mac_e<LOGR, FP, 2, 3>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
-                               I0, pack, kpack, share);
-        else if (eb == 4)
-            hipLaunchKernelGGL((k_ks_row_mac_e<LOGR, FP, 2, 4>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
-                               I0, pack, kpack, share);
-        else
-            hipLaunchKernelGGL((k_ks_row_mac_e<LOGR, FP, 3, 2>), g, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd,
-                               I0, pack, kpack, share);
-        return 0; // the E-variants leave the special limbs' inverse row pass to k_inv_row
-    }
     const dim3 grid(blocks / RowMacShape<LOGR>::S, cnt, B);
     share = (share && B > 1 && (grid.x * grid.y) % 8 == 0) ? 1 : 0;
-    if (ks_key_prefetch())
-        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, true>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
-                           pack, kpack, share, itw, tinv, inv_special);
-    else
-        hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP, false>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
-                           pack, kpack, share, itw, tinv, inv_special);
+    hipLaunchKernelGGL((k_ks_row_mac<LOGR, FP>), grid, dim3(256), 0, st, P, primes, tw, L, K, log_n, twd, I0,
+                       pack, kpack, share, itw, tinv, inv_special);
     return inv_special;
 }
 

@@ -84,6 +84,8 @@ public:
     double galois_key_gb() const;
     // key-switching key bytes streamed by this runner's key switches since the last reset
     double key_traffic_bytes(bool reset);
+    // operations of the runner's key-level context since the last reset, per level (mhe_op_counts)
+    std::vector<std::uint64_t> op_counts(int kind, bool reset);
     // the evaluation keys are in the engine's prepared format (mhe_key_prepare) rather than SEAL's
     bool keys_prepared() const { return keys_prepared_; }
     // resnet_plain_logits with this runner's parameters

@@ -40,6 +40,7 @@ def seal_lib():
             "mhe_resnet_infer_batch": (i32, [vp, dp, i32, i32, dp, ip, dp, dp, dp, dp]),
             "mhe_resnet_info": (i32, [vp, dp, dp, ip]),
             "mhe_resnet_key_traffic": (i32, [vp, dp, i32]),
+            "mhe_resnet_op_counts": (i32, [vp, i32, u64p, i32]),
             "mhe_resnet_key_format": (i32, [vp, ip]),
             "mhe_resnet_plain_logits": (i32, [vp, dp, dp]),
         }
@@ -118,6 +119,18 @@ class Runner:
         b = ctypes.c_double()
         _check(seal_lib().mhe_resnet_key_traffic(self._h, ctypes.byref(b), 1 if reset else 0))
         return b.value
+
+    OP_KINDS = ("keyswitch", "rescale", "tensor", "mulplain", "addsub", "scalar", "ntt", "galois")  # MHE_OPK_*
+
+    def op_counts(self, reset=False):
+        """{kind: [count per level 0..63]} of the operations run since the last reset (mhe_op_counts:
+        key switches per entry, the elementwise kinds per polynomial)."""
+        out = {}
+        for k, name in enumerate(self.OP_KINDS):
+            c = (ctypes.c_uint64 * 64)()
+            _check(seal_lib().mhe_resnet_op_counts(self._h, k, c, 1 if reset else 0))
+            out[name] = [int(x) for x in c]
+        return out
 
     def keys_prepared(self):
         """True when the evaluation keys are in the engine's prepared format (mhe_key_prepare)."""

@@ -22,6 +22,7 @@
 #include <stdexcept>
 
 #include "../../include/mhe.h"
+#include "trace.h"
 
 using namespace seal;
 using cd = std::complex<double>;
@@ -2084,10 +2085,17 @@ void Bootstrapper::modraise_inplace(Ciphertext &cipher)
     cipher.resize(context, context.first_parms_id(), 2);
     const std::size_t limbs = cipher.coeff_modulus_size();
     void *s = context.stream();
-    const std::uint64_t *src = encrypted_copy.store().dev_read(s);
-    std::uint64_t *dst = cipher.store().dev_write(s, true);
-    if (mhe_modraise(context.engine(), src, dst, 2, (int)limbs, s) != MHE_OK) throw std::runtime_error(mhe_last_error());
-    cipher.is_ntt_form() = false;
+    {
+        // the lift is one record of the evaluator trace (tests/trace_replay.py "modraise"), between
+        // the traced transform_from_ntt / transform_to_ntt
+        seal::trace::Scope tsc;
+        const std::string tin = tsc.top() ? seal::trace::ct(encrypted_copy) : std::string();
+        const std::uint64_t *src = encrypted_copy.store().dev_read(s);
+        std::uint64_t *dst = cipher.store().dev_write(s, true);
+        if (mhe_modraise(context.engine(), src, dst, 2, (int)limbs, s) != MHE_OK) throw std::runtime_error(mhe_last_error());
+        cipher.is_ntt_form() = false;
+        if (tsc.top()) seal::trace::record("modraise", { tin }, seal::trace::ct(cipher));
+    }
     evaluator.transform_to_ntt_inplace(cipher);
 }
 

@@ -513,6 +513,14 @@ double ResNetRunner::key_traffic_bytes(bool reset)
     return (double)b;
 }
 
+std::vector<std::uint64_t> ResNetRunner::op_counts(int kind, bool reset)
+{
+    std::vector<std::uint64_t> c(64, 0);
+    if (mhe_op_counts(impl_->context->engine(), kind, c.data(), (int)c.size(), reset ? 1 : 0) != 0)
+        throw std::runtime_error(mhe_last_error());
+    return c;
+}
+
 std::vector<double> ResNetRunner::plain_logits(const std::vector<double> &image) const
 {
     return resnet_plain_logits(impl_->prm, image, impl_->layer_num);

@@ -1,4 +1,5 @@
 // resnet_capi.cpp -- the C ABI of include/mhe_resnet_capi.h over ResNetRunner (mhe_resnet.h).
+#include <algorithm>
 #include "../../include/mhe_resnet_capi.h"
 
 #include "mhe_resnet.h"
@@ -138,6 +139,15 @@ int mhe_resnet_key_traffic(mhe_resnet *r, double *bytes, int reset)
     return guard([&] {
         const double b = r->runner->key_traffic_bytes(reset != 0);
         if (bytes) *bytes = b;
+    });
+}
+
+int mhe_resnet_op_counts(mhe_resnet *r, int kind, uint64_t *counts, int reset)
+{
+    return guard([&] {
+        if (!counts) throw std::invalid_argument("null argument");
+        const auto c = r->runner->op_counts(kind, reset != 0);
+        std::copy(c.begin(), c.end(), counts);
     });
 }
 

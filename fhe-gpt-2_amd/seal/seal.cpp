@@ -8,6 +8,7 @@
 //   context.cpp (modulus switching chain), ciphertext.h, plaintext.h, keygenerator.cpp,
 //   encryptor.cpp:88-166, decryptor.cpp (ckks_decrypt), ckks.h/ckks.cpp (CKKSEncoder),
 //   evaluator.cpp (all Evaluator entry points; line numbers cited per method).
+#include "lockstep_core.h"
 #include "stream_order.h"
 #include "seal/seal.h"
 
@@ -2242,30 +2243,13 @@ bool batched_launches()
 // ------------------------------------------------------------------------------ Lockstep
 struct Lockstep::Impl
 {
-    std::mutex mu;
-    std::condition_variable cv;
-    std::size_t active;
-    std::size_t arrived = 0;
-    std::uint64_t round = 0;
-    std::size_t rounds_run = 0, merged = 0;
-    std::vector<LsOp *> reqs;
-    explicit Impl(std::size_t m) : active(m) {}
-    // called with mu held once every active member has arrived: runs the round, wakes the members
-    void run_round(std::unique_lock<std::mutex> &lk)
+    detail::LockstepCore<LsOp> core;
+    explicit Impl(std::size_t m) : core(m) {}
+    // a round's merged call, run by the member that completes the round (lockstep_core.h)
+    static void execute(std::vector<LsOp *> &batch)
     {
-        std::vector<LsOp *> batch;
-        batch.swap(reqs);
-        lk.unlock();
-        {
-            LsDirect d;
-            batch[0]->ev->lockstep_execute(batch);
-        }
-        lk.lock();
-        arrived = 0;
-        round++;
-        rounds_run++;
-        if (batch.size() > 1) merged += batch.size();
-        cv.notify_all();
+        LsDirect d;
+        batch[0]->ev->lockstep_execute(batch);
     }
 };
 
@@ -2273,13 +2257,11 @@ Lockstep::Lockstep(std::size_t members) : impl_(std::make_unique<Impl>(members))
 Lockstep::~Lockstep() = default;
 std::size_t Lockstep::rounds() const
 {
-    std::lock_guard<std::mutex> g(impl_->mu);
-    return impl_->rounds_run;
+    return impl_->core.rounds();
 }
 std::size_t Lockstep::merged_calls() const
 {
-    std::lock_guard<std::mutex> g(impl_->mu);
-    return impl_->merged;
+    return impl_->core.merged();
 }
 
 Lockstep::Member::Member(Lockstep &group, bool active) : g_(group)
@@ -2295,10 +2277,7 @@ Lockstep::Member::~Member()
 {
     tl_ls = nullptr;
     tl_ls_member = nullptr;
-    Impl *g = g_.impl_.get();
-    std::unique_lock<std::mutex> lk(g->mu);
-    if (g->active) g->active--;
-    if (g->arrived > 0 && g->arrived >= g->active) g->run_round(lk);
+    g_.impl_->core.leave(Impl::execute);
 }
 
 bool Evaluator::lockstep_submit(LsOp &op) const
@@ -2306,14 +2285,7 @@ bool Evaluator::lockstep_submit(LsOp &op) const
     Lockstep::Impl *g = tl_ls;
     if (!g || tl_ls_direct > 0 || trace::enabled()) return false;
     op.ev = this;
-    std::unique_lock<std::mutex> lk(g->mu);
-    const std::uint64_t r = g->round;
-    g->reqs.push_back(&op);
-    if (++g->arrived >= g->active)
-        g->run_round(lk);
-    else
-        g->cv.wait(lk, [&] { return g->round != r; });
-    lk.unlock();
+    g->core.submit(&op, Lockstep::Impl::execute);
     if (op.err) std::rethrow_exception(op.err);
     return true;
 }

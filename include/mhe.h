@@ -78,6 +78,20 @@ int mhe_key_traffic(mhe_ctx *ctx, uint64_t *bytes, int reset);
 /* The same key slices counted in the prepared key format (mhe_key_prepare): 6 B per residue for
  * primes below 2^48, 8 B otherwise -- the bytes a switch streams when its key is prepared. */
 int mhe_key_traffic_prepared(mhe_ctx *ctx, uint64_t *bytes, int reset);
+/* Operations run on the context since the last reset, by kind and level (limbs): counts[l] for
+ * l < levels (reset != 0 zeroes every level of the kind).  Units: one key switch per entry
+ * (relinearization, rotation, switch_key), one polynomial for the rest (a 2-poly rescale counts
+ * 2, a plaintext product of a 2-poly ciphertext 2, an NTT of one poly 1).  The op mix of a
+ * workload, e.g. for a CPU cost estimate from per-op CPU timings.  No SEAL counterpart. */
+#define MHE_OPK_KEYSWITCH 0
+#define MHE_OPK_RESCALE 1
+#define MHE_OPK_TENSOR 2   /* ciphertext x ciphertext products (multiply / square), per product */
+#define MHE_OPK_MULPLAIN 3 /* ciphertext x plaintext products */
+#define MHE_OPK_ADDSUB 4   /* add / sub / negate (incl. the adds of fused product sums) */
+#define MHE_OPK_SCALAR 5   /* per-limb scalar multiply / add / set */
+#define MHE_OPK_NTT 6      /* forward or inverse NTT (encode, decode, transform_to/from_ntt) */
+#define MHE_OPK_GALOIS 7   /* NTT-domain Galois permutation */
+int mhe_op_counts(mhe_ctx *ctx, int kind, uint64_t *counts, int levels, int reset);
 /* A non-blocking HIP stream on the context's device (and its scratch workspace); the SEAL
  * shim gives every host thread its own, as the reference's OpenMP threads share one
  * Evaluator (cnn/infer_seal.cpp:404). */

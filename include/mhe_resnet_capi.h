@@ -43,6 +43,9 @@ int mhe_resnet_infer_batch(mhe_resnet *runner, const double *images, int count, 
 int mhe_resnet_info(mhe_resnet *runner, double *setup_s, double *galois_key_gb, int *galois_keys);
 /* key-switching key bytes the runner's key switches streamed since the last reset (reset != 0 zeroes) */
 int mhe_resnet_key_traffic(mhe_resnet *runner, double *bytes, int reset);
+/* operations of kind MHE_OPK_* (include/mhe.h) the runner ran since the last reset, counts[l] per
+ * level l < 64 (reset != 0 zeroes them) */
+int mhe_resnet_op_counts(mhe_resnet *runner, int kind, uint64_t *counts, int reset);
 /* *prepared = 1 when the runner's evaluation keys are in the engine's prepared format
  * (mhe_key_prepare), 0 when they are in SEAL's layout (MHE_KEY_PREPARE=0). */
 int mhe_resnet_key_format(mhe_resnet *runner, int *prepared);

@@ -8,6 +8,12 @@
 // used are written next to the trace: key_relin.bin, key_gal_<elt>.bin (u64 header: digits, limbs,
 // n; then [digits][2][limbs][n] in SEAL's layout, the special prime last).
 //   trace_caller_test <log N: 12 | 16> <dir> <comp_dir>
+//   trace_caller_test <log N> <dir> <comp_dir> boot <logn>
+// The boot mode traces one sparse bootstrap_real_3 instead (Bootstrapper.cpp:3166-3236 with
+// ModularReducer.cpp:61-80 and Polynomial.cpp:256-560): the ResNet chain {51} + 16 x {46} + 14 x
+// {51} + {51}, loge 10, K 25, cosine degree 59, 2 double-angle steps, inverse_deg 1, logn slots;
+// modraise, subsum, CoeffToSlot BSGS, EvalMod and SlotToCoeff all land in the trace.
+#include "mhe_boot.h"
 #include "mhe_cnn.h"
 #include "mhe_comp.h"
 
@@ -27,17 +33,102 @@ static void write_key(const std::string &path, const PolyStore &key, std::size_t
     f.write(reinterpret_cast<const char *>(key.host()), (std::streamsize)(key.words() * 8));
 }
 
+static void write_meta(const std::string &dir, const SEALContext &ctx, int logN)
+{
+    std::ofstream meta(dir + "/meta.json");
+    meta << "{\"log_n\": " << logN << ", \"moduli\": [";
+    const auto &q = ctx.key_context_data()->parms().coeff_modulus();
+    for (std::size_t i = 0; i < q.size(); i++) meta << (i ? ", " : "") << q[i].value();
+    meta << "], \"first_limbs\": " << ctx.first_context_data()->parms().coeff_modulus().size() << "}\n";
+}
+
+static void write_keys(const std::string &dir, const RelinKeys &rlk, const GaloisKeys &glk, std::size_t N)
+{
+    write_key(dir + "/key_relin.bin", rlk.key(0), rlk.limbs_of(0), N);
+    std::size_t gal = 0;
+    for (const auto &kv : glk.usage())
+    {
+        write_key(dir + "/key_gal_" + std::to_string(2 * kv.first + 1) + ".bin", glk.key(kv.first), kv.second, N);
+        gal++;
+    }
+    std::printf("trace written to %s (%zu Galois keys used)\n", dir.c_str(), gal);
+}
+
+// one sparse bootstrap under the trace (see the header)
+static int run_boot(int logN, const std::string &dir, long logn)
+{
+    const std::size_t N = (std::size_t)1 << logN;
+    const long loge = 10, boundary_K = 25, boot_deg = 59, scale_factor = 2, inverse_deg = 1;
+    const int logp = 46, logq = 51, remaining_level = 16, boot_level = 14, total_level = remaining_level + boot_level;
+    std::vector<int> bits{ logq };
+    for (int i = 0; i < remaining_level; i++) bits.push_back(logp);
+    for (int i = 0; i < boot_level; i++) bits.push_back(logq);
+    bits.push_back(51);
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(N);
+    parms.set_coeff_modulus(CoeffModulus::Create(N, bits));
+    parms.set_secret_key_hamming_weight(logN >= 16 ? 192 : 64);
+    parms.set_random_generator(
+        std::make_shared<Blake2xbPRNGFactory>(std::array<std::uint64_t, 8>{ 1, 2, 3, 4, 5, 6, 7, 8 }));
+    SEALContext ctx(parms, true, sec_level_type::none);
+    KeyGenerator keygen(ctx);
+    PublicKey pk;
+    keygen.create_public_key(pk);
+    RelinKeys rlk;
+    keygen.create_relin_keys(rlk);
+    GaloisKeys glk;
+    CKKSEncoder encoder(ctx);
+    Encryptor encryptor(ctx, pk);
+    Decryptor decryptor(ctx, keygen.secret_key());
+    Evaluator evaluator(ctx, encoder);
+    const double scale = std::pow(2.0, logp);
+    Bootstrapper bt(loge, logn, logN - 1, total_level, scale, boundary_K, boot_deg, scale_factor, inverse_deg, ctx, keygen,
+                    encoder, encryptor, decryptor, evaluator, rlk, glk);
+    bt.prepare_mod_polynomial();
+    std::vector<int> steps{ 0 };
+    for (int i = 0; i < logN - 1; i++) steps.push_back(1 << i);
+    bt.addLeftRotKeys_Linear_to_vector_3(steps);
+    keygen.create_deferred_galois_keys(steps, glk); // materialised (and grown) at the levels of use
+    bt.slot_vec.push_back(logn);
+    bt.generate_LT_coefficient_3();
+
+    const long n = 1L << logn, Nh = (long)N / 2;
+    std::mt19937_64 g(20261018);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    std::vector<double> z(n), msg(Nh);
+    for (auto &x : z) x = U(g);
+    for (long i = 0; i < Nh; i++) msg[i] = z[i % n];
+    Plaintext pt;
+    encoder.encode(msg, scale, pt);
+    Ciphertext ct, out;
+    encryptor.encrypt(pt, ct);
+    evaluator.mod_switch_to_inplace(ct, ctx.last_parms_id());
+    bt.bootstrap_real_3(out, ct);
+    Plaintext dp;
+    decryptor.decrypt(out, dp);
+    std::vector<double> got;
+    encoder.decode(dp, got);
+    double err = 0;
+    for (long i = 0; i < Nh; i++) err = std::max(err, std::fabs(got[i] - msg[i]));
+    std::printf("bootstrap_real_3 (N 2^%d, logn %ld): %zu -> %zu limbs, max error %.3g\n", logN, logn, (std::size_t)1,
+                out.coeff_modulus_size(), err);
+    write_keys(dir, rlk, glk, N);
+    write_meta(dir, ctx, logN);
+    return err < 1e-2 ? 0 : 1;
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 4)
     {
-        std::fprintf(stderr, "usage: trace_caller_test <log N> <dir> <comp_dir>\n");
+        std::fprintf(stderr, "usage: trace_caller_test <log N> <dir> <comp_dir> [boot <logn>]\n");
         return 2;
     }
     const int logN = std::atoi(argv[1]);
     const std::string dir = argv[2];
     setenv("MHE_EVAL_TRACE", dir.c_str(), 1); // before the first evaluator operation
     setenv("MHE_COMP_DIR", argv[3], 1);
+    if (argc > 5 && std::string(argv[4]) == "boot") return run_boot(logN, dir, std::atol(argv[5]));
     const std::size_t N = (std::size_t)1 << logN;
     // {51} + 8 x {46} + {51}: the ResNet chain's shape (cnn/infer_seal.cpp:288-316), shortened; 2^46 scale
     std::vector<int> bits{ 51 };
@@ -105,18 +196,7 @@ int main(int argc, char **argv)
     minimax_ReLU_seal(1, { 15 }, 13, tree, 1.7, 46, encryptor, evaluator, decryptor, encoder, pk, sk, rlk, cx, cr);
 
     // keys the sequence used, for the replay
-    write_key(dir + "/key_relin.bin", rlk.key(0), rlk.limbs_of(0), N);
-    std::size_t gal = 0;
-    for (const auto &kv : glk.usage())
-    {
-        write_key(dir + "/key_gal_" + std::to_string(2 * kv.first + 1) + ".bin", glk.key(kv.first), kv.second, N);
-        gal++;
-    }
-    std::ofstream meta(dir + "/meta.json");
-    meta << "{\"log_n\": " << logN << ", \"moduli\": [";
-    const auto &q = ctx.key_context_data()->parms().coeff_modulus();
-    for (std::size_t i = 0; i < q.size(); i++) meta << (i ? ", " : "") << q[i].value();
-    meta << "], \"first_limbs\": " << ctx.first_context_data()->parms().coeff_modulus().size() << "}\n";
-    std::printf("trace written to %s (%zu Galois keys used)\n", dir.c_str(), gal);
+    write_keys(dir, rlk, glk, N);
+    write_meta(dir, ctx, logN);
     return 0;
 }

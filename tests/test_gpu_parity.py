@@ -512,38 +512,16 @@ def test_hmult_fused_n16(fused_engines):
     assert np.array_equal(got, ch.oc.hmult(a, b, key))
 
 
-@pytest.mark.parametrize("chunk", [1, 3, 0])
-def test_switch_key_chunked_modup(chunk):
-    """ModUp processed in chunks of output primes (MHE_KS_CHUNK) is bit-identical."""
-    import os
-
-    old = os.environ.get("MHE_KS_CHUNK")
-    os.environ["MHE_KS_CHUNK"] = str(chunk)
-    try:
-        ch = Chain(12, SMALL_BITS, seed=30 + chunk)
-    finally:
-        if old is None:
-            del os.environ["MHE_KS_CHUNK"]
-        else:
-            os.environ["MHE_KS_CHUNK"] = old
-    L = ch.K - 1
-    key = ch.rand_key()
-    ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
-    got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), ch.up(key)))
-    assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
-
-
 # ------------------------------------------- every arithmetic / scheduling variant, bit-exact
 ENGINE_VARIANTS = [
     {"MHE_FP": "0"},                                  # integer Harvey/Shoup butterflies everywhere
     {"MHE_FP": "0", "MHE_KS_FUSED": "0"},             # integer, unfused row pass + k_ks_mac
     {"MHE_KS_FUSED": "0"},                            # FP64, unfused
     {"MHE_KS_COLGROUPS": "0"},                        # fused, one column-pass job per (I, J)
-    {"MHE_KS_COLGROUPS": "1", "MHE_KS_GROUPS": "3"},  # digit-major column pass, 3 digit groups
-    {"MHE_KS_FCHUNK": "3", "MHE_KS_GROUPS": "2"},     # output primes in chunks of 3
-    {"MHE_FP": "0", "MHE_KS_FCHUNK": "2", "MHE_KS_COLGROUPS": "2"},
+    {"MHE_KS_COLGROUPS": "1"},                        # digit-major column pass, one output-prime group
+    {"MHE_KS_COLGROUPS": "3", "MHE_KS_SHARE": "0"},   # three groups
+    {"MHE_FP": "0", "MHE_KS_COLGROUPS": "2"},
     {"MHE_HMULT_FUSED": "0"},                         # HMult: separate ModDown and rescale
-    {"MHE_FP": "0", "MHE_KS_GROUPS": "2"},            # integer, fused ModDown + rescale, 2 groups
 ]
 
 

@@ -34,3 +34,26 @@ def test_conv_bn_relu_sequence_matches_oracle(tmp_path, log_n):
     for op in ("rotate", "multiply_plain", "multiply_plain_add", "add_re", "sub_re", "mul_re", "rescale",
                "encode_for", "multiply_const"):
         assert counts.get(op, 0) > 0, f"{op} not exercised: {counts}"
+
+
+@pytest.mark.parametrize("log_n,logn", [(12, 9), (12, 10)])
+def test_sparse_bootstrap_matches_oracle(tmp_path, log_n, logn):
+    """One sparse bootstrap_real_3 (Bootstrapper.cpp:3166-3236) at N = 2^12 on the ResNet chain shape,
+    replayed op by op: modraise (:2894-2948), the subsum rotations, CoeffToSlot's three BSGS groups
+    (sflinv_3, :2531; bsgs / rotated_bsgs_linear_transform, :1952-2085) with the reference-order LT
+    diagonals, EvalMod (ModularReducer.cpp:61-80: the cosine heap polynomial of Polynomial.cpp:256-560,
+    two double-angle steps, the linear arcsine), SlotToCoeff (sfl_half_3, :2453) and the final
+    conjugate add -- every output word and scale equal to the oracle's."""
+    d = tmp_path / f"boot{log_n}_{logn}"
+    d.mkdir()
+    exe = os.path.join(ROOT, "build", "trace_caller_test")
+    r = subprocess.run([exe, str(log_n), str(d), os.path.join(ROOT, "tests", "golden", "comp"), "boot", str(logn)],
+                       capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rp = Replayer(str(d))
+    checked, counts = rp.replay()
+    print(f"N=2^{log_n}, logn {logn}: {checked} bootstrap operations match the oracle: {counts}")
+    for op in ("modraise", "ntt_inv", "ntt_fwd", "rotate", "galois", "encode_for", "multiply_plain",
+               "multiply_plain_add", "rescale", "mul_re", "add_re", "add_const", "multiply_const"):
+        assert counts.get(op, 0) > 0, f"{op} not exercised: {counts}"

@@ -179,6 +179,11 @@ class Replayer:
             a.data = a.data.copy()
             a.data[0] = ctx.sub(a.data[0], w) if op == "sub_plain" else ctx.add(a.data[0], w)
             return a
+        if op == "modraise":
+            # Bootstrapper::modraise_inplace's lift (Bootstrapper.cpp:2929-2945): coefficient form,
+            # one limb -> every limb of the first level, centred on q0
+            L = self.store.get(rec["out"])[0].L
+            return OCt(ctx.modraise(a.data, L), a.scale)
         if op == "ntt_fwd":
             return OCt(ctx.ntt(a.data, O.NTT_FWD), a.scale)
         if op == "ntt_inv":
