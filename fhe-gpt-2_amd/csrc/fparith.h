@@ -83,6 +83,23 @@ __device__ __forceinline__ double fp_from_u52(uint64_t x)
     return __longlong_as_double((long long)(x | 0x4330000000000000ull)) - FP_TWO52;
 }
 
+// The packed ModUp intermediate of the FP path (ntt.h tile16, primes q < 2^48) holds the centred
+// residue r = x - rint(x/q) q, |r| <= q/2 + 1 < 2^47, as 48-bit two's complement: r + 1.5 2^52 is a
+// double in [2^52, 2^53) whose mantissa is r + 2^51, and its low 48 bits are r mod 2^48 -- one add
+// instead of fp_canon's select and add.  Only the low 48 bits of the returned word are meaningful.
+__device__ __forceinline__ uint64_t fp_to_s48(double x, double q, double qinv)
+{
+    const double r = fp_reduce(x, q, qinv);
+    return (uint64_t)__double_as_longlong(r + 6755399441055744.0); // 1.5 * 2^52
+}
+
+// ... and back: flipping bit 47 of r mod 2^48 gives r + 2^47 in [0, 2^48); OR-ed under the exponent
+// of 2^52 (one XOR with both) and less 2^52 + 2^47, that is r exactly.
+__device__ __forceinline__ double fp_from_s48(uint64_t v48)
+{
+    return __longlong_as_double((long long)(v48 ^ 0x4330800000000000ull)) - 4644337115725824.0; // 2^52 + 2^47
+}
+
 // Forward Cooley-Tukey butterfly (the mathematics of dwthandler.h:122-125).
 __device__ __forceinline__ void fwd_bfly_f(double &x, double &y, const TwF w, double q, double qinv)
 {

@@ -872,11 +872,9 @@ struct JobStrided
 // Elementwise kernels process 2 residues per lane (16-B loads); n is a multiple of 512.
 #define ELEM_GRID(total2) dim3((unsigned)(((total2) + 255) / 256))
 
-__global__ void k_addsub(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
-                         size_t total2, int op)
+__device__ __forceinline__ void addsub_at(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs,
+                                          int log_n, size_t i2, int op)
 {
-    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 >= total2) return;
     const size_t i = i2 * 2;
     const int l = (int)((i >> log_n) % limbs);
     const u64 q = primes[l].q;
@@ -902,12 +900,17 @@ __global__ void k_addsub(const u64 *a, const u64 *b, u64 *out, const PrimeDev *p
     *(ulonglong2 *)(out + i) = r;
 }
 
-// dyadic product with b broadcast over polys (multiply_plain_ntt)
-__global__ void k_mulplain(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
-                           size_t total2)
+__global__ void k_addsub(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                         size_t total2, int op)
 {
     size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 >= total2) return;
+    if (i2 < total2) addsub_at(a, b, out, primes, limbs, log_n, i2, op);
+}
+
+// dyadic product with b broadcast over polys (multiply_plain_ntt)
+__device__ __forceinline__ void mulplain_at(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs,
+                                            int log_n, size_t i2)
+{
     const size_t i = i2 * 2;
     const size_t limb_words = (size_t)limbs << log_n;
     const int l = (int)((i >> log_n) % limbs);
@@ -920,12 +923,17 @@ __global__ void k_mulplain(const u64 *a, const u64 *b, u64 *out, const PrimeDev 
     *(ulonglong2 *)(out + i) = r;
 }
 
-// acc += a * b, b broadcast over polys (multiply_plain_ntt then add_inplace, one pass)
-__global__ void k_mulplain_add(const u64 *a, const u64 *b, u64 *acc, const PrimeDev *primes, int limbs, int log_n,
-                               size_t total2)
+__global__ void k_mulplain(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                           size_t total2)
 {
     size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 >= total2) return;
+    if (i2 < total2) mulplain_at(a, b, out, primes, limbs, log_n, i2);
+}
+
+// acc += a * b, b broadcast over polys (multiply_plain_ntt then add_inplace, one pass)
+__device__ __forceinline__ void mulplain_add_at(const u64 *a, const u64 *b, u64 *acc, const PrimeDev *primes,
+                                                int limbs, int log_n, size_t i2)
+{
     const size_t i = i2 * 2;
     const size_t limb_words = (size_t)limbs << log_n;
     const int l = (int)((i >> log_n) % limbs);
@@ -937,6 +945,13 @@ __global__ void k_mulplain_add(const u64 *a, const u64 *b, u64 *acc, const Prime
     r.x = addmod(z.x, mulmod(x.x, y.x, p), p.q);
     r.y = addmod(z.y, mulmod(x.y, y.y, p), p.q);
     *(ulonglong2 *)(acc + i) = r;
+}
+
+__global__ void k_mulplain_add(const u64 *a, const u64 *b, u64 *acc, const PrimeDev *primes, int limbs, int log_n,
+                               size_t total2)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 < total2) mulplain_add_at(a, b, acc, primes, limbs, log_n, i2);
 }
 
 // acc = (accumulate ? acc : 0) + sum_k a_k * b_k, up to 16 terms per launch (pointers in the kernel
@@ -973,11 +988,9 @@ struct ScalarTab
     u64 vq[64];
 };
 
-__global__ void k_scalar(const u64 *a, u64 *out, const PrimeDev *primes, ScalarTab s, int limbs, int log_n,
-                         size_t total2, int op)
+__device__ __forceinline__ void scalar_at(const u64 *a, u64 *out, const PrimeDev *primes, const ScalarTab &s, int limbs,
+                                          int log_n, size_t i2, int op)
 {
-    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 >= total2) return;
     const size_t i = i2 * 2;
     const int l = (int)((i >> log_n) % limbs);
     const u64 q = primes[l].q;
@@ -1002,12 +1015,17 @@ __global__ void k_scalar(const u64 *a, u64 *out, const PrimeDev *primes, ScalarT
     *(ulonglong2 *)(out + i) = r;
 }
 
-// ckks_multiply tile loop (evaluator.cpp:714-773) / ckks_square (:1000-1059), fused.
-__global__ void k_tensor(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
-                         size_t total2, int square)
+__global__ void k_scalar(const u64 *a, u64 *out, const PrimeDev *primes, ScalarTab s, int limbs, int log_n,
+                         size_t total2, int op)
 {
     size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 >= total2) return;
+    if (i2 < total2) scalar_at(a, out, primes, s, limbs, log_n, i2, op);
+}
+
+// ckks_multiply tile loop (evaluator.cpp:714-773) / ckks_square (:1000-1059), fused.
+__device__ __forceinline__ void tensor_at(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs,
+                                          int log_n, size_t i2, int square)
+{
     const size_t i = i2 * 2;
     const size_t ps = (size_t)limbs << log_n;
     const int l = (int)(i >> log_n);
@@ -1037,6 +1055,47 @@ __global__ void k_tensor(const u64 *a, const u64 *b, u64 *out, const PrimeDev *p
     *(ulonglong2 *)(out + i) = r0;
     *(ulonglong2 *)(out + ps + i) = r1;
     *(ulonglong2 *)(out + 2 * ps + i) = r2;
+}
+
+__global__ void k_tensor(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
+                         size_t total2, int square)
+{
+    size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 < total2) tensor_at(a, b, out, primes, limbs, log_n, i2, square);
+}
+
+// The same elementwise kernels over up to MHE_MAXB entries of one shape (entry = blockIdx.y): the
+// launches that mhe_launch_run coalesces, e.g. the same-numbered adds of the images of a
+// seal::FiberBatch
+struct ElemPtrs
+{
+    const u64 *a[MHE_MAXB];
+    const u64 *b[MHE_MAXB];
+    u64 *out[MHE_MAXB];
+};
+
+__global__ void k_elem_b(ElemPtrs P, const PrimeDev *primes, ScalarTab st, int limbs, int log_n, size_t total2,
+                         int kind, int op)
+{
+    const size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i2 >= total2) return;
+    const int e = blockIdx.y;
+    switch (kind)
+    {
+    case MHE_LK_ADDSUB: addsub_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2, op); break;
+    case MHE_LK_MULPLAIN: mulplain_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2); break;
+    case MHE_LK_MULPLAIN_ADD: mulplain_add_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2); break;
+    case MHE_LK_SCALAR: scalar_at(P.a[e], P.out[e], primes, st, limbs, log_n, i2, op); break;
+    case MHE_LK_TENSOR: tensor_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2, op); break;
+    }
+}
+
+__global__ void k_copy16_b(ElemPtrs P, size_t count)
+{
+    const int e = blockIdx.y;
+    uint4 *dst = reinterpret_cast<uint4 *>(P.out[e]);
+    const uint4 *src = reinterpret_cast<const uint4 *>(P.a[e]);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) dst[i] = src[i];
 }
 
 // Key-switching inner product (evaluator.cpp:2410-2463): for output prime I (I == L -> P),
@@ -1340,6 +1399,20 @@ static bool ranges_overlap(const u64 *a, size_t aw, const u64 *b, size_t bw)
 static void count_op(mhe_ctx *c, int kind, int L, unsigned long long k)
 {
     if (kind >= 0 && kind < MHE_OPK_KINDS && L >= 0 && L < MHE_OPK_LEVELS) c->opc[kind][L].fetch_add(k, std::memory_order_relaxed);
+}
+
+// launch coalescing (mhe_set_launch_hook): the calling thread's hook, off inside mhe_launch_run
+static thread_local mhe_launch_hook tl_hook = nullptr;
+static thread_local void *tl_hook_user = nullptr;
+static thread_local int tl_hook_off = 0;
+
+// true when the launch was handed to the hook (which ran it and set l.rc)
+static bool hooked(mhe_ctx *c, mhe_launch &l)
+{
+    if (!tl_hook || tl_hook_off) return false;
+    l.rc = -1;
+    tl_hook(c, &l, tl_hook_user);
+    return true;
 }
 
 // Forward NTT of [polys][limbs] (limb l on prime l).
@@ -2079,8 +2152,135 @@ MHE_EXPORT int mhe_memcpy_d2d(mhe_ctx *c, void *dst, const void *src, size_t byt
     TR("dst", dst, bytes / 8); TR("src", src, bytes / 8);
     TRC(0, 0, 0, 0);
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
+    if (bytes && dst != src)
+    {
+        mhe_launch l{};
+        l.kind = MHE_LK_COPY;
+        l.a = (const u64 *)src;
+        l.out = (u64 *)dst;
+        l.bytes = bytes;
+        l.stream = stream;
+        if (hooked(c, l)) return l.rc;
+    }
     HIP_TRY(mhe_internal_copy_d2d(dst, src, bytes, S(stream)));
     return MHE_OK;
+}
+
+// one launch as the entry point would have run it (the hook off)
+static int launch_one(mhe_ctx *c, mhe_launch &l)
+{
+    switch (l.kind)
+    {
+    case MHE_LK_ADDSUB:
+        return l.op == 0   ? mhe_add(c, l.a, l.b, l.out, l.polys, l.limbs, l.stream)
+               : l.op == 1 ? mhe_sub(c, l.a, l.b, l.out, l.polys, l.limbs, l.stream)
+                           : mhe_negate(c, l.a, l.out, l.polys, l.limbs, l.stream);
+    case MHE_LK_MULPLAIN: return mhe_multiply_plain(c, l.a, l.b, l.out, l.polys, l.limbs, l.stream);
+    case MHE_LK_MULPLAIN_ADD: return mhe_multiply_plain_add(c, l.a, l.b, l.out, l.polys, l.limbs, l.stream);
+    case MHE_LK_SCALAR:
+        return l.op == 0   ? mhe_multiply_scalar(c, l.a, l.scalars, l.out, l.polys, l.limbs, l.stream)
+               : l.op == 1 ? mhe_add_scalar(c, l.a, l.scalars, l.out, l.polys, l.limbs, l.stream)
+                           : mhe_set_scalar(c, l.scalars, l.out, l.polys, l.limbs, l.stream);
+    case MHE_LK_TENSOR:
+        return l.op ? mhe_ct_square(c, l.a, l.out, l.limbs, l.stream) : mhe_ct_multiply(c, l.a, l.b, l.out, l.limbs, l.stream);
+    case MHE_LK_COPY: return mhe_memcpy_d2d(c, l.out, l.a, l.bytes, l.stream);
+    }
+    return fail(MHE_ERR_ARG, "unknown launch kind");
+}
+
+static bool same_shape(const mhe_launch &x, const mhe_launch &y)
+{
+    if (x.kind != y.kind || x.op != y.op || x.polys != y.polys || x.limbs != y.limbs || x.bytes != y.bytes ||
+        x.stream != y.stream)
+        return false;
+    if (x.kind == MHE_LK_SCALAR)
+        for (int l = 0; l < x.limbs; l++)
+            if (x.scalars[l] != y.scalars[l]) return false;
+    return true;
+}
+
+MHE_EXPORT int mhe_set_launch_hook(mhe_launch_hook hook, void *user)
+{
+    tl_hook = hook;
+    tl_hook_user = user;
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_launch_run(mhe_ctx *c, mhe_launch *const *ls, int count)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    if (count < 0 || (count && !ls)) return fail(MHE_ERR_ARG, "invalid argument");
+    struct Off
+    {
+        Off() { tl_hook_off++; }
+        ~Off() { tl_hook_off--; }
+    } off;
+    std::vector<char> done((size_t)count, 0);
+    int first_err = MHE_OK;
+    for (int i = 0; i < count; i++)
+    {
+        if (done[i]) continue;
+        // entries of i's shape, in order, up to MHE_MAXB per launch
+        int grp[MHE_MAXB], B = 0;
+        for (int j = i; j < count && B < MHE_MAXB; j++)
+            if (!done[j] && same_shape(*ls[i], *ls[j])) grp[B++] = j;
+        for (int k = 0; k < B; k++) done[grp[k]] = 1;
+        mhe_launch &l0 = *ls[grp[0]];
+        const bool aligned16 = l0.kind != MHE_LK_COPY || (l0.bytes & 15) == 0;
+        bool ok_batch = B > 1 && aligned16;
+        if (ok_batch && l0.kind == MHE_LK_COPY)
+            for (int k = 0; k < B; k++)
+                ok_batch = ok_batch && (((uintptr_t)ls[grp[k]]->a | (uintptr_t)ls[grp[k]]->out) & 15) == 0;
+        if (!ok_batch)
+        {
+            for (int k = 0; k < B; k++)
+            {
+                mhe_launch &l = *ls[grp[k]];
+                l.rc = launch_one(c, l);
+                if (l.rc && !first_err) first_err = l.rc;
+            }
+            continue;
+        }
+        ElemPtrs P{};
+        for (int k = 0; k < B; k++)
+        {
+            P.a[k] = ls[grp[k]]->a;
+            P.b[k] = ls[grp[k]]->b;
+            P.out[k] = ls[grp[k]]->out;
+        }
+        const hipStream_t st = S(l0.stream);
+        if (l0.kind == MHE_LK_COPY)
+        {
+            const size_t cnt = l0.bytes / 16;
+            const unsigned grid = (unsigned)std::min<size_t>((cnt + 255) / 256, 4096);
+            hipLaunchKernelGGL(k_copy16_b, dim3(grid, (unsigned)B), dim3(256), 0, st, P, cnt);
+        }
+        else
+        {
+            ScalarTab t{};
+            if (l0.kind == MHE_LK_SCALAR)
+                for (int l = 0; l < l0.limbs; l++)
+                {
+                    t.v[l] = l0.scalars[l];
+                    t.vq[l] = host::shoup(l0.scalars[l], c->q[l]);
+                }
+            // a tensor product covers one pair of 2-poly ciphertexts ([limbs] residues per output poly)
+            const size_t total2 = ((size_t)(l0.kind == MHE_LK_TENSOR ? 1 : l0.polys) * l0.limbs << c->log_n) / 2;
+            const int opk = l0.kind == MHE_LK_ADDSUB ? MHE_OPK_ADDSUB
+                            : l0.kind == MHE_LK_SCALAR ? MHE_OPK_SCALAR
+                            : l0.kind == MHE_LK_TENSOR ? MHE_OPK_TENSOR
+                                                        : MHE_OPK_MULPLAIN;
+            count_op(c, opk, l0.limbs, (unsigned long long)B * (l0.kind == MHE_LK_TENSOR ? 1 : l0.polys));
+            if (l0.kind == MHE_LK_MULPLAIN_ADD) count_op(c, MHE_OPK_ADDSUB, l0.limbs, (unsigned long long)B * l0.polys);
+            hipLaunchKernelGGL(k_elem_b, dim3(ELEM_GRID(total2).x, (unsigned)B), dim3(256), 0, st, P, c->primes, t,
+                               l0.limbs, c->log_n, total2, l0.kind, l0.op);
+        }
+        const hipError_t e = hipGetLastError();
+        const int rc = e == hipSuccess ? MHE_OK : fail(MHE_ERR_DEVICE, hipGetErrorString(e));
+        for (int k = 0; k < B; k++) ls[grp[k]]->rc = rc;
+        if (rc && !first_err) first_err = rc;
+    }
+    return first_err;
 }
 
 MHE_EXPORT int mhe_ctx_set_timing(mhe_ctx *c, int on)
@@ -2270,11 +2470,26 @@ MHE_EXPORT int mhe_stream_wait(mhe_ctx *c, void *waiter, void *waitee)
     if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "invalid argument");
     if (waiter == waitee) return MHE_OK;
     HIP_TRY(hipSetDevice(c->device)); // the event must belong to the engine's device
-    hipEvent_t ev;
-    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    // A ring of events per thread and device, re-recorded in turn: a stream wait captures the
+    // event's state at the call, so a later record of the same event does not move it.  (Creating
+    // and destroying an event per wait cost host time, and destroying one still pending crashed
+    // under rocprofv3's API tracing in multi-stream runs, profiles/r04d.)
+    struct Ring
+    {
+        int device = -1;
+        hipEvent_t ev[64] = {};
+        unsigned next = 0;
+    };
+    static thread_local Ring ring[8];
+    Ring &r = ring[c->device & 7];
+    if (r.device != c->device)
+    {
+        for (auto &e : r.ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        r.device = c->device;
+    }
+    hipEvent_t ev = r.ev[r.next++ & 63];
     hipError_t e = hipEventRecord(ev, S(waitee));
     if (e == hipSuccess) e = hipStreamWaitEvent(S(waiter), ev, 0);
-    (void)hipEventDestroy(ev); // released by the runtime once the recorded work completes
     if (e != hipSuccess) return fail(MHE_ERR_DEVICE, hipGetErrorString(e));
     return MHE_OK;
 }
@@ -2309,6 +2524,18 @@ static int launch_addsub(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out, int p
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!out || (op < 2 && !b)) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    {
+        mhe_launch l{};
+        l.kind = MHE_LK_ADDSUB;
+        l.op = op;
+        l.a = a;
+        l.b = b;
+        l.out = out;
+        l.polys = polys;
+        l.limbs = limbs;
+        l.stream = st;
+        if (hooked(c, l)) return l.rc;
+    }
     count_op(c, MHE_OPK_ADDSUB, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_addsub, ELEM_GRID(total2), dim3(256), 0, S(st), a, b, out, c->primes, limbs, c->log_n,
@@ -2346,6 +2573,17 @@ MHE_EXPORT int mhe_multiply_plain(mhe_ctx *c, const uint64_t *a, const uint64_t 
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!b || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    {
+        mhe_launch l{};
+        l.kind = MHE_LK_MULPLAIN;
+        l.a = a;
+        l.b = b;
+        l.out = out;
+        l.polys = polys;
+        l.limbs = limbs;
+        l.stream = s;
+        if (hooked(c, l)) return l.rc;
+    }
     count_op(c, MHE_OPK_MULPLAIN, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_mulplain, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, out, c->primes, limbs, c->log_n,
@@ -2360,6 +2598,17 @@ MHE_EXPORT int mhe_multiply_plain_add(mhe_ctx *c, const uint64_t *a, const uint6
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!b || !acc) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    {
+        mhe_launch l{};
+        l.kind = MHE_LK_MULPLAIN_ADD;
+        l.a = a;
+        l.b = b;
+        l.out = acc;
+        l.polys = polys;
+        l.limbs = limbs;
+        l.stream = s;
+        if (hooked(c, l)) return l.rc;
+    }
     count_op(c, MHE_OPK_MULPLAIN, limbs, (unsigned long long)polys);
     count_op(c, MHE_OPK_ADDSUB, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
@@ -2404,7 +2653,6 @@ static int launch_scalar(mhe_ctx *c, const u64 *a, const u64 *scalars, u64 *out,
     int r = check_poly_args(c, a, polys, limbs);
     if (r) return r;
     if (!scalars || !out) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
-    count_op(c, MHE_OPK_SCALAR, limbs, (unsigned long long)polys);
     ScalarTab t;
     for (int l = 0; l < limbs; l++)
     {
@@ -2412,6 +2660,19 @@ static int launch_scalar(mhe_ctx *c, const u64 *a, const u64 *scalars, u64 *out,
         t.v[l] = scalars[l];
         t.vq[l] = host::shoup(scalars[l], c->q[l]);
     }
+    {
+        mhe_launch hl{};
+        hl.kind = MHE_LK_SCALAR;
+        hl.op = op;
+        hl.a = a;
+        hl.out = out;
+        hl.polys = polys;
+        hl.limbs = limbs;
+        hl.stream = s;
+        for (int l = 0; l < limbs; l++) hl.scalars[l] = scalars[l];
+        if (hooked(c, hl)) return hl.rc;
+    }
+    count_op(c, MHE_OPK_SCALAR, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_scalar, ELEM_GRID(total2), dim3(256), 0, S(s), a, out, c->primes, t, limbs, c->log_n,
                        total2, op);
@@ -2457,6 +2718,15 @@ MHE_EXPORT int mhe_ct_multiply(mhe_ctx *c, const uint64_t *a, const uint64_t *b,
     int r = check_poly_args(c, a, 2, limbs);
     if (r) return r;
     if (!b || !out3) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    mhe_launch l{};
+    l.kind = MHE_LK_TENSOR;
+    l.a = a;
+    l.b = b;
+    l.out = out3;
+    l.polys = 2;
+    l.limbs = limbs;
+    l.stream = s;
+    if (hooked(c, l)) return l.rc;
     return launch_tensor(c, a, b, out3, limbs, 0, S(s));
 }
 
@@ -2467,6 +2737,16 @@ MHE_EXPORT int mhe_ct_square(mhe_ctx *c, const uint64_t *a, uint64_t *out3, int 
     int r = check_poly_args(c, a, 2, limbs);
     if (r) return r;
     if (!out3) return fail(MHE_ERR_ARG, "invalid polynomial arguments");
+    mhe_launch l{};
+    l.kind = MHE_LK_TENSOR;
+    l.op = 1;
+    l.a = a;
+    l.b = a;
+    l.out = out3;
+    l.polys = 2;
+    l.limbs = limbs;
+    l.stream = s;
+    if (hooked(c, l)) return l.rc;
     return launch_tensor(c, a, a, out3, limbs, 1, S(s));
 }
 

@@ -767,7 +767,19 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
 #pragma unroll
                 for (int e = 0; e < E; e += 2)
                 {
-                    const u64 o0 = ar.out(v[e]), o1 = ar.out(v[e + 1]);
+                    // FP: the centred residue as 48-bit two's complement (fp_to_s48; k_ks_row_mac
+                    // reads it back with fp_from_s48); integer: the canonical residue
+                    u64 o0, o1;
+                    if constexpr (M != 0)
+                    {
+                        o0 = fp_to_s48(v[e], ar.q, ar.qinv);
+                        o1 = fp_to_s48(v[e + 1], ar.q, ar.qinv);
+                    }
+                    else
+                    {
+                        o0 = ar.out(v[e]);
+                        o1 = ar.out(v[e + 1]);
+                    }
                     // tile16(c + ((E t + e) << LC)) - tile16(c + ((E t) << LC)), E t a multiple of 16
                     const u32 k0 = ((u32)(e >> 4) << 12) | ((u32)(e & 15) << 4);
                     const u32 k1 = ((u32)((e + 1) >> 4) << 12) | ((u32)((e + 1) & 15) << 4);
@@ -775,7 +787,7 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
                     st_nt<0>(&lo[k1], (u32)o1);
                     // the same difference for tile16h in words: row pair (e & 15) / 2 of tile row e / 16
                     const u32 kw = ((u32)(e >> 4) << 11) | ((u32)((e & 15) >> 1) << 4);
-                    st_nt<0>(&hi[kw], (u32)(o0 >> 32) | ((u32)(o1 >> 32) << 16));
+                    st_nt<0>(&hi[kw], ((u32)(o0 >> 32) & 0xFFFFu) | ((u32)(o1 >> 32) << 16));
                 }
             }
             else
@@ -1207,7 +1219,15 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             {
                 T w[8];
 #pragma unroll
-                for (int e = 0; e < 8; e++) w[e] = ar.in52(vin[e]); // canonical column-pass output
+                for (int e = 0; e < 8; e++)
+                {
+                    // the column-pass output: FP and packed, a centred 48-bit residue (fp_to_s48);
+                    // otherwise canonical
+                    if constexpr (FPA)
+                        w[e] = pk ? fp_from_s48(vin[e]) : ar.in52(vin[e]);
+                    else
+                        w[e] = ar.in52(vin[e]);
+                }
                 row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
                 wave_lds_fence(); // the previous digit's reads of x0 come first
 #pragma unroll

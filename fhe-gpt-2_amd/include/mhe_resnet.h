@@ -72,9 +72,15 @@ public:
     ResNetResult infer(const std::vector<double> &image);
     // the same, writing the reference's per-stage log (op, time, remaining level, scale) to *log
     ResNetResult infer(const std::vector<double> &image, std::ostream *log);
+    // stage_syncs false: no host synchronisation around each ReLU / bootstrap (their times are then
+    // not measured; used by the FiberBatch images, whose fibers share one stream)
+    ResNetResult infer(const std::vector<double> &image, std::ostream *log, bool stage_syncs);
     // images on `threads` host threads at once, each on its own HIP stream (the reference runs one
     // image per OpenMP thread, infer_seal.cpp:404); results in image order
-    std::vector<ResNetResult> infer_batch(const std::vector<std::vector<double>> &images, int threads);
+    // fibers > 1: each host thread runs `fibers` images at a time as a seal::FiberBatch (one stream, their
+    // rotations, relinearizations, products and rescales merged into batched launches); 0 takes
+    // MHE_RESNET_FIBERS (default 1: one image per thread)
+    std::vector<ResNetResult> infer_batch(const std::vector<std::vector<double>> &images, int threads, int fibers = 0);
     double setup_seconds() const { return setup_s_; }
     // setup breakdown: the client's planning inference (deferred keys) and the truncated-key generation
     double plan_seconds() const { return plan_s_; }

@@ -727,6 +727,21 @@ bool batched_launches();
 // word for word those of the unbatched calls.  A member that leaves (scope end, exception) is no
 // longer waited for; calls whose kinds differ within a round run one by one.
 struct LsOp;
+// (not SEAL API) FiberBatch: the same merging as Lockstep, but the members are fibers on the calling
+// host thread instead of threads: run(count, work) runs work(0) .. work(count - 1) as fibers that
+// switch only at the merge points (rotations, relinearizations, reduced-error products, rescales),
+// so every round is collected without thread wake-ups, and every member's kernels -- merged or not
+// -- go to the calling thread's one stream, in order, with no cross-stream waits.  Exceptions are
+// per fiber; the first one is rethrown once every fiber has finished.
+class FiberBatch
+{
+public:
+    struct Impl;
+    static void run(std::size_t count, const std::function<void(std::size_t)> &work,
+                    std::size_t stack_bytes = (std::size_t)8 << 20);
+    static std::size_t last_rounds();  // merged rounds of the calling thread's last run()
+    static std::size_t last_merged();  // member calls those rounds merged
+};
 class Lockstep
 {
 public:
@@ -941,6 +956,7 @@ private:
     // Lockstep: hand `op` to the calling thread's group (false: no group, run it directly)
     bool lockstep_submit(LsOp &op) const;
     friend struct Lockstep::Impl;
+    friend class FiberBatch;
     void lockstep_execute(std::vector<LsOp *> &ops) const;
     std::size_t limbs_of(const parms_id_type &id) const;
     SEALContext context_;

@@ -533,6 +533,11 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img)
 
 ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *log)
 {
+    return infer(img, log, true);
+}
+
+ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *log, bool stage_syncs)
+{
     // infer_seal.cpp:404-577 (one image).  With `log`, every stage is written as the reference's
     // *_print wrappers write it to result/resnet{L}_cifar10_image{id}.txt (cnn_seal.cpp:106-123,
     // infer_seal.cpp:408-577): "<op>...", "time : <ms> ms", "remaining level : <chain index>",
@@ -545,6 +550,9 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
     ResNetResult res;
     using clk = std::chrono::steady_clock;
     auto sync = [&] { mhe_stream_sync(m.context->engine(), m.context->stream()); };
+    auto stage_sync = [&] {
+        if (stage_syncs || log) sync();
+    };
     std::vector<Ciphertext> cipher_pool(14);
     TensorCipher cnn, temp;
     int co = 0, st = 0;
@@ -588,7 +596,7 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
     for (long i = 0; i < n; i++) image[i] /= m.B; // for boundary [-1,1]
 
     cnn = TensorCipher((int)m.logn, 1, 32, 32, 3, 3, (int)init_p, image, encryptor, encoder, m.logq);
-    sync();
+    stage_sync();
     const auto total_start = clk::now();
     double t_boot = 0, t_relu = 0;
 
@@ -623,18 +631,18 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
                                          evaluator, m.B);
     op_end("multiplexed parallel batch normalization", cnn.cipher());
     auto relu = [&] {
-        sync();
+        stage_sync();
         const auto a = clk::now();
         op_begin();
         ReLU_seal(cnn, cnn, m.comp_no, m.deg, m.alpha, m.tree, m.scaled_val, m.logp, encryptor, evaluator, decryptor,
                   encoder, m.public_key, m.secret_key, m.relin_keys, m.B);
-        sync();
+        stage_sync();
         t_relu += std::chrono::duration<double>(clk::now() - a).count();
         op_end("approximate ReLU", cnn.cipher());
         print_values();
     };
     auto bootstrap = [&](int j) {
-        sync();
+        stage_sync();
         const auto a = clk::now();
         op_begin();
         Ciphertext c = cnn.cipher(), rtn;
@@ -643,7 +651,7 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
             m.boot[j]->bootstrap_real_3(rtn, c);
         }
         cnn.set_ciphertext(std::move(rtn));
-        sync();
+        stage_sync();
         t_boot += std::chrono::duration<double>(clk::now() - a).count();
         res.bootstraps++;
         const std::string tag = "bootstrapping " + std::to_string(res.bootstraps) + " result";
@@ -731,7 +739,8 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
     return res;
 }
 
-std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vector<double>> &images, int threads)
+std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vector<double>> &images, int threads,
+                                                    int fibers)
 {
     std::vector<ResNetResult> out(images.size());
     std::atomic<std::size_t> next{ 0 };
@@ -744,15 +753,35 @@ std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vecto
         const char *e = std::getenv("MHE_RESNET_LOCKSTEP");
         return e ? std::atoi(e) : 0;
     }();
+    if (fibers <= 0)
+    {
+        const char *e = std::getenv("MHE_RESNET_FIBERS");
+        fibers = e ? std::max(1, std::atoi(e)) : 1;
+    }
     const int nthreads = std::max(1, threads);
     std::unique_ptr<seal::Lockstep> group;
-    if (lockstep && nthreads > 1) group = std::make_unique<seal::Lockstep>((std::size_t)nthreads);
+    if (lockstep && nthreads > 1 && fibers <= 1) group = std::make_unique<seal::Lockstep>((std::size_t)nthreads);
+    std::atomic<std::size_t> fb_rounds{ 0 }, fb_merged{ 0 };
     auto work = [&] {
         std::unique_ptr<seal::Lockstep::Member> member;
         if (group) member = std::make_unique<seal::Lockstep::Member>(*group, lockstep == 1);
         try
         {
-            for (std::size_t i; (i = next.fetch_add(1)) < images.size();) out[i] = infer(images[i]);
+            if (fibers > 1)
+            {
+                // `fibers` images at a time on this thread as one FiberBatch
+                for (;;)
+                {
+                    const std::size_t i0 = next.fetch_add((std::size_t)fibers);
+                    if (i0 >= images.size()) break;
+                    const std::size_t cnt = std::min<std::size_t>((std::size_t)fibers, images.size() - i0);
+                    seal::FiberBatch::run(cnt, [&](std::size_t k) { out[i0 + k] = infer(images[i0 + k], nullptr, false); });
+                    fb_rounds += seal::FiberBatch::last_rounds();
+                    fb_merged += seal::FiberBatch::last_merged();
+                }
+            }
+            else
+                for (std::size_t i; (i = next.fetch_add(1)) < images.size();) out[i] = infer(images[i]);
         }
         catch (...)
         {
@@ -765,6 +794,9 @@ std::vector<ResNetResult> ResNetRunner::infer_batch(const std::vector<std::vecto
     for (auto &t : pool) t.join();
     if (group && std::getenv("MHE_RESNET_LOCKSTEP_STATS"))
         std::fprintf(stderr, "lockstep: %zu rounds, %zu member calls merged\n", group->rounds(), group->merged_calls());
+    if (fibers > 1 && std::getenv("MHE_RESNET_LOCKSTEP_STATS"))
+        std::fprintf(stderr, "fibers: %d per thread, %zu rounds, %zu member calls merged\n", fibers, fb_rounds.load(),
+                     fb_merged.load());
     if (err) std::rethrow_exception(err);
     return out;
 }

@@ -28,6 +28,8 @@
 #include <thread>
 #include <unordered_map>
 
+#include <ucontext.h>
+
 namespace seal
 {
 namespace
@@ -93,6 +95,8 @@ namespace
 thread_local Lockstep::Impl *tl_ls = nullptr;        // the calling thread's group, while merging
 thread_local Lockstep::Impl *tl_ls_member = nullptr; // the group the thread is a member of
 thread_local int tl_ls_direct = 0;            // > 0 inside a round's execution: calls run directly
+thread_local FiberBatch::Impl *tl_fb = nullptr; // the FiberBatch running on this thread
+bool fiber_merging(); // inside a FiberBatch fiber (defined with FiberBatch::Impl)
 struct LsDirect
 {
     LsDirect() { ++tl_ls_direct; }
@@ -1818,7 +1822,7 @@ void Evaluator::switch_key(Ciphertext &encrypted, const std::uint64_t *target, c
 
 void Evaluator::relinearize_inplace(Ciphertext &encrypted, const RelinKeys &relin_keys, MemoryPoolHandle) const
 {
-    if (tl_ls)
+    if (tl_ls || fiber_merging())
     {
         LsOp op;
         op.kind = LsOp::RELIN;
@@ -1983,7 +1987,7 @@ void Evaluator::rescale_to_next(const Ciphertext &encrypted, Ciphertext &destina
 
 void Evaluator::rescale_to_next_inplace(Ciphertext &encrypted, MemoryPoolHandle) const
 {
-    if (tl_ls)
+    if (tl_ls || fiber_merging())
     {
         LsOp op;
         op.kind = LsOp::RESC;
@@ -2162,7 +2166,7 @@ void Evaluator::rotate_internal(Ciphertext &encrypted, int steps, const GaloisKe
 void Evaluator::rotate_vector_inplace(Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                                       MemoryPoolHandle) const
 {
-    if (tl_ls)
+    if (tl_ls || fiber_merging())
     {
         LsOp op;
         op.kind = LsOp::ROT;
@@ -2201,7 +2205,7 @@ void Evaluator::apply_galois_to(const Ciphertext &encrypted, std::uint32_t galoi
 void Evaluator::rotate_vector(const Ciphertext &encrypted, int steps, const GaloisKeys &galois_keys,
                               Ciphertext &destination, MemoryPoolHandle) const
 {
-    if (tl_ls)
+    if (tl_ls || fiber_merging())
     {
         LsOp op;
         op.kind = LsOp::ROT;
@@ -2253,6 +2257,173 @@ struct Lockstep::Impl
     }
 };
 
+// ------------------------------------------------------------------------------ FiberBatch
+struct FiberBatch::Impl
+{
+    struct Fiber
+    {
+        ucontext_t ctx{};
+        std::unique_ptr<char[]> stack;
+        std::size_t idx = 0;
+        bool done = false, blocked = false;
+        std::exception_ptr err;
+    };
+    ucontext_t sched{};
+    std::vector<Fiber> fibers;
+    Fiber *current = nullptr;
+    std::vector<LsOp *> pending;
+    // elementwise engine launches parked by the fibers (mhe_set_launch_hook): one per fiber per round
+    std::vector<std::pair<mhe_ctx *, mhe_launch *>> launches;
+    std::size_t launch_rounds = 0, launches_merged = 0;
+    const std::function<void(std::size_t)> *work = nullptr;
+    std::size_t rounds = 0, merged = 0;
+
+    // makecontext passes int arguments: the group pointer in two halves
+    static void entry(unsigned lo, unsigned hi)
+    {
+        Impl *g = reinterpret_cast<Impl *>(((std::uintptr_t)hi << 32) | (std::uintptr_t)lo);
+        Fiber *f = g->current;
+        try
+        {
+            (*g->work)(f->idx);
+        }
+        catch (...)
+        {
+            f->err = std::current_exception();
+        }
+        f->done = true; // returns to uc_link = the scheduler
+    }
+    // fiber i's context: its own stack, entry(), back to the scheduler at the end
+    __attribute__((noinline)) void init(std::size_t i, std::size_t stack_bytes)
+    {
+        Fiber &f = fibers[i];
+        f.idx = i;
+        f.stack.reset(new char[stack_bytes]);
+        if (getcontext(&f.ctx) != 0) throw std::runtime_error("FiberBatch: getcontext failed");
+        f.ctx.uc_stack.ss_sp = f.stack.get();
+        f.ctx.uc_stack.ss_size = stack_bytes;
+        f.ctx.uc_link = &sched;
+        const std::uintptr_t self = reinterpret_cast<std::uintptr_t>(this);
+        makecontext(&f.ctx, reinterpret_cast<void (*)()>(&Impl::entry), 2, (unsigned)(self & 0xFFFFFFFFu),
+                    (unsigned)(self >> 32));
+    }
+    // the calling fiber's merge point: park `op` for the round and yield to the scheduler
+    void submit(LsOp &op)
+    {
+        Fiber *f = current;
+        pending.push_back(&op);
+        f->blocked = true;
+        swapcontext(&f->ctx, &sched);
+    }
+    // the engine's launch hook: inside a fiber the launch is parked for the round (the same-numbered
+    // elementwise launches of the fibers run as one batched launch); elsewhere it runs now
+    static void launch_hook(mhe_ctx *ctx, mhe_launch *l, void *user)
+    {
+        Impl *g = static_cast<Impl *>(user);
+        if (!g->current || tl_ls_direct > 0)
+        {
+            mhe_launch *one[1] = { l };
+            mhe_launch_run(ctx, one, 1);
+            return;
+        }
+        Fiber *f = g->current;
+        g->launches.push_back({ ctx, l });
+        f->blocked = true;
+        swapcontext(&f->ctx, &g->sched);
+    }
+    // one round's parked launches, grouped by context (mhe_launch_run batches equal shapes)
+    void run_launches()
+    {
+        while (!launches.empty())
+        {
+            mhe_ctx *ctx = launches.front().first;
+            std::vector<mhe_launch *> ls;
+            std::vector<std::pair<mhe_ctx *, mhe_launch *>> rest;
+            for (auto &p : launches) (p.first == ctx ? (void)ls.push_back(p.second) : rest.push_back(p));
+            mhe_launch_run(ctx, ls.data(), (int)ls.size());
+            launch_rounds++;
+            if (ls.size() > 1) launches_merged += ls.size();
+            launches.swap(rest);
+        }
+    }
+};
+
+namespace
+{
+thread_local std::size_t tl_fb_rounds = 0, tl_fb_merged = 0;
+bool fiber_merging()
+{
+    return tl_fb && tl_fb->current;
+}
+} // namespace
+
+void FiberBatch::run(std::size_t count, const std::function<void(std::size_t)> &work, std::size_t stack_bytes)
+{
+    if (tl_fb) throw std::logic_error("FiberBatch::run: already inside a fiber batch");
+    Impl g;
+    g.work = &work;
+    g.fibers.resize(count);
+    for (std::size_t i = 0; i < count; i++) g.init(i, stack_bytes);
+    tl_fb = &g;
+    mhe_set_launch_hook(&Impl::launch_hook, &g);
+    struct Reset
+    {
+        ~Reset()
+        {
+            mhe_set_launch_hook(nullptr, nullptr);
+            tl_fb = nullptr;
+        }
+    } reset;
+    for (;;)
+    {
+        // every runnable fiber runs to its next merge point (or its end)
+        bool ran = false;
+        for (auto &f : g.fibers)
+            if (!f.done && !f.blocked)
+            {
+                ran = true;
+                g.current = &f;
+                swapcontext(&g.sched, &f.ctx);
+                g.current = nullptr;
+            }
+        if (!g.pending.empty() || !g.launches.empty())
+        {
+            // one round: the parked elementwise launches as batched launches, the parked evaluator
+            // calls as one merged call (lockstep_execute), then every parked fiber resumes with its
+            // result or its own error (the fibers' data are independent, so the order is free)
+            g.run_launches();
+            if (!g.pending.empty())
+            {
+                std::vector<LsOp *> batch;
+                batch.swap(g.pending);
+                {
+                    LsDirect d;
+                    batch[0]->ev->lockstep_execute(batch);
+                }
+                g.rounds++;
+                if (batch.size() > 1) g.merged += batch.size();
+            }
+            for (auto &f : g.fibers) f.blocked = false;
+            continue;
+        }
+        if (!ran) break; // every fiber finished
+    }
+    tl_fb_rounds = g.rounds + g.launch_rounds;
+    tl_fb_merged = g.merged + g.launches_merged;
+    for (auto &f : g.fibers)
+        if (f.err) std::rethrow_exception(f.err);
+}
+
+std::size_t FiberBatch::last_rounds()
+{
+    return tl_fb_rounds;
+}
+
+std::size_t FiberBatch::last_merged()
+{
+    return tl_fb_merged;
+}
+
 Lockstep::Lockstep(std::size_t members) : impl_(std::make_unique<Impl>(members)) {}
 Lockstep::~Lockstep() = default;
 std::size_t Lockstep::rounds() const
@@ -2282,8 +2453,16 @@ Lockstep::Member::~Member()
 
 bool Evaluator::lockstep_submit(LsOp &op) const
 {
+    if (tl_ls_direct > 0 || trace::enabled()) return false;
+    if (fiber_merging())
+    {
+        op.ev = this;
+        tl_fb->submit(op);
+        if (op.err) std::rethrow_exception(op.err);
+        return true;
+    }
     Lockstep::Impl *g = tl_ls;
-    if (!g || tl_ls_direct > 0 || trace::enabled()) return false;
+    if (!g) return false;
     op.ev = this;
     g->core.submit(&op, Lockstep::Impl::execute);
     if (op.err) std::rethrow_exception(op.err);
@@ -2382,7 +2561,7 @@ void Evaluator::lockstep_execute(std::vector<LsOp *> &ops) const
 void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted, const std::vector<int> &steps,
                                const GaloisKeys &galois_keys, const std::vector<Ciphertext *> &destinations) const
 {
-    if (tl_ls)
+    if (tl_ls || fiber_merging())
     {
         LsOp op;
         op.kind = LsOp::ROT;
@@ -3007,7 +3186,7 @@ void Evaluator::sub_inplace_reduced_error(Ciphertext &encrypted1, const Cipherte
 void Evaluator::multiply_inplace_reduced_error(Ciphertext &encrypted1, const Ciphertext &encrypted2,
                                                const RelinKeys &relin_keys) const
 {
-    if (tl_ls)
+    if (tl_ls || fiber_merging())
     {
         LsOp op;
         op.kind = LsOp::MULRE;

@@ -92,6 +92,36 @@ int mhe_key_traffic_prepared(mhe_ctx *ctx, uint64_t *bytes, int reset);
 #define MHE_OPK_NTT 6      /* forward or inverse NTT (encode, decode, transform_to/from_ntt) */
 #define MHE_OPK_GALOIS 7   /* NTT-domain Galois permutation */
 int mhe_op_counts(mhe_ctx *ctx, int kind, uint64_t *counts, int levels, int reset);
+
+/* ---- launch coalescing (no SEAL counterpart) ----------------------------------------------------
+ * With a hook set on the calling thread, the elementwise entry points mhe_add, mhe_sub, mhe_negate,
+ * mhe_multiply_plain, mhe_multiply_plain_add, mhe_multiply_scalar, mhe_add_scalar, mhe_set_scalar,
+ * mhe_ct_multiply, mhe_ct_square and mhe_memcpy_d2d check their arguments, then hand a descriptor of
+ * their launch to the hook instead of launching.  The hook must get it run -- by mhe_launch_run,
+ * alone or together with other descriptors -- and return; the entry point then returns l->rc.
+ * mhe_launch_run runs descriptors of one context: entries of the same kind and shape (and scalars)
+ * as one batched launch of up to 8, the rest one by one; each gets its rc.  seal::FiberBatch uses this
+ * to turn the same-numbered elementwise calls of its fibers (the images of a batch) into one launch. */
+#define MHE_LK_ADDSUB 1       /* op: 0 add, 1 sub, 2 negate */
+#define MHE_LK_MULPLAIN 2
+#define MHE_LK_MULPLAIN_ADD 3 /* out is the accumulator */
+#define MHE_LK_SCALAR 4       /* op: 0 multiply, 1 add, 2 set; scalars per limb */
+#define MHE_LK_TENSOR 5       /* op: 1 square (b unused); out gets 3 polys */
+#define MHE_LK_COPY 6         /* bytes */
+typedef struct mhe_launch
+{
+    int kind, op;
+    const uint64_t *a, *b;
+    uint64_t *out;
+    int polys, limbs;
+    size_t bytes;
+    uint64_t scalars[64];
+    void *stream;
+    int rc;
+} mhe_launch;
+typedef void (*mhe_launch_hook)(mhe_ctx *ctx, mhe_launch *launch, void *user);
+int mhe_set_launch_hook(mhe_launch_hook hook, void *user); /* the calling thread's hook; NULL = off */
+int mhe_launch_run(mhe_ctx *ctx, mhe_launch *const *launches, int count);
 /* A non-blocking HIP stream on the context's device (and its scratch workspace); the SEAL
  * shim gives every host thread its own, as the reference's OpenMP threads share one
  * Evaluator (cnn/infer_seal.cpp:404). */

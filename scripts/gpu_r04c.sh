@@ -3,4 +3,4 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_trace_parity.py tests/test_seal_api.py tests/test_gpu_batch.py::test_seal_surface_batches_equal_one_by_one -m gpu -x -v -s --timeout 800 --timeout-method thread > gpurun_out/r04c_trace.log 2>&1 || exit $?
+timeout -k 10 900 python -u -m pytest tests/test_trace_parity.py tests/test_seal_api.py -m gpu -x -v -s --timeout 800 --timeout-method thread > gpurun_out/r04c_trace.log 2>&1 || exit $?

@@ -216,6 +216,44 @@ int main(int argc, char **argv)
             std::printf("lockstep: %zu rounds, %zu member calls merged\n", group.rounds(), group.merged_calls());
             check("Lockstep group (4 threads; rotations, relinearizations, products, rescales merged) == each alone",
                   ok && group.merged_calls() > 0);
+
+            // the same members as a FiberBatch on this thread (one stream, no thread wake-ups),
+            // including a fiber that throws half way: the others finish with the same words and the
+            // error comes back from run()
+            std::vector<std::vector<Ciphertext>> fibered(M);
+            FiberBatch::run(M, [&](std::size_t m) { sequence((int)m, fibered[m]); });
+            ok = true;
+            for (int m = 0; m < M; m++)
+            {
+                ok = ok && alone[m].size() == fibered[m].size();
+                for (std::size_t i = 0; ok && i < alone[m].size(); i++) ok = same(alone[m][i], fibered[m][i]);
+            }
+            std::printf("fibers: %zu rounds, %zu member calls merged\n", FiberBatch::last_rounds(),
+                        FiberBatch::last_merged());
+            check("FiberBatch (4 fibers on one thread; the same merges) == each alone", ok && FiberBatch::last_merged() > 0);
+            std::vector<std::vector<Ciphertext>> part(M);
+            bool fb_threw = false;
+            try
+            {
+                FiberBatch::run(M, [&](std::size_t m) {
+                    if (m == 2)
+                    {
+                        Ciphertext x = x0[m], r;
+                        ev.rotate_vector(x, 1, glk, r);
+                        throw std::runtime_error("fiber 2 fails");
+                    }
+                    sequence((int)m, part[m]);
+                });
+            }
+            catch (const std::runtime_error &e)
+            {
+                fb_threw = std::string(e.what()) == "fiber 2 fails";
+            }
+            ok = fb_threw;
+            for (int m = 0; m < M; m++)
+                if (m != 2)
+                    for (std::size_t i = 0; ok && i < alone[m].size(); i++) ok = same(alone[m][i], part[m][i]);
+            check("FiberBatch: a fiber's exception comes back from run(), the other fibers' words unchanged", ok);
         }
 
         bool threw = false;
