@@ -246,7 +246,7 @@ def resnet_cpu_estimate(ops, threads):
 RESNET20_CPU_S = 2188.8  # reference CPU SEAL, s/image, 1 thread per image (BASELINE.md / SURVEY.md §6)
 
 
-def resnet_leg(device, images, streams, layers=20):
+def resnet_leg(device, images, streams, layers=20, fibers=1):
     """Second half of BASELINE.json's metric: seconds per image of encrypted ResNet-20 CIFAR-10
     (config C3: multiplexed conv + approximate ReLU + 18 bootstraps at N=2^16; config C4's network
     with layers=110), through the runner's C ABI (include/mhe_resnet_capi.h) in this process, with
@@ -292,7 +292,7 @@ def resnet_leg(device, images, streams, layers=20):
     if world > 1:
         dist.barrier()
     t2 = time.perf_counter()
-    batch = runner.infer_batch(imgs, streams)
+    batch = runner.infer_batch(imgs, streams, fibers)
     batch_wall = time.perf_counter() - t2
     # every image's decrypted logits against the plain network (exact ReLU), on every rank -- the
     # keys there may have arrived over RCCL; a miss fails the leg
@@ -312,6 +312,9 @@ def resnet_leg(device, images, streams, layers=20):
         "batch_wall_s": round(batch_wall, 4),
         "batch_images": images,
         "streams": streams,
+        "fibers_per_stream": fibers,
+        "batch_mode": (f"{streams} host threads x {fibers} images as one seal::FiberBatch each (merged key switches, "
+                       "rescales and elementwise launches)" if fibers > 1 else f"{streams} host threads, one image each"),
         "setup_s": round(setup, 2),
         "galois_keys": info["galois_keys"],
         "galois_key_GB_resident": round(info["galois_key_gb"], 2),
@@ -519,7 +522,9 @@ def main():
     ap.add_argument("--resnet-layers", type=int, default=20, choices=(20, 110),
                     help="20: config C3 (ResNet-20); 110: config C4's network (ResNet-110, one image per GPU "
                          "with --resnet-images 1 --resnet-streams 1)")
-    ap.add_argument("--resnet-streams", type=int, default=4, help="images in flight per GPU (one stream each)")
+    ap.add_argument("--resnet-streams", type=int, default=4, help="host threads for the ResNet batch (one stream each)")
+    ap.add_argument("--resnet-fibers", type=int, default=1,
+                    help="images per host thread at a time as one seal::FiberBatch (1 = one image per thread)")
     ap.add_argument("--c4", choices=("auto", "on", "off"), default="auto",
                     help="config C4 leg (ResNet-110, one image per GPU on the shared key set); auto = when N > 1")
     ap.add_argument("--key-format", choices=("prepared", "seal"), default="prepared",
@@ -729,11 +734,11 @@ def main():
     torch.cuda.empty_cache()
     legs = []
     if args.resnet_images > 0:
-        legs.append((args.resnet_layers, args.resnet_images, args.resnet_streams))
+        legs.append((args.resnet_layers, args.resnet_images, args.resnet_streams, args.resnet_fibers))
     if args.c4 == "on" or (args.c4 == "auto" and world > 1):
-        legs.append((110, 1, 1))  # config C4: ResNet-110, one image per GPU, shared key set
-    for layers, images, streams in legs:
-        r = resnet_leg(local, images, streams, layers)
+        legs.append((110, 1, 1, 1))  # config C4: ResNet-110, one image per GPU, shared key set
+    for layers, images, streams, fibers in legs:
+        r = resnet_leg(local, images, streams, layers, fibers)
         t = torch.tensor([r["batch_wall_s"], r["sec_per_image_1stream"]], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -38,6 +38,7 @@ def seal_lib():
             "mhe_resnet_key_import": (i32, [vp, i32, u64, u64, u64, vp]),
             "mhe_resnet_finish_import": (i32, [vp]),
             "mhe_resnet_infer_batch": (i32, [vp, dp, i32, i32, dp, ip, dp, dp, dp, dp]),
+            "mhe_resnet_infer_batch_fibers": (i32, [vp, dp, i32, i32, i32, dp, ip, dp, dp, dp, dp]),
             "mhe_resnet_info": (i32, [vp, dp, dp, ip]),
             "mhe_resnet_key_traffic": (i32, [vp, dp, i32]),
             "mhe_resnet_op_counts": (i32, [vp, i32, u64p, i32]),
@@ -99,8 +100,9 @@ class Runner:
         _check(seal_lib().mhe_resnet_finish_import(self._h))
 
     # ------------------------------------------------------------------ inference
-    def infer_batch(self, images, threads):
-        """images: [B][3072] doubles -> dict(logits [B][10], labels [B], seconds, boot, relu, wall)."""
+    def infer_batch(self, images, threads, fibers=0):
+        """images: [B][3072] doubles -> dict(logits [B][10], labels [B], seconds, boot, relu, wall).
+        fibers > 1: that many images per host thread at a time as one seal::FiberBatch."""
         imgs = np.ascontiguousarray(images, dtype=np.float64)
         B = imgs.shape[0]
         logits = np.zeros((B, 10))
@@ -108,8 +110,8 @@ class Runner:
         sec, boot, relu = np.zeros(B), np.zeros(B), np.zeros(B)
         wall = ctypes.c_double()
         dp = ctypes.POINTER(ctypes.c_double)
-        _check(seal_lib().mhe_resnet_infer_batch(
-            self._h, imgs.ctypes.data_as(dp), B, threads, logits.ctypes.data_as(dp),
+        _check(seal_lib().mhe_resnet_infer_batch_fibers(
+            self._h, imgs.ctypes.data_as(dp), B, threads, fibers, logits.ctypes.data_as(dp),
             labels.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), sec.ctypes.data_as(dp), boot.ctypes.data_as(dp),
             relu.ctypes.data_as(dp), ctypes.byref(wall)))
         return {"logits": logits, "labels": labels, "seconds": sec, "boot": boot, "relu": relu, "wall": wall.value}

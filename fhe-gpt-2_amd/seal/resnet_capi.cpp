@@ -117,11 +117,17 @@ int mhe_resnet_finish_import(mhe_resnet *r)
 int mhe_resnet_infer_batch(mhe_resnet *r, const double *images, int count, int threads, double *logits, int *labels,
                            double *seconds, double *boot, double *relu, double *wall)
 {
+    return mhe_resnet_infer_batch_fibers(r, images, count, threads, 0, logits, labels, seconds, boot, relu, wall);
+}
+
+int mhe_resnet_infer_batch_fibers(mhe_resnet *r, const double *images, int count, int threads, int fibers,
+                                  double *logits, int *labels, double *seconds, double *boot, double *relu, double *wall)
+{
     return guard([&] {
         std::vector<std::vector<double>> imgs((std::size_t)count);
         for (int i = 0; i < count; i++) imgs[i].assign(images + (std::size_t)i * 3072, images + (std::size_t)(i + 1) * 3072);
         const auto t0 = std::chrono::steady_clock::now();
-        auto res = r->runner->infer_batch(imgs, threads);
+        auto res = r->runner->infer_batch(imgs, threads, fibers);
         if (wall) *wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int i = 0; i < count; i++)
         {

@@ -40,6 +40,11 @@ int mhe_resnet_finish_import(mhe_resnet *runner);
  * wall: the whole batch. */
 int mhe_resnet_infer_batch(mhe_resnet *runner, const double *images, int count, int threads, double *logits,
                            int *labels, double *seconds, double *boot, double *relu, double *wall);
+/* The same with `fibers` images per host thread at a time as one seal::FiberBatch (their key
+ * switches, rescales and elementwise launches merged; boot / relu times are then not measured);
+ * fibers 0 = MHE_RESNET_FIBERS (default 1, one image per thread). */
+int mhe_resnet_infer_batch_fibers(mhe_resnet *runner, const double *images, int count, int threads, int fibers,
+                                  double *logits, int *labels, double *seconds, double *boot, double *relu, double *wall);
 int mhe_resnet_info(mhe_resnet *runner, double *setup_s, double *galois_key_gb, int *galois_keys);
 /* key-switching key bytes the runner's key switches streamed since the last reset (reset != 0 zeroes) */
 int mhe_resnet_key_traffic(mhe_resnet *runner, double *bytes, int reset);
