@@ -517,13 +517,13 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host cores for the CPU baseline (16 = one GPU's share of the box's CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--resnet-images", type=int, default=4,
+    ap.add_argument("--resnet-images", type=int, default=8,
                     help="ResNet-20 CIFAR-10 images per GPU for the sec/image leg (0 = skip)")
     ap.add_argument("--resnet-layers", type=int, default=20, choices=(20, 110),
                     help="20: config C3 (ResNet-20); 110: config C4's network (ResNet-110, one image per GPU "
                          "with --resnet-images 1 --resnet-streams 1)")
-    ap.add_argument("--resnet-streams", type=int, default=4, help="host threads for the ResNet batch (one stream each)")
-    ap.add_argument("--resnet-fibers", type=int, default=1,
+    ap.add_argument("--resnet-streams", type=int, default=2, help="host threads for the ResNet batch (one stream each)")
+    ap.add_argument("--resnet-fibers", type=int, default=4,
                     help="images per host thread at a time as one seal::FiberBatch (1 = one image per thread)")
     ap.add_argument("--c4", choices=("auto", "on", "off"), default="auto",
                     help="config C4 leg (ResNet-110, one image per GPU on the shared key set); auto = when N > 1")

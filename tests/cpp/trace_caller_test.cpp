@@ -9,10 +9,15 @@
 // n; then [digits][2][limbs][n] in SEAL's layout, the special prime last).
 //   trace_caller_test <log N: 12 | 16> <dir> <comp_dir>
 //   trace_caller_test <log N> <dir> <comp_dir> boot <logn>
+//   trace_caller_test <log N> <dir> <comp_dir> layers
 // The boot mode traces one sparse bootstrap_real_3 instead (Bootstrapper.cpp:3166-3236 with
 // ModularReducer.cpp:61-80 and Polynomial.cpp:256-560): the ResNet chain {51} + 16 x {46} + 14 x
 // {51} + {51}, loge 10, K 25, cosine degree 59, 2 double-angle steps, inverse_deg 1, logn slots;
 // modraise, subsum, CoeffToSlot BSGS, EvalMod and SlotToCoeff all land in the trace.
+// The layers mode traces the remaining ResNet layers in network order (cnn/infer_seal.cpp:
+// 520-560): a stride-2 downsampling (cnn_seal.cpp:610-679), the residual add with a second tensor of
+// the downsampled shape (:593-609), the average pooling (:680-746) and the fully connected layer
+// (:747-787).
 #include "mhe_boot.h"
 #include "mhe_cnn.h"
 #include "mhe_comp.h"
@@ -117,11 +122,88 @@ static int run_boot(int logN, const std::string &dir, long logn)
     return err < 1e-2 ? 0 : 1;
 }
 
+// downsampling -> residual add -> average pooling -> FC under the trace (see the header)
+static int run_layers(int logN, const std::string &dir)
+{
+    const std::size_t N = (std::size_t)1 << logN;
+    std::vector<int> bits{ 51 };
+    for (int i = 0; i < 8; i++) bits.push_back(46);
+    bits.push_back(51);
+    EncryptionParameters parms(scheme_type::ckks);
+    parms.set_poly_modulus_degree(N);
+    parms.set_coeff_modulus(CoeffModulus::Create(N, bits));
+    parms.set_secret_key_hamming_weight(logN >= 16 ? 192 : 64);
+    parms.set_random_generator(
+        std::make_shared<Blake2xbPRNGFactory>(std::array<std::uint64_t, 8>{ 1, 2, 3, 4, 5, 6, 7, 8 }));
+    SEALContext ctx(parms, true, sec_level_type::none);
+    KeyGenerator keygen(ctx);
+    PublicKey pk;
+    keygen.create_public_key(pk);
+    RelinKeys rlk;
+    keygen.create_relin_keys(rlk);
+    GaloisKeys glk;
+    keygen.create_deferred_galois_keys(glk);
+    CKKSEncoder encoder(ctx);
+    Encryptor encryptor(ctx, pk);
+    Decryptor decryptor(ctx, keygen.secret_key());
+    Evaluator evaluator(ctx, encoder);
+    const int logn = logN - 1;
+    const long n = 1L << logn;
+    // ResNet-20's first downsampling at N = 2^16 (k 1, h = w = 32, c = t = 16, p = 2), scaled down to
+    // h = w = 8, c = t = 8 at N = 2^12; downsampled to k 2, h / 2, 2c, t / 2
+    const int h = logN >= 16 ? 32 : 8, c = logN >= 16 ? 16 : 8, t = c, p = (int)(n / (h * h * t));
+    std::mt19937_64 g(20261019);
+    std::uniform_real_distribution<double> U(-1.0, 1.0);
+    std::vector<double> img(n, 0.0);
+    for (int r = 0; r < p; r++)
+        for (int i = 0; i < c * h * h; i++) img[(std::size_t)r * (n / p) + i] = 0.5 * U(g);
+    TensorCipher in(logn, 1, h, h, c, t, p, img, encryptor, encoder, 46);
+    Ciphertext ct = in.cipher();
+    while (ct.coeff_modulus_size() > 6) evaluator.mod_switch_to_next_inplace(ct);
+    in.set_ciphertext(ct);
+    TensorCipher ds;
+    multiplexed_parallel_downsampling_seal(in, ds, evaluator, glk);
+    // the residual branch: a fresh tensor of the downsampled shape at its level
+    std::vector<double> img2(n, 0.0);
+    const long blk = (long)ds.k() * ds.k() * ds.h() * ds.w() * ds.t();
+    for (int r = 0; r < ds.p(); r++)
+        for (long i = 0; i < blk; i++) img2[(std::size_t)r * (n / ds.p()) + i] = 0.25 * U(g);
+    TensorCipher res(logn, ds.k(), ds.h(), ds.w(), ds.c(), ds.t(), ds.p(), img2, encryptor, encoder, 46);
+    Ciphertext rc = res.cipher();
+    evaluator.mod_switch_to_inplace(rc, ds.cipher().parms_id());
+    res.set_ciphertext(rc);
+    TensorCipher sum;
+    cnn_add_seal(ds, res, sum, evaluator);
+    TensorCipher pooled, logits;
+    std::ofstream devnull;
+    averagepooling_seal_scale(sum, pooled, evaluator, glk, 1.0, encoder, decryptor, devnull);
+    const int q = 10, r = pooled.c();
+    std::vector<double> fc(q * r), bias(q);
+    for (auto &v : fc) v = 0.5 * U(g);
+    for (auto &v : bias) v = 0.1 * U(g);
+    matrix_multiplication_seal(pooled, logits, fc, bias, q, r, evaluator, glk);
+    Plaintext dp;
+    decryptor.decrypt(logits.cipher(), dp);
+    std::vector<double> got;
+    encoder.decode(dp, got);
+    // the layers' semantics are checked end to end by the ResNet runner against the plain network
+    // (resnet_test / test_resnet.py); here only that the logits decrypt to bounded values
+    double mag = 0;
+    for (int i = 0; i < q; i++) mag = std::max(mag, std::fabs(got[i]));
+    std::printf("layers (N 2^%d): downsample %dx%dx%d -> %dx%dx%d, add, avgpool, fc %dx%d: %zu limbs left, "
+                "max |logit| %.3g\n",
+                logN, h, h, c, ds.h(), ds.w(), ds.c(), q, r, logits.cipher().coeff_modulus_size(), mag);
+    if (!(mag < 100.0)) return 1;
+    write_keys(dir, rlk, glk, N);
+    write_meta(dir, ctx, logN);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 4)
     {
-        std::fprintf(stderr, "usage: trace_caller_test <log N> <dir> <comp_dir> [boot <logn>]\n");
+        std::fprintf(stderr, "usage: trace_caller_test <log N> <dir> <comp_dir> [boot <logn> | layers]\n");
         return 2;
     }
     const int logN = std::atoi(argv[1]);
@@ -129,6 +211,7 @@ int main(int argc, char **argv)
     setenv("MHE_EVAL_TRACE", dir.c_str(), 1); // before the first evaluator operation
     setenv("MHE_COMP_DIR", argv[3], 1);
     if (argc > 5 && std::string(argv[4]) == "boot") return run_boot(logN, dir, std::atol(argv[5]));
+    if (argc > 4 && std::string(argv[4]) == "layers") return run_layers(logN, dir);
     const std::size_t N = (std::size_t)1 << logN;
     // {51} + 8 x {46} + {51}: the ResNet chain's shape (cnn/infer_seal.cpp:288-316), shortened; 2^46 scale
     std::vector<int> bits{ 51 };

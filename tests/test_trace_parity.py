@@ -57,3 +57,23 @@ def test_sparse_bootstrap_matches_oracle(tmp_path, log_n, logn):
     for op in ("modraise", "ntt_inv", "ntt_fwd", "rotate", "galois", "encode_for", "multiply_plain",
                "multiply_plain_add", "rescale", "mul_re", "add_re", "add_const", "multiply_const"):
         assert counts.get(op, 0) > 0, f"{op} not exercised: {counts}"
+
+
+@pytest.mark.parametrize("log_n", [12, 16])
+def test_downsample_add_avgpool_fc_match_oracle(tmp_path, log_n):
+    """The ResNet layers the conv / BN / ReLU trace does not reach, in network order
+    (cnn/infer_seal.cpp:520-560): multiplexed_parallel_downsampling_seal (cnn/cnn_seal.cpp:610-679),
+    cnn_add_seal (:593-609), averagepooling_seal_scale (:680-746) and matrix_multiplication_seal
+    (:747-787) -- every operation word for word and scale for scale against the oracle."""
+    d = tmp_path / f"layers{log_n}"
+    d.mkdir()
+    exe = os.path.join(ROOT, "build", "trace_caller_test")
+    r = subprocess.run([exe, str(log_n), str(d), os.path.join(ROOT, "tests", "golden", "comp"), "layers"],
+                       capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rp = Replayer(str(d))
+    checked, counts = rp.replay()
+    print(f"N=2^{log_n}: {checked} layer operations match the oracle: {counts}")
+    for op in ("rotate", "multiply_plain", "add_re", "rescale", "encode_for"):
+        assert counts.get(op, 0) > 0, f"{op} not exercised: {counts}"
