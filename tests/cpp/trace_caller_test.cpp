@@ -168,10 +168,13 @@ static int run_layers(int logN, const std::string &dir)
     const long blk = (long)ds.k() * ds.k() * ds.h() * ds.w() * ds.t();
     for (int r = 0; r < ds.p(); r++)
         for (long i = 0; i < blk; i++) img2[(std::size_t)r * (n / ds.p()) + i] = 0.25 * U(g);
-    TensorCipher res(logn, ds.k(), ds.h(), ds.w(), ds.c(), ds.t(), ds.p(), img2, encryptor, encoder, 46);
-    Ciphertext rc = res.cipher();
+    // (the data constructor takes k = 1 only, as the reference's: encrypt the k = 2 layout directly)
+    Plaintext p2;
+    encoder.encode(img2, std::pow(2.0, 46), p2);
+    Ciphertext rc;
+    encryptor.encrypt(p2, rc);
     evaluator.mod_switch_to_inplace(rc, ds.cipher().parms_id());
-    res.set_ciphertext(rc);
+    TensorCipher res(logn, ds.k(), ds.h(), ds.w(), ds.c(), ds.t(), ds.p(), rc);
     TensorCipher sum;
     cnn_add_seal(ds, res, sum, evaluator);
     TensorCipher pooled, logits;
