@@ -44,6 +44,9 @@ SIGNATURES = {
                                               vp]),
     "mhe_key_traffic": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_op_counts": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int]),
+    # launch hook (seal::FiberBatch coalesces elementwise launches through it; Python never sets one)
+    "mhe_set_launch_hook": (ctypes.c_int, [vp, vp]),
+    "mhe_launch_run": (ctypes.c_int, [vp, vp, ctypes.c_int]),
     "mhe_key_prepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_unprepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_is_prepared": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), vp]),
