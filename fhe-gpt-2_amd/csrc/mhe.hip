@@ -24,6 +24,7 @@
 #include "../../include/mhe.h"
 #include "arith.h"
 #include "ntt.h"
+#include "hoist.h"
 
 #define MHE_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -183,6 +184,13 @@ struct Workspace
     u64 *acc = nullptr;
     u64 *tmp = nullptr;   // [L][n]        permuted c1 for Galois
     u64 *ct3 = nullptr;   // [3][L][n]     tensor output for hmult
+    // hoisted rotations (hoist.h): the ModUp of up to MHE_MAXB inputs, [K][K-1][n] each, and one
+    // zero-coefficient flag per input
+    u64 *hoist_base = nullptr;
+    int hoist_entries = 0;
+    u64 *hoist[MHE_MAXB] = {};
+    u64 *hacc[MHE_MAXB * MHE_HOIST_R] = {}; // [2][K][n] key products of each hoisted rotation
+    int *flags = nullptr;
     // kernel timing (mhe_ctx_set_timing): event pairs recorded around the two dominant
     // key-switch kernels on this stream, read back by mhe_kernel_time
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
@@ -229,6 +237,10 @@ struct mhe_ctx
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
     int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
+    int ks_hoist = 1; // batched rotations of one input share its ModUp (hoist.h; MHE_KS_HOIST=0: one ModUp each)
+    TwF *cmodf = nullptr; // [K][K]: (q_j mod q_i, (q_j mod q_i) / q_i) as doubles, j major (hoist.h)
+    std::mutex mask_mu;
+    std::map<u32, u64 *> masks; // Galois element -> NTT of its negation mask, [K][n] (hoist.h)
     std::mutex mu;
     std::map<hipStream_t, Workspace> ws;
 };
@@ -449,6 +461,41 @@ struct JobModUpRow
         const int I = I0 + y / L, J = y % L;
         const int pi = (I == L) ? K - 1 : I;
         return View{ modup + ((size_t)y << log_n), primes[pi], tw + ((size_t)pi << log_n), I == J };
+    }
+};
+
+// The hoisted ModUp's row pass (hoist.h): src [I][J][n] column-pass output -> dst the same layout,
+// canonical, each 256-slot block stored in bit-reversed order.  BREV (n = 2^16, 256-slot rows): the
+// row pass reads its LDS row bit-reversed and stores contiguously; otherwise the store scatters
+// inside the block (out of place: at n < 2^16 a block spans rows of several workgroups).
+template <bool BREV>
+struct JobModUpRowH
+{
+    const u64 *src;
+    u64 *dst;
+    const PrimeDev *primes;
+    const Tw *tw;
+    int L, K, log_n;
+    struct View
+    {
+        const u64 *src;
+        u64 *dst;
+        PrimeDev p;
+        const Tw *tw;
+        bool skip;
+        static constexpr bool brev = BREV;
+        __device__ u64 load(u32 x) const { return src[x]; }
+        __device__ void store(u32 x, u64 v) const
+        {
+            dst[BREV ? x : ((x & ~255u) | brev8(x & 255u))] = csub(csub(v, p.two_q), p.q);
+        }
+    };
+    __device__ View view(int y) const
+    {
+        const int I = y / L, J = y % L;
+        const int pi = (I == L) ? K - 1 : I;
+        const size_t off = (size_t)y << log_n;
+        return View{ src + off, dst + off, primes[pi], tw + ((size_t)pi << log_n), I == J };
     }
 };
 
@@ -850,6 +897,7 @@ struct JobStrided
     const Tw *tw;
     int log_n;
     int mode; // inverse store: 0 lazy, 1 full
+    const int *run_if = nullptr; // non-null: every job returns unless *run_if != 0 (hoist.h fallback)
     struct View
     {
         const u64 *src;
@@ -864,7 +912,8 @@ struct JobStrided
     __device__ View view(int y) const
     {
         const int pi = prime0 + prime_step * y;
-        return View{ src + y * src_stride, dst + y * dst_stride, primes[pi], tw + ((size_t)pi << log_n), mode, false };
+        return View{ src + y * src_stride, dst + y * dst_stride, primes[pi], tw + ((size_t)pi << log_n), mode,
+                     run_if && !*run_if };
     }
 };
 
@@ -1486,6 +1535,95 @@ static int ks_check_key(mhe_ctx *c, const KsJob &j, int L, hipStream_t st, int *
     return MHE_OK;
 }
 
+// Step 4 of a (batched) key switch, the ModDown (evaluator.cpp:2466-2524), over the key inner
+// products in w->e[e].acc (or accs[e]): ct_e += ModDown(acc_e), or with rescale_out the fused HMult tail (see
+// run_switch_key_batch).  special_inv_done: the key MAC already ran the special limbs' inverse
+// row pass.
+static void run_moddown(mhe_ctx *c, const KsJob *jobs, int B, int L, Workspace *w, int special_inv_done, int c1_write,
+                        hipStream_t st, u64 *const *accs = nullptr)
+{
+    // key products of entry e: accs[e] when given (hoisted rotations), else the entry's scratch
+    auto A = [&](int e) { return accs ? accs[e] : w->e[e].acc; };
+    const bool hm = jobs[0].rescale_out != nullptr;
+    const int log_n = c->log_n;
+    const size_t n = c->n;
+    // ModDown (evaluator.cpp:2466-2524): INTT_lazy of the special limbs, then fused
+    //    lift + NTT + (c + 4q - t) * P^-1 + add.
+    {
+        JobB<JobStrided> j;
+        j.per = 2;
+        for (int e = 0; e < B; e++)
+            j.j[e] = JobStrided{ A(e) + (size_t)L * n, A(e) + (size_t)L * n, (size_t)(L + 1) * n,
+                                 (size_t)(L + 1) * n, c->K - 1, 0, c->primes, c->itw, log_n, 0 };
+        if (!special_inv_done) inv_row(j, log_n, 2 * B, c->nm, st);
+        // the special limbs' inverse column pass runs inside the lift column pass (k_icol_lift)
+        // (not in the HMult tail: JobMDRCol reads the fully inverse-transformed special limbs)
+        ColSrc cs{};
+        cs.stride = (size_t)(L + 1) * n;
+        cs.per = 2;
+        cs.primes = c->primes;
+        cs.itw = c->itw;
+        cs.pi = c->K - 1;
+        for (int e = 0; e < B; e++) cs.src[e] = A(e) + (size_t)L * n;
+        const bool fuse = c->icol_fused && (!hm || L < 2);
+        if (!fuse) inv_col(j, log_n, 2 * B, c->nm, st);
+        if (!hm || L < 2)
+        {
+            JobB<JobModDownCol> dc;
+            dc.per = 2 * L;
+            JobB<JobModDownRow> dr;
+            dr.per = 2 * L;
+            for (int e = 0; e < B; e++)
+            {
+                dc.j[e] = JobModDownCol{ A(e), w->e[e].modup, c->primes, c->tw, L, c->K, log_n };
+                dr.j[e] = JobModDownRow{ w->e[e].modup, A(e), jobs[e].ct, c->primes, c->tw, c->invq, L, c->K, log_n };
+                dr.j[e].fp = c->nm.fp ? 1 : 0;
+                dr.j[e].c1_write = c1_write;
+            }
+            if (fuse)
+                icol_lift(cs, dc, 2 * B, L, log_n, c->nm, st);
+            else
+                fwd_col(dc, log_n, 2 * L * B, c->nm, st);
+            fwd_row(dr, log_n, 2 * L * B, c->nm, st);
+        }
+        else
+        {
+            // ModDown of limb L-1 only, its INTT (the rescale's "last"), then ModDown and
+            // rescale of the other limbs through one forward NTT each
+            JobB<JobModDownCol> dc;
+            dc.per = 2;
+            JobB<JobModDownRow> dr;
+            dr.per = 2;
+            JobB<JobLastInv> li;
+            li.per = 2;
+            JobB<JobStrided> j2;
+            j2.per = 2;
+            JobB<JobMDRCol> mc;
+            mc.per = 2 * (L - 1);
+            JobB<JobMDRRow> mr;
+            mr.per = 2 * (L - 1);
+            for (int e = 0; e < B; e++)
+            {
+                dc.j[e] = JobModDownCol{ A(e), w->e[e].modup, c->primes, c->tw, L, c->K, log_n, L - 1 };
+                dr.j[e] = JobModDownRow{ w->e[e].modup, A(e), jobs[e].ct, c->primes, c->tw, c->invq, L, c->K, log_n, L - 1 };
+                dr.j[e].fp = c->nm.fp ? 1 : 0;
+                li.j[e] = JobLastInv{ jobs[e].ct, w->e[e].coeff, c->primes, c->itw, L, log_n, 1 };
+                j2.j[e] = JobStrided{ w->e[e].coeff, w->e[e].coeff, n, n, L - 1, 0, c->primes, c->itw, log_n, 1 };
+                mc.j[e] = JobMDRCol{ A(e), w->e[e].coeff, w->e[e].modup, c->primes, c->tw, c->invq, L, c->K, log_n,
+                                     c->nm.fp ? 1 : 0 };
+                mr.j[e] = JobMDRRow{ w->e[e].modup, A(e), jobs[e].ct, jobs[e].rescale_out, c->primes, c->tw, c->invq,
+                                     L, c->K, log_n, c->nm.fp ? 1 : 0 };
+            }
+            fwd_col(dc, log_n, 2 * B, c->nm, st);
+            fwd_row(dr, log_n, 2 * B, c->nm, st);
+            inv_row(li, log_n, 2 * B, c->nm, st);
+            inv_col(j2, log_n, 2 * B, c->nm, st);
+            fwd_col(mc, log_n, 2 * (L - 1) * B, c->nm, st);
+            fwd_row(mr, log_n, 2 * (L - 1) * B, c->nm, st);
+        }
+    }
+}
+
 // switch_key_inplace (evaluator.cpp:2281-2525) for B <= MHE_MAXB independent entries of one
 // level L, every kernel launched once for all of them: ct_e[2][L][n] += KS(target_e[L][n]).
 // rescale_out != nullptr (HMult; all entries or none): ct_e is the first two polys of a product,
@@ -1602,81 +1740,7 @@ static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hip
                                c->K, jobs[0].key_limbs, log_n, I0);
         }
     }
-    // 4. ModDown (evaluator.cpp:2466-2524): INTT_lazy of the special limbs, then fused
-    //    lift + NTT + (c + 4q - t) * P^-1 + add.
-    {
-        JobB<JobStrided> j;
-        j.per = 2;
-        for (int e = 0; e < B; e++)
-            j.j[e] = JobStrided{ w->e[e].acc + (size_t)L * n, w->e[e].acc + (size_t)L * n, (size_t)(L + 1) * n,
-                                 (size_t)(L + 1) * n, c->K - 1, 0, c->primes, c->itw, log_n, 0 };
-        if (!special_inv_done) inv_row(j, log_n, 2 * B, c->nm, st);
-        // the special limbs' inverse column pass runs inside the lift column pass (k_icol_lift)
-        // (not in the HMult tail: JobMDRCol reads the fully inverse-transformed special limbs)
-        ColSrc cs{};
-        cs.stride = (size_t)(L + 1) * n;
-        cs.per = 2;
-        cs.primes = c->primes;
-        cs.itw = c->itw;
-        cs.pi = c->K - 1;
-        for (int e = 0; e < B; e++) cs.src[e] = w->e[e].acc + (size_t)L * n;
-        const bool fuse = c->icol_fused && (!hm || L < 2);
-        if (!fuse) inv_col(j, log_n, 2 * B, c->nm, st);
-        if (!hm || L < 2)
-        {
-            JobB<JobModDownCol> dc;
-            dc.per = 2 * L;
-            JobB<JobModDownRow> dr;
-            dr.per = 2 * L;
-            for (int e = 0; e < B; e++)
-            {
-                dc.j[e] = JobModDownCol{ w->e[e].acc, w->e[e].modup, c->primes, c->tw, L, c->K, log_n };
-                dr.j[e] = JobModDownRow{ w->e[e].modup, w->e[e].acc, jobs[e].ct, c->primes, c->tw, c->invq, L, c->K, log_n };
-                dr.j[e].fp = c->nm.fp ? 1 : 0;
-                dr.j[e].c1_write = c1_write;
-            }
-            if (fuse)
-                icol_lift(cs, dc, 2 * B, L, log_n, c->nm, st);
-            else
-                fwd_col(dc, log_n, 2 * L * B, c->nm, st);
-            fwd_row(dr, log_n, 2 * L * B, c->nm, st);
-        }
-        else
-        {
-            // ModDown of limb L-1 only, its INTT (the rescale's "last"), then ModDown and
-            // rescale of the other limbs through one forward NTT each
-            JobB<JobModDownCol> dc;
-            dc.per = 2;
-            JobB<JobModDownRow> dr;
-            dr.per = 2;
-            JobB<JobLastInv> li;
-            li.per = 2;
-            JobB<JobStrided> j2;
-            j2.per = 2;
-            JobB<JobMDRCol> mc;
-            mc.per = 2 * (L - 1);
-            JobB<JobMDRRow> mr;
-            mr.per = 2 * (L - 1);
-            for (int e = 0; e < B; e++)
-            {
-                dc.j[e] = JobModDownCol{ w->e[e].acc, w->e[e].modup, c->primes, c->tw, L, c->K, log_n, L - 1 };
-                dr.j[e] = JobModDownRow{ w->e[e].modup, w->e[e].acc, jobs[e].ct, c->primes, c->tw, c->invq, L, c->K, log_n, L - 1 };
-                dr.j[e].fp = c->nm.fp ? 1 : 0;
-                li.j[e] = JobLastInv{ jobs[e].ct, w->e[e].coeff, c->primes, c->itw, L, log_n, 1 };
-                j2.j[e] = JobStrided{ w->e[e].coeff, w->e[e].coeff, n, n, L - 1, 0, c->primes, c->itw, log_n, 1 };
-                mc.j[e] = JobMDRCol{ w->e[e].acc, w->e[e].coeff, w->e[e].modup, c->primes, c->tw, c->invq, L, c->K, log_n,
-                                     c->nm.fp ? 1 : 0 };
-                mr.j[e] = JobMDRRow{ w->e[e].modup, w->e[e].acc, jobs[e].ct, jobs[e].rescale_out, c->primes, c->tw, c->invq,
-                                     L, c->K, log_n, c->nm.fp ? 1 : 0 };
-            }
-            fwd_col(dc, log_n, 2 * B, c->nm, st);
-            fwd_row(dr, log_n, 2 * B, c->nm, st);
-            inv_row(li, log_n, 2 * B, c->nm, st);
-            inv_col(j2, log_n, 2 * B, c->nm, st);
-            fwd_col(mc, log_n, 2 * (L - 1) * B, c->nm, st);
-            fwd_row(mr, log_n, 2 * (L - 1) * B, c->nm, st);
-        }
-    }
+    run_moddown(c, jobs, B, L, w, special_inv_done, c1_write, st);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }
@@ -1848,6 +1912,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     if (const char *f = getenv("MHE_KS_PACK")) c->ks_pack = atoi(f);
     if (const char *f = getenv("MHE_GALOIS_FUSED")) c->galois_fused = atoi(f);
     if (const char *f = getenv("MHE_ICOL_FUSED")) c->icol_fused = atoi(f);
+    if (const char *f = getenv("MHE_KS_HOIST")) c->ks_hoist = atoi(f);
     std::vector<Tw> tw((size_t)count * n), itw((size_t)count * n), invq((size_t)count * count);
     c->primes_h.resize(count);
     for (int k = 0; k < count; k++)
@@ -1919,6 +1984,19 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
         if (atoi(f) == 0) fp = fp_data = false;
     bool mix = !fp && fp_data && count > 1;
     if (const char *f = getenv("MHE_KS_MIX")) mix = mix && atoi(f) != 0;
+    if (e == hipSuccess && fp)
+    {
+        // hoisted rotations (hoist.h): q_j mod q_i and its quotient by q_i
+        std::vector<TwF> cm((size_t)count * count);
+        for (int j = 0; j < count; j++)
+            for (int i = 0; i < count; i++)
+            {
+                const u64 r = moduli[j] % moduli[i];
+                cm[(size_t)j * count + i] = make_double2((double)r, (double)r / (double)moduli[i]);
+            }
+        e = hipMalloc(&c->cmodf, sizeof(TwF) * cm.size());
+        if (e == hipSuccess) e = hipMemcpy(c->cmodf, cm.data(), sizeof(TwF) * cm.size(), hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess && (fp || mix))
     {
         std::vector<TwF> twf((size_t)2 * count * n);
@@ -1946,6 +2024,7 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
     }
     if (e != hipSuccess)
     {
+        (void)hipFree(c->cmodf);
         (void)hipFree(c->twf);
         (void)hipFree(c->primes);
         (void)hipFree(c->tw);
@@ -1964,9 +2043,12 @@ MHE_EXPORT int mhe_ctx_destroy(mhe_ctx *c)
 {
     if (!c) return MHE_OK;
     (void)hipSetDevice(c->device);
+    for (auto &kv : c->masks) (void)hipFree(kv.second);
     for (auto &kv : c->ws)
     {
         if (kv.second.base) (void)hipFree(kv.second.base);
+        if (kv.second.hoist_base) (void)hipFree(kv.second.hoist_base);
+        if (kv.second.flags) (void)hipFree(kv.second.flags);
         for (auto &v : kv.second.ev)
             for (auto &e : v)
             {
@@ -1979,6 +2061,7 @@ MHE_EXPORT int mhe_ctx_destroy(mhe_ctx *c)
     (void)hipFree(c->itw);
     (void)hipFree(c->invq);
     (void)hipFree(c->twf);
+    (void)hipFree(c->cmodf);
     delete c;
     mhe_internal_ctx_count(-1);
     return MHE_OK;
@@ -2846,6 +2929,317 @@ MHE_EXPORT int mhe_apply_galois_to(mhe_ctx *c, const uint64_t *in, uint64_t *out
     return run_switch_key(c, out, w->tmp, key, key_limbs, limbs, st);
 }
 
+// ------------------------------------------------------------------ hoisted rotations (hoist.h)
+// The ModUp buffers of up to `entries` hoisted inputs on stream st ([K][K-1][n] each: every level),
+// the key products of up to MHE_MAXB * MHE_HOIST_R of their rotations and the inputs' flags.
+static int get_hoist(mhe_ctx *c, hipStream_t st, int entries, Workspace **out)
+{
+    Workspace *w;
+    int r = get_ws(c, st, c->K - 1, &w, MHE_MAXB);
+    if (r) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (w->hoist_entries < entries)
+    {
+        HIP_TRY(hipSetDevice(c->device));
+        if (w->hoist_base) HIP_TRY(hipFree(w->hoist_base));
+        w->hoist_base = nullptr;
+        w->hoist_entries = 0;
+        const size_t per = (size_t)c->K * (c->K - 1) * c->n, pacc = (size_t)2 * c->K * c->n;
+        const int na = MHE_MAXB * MHE_HOIST_R;
+        if (hipMalloc(&w->hoist_base, ((size_t)entries * per + (size_t)na * pacc) * sizeof(u64)) != hipSuccess)
+            return fail(MHE_ERR_MEMORY, "workspace allocation failed");
+        for (int i = 0; i < entries; i++) w->hoist[i] = w->hoist_base + (size_t)i * per;
+        for (int i = 0; i < na; i++) w->hacc[i] = w->hoist_base + (size_t)entries * per + (size_t)i * pacc;
+        w->hoist_entries = entries;
+    }
+    if (!w->flags && hipMalloc(&w->flags, MHE_MAXB * sizeof(int)) != hipSuccess)
+        return fail(MHE_ERR_MEMORY, "workspace allocation failed");
+    *out = w;
+    return MHE_OK;
+}
+
+// M^g = NTT of Galois element g's negation mask under every prime of the context, [K][n]
+// canonical; built once per element on stream st (which then waits for it: other streams use the
+// table without an event).
+static int get_mask(mhe_ctx *c, u32 elt, hipStream_t st, const u64 **out)
+{
+    std::lock_guard<std::mutex> g(c->mask_mu);
+    auto it = c->masks.find(elt);
+    if (it != c->masks.end())
+    {
+        *out = it->second;
+        return MHE_OK;
+    }
+    u64 *m = nullptr;
+    const size_t total = (size_t)c->K * c->n;
+    HIP_TRY(hipSetDevice(c->device));
+    if (hipMalloc(&m, total * sizeof(u64)) != hipSuccess) return fail(MHE_ERR_MEMORY, "Galois mask allocation failed");
+    hipLaunchKernelGGL(k_negmask, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, m, elt, c->K, c->log_n);
+    JobFwdPlain j;
+    j.src = m;
+    j.dst = m;
+    j.primes = c->primes;
+    j.tw = c->tw;
+    j.limbs = c->K;
+    j.log_n = c->log_n;
+    j.mode = 0;
+    fwd_col(j, c->log_n, c->K, c->nm, st);
+    j.mode = 1;
+    fwd_row(j, c->log_n, c->K, c->nm, st);
+    HIP_LAUNCH_CHECK();
+    HIP_TRY(hipStreamSynchronize(st));
+    c->masks[elt] = m;
+    *out = m;
+    return MHE_OK;
+}
+
+static void launch_hoist_mac(int R, dim3 grid, hipStream_t st, const HoistPtrs &hp, const PrimeDev *primes,
+                             const TwF *cm, int L, int K, int log_n)
+{
+    switch (R)
+    {
+#define HM(r) case r: hipLaunchKernelGGL((k_ks_hoist_mac<r>), grid, dim3(256), 0, st, hp, primes, cm, L, K, log_n, 0); break;
+        HM(1) HM(2) HM(3) HM(4) HM(5) HM(6) HM(7) HM(8)
+#undef HM
+    }
+}
+static void launch_hoist_mac_sh(int R, dim3 grid, hipStream_t st, const HoistShared &hs, const PrimeDev *primes,
+                                const TwF *cm, int L, int K, int log_n)
+{
+    switch (R)
+    {
+#define HM(r) case r: hipLaunchKernelGGL((k_ks_hoist_mac_sh<r>), grid, dim3(1024), 0, st, hs, primes, cm, L, K, log_n); break;
+        HM(1) HM(2) HM(3) HM(4) HM(5) HM(6) HM(7) HM(8)
+#undef HM
+    }
+}
+
+static bool hoist_ok(const mhe_ctx *c)
+{
+    return c->ks_hoist && c->ks_fused && c->galois_fused && c->ks_colgroups > 0 && c->nm.fp == 1 && c->nm_ks.fp == 1 &&
+           c->cmodf;
+}
+
+// Rotations of H <= MHE_MAXB inputs at L limbs, entry i rotating input ent_in[i] (index into in)
+// by elts[i] into out[i]: ModUp of every input once (INTT -> column pass -> row pass, canonical
+// D in the hoist buffers, plus the zero scan), then per chunk of entries the permutation of c0 /
+// c1 into out, the hoisted key MAC (hoist.h), the classic ModUp + MAC for flagged inputs only
+// (their kernels return at once otherwise), and the ModDown (c1 written).
+static int run_galois_hoisted(mhe_ctx *c, const u64 *const *in, int H, int count, const int *ent_in,
+                              u64 *const *out, const u32 *elts, const u64 *const *keys, const int *key_limbs, int L,
+                              hipStream_t st)
+{
+    Workspace *w;
+    int r = get_hoist(c, st, H, &w);
+    if (r) return r;
+    const int log_n = c->log_n;
+    const size_t n = c->n, ps = (size_t)L * n;
+    std::vector<const u64 *> masks(count);
+    std::vector<u32> elt_inv(count);
+    for (int i = 0; i < count; i++)
+    {
+        if ((r = get_mask(c, elts[i], st, &masks[i]))) return r;
+        u64 inv = 0;
+        host::invmod(elts[i], 2 * n, inv); // odd: a unit mod 2N
+        elt_inv[i] = (u32)inv;
+    }
+    // 1. ModUp of each input's c1: INTT (evaluator.cpp:2351-2354) into entry slot h's coeff, the zero
+    //    scan, the column pass into hoist[h] (64-bit, natural order), the row pass in place
+    {
+        JobB<JobStrided> j;
+        j.per = L;
+        for (int h = 0; h < H; h++)
+            j.j[h] = JobStrided{ in[h] + ps, w->e[h].coeff, n, n, 0, 1, c->primes, c->itw, log_n, 0 };
+        inv_row(j, log_n, H * L, c->nm, st);
+        for (int h = 0; h < H; h++)
+        {
+            j.j[h].src = w->e[h].coeff;
+            j.j[h].mode = 1;
+        }
+        inv_col(j, log_n, H * L, c->nm, st);
+        HIP_TRY(hipMemsetAsync(w->flags, 0, MHE_MAXB * sizeof(int), st));
+        for (int h = 0; h < H; h++)
+            hipLaunchKernelGGL(k_zero_scan, dim3((unsigned)((ps + 255) / 256)), dim3(256), 0, st, w->e[h].coeff, log_n, ps,
+                               w->flags + h);
+        KsPtrs kp{};
+        for (int h = 0; h < H; h++)
+        {
+            kp.coeff[h] = w->e[h].coeff;
+            kp.inter[h] = w->e[h].modup;
+        }
+        const int IG = c->ks_colgroups < L + 1 ? c->ks_colgroups : L + 1;
+        modup_col(kp, H, c->primes, c->tw, L, c->K, log_n, c->nm_ks, 0, L + 1, IG, 0, st);
+        auto row = [&](auto brev) {
+            JobB<JobModUpRowH<decltype(brev)::value>> rj;
+            rj.per = (L + 1) * L;
+            for (int h = 0; h < H; h++) rj.j[h] = { w->e[h].modup, w->hoist[h], c->primes, c->tw, L, c->K, log_n };
+            fwd_row(rj, log_n, H * (L + 1) * L, c->nm, st);
+        };
+        if (log_n == 16)
+            row(std::true_type{});
+        else
+            row(std::false_type{});
+        HIP_LAUNCH_CHECK();
+    }
+    // 2. the hoisted key MAC: items of one input and up to MHE_HOIST_R of its rotations (sorted by
+    //    key, so the items of images rotated alike list the same keys and share their rows), up to
+    //    MHE_MAXB items per launch; rotation i's key products go to w->hacc[i]
+    const int pack = (c->ks_pack && c->ks_colgroups > 0) ? 1 : 0;
+    {
+        std::vector<std::vector<int>> per(H);
+        for (int i = 0; i < count; i++) per[ent_in[i]].push_back(i);
+        std::vector<std::pair<int, std::vector<int>>> items;
+        for (int h = 0; h < H; h++)
+        {
+            std::stable_sort(per[h].begin(), per[h].end(), [&](int a, int b) { return keys[a] < keys[b]; });
+            for (size_t r0 = 0; r0 < per[h].size(); r0 += MHE_HOIST_R)
+                items.emplace_back(h, std::vector<int>(per[h].begin() + r0,
+                                                       per[h].begin() + std::min(per[h].size(), r0 + MHE_HOIST_R)));
+        }
+        // items with one key list (the images of a FiberBatch rotated alike): the shared-key kernel,
+        // up to MHE_MAXB items per launch; the rest one launch per up to MHE_MAXB items
+        std::vector<char> done(items.size(), 0);
+        for (size_t z0 = 0; z0 < items.size(); z0++)
+        {
+            if (done[z0]) continue;
+            std::vector<size_t> same{ z0 };
+            for (size_t z = z0 + 1; z < items.size() && same.size() < (size_t)MHE_MAXB; z++)
+            {
+                if (done[z] || items[z].second.size() != items[z0].second.size()) continue;
+                bool eq = true;
+                for (size_t r = 0; eq && r < items[z].second.size(); r++)
+                {
+                    const int a = items[z].second[r], b = items[z0].second[r];
+                    eq = keys[a] == keys[b] && key_limbs[a] == key_limbs[b] && elts[a] == elts[b];
+                }
+                if (eq) same.push_back(z);
+            }
+            if (same.size() < 2) continue;
+            HoistShared hs{};
+            hs.Z = (int)same.size();
+            const std::vector<int> &r0 = items[z0].second;
+            for (size_t r = 0; r < r0.size(); r++)
+            {
+                hs.key[r] = keys[r0[r]];
+                hs.mask[r] = masks[r0[r]];
+                hs.einv[r] = elt_inv[r0[r]];
+                hs.key_limbs[r] = key_limbs[r0[r]];
+            }
+            for (int z = 0; z < hs.Z; z++)
+            {
+                const auto &it = items[same[z]];
+                hs.D[z] = w->hoist[it.first];
+                hs.c1[z] = in[it.first] + ps;
+                hs.flag[z] = w->flags + it.first;
+                for (size_t r = 0; r < it.second.size(); r++) hs.acc[z][r] = w->hacc[it.second[r]];
+                done[same[z]] = 1;
+            }
+            hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
+            const int per_wg = r0.size() <= 4 ? 8 : 4; // 4 lane groups x items per lane
+            launch_hoist_mac_sh((int)r0.size(), dim3((unsigned)(n / 256), (unsigned)(L + 1), (unsigned)((hs.Z + per_wg - 1) / per_wg)),
+                                st, hs, c->primes, c->cmodf, L, c->K, log_n);
+            timing_end(tm, st);
+        }
+        std::vector<std::pair<int, std::vector<int>>> left;
+        for (size_t z = 0; z < items.size(); z++)
+            if (!done[z]) left.push_back(items[z]);
+        items.swap(left);
+        // one rotation count per launch (k_ks_hoist_mac<R>): items ordered by it
+        std::stable_sort(items.begin(), items.end(),
+                         [](const std::pair<int, std::vector<int>> &a, const std::pair<int, std::vector<int>> &b) {
+                             return a.second.size() > b.second.size();
+                         });
+        for (size_t z0 = 0; z0 < items.size();)
+        {
+            size_t zn = z0 + 1;
+            while (zn < items.size() && zn - z0 < (size_t)MHE_MAXB && items[zn].second.size() == items[z0].second.size()) zn++;
+            const int Z = (int)(zn - z0);
+            HoistPtrs hp{};
+            for (int z = 0; z < Z; z++)
+            {
+                const int h = items[z0 + z].first;
+                const std::vector<int> &rs = items[z0 + z].second;
+                hp.D[z] = w->hoist[h];
+                hp.c1[z] = in[h] + ps;
+                hp.flag[z] = w->flags + h;
+                hp.R[z] = (int)rs.size();
+                for (size_t r = 0; r < rs.size(); r++)
+                {
+                    const int i = rs[r];
+                    hp.key[z][r] = keys[i];
+                    hp.mask[z][r] = masks[i];
+                    hp.acc[z][r] = w->hacc[i];
+                    hp.einv[z][r] = elt_inv[i];
+                    hp.key_limbs[z][r] = key_limbs[i];
+                }
+            }
+            const dim3 grid((unsigned)(n / 256), (unsigned)(L + 1), (unsigned)Z);
+            hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
+            launch_hoist_mac(hp.R[0], grid, st, hp, c->primes, c->cmodf, L, c->K, log_n);
+            timing_end(tm, st);
+            z0 = zn;
+        }
+        HIP_LAUNCH_CHECK();
+    }
+    // 3. per MHE_MAXB rotations: c0 / c1 permuted into out, the classic ModUp + MAC of flagged
+    //    inputs (their kernels return at once otherwise), the ModDown (c1 written)
+    std::vector<int> order(count);
+    for (int i = 0; i < count; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return keys[a] < keys[b]; });
+    for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
+    {
+        const int B = std::min(MHE_MAXB, count - i0);
+        GalPtrs gp{};
+        KsPtrs kp{};
+        KsJob jobs[MHE_MAXB];
+        u64 *accs[MHE_MAXB];
+        JobB<JobStrided> ij;
+        ij.per = L;
+        int share = B > 1 ? 1 : 0;
+        for (int e = 0; e < B; e++)
+        {
+            const int i = order[i0 + e], h = ent_in[i];
+            gp.in[e] = in[h];
+            gp.out[e] = out[i];
+            gp.elt[e] = elts[i];
+            jobs[e] = KsJob{ out[i], out[i] + ps, keys[i], key_limbs[i], nullptr };
+            accs[e] = w->hacc[i];
+            // the classic path of a flagged input: INTT of the permuted c1, ModUp, fused MAC
+            ij.j[e] = JobStrided{ out[i] + ps, w->e[e].coeff, n, n, 0, 1, c->primes, c->itw, log_n, 0, w->flags + h };
+            kp.coeff[e] = w->e[e].coeff;
+            kp.inter[e] = w->e[e].modup;
+            kp.target[e] = out[i] + ps;
+            kp.key[e] = keys[i];
+            kp.acc[e] = w->hacc[i];
+            kp.key_limbs[e] = key_limbs[i];
+            kp.run_if[e] = w->flags + h;
+            if (keys[i] != keys[order[i0]] || key_limbs[i] != key_limbs[order[i0]]) share = 0;
+        }
+        if (!c->ks_share) share = 0;
+        int kpack = 1;
+        for (int e = 0; e < B; e++)
+            if ((r = ks_check_key(c, jobs[e], L, st, &kpack))) return r;
+        count_op(c, MHE_OPK_GALOIS, L, 2ull * B);
+        count_op(c, MHE_OPK_KEYSWITCH, L, (unsigned long long)B);
+        const size_t total = 2 * ps;
+        hipLaunchKernelGGL(k_galois_b, dim3((unsigned)((total + 255) / 256), (unsigned)B), dim3(256), 0, st, gp, log_n,
+                           total);
+        inv_row(ij, log_n, B * L, c->nm, st);
+        for (int e = 0; e < B; e++)
+        {
+            ij.j[e].src = w->e[e].coeff;
+            ij.j[e].mode = 1;
+        }
+        inv_col(ij, log_n, B * L, c->nm, st);
+        const int IG = c->ks_colgroups < L + 1 ? c->ks_colgroups : L + 1;
+        modup_col(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm_ks, 0, L + 1, IG, pack, st);
+        ks_row_mac_chunk(kp, B, c->primes, c->tw, L, c->K, log_n, c->nm_ks, 0, L + 1, pack, kpack, share, c->itw, 0, st);
+        HIP_LAUNCH_CHECK();
+        run_moddown(c, jobs, B, L, w, 0, 1, st, accs);
+    }
+    return MHE_OK;
+}
+
 MHE_EXPORT int mhe_apply_galois_batch(mhe_ctx *c, int count, const uint64_t *const *in, uint64_t *const *out,
                                       const uint32_t *elts, const uint64_t *const *keys, const int *key_limbs, int limbs,
                                       void *s)
@@ -2877,19 +3271,90 @@ MHE_EXPORT int mhe_apply_galois_batch(mhe_ctx *c, int count, const uint64_t *con
             if ((r = mhe_apply_galois_to(c, in[i], out[i], elts[i], keys[i], key_limbs[i], limbs, s))) return r;
         return MHE_OK;
     }
-    for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
+    // inputs rotated more than once share their ModUp (hoist.h), up to MHE_MAXB inputs per pass
+    std::vector<int> rest;
+    if (hoist_ok(c) && count > 1 && c->n >= 256)
     {
-        const int B = std::min(MHE_MAXB, count - i0);
+        std::vector<const u64 *> uin;
+        std::vector<std::vector<int>> uent;
+        for (int i = 0; i < count; i++)
+        {
+            size_t u = 0;
+            while (u < uin.size() && uin[u] != in[i]) u++;
+            if (u == uin.size())
+            {
+                uin.push_back(in[i]);
+                uent.emplace_back();
+            }
+            uent[u].push_back(i);
+        }
+        std::vector<const u64 *> hin;
+        std::vector<int> ent_in;
+        std::vector<u64 *> hout;
+        std::vector<u32> hel;
+        std::vector<const u64 *> hkey;
+        std::vector<int> hkl;
+        auto flush = [&]() -> int {
+            if (hin.empty()) return MHE_OK;
+            const int rr = run_galois_hoisted(c, hin.data(), (int)hin.size(), (int)ent_in.size(), ent_in.data(), hout.data(),
+                                              hel.data(), hkey.data(), hkl.data(), limbs, st);
+            hin.clear();
+            ent_in.clear();
+            hout.clear();
+            hel.clear();
+            hkey.clear();
+            hkl.clear();
+            return rr;
+        };
+        for (size_t u = 0; u < uin.size(); u++)
+        {
+            if (uent[u].size() < 2)
+            {
+                rest.push_back(uent[u][0]);
+                continue;
+            }
+            // at most MHE_MAXB inputs and MHE_MAXB * MHE_HOIST_R rotations per pass (w->hacc)
+            if ((hin.size() == MHE_MAXB || ent_in.size() + uent[u].size() > (size_t)MHE_MAXB * MHE_HOIST_R) &&
+                (r = flush()))
+                return r;
+            if (uent[u].size() > (size_t)MHE_MAXB * MHE_HOIST_R)
+            {
+                // more rotations than one pass holds: the classic path (never in the callers' shapes)
+                for (int i : uent[u]) rest.push_back(i);
+                continue;
+            }
+            const int h = (int)hin.size();
+            hin.push_back(uin[u]);
+            for (int i : uent[u])
+            {
+                ent_in.push_back(h);
+                hout.push_back(out[i]);
+                hel.push_back(elts[i]);
+                hkey.push_back(keys[i]);
+                hkl.push_back(key_limbs[i]);
+            }
+        }
+        if ((r = flush())) return r;
+    }
+    else
+        for (int i = 0; i < count; i++) rest.push_back(i);
+    // entries of one key side by side: a launch of them shares the key stream (k_ks_row_mac share)
+    std::stable_sort(rest.begin(), rest.end(), [&](int a, int b) { return keys[a] < keys[b]; });
+    const int nrest = (int)rest.size();
+    for (int i0 = 0; i0 < nrest; i0 += MHE_MAXB)
+    {
+        const int B = std::min(MHE_MAXB, nrest - i0);
         // out_e <- perm_e(in_e), both polys, one launch (evaluator.cpp:2193-2214; SEAL zeroes c1 and
         // adds KS_1, the same words as writing it)
         GalPtrs gp{};
         KsJob jobs[MHE_MAXB];
         for (int e = 0; e < B; e++)
         {
-            gp.in[e] = in[i0 + e];
-            gp.out[e] = out[i0 + e];
-            gp.elt[e] = elts[i0 + e];
-            jobs[e] = KsJob{ out[i0 + e], out[i0 + e] + ps, keys[i0 + e], key_limbs[i0 + e], nullptr };
+            const int i = rest[i0 + e];
+            gp.in[e] = in[i];
+            gp.out[e] = out[i];
+            gp.elt[e] = elts[i];
+            jobs[e] = KsJob{ out[i], out[i] + ps, keys[i], key_limbs[i], nullptr };
         }
         const size_t total = 2 * ps;
         count_op(c, MHE_OPK_GALOIS, limbs, 2ull * B);

@@ -339,6 +339,24 @@ struct PreOf<V, std::void_t<typename V::Pre>>
     static constexpr bool value = MHE_ROW_PRE != 0;
 };
 
+// A View with `static constexpr bool brev = true` stores position x of each 256-slot block from slot
+// brev8(x & 255) of the block (hoisted rotations, hoist.h): with 256-slot rows (LOGR = 8) the row
+// pass reads its LDS row at the bit-reversed index and its stores stay contiguous.
+template <class V, class = void>
+struct BrevOf
+{
+    static constexpr bool value = false;
+};
+template <class V>
+struct BrevOf<V, std::void_t<decltype(V::brev)>>
+{
+    static constexpr bool value = V::brev;
+};
+__device__ __forceinline__ u32 brev8_ntt(u32 x)
+{
+    return __builtin_bitreverse32(x) >> 24;
+}
+
 // LDS image of a row pass's transposes.  The in-lane phase writes position t + TPS e and the
 // cross-lane phase reads E t + e (and back); with a plain padded row the second pattern puts the
 // 16 lanes of a sub-transform on a stride of E 8-byte words, an 8-way bank conflict at LOGR = 8
@@ -405,7 +423,9 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long t
 #pragma unroll
     for (int e = 0; e < E; e++)
     {
-        const u64 o = ar.out(lds[RL::at(sl, t + TPS * e)]);
+        int src = t + TPS * e;
+        if constexpr (BrevOf<VW>::value && LOGR == 8) src = (int)brev8_ntt((u32)src); // launched at LOGR 8 only
+        const u64 o = ar.out(lds[RL::at(sl, src)]);
         if constexpr (PRE)
             V.store(base + t + TPS * e, o, pr[e]);
         else
@@ -603,6 +623,7 @@ struct KsPtrs
     const u64 *key[MHE_MAXB];    // [digits][2][key_limbs][n]
     u64 *acc[MHE_MAXB];          // key inner products [2][L+1][n]
     int key_limbs[MHE_MAXB];
+    const int *run_if[MHE_MAXB]; // non-null: the entry's workgroups return unless *run_if != 0 (hoist.h fallback)
 };
 
 #ifndef MHE_MODUP_OCC
@@ -622,6 +643,7 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
                                                    const Tw *__restrict__ tw_all, int L, int K, int log_n,
                                                    long long twd, int I0, int Icnt, int pack, int X, int IG, int xcd)
 {
+    if (P.run_if[blockIdx.y] && !*P.run_if[blockIdx.y]) return; // uniform, before any barrier
     const u64 *__restrict__ coeff = P.coeff[blockIdx.y];
     u64 *__restrict__ modup = P.inter[blockIdx.y];
     using SH = Shape<LOGR, LOGT>;
@@ -1066,6 +1088,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
         bx = tile % X;
         by = tile / X;
     }
+    if (P.run_if[bz] && !*P.run_if[bz]) return; // uniform, before any barrier
     // batch entry bz: inter [cnt][L][n] column-pass output, target [L][n] NTT form,
     // key [digits][2][key_limbs][n], acc [2][L+1][n]
     const u64 *__restrict__ inter = P.inter[bz];

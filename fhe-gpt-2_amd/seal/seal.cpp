@@ -2638,17 +2638,11 @@ void Evaluator::rotate_vectors(const std::vector<const Ciphertext *> &encrypted,
     {
         std::vector<std::size_t> idx = g.second;
         if (idx.size() < 2) continue;
-        // entries of one key side by side; when every key has several entries (the members of a
-        // Lockstep group), one launch per key, so its entries share the key stream (k_ks_row_mac)
+        // one call for the level: the engine runs the rotations of an input that appears more than
+        // once off one shared ModUp (csrc/hoist.h) and puts the entries of one key side by side in
+        // its launches, so they share the key stream (k_ks_row_mac / k_ks_hoist_mac)
         std::stable_sort(idx.begin(), idx.end(), [&](std::size_t a, std::size_t b) { return elt[a] < elt[b]; });
-        std::map<std::uint32_t, std::vector<std::size_t>> by_elt;
-        for (std::size_t i : idx) by_elt[elt[i]].push_back(i);
-        bool shared = by_elt.size() > 1;
-        for (auto &e : by_elt) shared = shared && e.second.size() >= 2;
-        if (shared)
-            for (auto &e : by_elt) launch(e.second, g.first);
-        else
-            launch(idx, g.first);
+        launch(idx, g.first);
     }
     for (std::size_t i = 0; i < encrypted.size(); i++)
         if (!done[i]) rotate_vector(*encrypted[i], steps[i], galois_keys, *destinations[i]);

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--limbs", type=int, default=31)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--ops", default="rescale,rescale4,ks,ks4,ks4s,rot4,ntt,hmult")
+    ap.add_argument("--bsgs", default="8x7", help="inputs x rotations of the bsgs op (keys shared over inputs)")
     a = ap.parse_args()
     log_n, n = 16, 1 << 16
     bits = [51] + [46] * 16 + [51] * 14 + [51]
@@ -50,6 +51,18 @@ def main():
     outs = [eng.empty(2, L - 1, n) for _ in range(4)]
     rot_out = [eng.empty(2, L, n) for _ in range(4)]
     elts = [pow(5, s, 2 * n) for s in (1, 2, 4, 8)]
+    # bsgs: the BSGS baby steps of several images (FiberBatch): each input rotated R ways, the R keys
+    # shared by the inputs -- the hoisted path (csrc/hoist.h) unless MHE_KS_HOIST=0
+    if "bsgs" in a.ops:
+        H, R = (int(x) for x in a.bsgs.split("x"))
+        bkeys = [rnd(L, 2, K, n, limbs=K) for _ in range(R)]
+        for k in bkeys:
+            eng.key_prepare(k)
+        bin_ = [rnd(2, L, n, limbs=L) for _ in range(H)]
+        b_in = [c for c in bin_ for _ in range(R)]
+        b_el = [pow(5, s + 1, 2 * n) for _ in range(H) for s in range(R)]
+        b_k = [bkeys[s] for _ in range(H) for s in range(R)]
+        b_out = [eng.empty(2, L, n) for _ in b_in]
 
     ops = {
         "rescale": lambda: eng.rescale_to_next(cts[0], outs[0]),
@@ -58,6 +71,7 @@ def main():
         "ks4": lambda: eng.switch_key_batch([c[:2] for c in ct3], [c[2] for c in ct3], keys),
         "ks4s": lambda: eng.switch_key_batch([c[:2] for c in ct3], [c[2] for c in ct3], [keys[0]] * 4),
         "rot4": lambda: eng.apply_galois_batch(cts, elts, keys, rot_out),
+        "bsgs": lambda: eng.apply_galois_batch(b_in, b_el, b_k, b_out),
         "ntt": lambda: eng.ntt_forward(cts[1]),
         "hmult": lambda: eng.hmult(cts[2], cts[3], keys[0], outs[1]),
     }
@@ -74,7 +88,8 @@ def main():
         t1.record(st)
         torch.cuda.synchronize()
         us = t0.elapsed_time(t1) * 1000 / a.reps
-        print(json.dumps({"op": name, "limbs": L, "us": round(us, 2), "lib": os.environ.get("MHE_LIB_PATH", "libmhe.so")}),
+        print(json.dumps({"op": name if name != "bsgs" else "bsgs" + a.bsgs, "limbs": L, "us": round(us, 2),
+                          "hoist": os.environ.get("MHE_KS_HOIST", "1"), "lib": os.environ.get("MHE_LIB_PATH", "libmhe.so")}),
               flush=True)
 
 

@@ -79,6 +79,107 @@ def test_rotate_batch_prepared_keys_n16(resnet):
         assert np.array_equal(ch.down(outs[i]), ch.oc.apply_galois(ct, elts[i], full[i]))
 
 
+def with_zero_coeffs(ch, L, zeros):
+    """A ciphertext whose c1 (coefficient form) has zero coefficients: `zeros` random slots >= 1 per
+    limb, "slot0" (slot 0 only, never negated by a rotation) or "all".  A hoisted rotation's
+    identity fails at a zero moved to a negated slot (csrc/hoist.h), so the engine must take the
+    classic path for such an input, decided on the device."""
+    ct = ch.rand(2, L, ch.n)
+    c1 = ch.rand(L, ch.n)
+    if zeros == "all":
+        c1[:] = 0
+    elif zeros == "slot0":
+        c1[:, 0] = 0
+    else:
+        for l in range(L):
+            c1[l, ch.rng.choice(np.arange(1, ch.n), zeros, replace=False)] = 0
+    ct[1] = ch.oc.ntt(c1)
+    return ct
+
+
+@pytest.mark.parametrize("zeros", [0, "slot0", 1, 7, "all"])
+def test_rotate_batch_hoisted_zero_coefficients(small, zeros):
+    """One input rotated 4 ways (the hoisted path: one shared ModUp) with zero coefficients in its
+    c1: every output still equals the oracle's one-at-a-time apply_galois."""
+    ch = small
+    L = 4
+    ct = with_zero_coeffs(ch, L, zeros)
+    steps = [1, 3, -2, 17]
+    elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
+    keys = [ch.rand_key() for _ in steps]
+    outs = ch.eng.apply_galois_batch([ch.up(ct)] * len(steps), elts, [ch.up(k) for k in keys])
+    for i in range(len(steps)):
+        assert np.array_equal(ch.down(outs[i]), ch.oc.apply_galois(ct, elts[i], keys[i])), f"step {steps[i]}"
+
+
+def test_rotate_batch_hoisted_mixed(small):
+    """10 inputs in one call -- 8 rotated 2-4 ways (hoisted, in two passes of at most 8 inputs), two
+    rotated once (the classic path), one with zero coefficients among them -- shared and distinct
+    keys, full and level-truncated."""
+    ch = small
+    L = 5
+    shared = ch.rand_key()
+    cts = [with_zero_coeffs(ch, L, 3) if i == 4 else ch.rand(2, L, ch.n) for i in range(10)]
+    srcs = [ch.up(c) for c in cts]
+    reps = [2, 3, 4, 2, 3, 1, 2, 4, 1, 2]
+    ins, elts, keys, dkeys, which = [], [], [], [], []
+    for i, r in enumerate(reps):
+        for k in range(r):
+            step = [1, 2, 5, -3][k]
+            key = shared if (i + k) % 2 else ch.rand_key()
+            ins.append(srcs[i])
+            elts.append(mhe.galois_elt_from_step(ch.log_n, step))
+            keys.append(key)
+            dkeys.append(ch.up(key if k % 2 else truncated(key, L)))
+            which.append(i)
+    outs = ch.eng.apply_galois_batch(ins, elts, dkeys)
+    for j in range(len(ins)):
+        want = ch.oc.apply_galois(cts[which[j]], elts[j], keys[j])
+        assert np.array_equal(ch.down(outs[j]), want), f"entry {j} (input {which[j]})"
+    for c, s in zip(cts, srcs):
+        assert np.array_equal(ch.down(s), c)  # inputs untouched
+
+
+@pytest.mark.parametrize("L", [1, 6])
+def test_rotate_batch_hoisted_shared_keys(small, L):
+    """4 inputs rotated by the same 3 keys (a FiberBatch's baby steps): the keys' mask sums are taken
+    once per key (k_hoist_kc); one input has zero coefficients, one key is level-truncated."""
+    ch = small
+    cts = [ch.rand(2, L, ch.n), ch.rand(2, L, ch.n), with_zero_coeffs(ch, L, 4), ch.rand(2, L, ch.n)]
+    steps = [1, -4, 9]
+    elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
+    keys = [ch.rand_key() for _ in steps]
+    dkeys = [ch.up(truncated(k, L) if i == 1 else k) for i, k in enumerate(keys)]
+    srcs = [ch.up(c) for c in cts]
+    ins = [s for s in srcs for _ in steps]
+    outs = ch.eng.apply_galois_batch(ins, elts * len(cts), dkeys * len(cts))
+    for j in range(len(ins)):
+        want = ch.oc.apply_galois(cts[j // 3], elts[j % 3], keys[j % 3])
+        assert np.array_equal(ch.down(outs[j]), want), f"input {j // 3} step {steps[j % 3]}"
+
+
+def test_rotate_batch_hoisted_n16(resnet):
+    """N = 2^16, ResNet chain at 12 limbs, prepared keys: 3 inputs x 3 rotations (BSGS baby steps of
+    three images), one input with zero coefficients."""
+    ch = resnet
+    L = 12
+    cts = [ch.rand(2, L, ch.n), with_zero_coeffs(ch, L, 2), ch.rand(2, L, ch.n)]
+    steps = [1, 2, 3]
+    keys = [truncated(ch.rand_key(digits=L), L) for _ in steps]
+    dkeys = [ch.eng.key_prepare(ch.up(k)) for k in keys]
+    full = [np.zeros((L, 2, ch.K, ch.n), np.uint64) for _ in keys]
+    for f, k in zip(full, keys):
+        f[:, :, :L] = k[:, :, :L]
+        f[:, :, -1] = k[:, :, -1]
+    elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
+    srcs = [ch.up(c) for c in cts]
+    ins = [s for s in srcs for _ in steps]
+    outs = ch.eng.apply_galois_batch(ins, elts * 3, dkeys * 3)
+    for j in range(9):
+        want = ch.oc.apply_galois(cts[j // 3], elts[j % 3], full[j % 3])
+        assert np.array_equal(ch.down(outs[j]), want), f"input {j // 3} step {steps[j % 3]}"
+
+
 @pytest.mark.parametrize("size", [1, 2, 3])
 @pytest.mark.parametrize("count", [1, 5, 9])
 def test_rescale_batch(small, size, count):
