@@ -1064,9 +1064,6 @@ template <int LOGR, bool FP, bool MIX = false>
 #ifndef MHE_KS_XCH
 #define MHE_KS_XCH 2 // LDS transpose buffers of the fused MAC (1 or 2)
 #endif
-#ifndef MHE_KS_DPF
-#define MHE_KS_DPF 1 // fused MAC: load the next digit one digit ahead (1), two ahead (2) or at the top of the digit (0)
-#endif
 __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int log_n,
                                                        long long twd, int I0, int pack, int kpack, int share,
@@ -1159,179 +1156,171 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
         }
 
         // digit J of this output prime: the input limb itself (J == I, already NTT form) or the
-        // column-pass output, packed (tile16) when the column pass packed it
+        // column-pass output, packed (tile16) when the column pass packed it.  The digit loop is
+        // instantiated per (packed intermediate, prepared key) pair -- uniform per workgroup -- and
+        // issues the same load instructions every digit (the input limb of J == I read with the
+        // packed shape when the intermediate is packed: its residues are below 2^48 too; the last
+        // digit's prefetch repeated past the end): with a data-dependent load count the compiler
+        // drained every load in flight (vmcnt(0)) at the top of each digit.
         const bool pk = inter_packed(pack, p.q); // uniform per workgroup
-        auto load_digit = [&](int J, u64 (&v)[8]) {
-            if (J == I)
-            {
-                const u64 *src = target + (size_t)J * n + base;
-#pragma unroll
-                for (int e = 0; e < 8; e++) v[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
-            }
-            else if (pk)
-            {
-                const u32 *lo = reinterpret_cast<const u32 *>(inter + ((size_t)(I - I0) * L + J) * n);
-                const unsigned short *hi = reinterpret_cast<const unsigned short *>(lo + n);
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                {
-                    const u32 idx = base + lay(t, e, B_A);
-                    v[e] = (u64)ld_nt<2>(&lo[tile16(idx)]) | ((u64)ld_nt<2>(&hi[tile16h(idx)]) << 32);
-                }
-            }
-            else
-            {
-                const u64 *src = inter + ((size_t)(I - I0) * L + J) * n + base;
-#pragma unroll
-                for (int e = 0; e < 8; e++) v[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
-            }
-        };
-        u64 vin[8];
-        u64 vin2[8]; // MHE_KS_DPF == 2: the digit after next, two loads in flight
-        if (MHE_KS_DPF) load_digit(j0, vin);
-        if (MHE_KS_DPF == 2 && j0 + 1 < j1) load_digit(j0 + 1, vin2);
-        lds_barrier(); // twiddles visible
-
         // key limbs of a digit: issued at the top of the digit, consumed after the digit's NTT (a
         // one-digit-ahead key prefetch measured equal and costs 32 VGPRs)
         // a prepared key (mhe_key_prepare) holds the limbs of primes below 2^48 as a 32-bit plane
         // [n] and a 16-bit plane [n] in natural order (6 of the slot's 8 bytes per residue)
         const bool kpk = kpack && p.q < (1ull << 48) && key[(size_t)ki * n + n - 1] == KEY_PACK_TAG; // uniform
-        auto load_key = [&](int J, u64 (&ka)[8], u64 (&kb)[8]) {
-            const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
-            const u64 *k1 = k0 + kstride;
-            if (kpk)
-            {
-                const u32 *l0 = reinterpret_cast<const u32 *>(k0) + base;
-                const u32 *l1 = reinterpret_cast<const u32 *>(k1) + base;
-                const unsigned short *h0 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k0) + n) + base;
-                const unsigned short *h1 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k1) + n) + base;
-#pragma unroll
-                for (int e = 0; e < 8; e++)
+        auto loop = [&](auto pk_c, auto kpk_c) {
+            constexpr bool PK = decltype(pk_c)::value, KPK = decltype(kpk_c)::value;
+            auto load_digit = [&](int J, u64 (&v)[8]) {
+                const bool self = J == I; // uniform
+                if constexpr (PK)
                 {
-                    const u32 r = lay(t, e, B_A);
-                    ka[e] = (u64)ld_nt<1>(&l0[r]) | ((u64)ld_nt<1>(&h0[r]) << 32);
-                    kb[e] = (u64)ld_nt<1>(&l1[r]) | ((u64)ld_nt<1>(&h1[r]) << 32);
-                }
-            }
-            else
-            {
+                    const u32 *lo = self ? reinterpret_cast<const u32 *>(target + (size_t)J * n)
+                                         : reinterpret_cast<const u32 *>(inter + ((size_t)(I - I0) * L + J) * n);
+                    const unsigned short *hi = self ? reinterpret_cast<const unsigned short *>(target + (size_t)J * n)
+                                                    : reinterpret_cast<const unsigned short *>(lo + n);
 #pragma unroll
-                for (int e = 0; e < 8; e++)
-                {
-                    ka[e] = ld_nt<1>(&k0[base + lay(t, e, B_A)]);
-                    kb[e] = ld_nt<1>(&k1[base + lay(t, e, B_A)]);
-                }
-            }
-        };
-        u64 kk0[8], kk1[8];
-        for (int J = j0; J < j1; J++)
-        {
-            u64 vnext[8];
-            load_key(J, kk0, kk1);
-            if (!MHE_KS_DPF)
-                load_digit(J, vin); // no prefetch: occupancy hides the latency instead
-            else if (MHE_KS_DPF == 2)
-            {
-                if (J + 2 < j1) load_digit(J + 2, vnext);
-            }
-            else if (J + 1 < j1)
-                load_digit(J + 1, vnext);
-            T d[8]; // the digit in the coalesced layout, NTT form
-            if (J != I)
-            {
-                T w[8];
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                {
-                    // the column-pass output: FP and packed, a centred 48-bit residue (fp_to_s48);
-                    // otherwise canonical
-                    if constexpr (FPA)
-                        w[e] = pk ? fp_from_s48(vin[e]) : ar.in52(vin[e]);
-                    else
-                        w[e] = ar.in52(vin[e]);
-                }
-                row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
-                wave_lds_fence(); // the previous digit's reads of x0 come first
-#pragma unroll
-                for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
-                wave_lds_fence();
-#pragma unroll
-                for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
-                row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
-                T *xl = x1;
-                int bl = B_B;
-                if (LOGR > 6)
-                {
-                    wave_lds_fence();
-#pragma unroll
-                    for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
-                    wave_lds_fence();
-#pragma unroll
-                    for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
-                    row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
-                    xl = x0;
-                    bl = 0;
-                }
-                // back to the coalesced layout of the key stream (integer: canonical digits
-                // keep the 128-bit sums exact for any digit count below 2^8)
-                wave_lds_fence();
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                {
-                    if constexpr (FPA)
-                        xl[swz(lay(t, e, bl))] = w[e];
-                    else
-                        xl[swz(lay(t, e, bl))] = ar.canon(w[e]);
-                }
-                wave_lds_fence();
-#pragma unroll
-                for (int e = 0; e < 8; e++) d[e] = xl[swz(lay(t, e, B_A))];
-            }
-            else
-            {
-#pragma unroll
-                for (int e = 0; e < 8; e++) d[e] = ar.in52(vin[e]); // the target: a canonical ciphertext limb
-            }
-            if constexpr (FPA)
-            {
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                {
-                    const double dv = LZ ? d[e] : fp_reduce(d[e], ar.q, ar.qinv);
-                    a0[e] += fp_mulmod_gen(dv, fp_from_u52(kk0[e]), ar.q, ar.qinv); // canonical key residues
-                    a1[e] += fp_mulmod_gen(dv, fp_from_u52(kk1[e]), ar.q, ar.qinv);
-                    if (!LZ && ((J - j0) & 1))
+                    for (int e = 0; e < 8; e++)
                     {
-                        a0[e] = fp_reduce(a0[e], ar.q, ar.qinv);
-                        a1[e] = fp_reduce(a1[e], ar.q, ar.qinv);
+                        const u32 idx = base + lay(t, e, B_A);
+                        const u32 il = self ? 2 * idx : tile16(idx), ih = self ? 4 * idx + 2 : tile16h(idx);
+                        v[e] = (u64)ld_nt<2>(&lo[il]) | ((u64)ld_nt<2>(&hi[ih]) << 32);
                     }
                 }
-            }
-            else
-            {
-#pragma unroll
-                for (int e = 0; e < 8; e++)
+                else
                 {
-                    mac128(a0[e], d[e], kk0[e]);
-                    mac128(a1[e], d[e], kk1[e]);
-                }
-            }
-            if (MHE_KS_DPF == 2)
-            {
+                    const u64 *src = (self ? target + (size_t)J * n : inter + ((size_t)(I - I0) * L + J) * n) + base;
 #pragma unroll
-                for (int e = 0; e < 8; e++)
-                {
-                    vin[e] = vin2[e];
-                    vin2[e] = vnext[e];
+                    for (int e = 0; e < 8; e++) v[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
                 }
-            }
-            else if (MHE_KS_DPF)
+            };
+            auto load_key = [&](int J, u64 (&ka)[8], u64 (&kb)[8]) {
+                const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
+                const u64 *k1 = k0 + kstride;
+                if constexpr (KPK)
+                {
+                    const u32 *l0 = reinterpret_cast<const u32 *>(k0) + base;
+                    const u32 *l1 = reinterpret_cast<const u32 *>(k1) + base;
+                    const unsigned short *h0 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k0) + n) + base;
+                    const unsigned short *h1 = reinterpret_cast<const unsigned short *>(reinterpret_cast<const u32 *>(k1) + n) + base;
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        const u32 r = lay(t, e, B_A);
+                        ka[e] = (u64)ld_nt<1>(&l0[r]) | ((u64)ld_nt<1>(&h0[r]) << 32);
+                        kb[e] = (u64)ld_nt<1>(&l1[r]) | ((u64)ld_nt<1>(&h1[r]) << 32);
+                    }
+                }
+                else
+                {
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        ka[e] = ld_nt<1>(&k0[base + lay(t, e, B_A)]);
+                        kb[e] = ld_nt<1>(&k1[base + lay(t, e, B_A)]);
+                    }
+                }
+            };
+            u64 vin[8];
+            load_digit(j0, vin);
+            lds_barrier(); // twiddles visible
+            u64 kk0[8], kk1[8];
+            for (int J = j0; J < j1; J++)
             {
+                u64 vnext[8];
+                load_key(J, kk0, kk1);
+                load_digit(J + 1 < j1 ? J + 1 : J, vnext); // one digit ahead (the last one again at the end)
+                T d[8]; // the digit in the coalesced layout, NTT form
+                if (J != I)
+                {
+                    T w[8];
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        // the column-pass output: FP and packed, a centred 48-bit residue (fp_to_s48);
+                        // otherwise canonical
+                        if constexpr (FPA)
+                            w[e] = PK ? fp_from_s48(vin[e]) : ar.in52(vin[e]);
+                        else
+                            w[e] = ar.in52(vin[e]);
+                    }
+                    row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
+                    wave_lds_fence(); // the previous digit's reads of x0 come first
+#pragma unroll
+                    for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
+                    wave_lds_fence();
+#pragma unroll
+                    for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
+                    row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
+                    T *xl = x1;
+                    int bl = B_B;
+                    if (LOGR > 6)
+                    {
+                        wave_lds_fence();
+#pragma unroll
+                        for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
+                        wave_lds_fence();
+#pragma unroll
+                        for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
+                        row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
+                        xl = x0;
+                        bl = 0;
+                    }
+                    // back to the coalesced layout of the key stream (integer: canonical digits
+                    // keep the 128-bit sums exact for any digit count below 2^8)
+                    wave_lds_fence();
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        if constexpr (FPA)
+                            xl[swz(lay(t, e, bl))] = w[e];
+                        else
+                            xl[swz(lay(t, e, bl))] = ar.canon(w[e]);
+                    }
+                    wave_lds_fence();
+#pragma unroll
+                    for (int e = 0; e < 8; e++) d[e] = xl[swz(lay(t, e, B_A))];
+                }
+                else
+                {
+#pragma unroll
+                    for (int e = 0; e < 8; e++) d[e] = ar.in52(vin[e]); // the target: a canonical ciphertext limb
+                }
+                if constexpr (FPA)
+                {
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        const double dv = LZ ? d[e] : fp_reduce(d[e], ar.q, ar.qinv);
+                        a0[e] += fp_mulmod_gen(dv, fp_from_u52(kk0[e]), ar.q, ar.qinv); // canonical key residues
+                        a1[e] += fp_mulmod_gen(dv, fp_from_u52(kk1[e]), ar.q, ar.qinv);
+                        if (!LZ && ((J - j0) & 1))
+                        {
+                            a0[e] = fp_reduce(a0[e], ar.q, ar.qinv);
+                            a1[e] = fp_reduce(a1[e], ar.q, ar.qinv);
+                        }
+                    }
+                }
+                else
+                {
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        mac128(a0[e], d[e], kk0[e]);
+                        mac128(a1[e], d[e], kk1[e]);
+                    }
+                }
 #pragma unroll
                 for (int e = 0; e < 8; e++) vin[e] = vnext[e];
             }
-        }
+        };
+        if (pk && kpk)
+            loop(std::true_type{}, std::true_type{});
+        else if (pk)
+            loop(std::true_type{}, std::false_type{});
+        else if (kpk)
+            loop(std::false_type{}, std::true_type{});
+        else
+            loop(std::false_type{}, std::false_type{});
         u64 *o0 = acc + (size_t)I * n + base;
         u64 *o1 = o0 + (size_t)(L + 1) * n;
         if (inv_special && I == L) // uniform per workgroup
