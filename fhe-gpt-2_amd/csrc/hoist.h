@@ -101,7 +101,10 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
         mk[r] = fp_from_u52(P.mask[bz][r][(size_t)pi * n + k[r]]);
         a0[r] = a1[r] = 0.0;
     }
-    auto load = [&](int J, u64 &dv, u64 (&w0)[R], u64 (&w1)[R]) {
+    // the same load instructions every digit (KP: every key prepared / none / per key), so the
+    // compiler counts the waits of the one-digit-ahead prefetch instead of draining it
+    auto load = [&](int J, u64 &dv, u64 (&w0)[R], u64 (&w1)[R], auto kp_tag) {
+        constexpr int KP = decltype(kp_tag)::value;
         dv = (J == I) ? c1[(size_t)J * n + m] : D[(size_t)J * n + bx * 256u + u];
 #pragma unroll
         for (int r = 0; r < R; r++)
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
             const size_t ks = (size_t)P.key_limbs[bz][r] * n;
             const u64 *k0 = kslot(r) + (size_t)(2 * J) * ks;
             const u64 *k1 = k0 + ks;
-            if ((kpm >> r) & 1)
+            if (KP == 1 || (KP == -1 && ((kpm >> r) & 1)))
             {
                 const u32 *l0 = reinterpret_cast<const u32 *>(k0), *l1 = reinterpret_cast<const u32 *>(k1);
                 w0[r] = (u64)l0[k[r]] | ((u64)reinterpret_cast<const unsigned short *>(l0 + n)[k[r]] << 32);
@@ -124,12 +127,13 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
     };
     // lazy sums while L products (|.| < 1.25p each) add up exactly, else a reduction every second digit
     const bool lz = p.q < (1ull << 47) && (double)L * 1.25 * q < 9007199254740992.0;
+    auto run = [&](auto kp_tag) {
     u64 dv, w0[R], w1[R];
-    load(0, dv, w0, w1);
+    load(0, dv, w0, w1, kp_tag);
     for (int J = 0; J < L; J++)
     {
         u64 ndv = 0, nw0[R], nw1[R];
-        if (J + 1 < L) load(J + 1, ndv, nw0, nw1);
+        load(J + 1 < L ? J + 1 : J, ndv, nw0, nw1, kp_tag); // the last digit again at the end
         const double dd = fp_from_u52(dv);
         const TwF c = cm[(size_t)J * K + pi]; // (q_J mod p, / p); (0, 0) for J == I
 #pragma unroll
@@ -153,6 +157,13 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
             w1[r] = nw1[r];
         }
     }
+    };
+    if (kpm == (1u << R) - 1)
+        run(std::integral_constant<int, 1>{});
+    else if (kpm == 0)
+        run(std::integral_constant<int, 0>{});
+    else
+        run(std::integral_constant<int, -1>{});
 #pragma unroll
     for (int r = 0; r < R; r++)
     {
