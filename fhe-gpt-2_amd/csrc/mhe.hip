@@ -237,7 +237,7 @@ struct mhe_ctx
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
     int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
-    int ks_hoist = 1; // batched rotations of one input share its ModUp (hoist.h; MHE_KS_HOIST=0: one ModUp each)
+    int ks_hoist = 0; // batched rotations of one input share their ModUp (hoist.h): MHE_KS_HOIST=1 (off by default until an intermittent wrong image in an 8-image fiber batch is explained)
     TwF *cmodf = nullptr; // [K][K]: (q_j mod q_i, (q_j mod q_i) / q_i) as doubles, j major (hoist.h)
     std::mutex mask_mu;
     std::map<u32, u64 *> masks; // Galois element -> NTT of its negation mask, [K][n] (hoist.h)
@@ -297,7 +297,13 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int en
     Workspace &w = c->ws[st];
     if (w.max_limbs < limbs || w.entries < entries)
     {
-        if (w.base) HIP_TRY(hipFree(w.base));
+        // the stream's queued kernels may still use the old scratch: drain them before it is freed
+        // (and possibly handed out again by the next allocation)
+        if (w.base)
+        {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(w.base));
+        }
         w.base = nullptr;
         const int E = std::max(entries, w.entries);
         const size_t n = c->n, L = std::max(limbs, w.max_limbs);
@@ -2938,10 +2944,16 @@ static int get_hoist(mhe_ctx *c, hipStream_t st, int entries, Workspace **out)
     int r = get_ws(c, st, c->K - 1, &w, MHE_MAXB);
     if (r) return r;
     std::lock_guard<std::mutex> g(c->mu);
+    // sized for MHE_MAXB inputs at the first use, so it never grows under queued kernels
+    entries = MHE_MAXB;
     if (w->hoist_entries < entries)
     {
         HIP_TRY(hipSetDevice(c->device));
-        if (w->hoist_base) HIP_TRY(hipFree(w->hoist_base));
+        if (w->hoist_base)
+        {
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipFree(w->hoist_base));
+        }
         w->hoist_base = nullptr;
         w->hoist_entries = 0;
         const size_t per = (size_t)c->K * (c->K - 1) * c->n, pacc = (size_t)2 * c->K * c->n;
