@@ -55,26 +55,15 @@ __device__ __forceinline__ u32 galois_src(u32 k, u32 elt, int log_n)
 // consecutive).  Each D word is read once (coalesced) for all the item's rotations: rotation r
 // uses it at its output slot k = pi_{g_r^-1}(m) (pi_g^-1 = pi_{g^-1}), and that slot's key words,
 // mask word and key products are read / written there -- inside one 256-slot row, since pi maps
-// rows to rows.  share: the items of one tile run on one XCD (ids 8 apart) when they rotate by the
-// same keys, so the key rows are fetched from HBM once for all of them.  FP64 arithmetic (every
-// prime below 2^51); cm[J * K + pi] = (q_J mod p, (q_J mod p) / p).
+// rows to rows.  FP64 arithmetic (every prime below 2^51); cm[J * K + pi] = (q_J mod p, (q_J mod p) / p).
 // R (the item's rotation count) is a template parameter so the digit loop is straight-line code: all
 // 2R key words and the D word of digit J + 1 are in flight while digit J's products run.  Used when
 // the items of a launch rotate by different keys; k_ks_hoist_mac_sh below when they share them.
 template <int R>
 __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtrs P, const PrimeDev *__restrict__ primes,
-                                                         const TwF *__restrict__ cm, int L, int K, int log_n, int share)
+                                                         const TwF *__restrict__ cm, int L, int K, int log_n)
 {
-    u32 bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-    if (share)
-    {
-        const u32 X = gridDim.x, Y = gridDim.y, Bn = gridDim.z;
-        const u32 id = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
-        const u32 r = id % (8 * Bn), tile = (id / (8 * Bn)) * 8 + r % 8;
-        bz = r / 8;
-        bx = tile % X;
-        by = tile / X;
-    }
+    const u32 bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
     if (*P.flag[bz]) return; // uniform: the classic path computes this item's rotations
     const size_t n = (size_t)1 << log_n;
     const int I = (int)by;

@@ -195,6 +195,9 @@ struct Workspace
     // key-switch kernels on this stream, read back by mhe_kernel_time
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
     size_t ev_used[2] = { 0, 0 };
+    size_t bytes = 0, hoist_bytes = 0; // device bytes of base / hoist_base (mhe_scratch_bytes)
+    int hoist_limbs = 0;                // the hoisting buffers' level (per-input ModUp of up to this many limbs)
+    std::mutex mu;                      // growth of this stream's buffers
 };
 
 enum TimedKernel
@@ -237,7 +240,9 @@ struct mhe_ctx
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
     int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
-    int ks_hoist = 0; // batched rotations of one input share their ModUp (hoist.h): MHE_KS_HOIST=1 (off by default until an intermittent wrong image in an 8-image fiber batch is explained)
+    int ks_hoist = 0; // batched rotations of one input share their ModUp (hoist.h): MHE_KS_HOIST=1 or mhe_ctx_set_hoist
+    int hoist_check = 0; // recompute every hoisted rotation by the classic path and compare (mhe_ctx_set_hoist)
+    std::atomic<unsigned long long> hoist_rot{ 0 }, hoist_mac{ 0 }, hoist_bad{ 0 }; // mhe_hoist_stats
     TwF *cmodf = nullptr; // [K][K]: (q_j mod q_i, (q_j mod q_i) / q_i) as doubles, j major (hoist.h)
     std::mutex mask_mu;
     std::map<u32, u64 *> masks; // Galois element -> NTT of its negation mask, [K][n] (hoist.h)
@@ -291,20 +296,28 @@ static void timing_end(hipEvent_t *pair, hipStream_t st)
 }
 
 // The scratch of stream st, for ciphertexts of up to `limbs` limbs and `entries` batch entries.
-static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int entries = 1)
+// The context lock only guards the map; growing one stream's scratch (which drains that stream
+// first: its queued kernels may still use the old buffers) holds that workspace's own lock, so
+// other threads' streams are not held up by the drain.
+static Workspace &ws_of(mhe_ctx *c, hipStream_t st)
 {
     std::lock_guard<std::mutex> g(c->mu);
-    Workspace &w = c->ws[st];
+    return c->ws[st];
+}
+
+static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int entries = 1)
+{
+    Workspace &w = ws_of(c, st);
+    std::lock_guard<std::mutex> g(w.mu);
     if (w.max_limbs < limbs || w.entries < entries)
     {
-        // the stream's queued kernels may still use the old scratch: drain them before it is freed
-        // (and possibly handed out again by the next allocation)
         if (w.base)
         {
             HIP_TRY(hipStreamSynchronize(st));
             HIP_TRY(hipFree(w.base));
         }
         w.base = nullptr;
+        w.bytes = 0;
         const int E = std::max(entries, w.entries);
         const size_t n = c->n, L = std::max(limbs, w.max_limbs);
         const size_t Lc = L < 3 ? 3 : L;
@@ -317,6 +330,7 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int en
             w.entries = 0;
             return fail(MHE_ERR_MEMORY, "workspace allocation failed");
         }
+        w.bytes = words * sizeof(u64);
         for (int i = 0; i < E; i++)
         {
             w.e[i].coeff = w.base + (size_t)i * per;
@@ -2379,6 +2393,52 @@ MHE_EXPORT int mhe_ctx_set_timing(mhe_ctx *c, int on)
     return MHE_OK;
 }
 
+static bool hoist_ok(const mhe_ctx *c);
+
+MHE_EXPORT int mhe_ctx_set_hoist(mhe_ctx *c, int on, int check)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    c->ks_hoist = on ? 1 : 0;
+    c->hoist_check = check ? 1 : 0;
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_ctx_get_hoist(mhe_ctx *c, int *on, int *check)
+{
+    if (!valid_ctx(c) || !on || !check) return fail(MHE_ERR_ARG, "invalid argument");
+    *on = hoist_ok(c) ? 1 : 0;
+    *check = c->hoist_check;
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_hoist_stats(mhe_ctx *c, uint64_t *rotations, uint64_t *mac_launches, uint64_t *check_mismatches,
+                               int reset)
+{
+    if (!valid_ctx(c) || !rotations || !mac_launches || !check_mismatches) return fail(MHE_ERR_ARG, "invalid argument");
+    *rotations = reset ? c->hoist_rot.exchange(0) : c->hoist_rot.load();
+    *mac_launches = reset ? c->hoist_mac.exchange(0) : c->hoist_mac.load();
+    *check_mismatches = reset ? c->hoist_bad.exchange(0) : c->hoist_bad.load();
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_scratch_bytes(mhe_ctx *c, uint64_t *workspace, uint64_t *hoisting, uint64_t *masks, int *streams)
+{
+    if (!valid_ctx(c) || !workspace || !hoisting || !masks || !streams) return fail(MHE_ERR_ARG, "invalid argument");
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        *workspace = *hoisting = 0;
+        for (auto &kv : c->ws)
+        {
+            *workspace += kv.second.bytes;
+            *hoisting += kv.second.hoist_bytes;
+        }
+        *streams = (int)c->ws.size();
+    }
+    std::lock_guard<std::mutex> g(c->mask_mu);
+    *masks = (uint64_t)c->masks.size() * c->K * c->n * sizeof(u64);
+    return MHE_OK;
+}
+
 MHE_EXPORT int mhe_kernel_time(mhe_ctx *c, int kernel, double *total_ms, int *launches)
 {
     if (!valid_ctx(c) || kernel < 0 || kernel > 1 || !total_ms || !launches) return fail(MHE_ERR_ARG, "invalid argument");
@@ -2423,6 +2483,14 @@ MHE_EXPORT int mhe_stream_destroy(mhe_ctx *c, void *stream)
         {
             (void)hipStreamSynchronize(S(stream));
             if (it->second.base) (void)hipFree(it->second.base);
+            if (it->second.hoist_base) (void)hipFree(it->second.hoist_base);
+            if (it->second.flags) (void)hipFree(it->second.flags);
+            for (auto &v : it->second.ev)
+                for (auto &e : v)
+                {
+                    (void)hipEventDestroy(e.first);
+                    (void)hipEventDestroy(e.second);
+                }
             c->ws.erase(it);
         }
     }
@@ -2938,16 +3006,17 @@ MHE_EXPORT int mhe_apply_galois_to(mhe_ctx *c, const uint64_t *in, uint64_t *out
 // ------------------------------------------------------------------ hoisted rotations (hoist.h)
 // The ModUp buffers of up to `entries` hoisted inputs on stream st ([K][K-1][n] each: every level),
 // the key products of up to MHE_MAXB * MHE_HOIST_R of their rotations and the inputs' flags.
-static int get_hoist(mhe_ctx *c, hipStream_t st, int entries, Workspace **out)
+static int get_hoist(mhe_ctx *c, hipStream_t st, int entries, int ws_entries, int L, Workspace **out)
 {
     Workspace *w;
-    int r = get_ws(c, st, c->K - 1, &w, MHE_MAXB);
+    int r = get_ws(c, st, c->K - 1, &w, std::max(entries, ws_entries));
     if (r) return r;
-    std::lock_guard<std::mutex> g(c->mu);
-    // sized for MHE_MAXB inputs at the first use, so it never grows under queued kernels
-    entries = MHE_MAXB;
-    if (w->hoist_entries < entries)
+    std::lock_guard<std::mutex> g(w->mu);
+    // per input [L+1][L][n] (the pass's level), the key products of up to MHE_MAXB * MHE_HOIST_R
+    // rotations at that level; grown (after draining the stream) when a pass needs more
+    if (w->hoist_entries < entries || w->hoist_limbs < L)
     {
+        const int E = std::max(entries, w->hoist_entries), HL = std::max(L, w->hoist_limbs);
         HIP_TRY(hipSetDevice(c->device));
         if (w->hoist_base)
         {
@@ -2956,13 +3025,17 @@ static int get_hoist(mhe_ctx *c, hipStream_t st, int entries, Workspace **out)
         }
         w->hoist_base = nullptr;
         w->hoist_entries = 0;
-        const size_t per = (size_t)c->K * (c->K - 1) * c->n, pacc = (size_t)2 * c->K * c->n;
+        w->hoist_limbs = 0;
+        w->hoist_bytes = 0;
+        const size_t per = (size_t)(HL + 1) * HL * c->n, pacc = (size_t)2 * (HL + 1) * c->n;
         const int na = MHE_MAXB * MHE_HOIST_R;
-        if (hipMalloc(&w->hoist_base, ((size_t)entries * per + (size_t)na * pacc) * sizeof(u64)) != hipSuccess)
-            return fail(MHE_ERR_MEMORY, "workspace allocation failed");
-        for (int i = 0; i < entries; i++) w->hoist[i] = w->hoist_base + (size_t)i * per;
-        for (int i = 0; i < na; i++) w->hacc[i] = w->hoist_base + (size_t)entries * per + (size_t)i * pacc;
-        w->hoist_entries = entries;
+        const size_t bytes = ((size_t)E * per + (size_t)na * pacc) * sizeof(u64);
+        if (hipMalloc(&w->hoist_base, bytes) != hipSuccess) return fail(MHE_ERR_MEMORY, "workspace allocation failed");
+        for (int i = 0; i < E; i++) w->hoist[i] = w->hoist_base + (size_t)i * per;
+        for (int i = 0; i < na; i++) w->hacc[i] = w->hoist_base + (size_t)E * per + (size_t)i * pacc;
+        w->hoist_entries = E;
+        w->hoist_limbs = HL;
+        w->hoist_bytes = bytes;
     }
     if (!w->flags && hipMalloc(&w->flags, MHE_MAXB * sizeof(int)) != hipSuccess)
         return fail(MHE_ERR_MEMORY, "workspace allocation failed");
@@ -3010,7 +3083,7 @@ static void launch_hoist_mac(int R, dim3 grid, hipStream_t st, const HoistPtrs &
 {
     switch (R)
     {
-#define HM(r) case r: hipLaunchKernelGGL((k_ks_hoist_mac<r>), grid, dim3(256), 0, st, hp, primes, cm, L, K, log_n, 0); break;
+#define HM(r) case r: hipLaunchKernelGGL((k_ks_hoist_mac<r>), grid, dim3(256), 0, st, hp, primes, cm, L, K, log_n); break;
         HM(1) HM(2) HM(3) HM(4) HM(5) HM(6) HM(7) HM(8)
 #undef HM
     }
@@ -3032,6 +3105,86 @@ static bool hoist_ok(const mhe_ctx *c)
            c->cmodf;
 }
 
+// counts words that differ between a and b (mhe_ctx_set_hoist's check); first[0] = lowest index
+__global__ void k_cmp_words(const u64 *__restrict__ a, const u64 *__restrict__ b, size_t total,
+                            unsigned long long *bad)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total || a[i] == b[i]) return;
+    atomicAdd(bad, 1ull);
+    atomicMin(bad + 1, (unsigned long long)i);
+}
+
+// The check of a hoisted pass: every rotation again by SEAL's order (permutation, then the classic
+// key switch of the permuted c1) into scratch, compared word for word with the hoisted output.
+static int hoist_check_pass(mhe_ctx *c, const u64 *const *in, int count, const int *ent_in, u64 *const *out,
+                            const u32 *elts, const u64 *const *keys, const int *key_limbs, int L, hipStream_t st,
+                            const int *flags)
+{
+    const size_t ps = (size_t)L * c->n;
+    u64 *tmp = nullptr;
+    unsigned long long *cnt = nullptr;
+    HIP_TRY(hipSetDevice(c->device));
+    if (hipMalloc(&tmp, (size_t)MHE_MAXB * 2 * ps * sizeof(u64)) != hipSuccess)
+        return fail(MHE_ERR_MEMORY, "hoist check: allocation failed");
+    if (hipMalloc(&cnt, 2 * MHE_MAXB * sizeof(unsigned long long) + MHE_MAXB * sizeof(int)) != hipSuccess)
+    {
+        (void)hipFree(tmp);
+        return fail(MHE_ERR_MEMORY, "hoist check: allocation failed");
+    }
+    int *fl = reinterpret_cast<int *>(cnt + 2 * MHE_MAXB);
+    int r = MHE_OK;
+    for (int i0 = 0; i0 < count && r == MHE_OK; i0 += MHE_MAXB)
+    {
+        const int B = std::min(MHE_MAXB, count - i0);
+        GalPtrs gp{};
+        KsJob jobs[MHE_MAXB];
+        std::vector<unsigned long long> init(2 * MHE_MAXB);
+        for (int e = 0; e < B; e++)
+        {
+            const int i = i0 + e;
+            u64 *t = tmp + (size_t)e * 2 * ps;
+            gp.in[e] = in[ent_in[i]];
+            gp.out[e] = t;
+            gp.elt[e] = elts[i];
+            jobs[e] = KsJob{ t, t + ps, keys[i], key_limbs[i], nullptr };
+            init[2 * e] = 0;
+            init[2 * e + 1] = ~0ull;
+        }
+        HIP_TRY(hipMemcpyAsync(cnt, init.data(), init.size() * sizeof(unsigned long long), hipMemcpyHostToDevice, st));
+        for (int e = 0; e < B; e++)
+            HIP_TRY(hipMemcpyAsync(fl + e, flags + ent_in[i0 + e], sizeof(int), hipMemcpyDeviceToDevice, st));
+        hipLaunchKernelGGL(k_galois_b, dim3((unsigned)((2 * ps + 255) / 256), (unsigned)B), dim3(256), 0, st, gp,
+                           c->log_n, 2 * ps);
+        HIP_LAUNCH_CHECK();
+        if ((r = run_switch_key_batch(c, jobs, B, L, st, 1))) break;
+        for (int e = 0; e < B; e++)
+            hipLaunchKernelGGL(k_cmp_words, dim3((unsigned)((2 * ps + 255) / 256)), dim3(256), 0, st,
+                               tmp + (size_t)e * 2 * ps, out[i0 + e], 2 * ps, cnt + 2 * e);
+        HIP_LAUNCH_CHECK();
+        std::vector<unsigned long long> got(2 * MHE_MAXB);
+        std::vector<int> hf(MHE_MAXB);
+        HIP_TRY(hipMemcpyAsync(got.data(), cnt, got.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(hf.data(), fl, MHE_MAXB * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int e = 0; e < B; e++)
+        {
+            if (!got[2 * e]) continue;
+            c->hoist_bad += got[2 * e];
+            const unsigned long long f = got[2 * e + 1];
+            fprintf(stderr,
+                    "[hoist check] stream %p L %d entry %d/%d (input %d, elt %u, key %p, key_limbs %d, zero flag %d): "
+                    "%llu words differ, first at poly %llu limb %llu slot %llu\n",
+                    (void *)st, L, i0 + e, count, ent_in[i0 + e], elts[i0 + e], (const void *)keys[i0 + e],
+                    key_limbs[i0 + e], hf[e], got[2 * e], f / ps, (f % ps) / c->n, f % c->n);
+        }
+    }
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(tmp);
+    (void)hipFree(cnt);
+    return r;
+}
+
 // Rotations of H <= MHE_MAXB inputs at L limbs, entry i rotating input ent_in[i] (index into in)
 // by elts[i] into out[i]: ModUp of every input once (INTT -> column pass -> row pass, canonical
 // D in the hoist buffers, plus the zero scan), then per chunk of entries the permutation of c0 /
@@ -3042,7 +3195,7 @@ static int run_galois_hoisted(mhe_ctx *c, const u64 *const *in, int H, int count
                               hipStream_t st)
 {
     Workspace *w;
-    int r = get_hoist(c, st, H, &w);
+    int r = get_hoist(c, st, H, std::min(count, MHE_MAXB), L, &w); // step 3 uses up to MHE_MAXB entry slots
     if (r) return r;
     const int log_n = c->log_n;
     const size_t n = c->n, ps = (size_t)L * n;
@@ -3150,6 +3303,7 @@ static int run_galois_hoisted(mhe_ctx *c, const u64 *const *in, int H, int count
             const int per_wg = r0.size() <= 4 ? 8 : 4; // 4 lane groups x items per lane
             launch_hoist_mac_sh((int)r0.size(), dim3((unsigned)(n / 256), (unsigned)(L + 1), (unsigned)((hs.Z + per_wg - 1) / per_wg)),
                                 st, hs, c->primes, c->cmodf, L, c->K, log_n);
+            c->hoist_mac++;
             timing_end(tm, st);
         }
         std::vector<std::pair<int, std::vector<int>>> left;
@@ -3188,6 +3342,7 @@ static int run_galois_hoisted(mhe_ctx *c, const u64 *const *in, int H, int count
             const dim3 grid((unsigned)(n / 256), (unsigned)(L + 1), (unsigned)Z);
             hipEvent_t *tm = timing_slot(c, w, TK_KS_ROW_MAC, st);
             launch_hoist_mac(hp.R[0], grid, st, hp, c->primes, c->cmodf, L, c->K, log_n);
+            c->hoist_mac++;
             timing_end(tm, st);
             z0 = zn;
         }
@@ -3249,6 +3404,8 @@ static int run_galois_hoisted(mhe_ctx *c, const u64 *const *in, int H, int count
         HIP_LAUNCH_CHECK();
         run_moddown(c, jobs, B, L, w, 0, 1, st, accs);
     }
+    c->hoist_rot += (unsigned long long)count;
+    if (c->hoist_check) return hoist_check_pass(c, in, count, ent_in, out, elts, keys, key_limbs, L, st, w->flags);
     return MHE_OK;
 }
 
@@ -3411,7 +3568,12 @@ MHE_EXPORT int mhe_switch_key_batch(mhe_ctx *c, int count, uint64_t *const *ct, 
     if (r) return r;
     if (count < 0 || (count && (!ct || !target || !keys || !key_limbs))) return fail(MHE_ERR_ARG, "invalid argument");
     for (int i = 0; i < count; i++)
+    {
         if (!ct[i] || !target[i] || !keys[i]) return fail(MHE_ERR_ARG, "target_iter");
+        // every key before the first launch: the switches work in place, chunk by chunk
+        if (key_limbs[i] < limbs + 1 || key_limbs[i] > c->K)
+            return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
+    }
     for (int i0 = 0; i0 < count; i0 += MHE_MAXB)
     {
         const int B = std::min(MHE_MAXB, count - i0);

@@ -50,6 +50,10 @@ struct ResNetResult
     double seconds = 0;         // total_time of the reference: encryption excluded, decryption excluded
     double boot_seconds = 0, relu_seconds = 0, linear_seconds = 0;
     int bootstraps = 0;
+    // 64-bit digest of the output ciphertext's words, level and scale (FNV-1a over the u64 words):
+    // equal digests mean bit-identical ciphertexts (the FiberBatch check compares an image batched
+    // with the same image run alone)
+    std::uint64_t digest = 0;
 };
 
 class ResNetRunner
@@ -65,8 +69,11 @@ public:
         import
     };
     // comp_dir: directory holding d<alpha>.txt of the approximate ReLU (mhe_comp.h)
+    // rng_seed != 0: the context's PRNG factory uses that fixed seed for every generator it makes
+    // (SEAL's Blake2xbPRNGFactory(default_seed), a debugging mode: keys and every encryption become
+    // deterministic, so two runs of one image give the same words; never for real use)
     ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir,
-                 KeySource keys = KeySource::generate);
+                 KeySource keys = KeySource::generate, std::uint64_t rng_seed = 0);
     ~ResNetRunner();
     // one image: 3 x 32 x 32 values (channel-major, the test_values.txt order), before /B
     ResNetResult infer(const std::vector<double> &image);
@@ -92,6 +99,12 @@ public:
     double key_traffic_bytes(bool reset);
     // operations of the runner's key-level context since the last reset, per level (mhe_op_counts)
     std::vector<std::uint64_t> op_counts(int kind, bool reset);
+    // hoisted rotations of the runner's engine (mhe_ctx_set_hoist): on / off, with the classic-path
+    // check; stats: (hoisted rotations, hoisted MAC launches, differing words under check) since reset
+    void set_hoist(bool on, bool check = false);
+    std::vector<std::uint64_t> hoist_stats(bool reset);
+    // bytes of device scratch the engine holds (per-stream workspaces, hoisting buffers, Galois masks)
+    std::size_t scratch_bytes() const;
     // the evaluation keys are in the engine's prepared format (mhe_key_prepare) rather than SEAL's
     bool keys_prepared() const { return keys_prepared_; }
     // resnet_plain_logits with this runner's parameters

@@ -741,6 +741,9 @@ public:
                     std::size_t stack_bytes = (std::size_t)8 << 20);
     static std::size_t last_rounds();  // merged rounds of the calling thread's last run()
     static std::size_t last_merged();  // member calls those rounds merged
+    // index of the fiber running on the calling thread, -1 outside a FiberBatch (state that the
+    // reference keeps per thread must be kept per fiber: the fibers of a thread interleave)
+    static long current();
 };
 class Lockstep
 {

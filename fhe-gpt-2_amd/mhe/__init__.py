@@ -32,6 +32,12 @@ SIGNATURES = {
     "mhe_free": (ctypes.c_int, [vp, vp]),
     "mhe_ctx_set_timing": (ctypes.c_int, [vp, ctypes.c_int]),
     "mhe_kernel_time": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+    "mhe_ctx_set_hoist": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
+    "mhe_ctx_get_hoist": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "mhe_hoist_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "mhe_scratch_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]),
     "mhe_malloc_async": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t, vp]),
     "mhe_free_async": (ctypes.c_int, [vp, vp, vp]),
     "mhe_memcpy_h2d": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp]),
@@ -200,6 +206,29 @@ class Engine:
 
     def synchronize(self):
         _check(lib().mhe_stream_sync(self._h, self.stream()))
+
+    def set_hoist(self, on, check=False):
+        """mhe_ctx_set_hoist: hoisted rotations on / off for this context (check: every hoisted
+        rotation is recomputed by the classic path and compared, mismatches counted)."""
+        _check(lib().mhe_ctx_set_hoist(self._h, 1 if on else 0, 1 if check else 0))
+
+    def hoist(self):
+        """(effective hoisting on, check on) of this context."""
+        on, chk = ctypes.c_int(), ctypes.c_int()
+        _check(lib().mhe_ctx_get_hoist(self._h, ctypes.byref(on), ctypes.byref(chk)))
+        return bool(on.value), bool(chk.value)
+
+    def hoist_stats(self, reset=False):
+        """(hoisted rotations, hoisted key-MAC launches, words that differed under check)."""
+        r, m, b = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().mhe_hoist_stats(self._h, ctypes.byref(r), ctypes.byref(m), ctypes.byref(b), 1 if reset else 0))
+        return r.value, m.value, b.value
+
+    def scratch_bytes(self):
+        """mhe_scratch_bytes: (workspace, hoisting, Galois masks) device bytes and the stream count."""
+        w, h, m, n = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        _check(lib().mhe_scratch_bytes(self._h, ctypes.byref(w), ctypes.byref(h), ctypes.byref(m), ctypes.byref(n)))
+        return w.value, h.value, m.value, n.value
 
     def reserve(self, max_limbs):
         _check(lib().mhe_ctx_reserve(self._h, max_limbs, self.stream()))

@@ -1638,9 +1638,16 @@ bool Bootstrapper::PtKey::operator<(const PtKey &o) const
 namespace
 {
 std::mutex g_pt_mu;
-// the input scale of the bootstrap running on this thread (Bootstrapper objects are shared by the
-// threads of an image batch, like the reference's OpenMP team shares bootstrapper_1..3)
-thread_local double tl_initial_scale = 0;
+// the input scale of the bootstrap running on this thread -- and fiber: the fibers of a
+// seal::FiberBatch interleave on one thread at every merge point (Bootstrapper objects are shared by
+// the threads of an image batch, like the reference's OpenMP team shares bootstrapper_1..3)
+thread_local std::vector<double> tl_initial_scales;
+double &initial_scale_slot()
+{
+    const std::size_t i = (std::size_t)(seal::FiberBatch::current() + 1);
+    if (tl_initial_scales.size() <= i) tl_initial_scales.resize(i + 1, 0.0);
+    return tl_initial_scales[i];
+}
 bool pt_cache_on()
 {
     const char *e = std::getenv("MHE_BOOT_PT_CACHE");
@@ -1882,7 +1889,7 @@ void Bootstrapper::sfl_half_3(Ciphertext &rtncipher, Ciphertext &cipher)
     const double mod_zero = (double)modulus[0].value();
     const double curr_mod = (double)modulus[curr_level].value();
     // fftcoeff3_scale = fftcoeff3 * curr_mod * q0 * final_scale / (2 s^2 initial_scale)
-    const double init = tl_initial_scale != 0 ? tl_initial_scale : initial_scale;
+    const double init = initial_scale_slot() != 0 ? initial_scale_slot() : initial_scale;
     const double coeff_scale = curr_mod * mod_zero * final_scale / (2 * tmpct2.scale() * tmpct2.scale() * init);
     bsgs_linear_transform(rtncipher, tmpct2, totlen3, basicstep3, (int)logn + 1, fftcoeff3[slot_index],
                           coeff_scale);
@@ -1940,7 +1947,7 @@ void Bootstrapper::sfl_full_common(Ciphertext &rtncipher, Ciphertext &cipher, bo
     const auto curr_level = context.get_context_data(tmpct2.parms_id())->chain_index();
     const double mod_zero = (double)modulus[0].value();
     const double curr_mod = (double)modulus[curr_level].value();
-    const double init = tl_initial_scale != 0 ? tl_initial_scale : initial_scale;
+    const double init = initial_scale_slot() != 0 ? initial_scale_slot() : initial_scale;
     const double coeff_scale =
         curr_mod * mod_zero * final_scale / ((half ? 2 : 1) * tmpct2.scale() * tmpct2.scale() * init);
     rotated_bsgs_linear_transform(rtncipher, tmpct2, totlen3, basicstep3, (int)logn, fftcoeff3[slot_index],
@@ -2026,7 +2033,7 @@ void Bootstrapper::bootstrap_full_3(Ciphertext &rtncipher, Ciphertext &cipher)
 void Bootstrapper::bootstrap_3(Ciphertext &rtncipher, Ciphertext &cipher)
 {
     // Bootstrapper.cpp:3421-3425
-    tl_initial_scale = cipher.scale();
+    initial_scale_slot() = cipher.scale();
     if (logn != logNh) throw std::logic_error("complex sparse-slot bootstrapping is not provided: use bootstrap_real_3");
     bootstrap_full_3(rtncipher, cipher);
 }
@@ -2136,7 +2143,7 @@ void Bootstrapper::bootstrap_sparse_real_3(Ciphertext &rtncipher, Ciphertext &ci
     {
         const auto curr_level = context.get_context_data(modrtn.parms_id())->chain_index();
         const double mod_zero = (double)modulus[0].value(), curr_mod = (double)modulus[curr_level].value();
-        const double init = tl_initial_scale != 0 ? tl_initial_scale : initial_scale;
+        const double init = initial_scale_slot() != 0 ? initial_scale_slot() : initial_scale;
         const double scale_adj = curr_mod * mod_zero * final_scale / (modrtn.scale() * modrtn.scale() * init);
         std::vector<cd> stc_vec(Nh, 0.0);
         for (long i = 0; i < Nh; i++) stc_vec[i] = i % 2 == 0 ? cd(scale_adj) : cd(0, 1.0) * scale_adj;
@@ -2159,7 +2166,7 @@ void Bootstrapper::bootstrap_sparse_real_3(Ciphertext &rtncipher, Ciphertext &ci
 void Bootstrapper::bootstrap_real_3(Ciphertext &rtncipher, Ciphertext &cipher)
 {
     // Bootstrapper.cpp:3421-3425 (initial_scale kept per thread)
-    tl_initial_scale = cipher.scale();
+    initial_scale_slot() = cipher.scale();
     if (logn == logNh)
         bootstrap_full_real_3(rtncipher, cipher);
     else

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdint>
+#include <cstring>
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
@@ -295,7 +296,7 @@ struct ResNetRunner::Impl
 };
 
 ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir,
-                           KeySource keys)
+                           KeySource keys, std::uint64_t rng_seed)
     : impl_(std::make_unique<Impl>())
 {
     t0_ = std::chrono::steady_clock::now();
@@ -318,6 +319,12 @@ ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, co
     m.parms.set_poly_modulus_degree(poly_modulus_degree);
     m.parms.set_coeff_modulus(CoeffModulus::Create(poly_modulus_degree, coeff_bit_vec));
     m.parms.set_secret_key_hamming_weight(192);
+    if (rng_seed)
+    {
+        prng_seed_type seed{};
+        seed[0] = rng_seed;
+        m.parms.set_random_generator(std::make_shared<Blake2xbPRNGFactory>(seed));
+    }
     m.context = std::make_unique<SEALContext>(m.parms);
     m.encoder = std::make_unique<CKKSEncoder>(*m.context);
     m.evaluator = std::make_unique<Evaluator>(*m.context, *m.encoder);
@@ -511,6 +518,28 @@ double ResNetRunner::key_traffic_bytes(bool reset)
     const int rc = mhe_key_traffic(eng, &b, reset ? 1 : 0) | mhe_key_traffic_prepared(eng, &other, reset ? 1 : 0);
     if (rc != 0) throw std::runtime_error(mhe_last_error());
     return (double)b;
+}
+
+void ResNetRunner::set_hoist(bool on, bool check)
+{
+    if (mhe_ctx_set_hoist(impl_->context->engine(), on ? 1 : 0, check ? 1 : 0) != 0)
+        throw std::runtime_error(mhe_last_error());
+}
+
+std::vector<std::uint64_t> ResNetRunner::hoist_stats(bool reset)
+{
+    std::vector<std::uint64_t> v(3, 0);
+    if (mhe_hoist_stats(impl_->context->engine(), &v[0], &v[1], &v[2], reset ? 1 : 0) != 0)
+        throw std::runtime_error(mhe_last_error());
+    return v;
+}
+
+std::size_t ResNetRunner::scratch_bytes() const
+{
+    std::uint64_t w = 0, h = 0, m = 0;
+    int st = 0;
+    if (mhe_scratch_bytes(impl_->context->engine(), &w, &h, &m, &st) != 0) throw std::runtime_error(mhe_last_error());
+    return (std::size_t)(w + h + m);
 }
 
 std::vector<std::uint64_t> ResNetRunner::op_counts(int kind, bool reset)
@@ -721,6 +750,27 @@ ResNetResult ResNetRunner::infer(const std::vector<double> &img, std::ostream *l
     res.relu_seconds = t_relu;
     res.linear_seconds = res.seconds - t_boot - t_relu;
 
+    {
+        // FNV-1a over the output ciphertext's words, its size, level and scale bits
+        const Ciphertext &out = cnn.cipher();
+        std::uint64_t h = 0xcbf29ce484222325ull;
+        auto mix = [&](std::uint64_t v) {
+            for (int b = 0; b < 8; b++)
+            {
+                h ^= (v >> (8 * b)) & 0xff;
+                h *= 0x100000001b3ull;
+            }
+        };
+        const std::uint64_t *w = out.store().host();
+        for (std::size_t i = 0; i < out.store().words(); i++) mix(w[i]);
+        double sc = out.scale();
+        std::uint64_t sb;
+        std::memcpy(&sb, &sc, sizeof sb);
+        mix(out.size());
+        mix(out.coeff_modulus_size());
+        mix(sb);
+        res.digest = h;
+    }
     Plaintext plain;
     decryptor.decrypt(cnn.cipher(), plain);
     std::vector<std::complex<double>> rtn_vec;

@@ -2414,6 +2414,11 @@ void FiberBatch::run(std::size_t count, const std::function<void(std::size_t)> &
         if (f.err) std::rethrow_exception(f.err);
 }
 
+long FiberBatch::current()
+{
+    return (tl_fb && tl_fb->current) ? (long)tl_fb->current->idx : -1;
+}
+
 std::size_t FiberBatch::last_rounds()
 {
     return tl_fb_rounds;
@@ -2678,6 +2683,16 @@ void Evaluator::relinearize_inplace_many(const std::vector<Ciphertext *> &encryp
         if (c->size() == 3) groups[lv.L].push_back(c);
     }
     void *s = context_.stream();
+    // every group's key first (a missing or truncated key throws before any entry is changed: the
+    // switches below work in place, and a merged Lockstep / FiberBatch call that throws re-runs its
+    // members one by one, lockstep_execute)
+    std::map<std::size_t, std::pair<const std::uint64_t *, int>> gkey;
+    for (auto &g : groups)
+    {
+        std::size_t kl = 0;
+        const std::uint64_t *k = relin_keys.key_for(RelinKeys::get_index(2), g.first, s, kl);
+        gkey[g.first] = { k, (int)kl };
+    }
     for (auto &g : groups)
     {
         std::vector<Ciphertext *> &v = g.second;
@@ -2688,9 +2703,8 @@ void Evaluator::relinearize_inplace_many(const std::vector<Ciphertext *> &encryp
         std::vector<int> kls;
         for (Ciphertext *c : v)
         {
-            std::size_t kl = 0;
-            keys.push_back(relin_keys.key_for(RelinKeys::get_index(2), L, s, kl));
-            kls.push_back((int)kl);
+            keys.push_back(gkey[L].first);
+            kls.push_back(gkey[L].second);
             std::uint64_t *d = c->store().dev_write(s);
             ct.push_back(d);
             target.push_back(d + 2 * L * c->poly_modulus_degree());
@@ -2789,46 +2803,48 @@ void Evaluator::rescale_to_next_inplace_many(const std::vector<Ciphertext *> &en
                     level_of(context_, next->parms_id(), "parms_id"));
         groups[{ lv.L, c->size() }].push_back(c);
     }
+    // every group's results go to fresh buffers first and are committed after the last launch, so
+    // a failing group leaves every entry unchanged (a merged Lockstep / FiberBatch call that throws
+    // re-runs its members one by one, lockstep_execute)
     void *s = context_.stream();
+    struct Staged
+    {
+        Ciphertext *c;
+        PolyStore out;
+        parms_id_type next;
+        double scale;
+        std::size_t size;
+    };
+    std::vector<Staged> staged;
+    staged.reserve(encrypted.size());
     for (auto &g : groups)
     {
         std::vector<Ciphertext *> &v = g.second;
-        if (v.size() < 2)
-        {
-            for (Ciphertext *c : v) rescale_to_next_inplace(*c);
-            continue;
-        }
         const std::size_t size = g.first.second;
-        std::vector<PolyStore> outs(v.size());
         std::vector<const std::uint64_t *> in;
         std::vector<std::uint64_t *> out;
-        std::vector<double> scales;
-        parms_id_type next_id{};
-        for (std::size_t i = 0; i < v.size(); i++)
+        for (Ciphertext *cp : v)
         {
-            Ciphertext &c = *v[i];
+            Ciphertext &c = *cp;
             Level lv = check_ct(context_, c, "encrypted");
-            if (context_.last_parms_id() == c.parms_id()) throw std::invalid_argument("end of modulus switching chain reached");
-            if (!c.is_ntt_form()) throw std::invalid_argument("CKKS encrypted must be in NTT form");
             auto next = lv.cd->next_context_data();
-            const double new_scale = c.scale() / (double)lv.cd->parms().coeff_modulus().back().value();
-            check_scale(new_scale, level_of(context_, next->parms_id(), "parms_id"));
-            scales.push_back(new_scale);
-            next_id = next->parms_id();
-            outs[i].bind(context_);
-            outs[i].resize_words(size * (lv.L - 1) * lv.n, false);
+            staged.push_back({ cp, PolyStore(), next->parms_id(),
+                               c.scale() / (double)lv.cd->parms().coeff_modulus().back().value(), size });
+            PolyStore &o = staged.back().out;
+            o.bind(context_);
+            o.resize_words(size * (lv.L - 1) * lv.n, false);
             in.push_back(c.store().dev_read(s));
-            out.push_back(outs[i].dev_write(s, true));
+            out.push_back(o.dev_write(s, true));
         }
         chk(mhe_rescale_batch(context_.engine(), (int)v.size(), in.data(), out.data(), (int)size, (int)g.first.first, s));
-        for (std::size_t i = 0; i < v.size(); i++)
-        {
-            const bool ntt = v[i]->is_ntt_form();
-            v[i]->store() = std::move(outs[i]);
-            v[i]->resize(context_, next_id, size);
-            v[i]->scale() = scales[i];
-            v[i]->is_ntt_form() = ntt;
-        }
+    }
+    for (Staged &e : staged)
+    {
+        const bool ntt = e.c->is_ntt_form();
+        e.c->store() = std::move(e.out);
+        e.c->resize(context_, e.next, e.size);
+        e.c->scale() = e.scale;
+        e.c->is_ntt_form() = ntt;
     }
     if (tsc.top())
         for (std::size_t i = 0; i < encrypted.size(); i++) trace::record("rescale", { tin[i] }, trace::ct(*encrypted[i]));

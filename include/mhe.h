@@ -131,6 +131,21 @@ int mhe_launch_run(mhe_ctx *ctx, mhe_launch *const *launches, int count);
  * pass) and resets. */
 int mhe_ctx_set_timing(mhe_ctx *ctx, int on);
 int mhe_kernel_time(mhe_ctx *ctx, int kernel, double *total_ms, int *launches);
+/* Hoisted rotations (no SEAL counterpart; csrc/hoist.h): the rotations of an input that appears
+ * more than once in one mhe_apply_galois_batch share one ModUp of the unrotated c1 (bit-identical
+ * to SEAL's one-at-a-time switch_key_inplace).  on = 1 turns it on for this context, 0 off (the
+ * default, or MHE_KS_HOIST at context creation).  check = 1 also recomputes every hoisted
+ * rotation by the classic path on the same stream and compares the words (a debugging aid: one
+ * host sync per hoisted pass; mismatches are counted and described on stderr).
+ * mhe_hoist_stats: rotations that went through the hoisted path, launches of the hoisted key-MAC
+ * kernels, and words that differed under check, since the last reset. */
+int mhe_ctx_set_hoist(mhe_ctx *ctx, int on, int check);
+int mhe_ctx_get_hoist(mhe_ctx *ctx, int *on, int *check);
+int mhe_hoist_stats(mhe_ctx *ctx, uint64_t *rotations, uint64_t *mac_launches, uint64_t *check_mismatches, int reset);
+/* Device scratch the context holds: per-stream workspaces (key-switch / rescale scratch for up to
+ * 8 batch entries at the key level), hoisting buffers, Galois negation-mask tables, and the number
+ * of streams with a workspace. */
+int mhe_scratch_bytes(mhe_ctx *ctx, uint64_t *workspace, uint64_t *hoisting, uint64_t *masks, int *streams);
 int mhe_stream_create(mhe_ctx *ctx, void **stream);
 int mhe_stream_destroy(mhe_ctx *ctx, void *stream);
 

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 
 static void on_fault(int sig)
 {
@@ -28,6 +29,91 @@ static void on_fault(int sig)
     std::raise(sig);
 }
 
+static std::vector<double> synthetic_image(int id)
+{
+    std::mt19937_64 g(id);
+    std::uniform_real_distribution<double> U(-2.5, 2.5);
+    std::vector<double> img(3072);
+    for (auto &x : img) x = U(g);
+    return img;
+}
+
+// resnet_test <params> <comp_dir> fibercheck [images] [threads] [fibers]: the images of a FiberBatch
+// (threads x fibers at a time, merged key switches / rescales / elementwise launches) must give the
+// words each image gives run alone (cnn/infer_seal.cpp:404-577 runs images independently, so every
+// image's output is the one-image output).  A fixed PRNG seed makes encryption deterministic; the
+// output ciphertexts are compared through their digests (FNV-1a over words, level, scale), with
+// hoisted rotations off and on (on: the engine also recomputes every hoisted rotation by the
+// classic path and counts differing words).
+static int fibercheck(const ResNetParams &prm, const char *comp_dir, int images, int threads, int fibers)
+{
+    ResNetRunner runner(20, prm, comp_dir, ResNetRunner::KeySource::generate, 0x5eedull);
+    std::printf("setup: %.2f s, %zu Galois keys, %.1f GB\n", runner.setup_seconds(), runner.galois_keys(),
+                runner.galois_key_gb());
+    std::vector<std::vector<double>> batch;
+    for (int id = 0; id < images; id++) batch.push_back(synthetic_image(id));
+    int fail = 0;
+    runner.set_hoist(false);
+    std::vector<ResNetResult> alone;
+    for (int id = 0; id < images; id++)
+    {
+        alone.push_back(runner.infer(batch[id]));
+        const std::vector<double> want = runner.plain_logits(batch[id]);
+        double err = 0, mag = 0;
+        for (int i = 0; i < 10; i++)
+        {
+            err = std::max(err, std::fabs(alone[id].logits[i] - want[i]));
+            mag = std::max(mag, std::fabs(want[i]));
+        }
+        std::printf("alone image %d: digest %016llx, %.3f s, max |logit error| %.3g of %.3g\n", id,
+                    (unsigned long long)alone[id].digest, alone[id].seconds, err, mag);
+        if (!(err < 0.05 * std::max(1.0, mag))) fail++;
+    }
+    {
+        // hoisting inside one image (the BSGS baby steps of its bootstraps)
+        runner.set_hoist(true, true);
+        runner.hoist_stats(true);
+        const ResNetResult r = runner.infer(batch[0]);
+        const auto st = runner.hoist_stats(true);
+        const bool ok = r.digest == alone[0].digest && st[2] == 0 && st[0] > 0;
+        std::printf("alone image 0, hoisting on: digest %016llx %s (%llu hoisted rotations, %llu hoisted MAC launches, "
+                    "%llu words differing from the classic path)\n",
+                    (unsigned long long)r.digest, ok ? "equal" : "DIFFERS", (unsigned long long)st[0],
+                    (unsigned long long)st[1], (unsigned long long)st[2]);
+        fail += ok ? 0 : 1;
+    }
+    for (int hoist = 0; hoist < 2; hoist++)
+    {
+        runner.set_hoist(hoist != 0, hoist != 0);
+        runner.hoist_stats(true);
+        const auto t0 = std::chrono::steady_clock::now();
+        const std::vector<ResNetResult> rs = runner.infer_batch(batch, threads, fibers);
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        const auto st = runner.hoist_stats(true);
+        int bad = 0;
+        for (int id = 0; id < images; id++)
+            if (rs[id].digest != alone[id].digest)
+            {
+                bad++;
+                std::printf("  image %d: digest %016llx != alone %016llx, logits", id, (unsigned long long)rs[id].digest,
+                            (unsigned long long)alone[id].digest);
+                for (double v : rs[id].logits) std::printf(" %.4f", v);
+                std::printf("\n");
+            }
+        std::printf("batch %d images as %d threads x %d fibers, hoisting %s: %d of %d digests differ from alone; "
+                    "%.3f s (%.3f images/s); %llu hoisted rotations, %llu MAC launches, %llu differing words; "
+                    "scratch %.1f GB\n",
+                    images, threads, fibers, hoist ? "on" : "off", bad, images, wall, images / wall,
+                    (unsigned long long)st[0], (unsigned long long)st[1], (unsigned long long)st[2],
+                    runner.scratch_bytes() / 1e9);
+        if (hoist && st[0] == 0) bad++;
+        fail += bad + (int)st[2];
+    }
+    runner.set_hoist(false);
+    std::printf("%s\n", fail ? "FAILED" : "ok");
+    return fail ? 1 : 0;
+}
+
 int main(int argc, char **argv)
 {
     std::signal(SIGSEGV, on_fault);
@@ -37,6 +123,9 @@ int main(int argc, char **argv)
         std::fprintf(stderr, "usage: resnet_test <params.bin|.d7> <comp_dir> [images (-1: load only)] [layers] [threads]\n");
         return 2;
     }
+    if (argc > 3 && std::string(argv[3]) == "fibercheck")
+        return fibercheck(load_resnet_params_bin(argv[1], 20), argv[2], argc > 4 ? std::atoi(argv[4]) : 4,
+                          argc > 5 ? std::atoi(argv[5]) : 2, argc > 6 ? std::atoi(argv[6]) : 2);
     const int images = argc > 3 ? std::atoi(argv[3]) : 1;
     const std::size_t layers = argc > 4 ? std::atoi(argv[4]) : 20;
     const int threads = argc > 5 ? std::atoi(argv[5]) : 0;

@@ -24,6 +24,31 @@ def resnet():
     return Chain(16, RESNET_BITS, seed=12)
 
 
+class hoisting:
+    """Hoisted rotations on for the block (mhe_ctx_set_hoist; the context default is off), with
+    the engine's own check (every hoisted rotation recomputed by the classic path and compared).
+    On exit: the hoisted key-MAC kernels must have run (mhe_hoist_stats) and the check must have
+    found no differing word; hoisting goes off again."""
+
+    def __init__(self, eng, min_rotations=1):
+        self.eng, self.min_rotations = eng, min_rotations
+
+    def __enter__(self):
+        self.eng.set_hoist(True, check=True)
+        assert self.eng.hoist() == (True, True)
+        self.eng.hoist_stats(reset=True)
+        return self
+
+    def __exit__(self, *exc):
+        self.eng.synchronize()
+        rot, mac, bad = self.eng.hoist_stats(reset=True)
+        self.eng.set_hoist(False)
+        if exc[0] is None:
+            assert rot >= self.min_rotations and mac >= 1, (rot, mac)
+            assert bad == 0, f"{bad} words of hoisted rotations differ from the classic path"
+        return False
+
+
 def truncated(key, L):
     """The level-L slice of a key: L digits, data primes 0..L-1 and the special prime."""
     return np.ascontiguousarray(np.concatenate([key[:L, :, :L], key[:L, :, -1:]], axis=2))
@@ -107,7 +132,8 @@ def test_rotate_batch_hoisted_zero_coefficients(small, zeros):
     steps = [1, 3, -2, 17]
     elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
     keys = [ch.rand_key() for _ in steps]
-    outs = ch.eng.apply_galois_batch([ch.up(ct)] * len(steps), elts, [ch.up(k) for k in keys])
+    with hoisting(ch.eng, len(steps)):
+        outs = ch.eng.apply_galois_batch([ch.up(ct)] * len(steps), elts, [ch.up(k) for k in keys])
     for i in range(len(steps)):
         assert np.array_equal(ch.down(outs[i]), ch.oc.apply_galois(ct, elts[i], keys[i])), f"step {steps[i]}"
 
@@ -132,7 +158,8 @@ def test_rotate_batch_hoisted_mixed(small):
             keys.append(key)
             dkeys.append(ch.up(key if k % 2 else truncated(key, L)))
             which.append(i)
-    outs = ch.eng.apply_galois_batch(ins, elts, dkeys)
+    with hoisting(ch.eng, len(ins) - 2):
+        outs = ch.eng.apply_galois_batch(ins, elts, dkeys)
     for j in range(len(ins)):
         want = ch.oc.apply_galois(cts[which[j]], elts[j], keys[j])
         assert np.array_equal(ch.down(outs[j]), want), f"entry {j} (input {which[j]})"
@@ -152,7 +179,8 @@ def test_rotate_batch_hoisted_shared_keys(small, L):
     dkeys = [ch.up(truncated(k, L) if i == 1 else k) for i, k in enumerate(keys)]
     srcs = [ch.up(c) for c in cts]
     ins = [s for s in srcs for _ in steps]
-    outs = ch.eng.apply_galois_batch(ins, elts * len(cts), dkeys * len(cts))
+    with hoisting(ch.eng, len(ins)):
+        outs = ch.eng.apply_galois_batch(ins, elts * len(cts), dkeys * len(cts))
     for j in range(len(ins)):
         want = ch.oc.apply_galois(cts[j // 3], elts[j % 3], keys[j % 3])
         assert np.array_equal(ch.down(outs[j]), want), f"input {j // 3} step {steps[j % 3]}"
@@ -174,10 +202,42 @@ def test_rotate_batch_hoisted_n16(resnet):
     elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
     srcs = [ch.up(c) for c in cts]
     ins = [s for s in srcs for _ in steps]
-    outs = ch.eng.apply_galois_batch(ins, elts * 3, dkeys * 3)
+    with hoisting(ch.eng, 9):
+        outs = ch.eng.apply_galois_batch(ins, elts * 3, dkeys * 3)
     for j in range(9):
         want = ch.oc.apply_galois(cts[j // 3], elts[j % 3], full[j % 3])
         assert np.array_equal(ch.down(outs[j]), want), f"input {j // 3} step {steps[j % 3]}"
+
+
+@pytest.mark.parametrize("zero_input", [None, 3])
+def test_rotate_batch_hoisted_fiber_bsgs_shape(resnet, zero_input):
+    """The shape the ResNet FiberBatch runs in its bootstraps: 8 inputs (the images of
+    2 threads x 4 fibers share nothing, one thread's 4 are merged -- here all 8) x 7 baby-step
+    rotations sharing the 7 keys (k_ks_hoist_mac_sh, R = 7, one item per lane group), N = 2^16 at
+    24 limbs, prepared level-truncated keys, optionally one input with zero coefficients (its
+    rotations take the classic path inside the same launch sequence).  Every output equals the
+    engine's classic path (hoisting off), and two entries equal the oracle."""
+    ch = resnet
+    L = 24
+    steps = [1, 2, 3, 4, 5, 6, 7]
+    keys = [truncated(ch.rand_key(digits=L), L) for _ in steps]
+    dkeys = [ch.eng.key_prepare(ch.up(k)) for k in keys]
+    cts = [with_zero_coeffs(ch, L, 2) if i == zero_input else ch.rand(2, L, ch.n) for i in range(8)]
+    srcs = [ch.up(c) for c in cts]
+    elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
+    ins = [s for s in srcs for _ in steps]
+    with hoisting(ch.eng, len(ins)):
+        outs = ch.eng.apply_galois_batch(ins, elts * 8, dkeys * 8)
+    classic = ch.eng.apply_galois_batch(ins, elts * 8, dkeys * 8)  # hoisting off again
+    for j in range(len(ins)):
+        assert np.array_equal(ch.down(outs[j]), ch.down(classic[j])), f"input {j // 7} step {steps[j % 7]}"
+    full = [np.zeros((L, 2, ch.K, ch.n), np.uint64) for _ in keys]
+    for f, k in zip(full, keys):
+        f[:, :, :L] = k[:, :, :L]
+        f[:, :, -1] = k[:, :, -1]
+    for j in (5, 7 * (zero_input or 0) + 3):
+        want = ch.oc.apply_galois(cts[j // 7], elts[j % 7], full[j % 7])
+        assert np.array_equal(ch.down(outs[j]), want), f"input {j // 7} step {steps[j % 7]} vs oracle"
 
 
 @pytest.mark.parametrize("size", [1, 2, 3])

@@ -95,6 +95,26 @@ def test_resnet20_end_to_end():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.gpu
+def test_resnet20_fiber_batch_words_equal_alone():
+    """The bench's batched ResNet mode against the reference's per-image definition
+    (cnn/infer_seal.cpp:404-577 runs every image on its own): 4 ResNet-20 images as 2 host threads x
+    2 fibers (seal::FiberBatch: merged rotations / relinearizations / rescales, coalesced
+    elementwise launches) must each give the output ciphertext words of the same image run alone,
+    with hoisted rotations off and on; with hoisting on, every hoisted rotation is also recomputed
+    by the classic path and must match word for word (tests/cpp/resnet_test.cpp fibercheck).
+    Encryption is made deterministic by a fixed PRNG seed (SEAL's Blake2xbPRNGFactory(seed))."""
+    _build()
+    r = subprocess.run([os.path.join(ROOT, "build", "resnet_test"),
+                        os.path.join(ROOT, "tests", "golden", "resnet", "resnet20_params.bin"),
+                        os.path.join(ROOT, "tests", "golden", "comp"), "fibercheck", "4", "2", "2"],
+                       capture_output=True, text=True, timeout=900)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("0 of 4 digests differ from alone") == 2, r.stdout
+
+
 def test_resnet_params_fixture():
     """The packed parameter fixture has ResNet-20's 271098 values in import_parameters_cifar10
     order (cnn/infer_seal.cpp:3-100): 19 conv weight tensors, 19 x 4 batch-norm vectors, FC."""
