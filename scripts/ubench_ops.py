@@ -28,11 +28,14 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--ops", default="rescale,rescale4,ks,ks4,ks4s,rot4,ntt,hmult")
     ap.add_argument("--bsgs", default="8x7", help="inputs x rotations of the bsgs op (keys shared over inputs)")
+    ap.add_argument("--hoist", type=int, default=None, help="hoisted rotations on (1) / off (0); default: the context's")
     a = ap.parse_args()
     log_n, n = 16, 1 << 16
     bits = [51] + [46] * 16 + [51] * 14 + [51]
     moduli = mhe.coeff_modulus_create(n, bits)
     eng = mhe.Engine(log_n, moduli, device=0)
+    if a.hoist is not None:
+        eng.set_hoist(bool(a.hoist))
     K, L = len(moduli), a.limbs
     qs = torch.tensor(np.array(moduli, np.uint64).view(np.int64), device=eng.torch_device)
 
@@ -52,7 +55,7 @@ def main():
     rot_out = [eng.empty(2, L, n) for _ in range(4)]
     elts = [pow(5, s, 2 * n) for s in (1, 2, 4, 8)]
     # bsgs: the BSGS baby steps of several images (FiberBatch): each input rotated R ways, the R keys
-    # shared by the inputs -- the hoisted path (csrc/hoist.h) unless MHE_KS_HOIST=0
+    # shared by the inputs -- the hoisted path (csrc/hoist.h) when hoisting is on (--hoist 1)
     if "bsgs" in a.ops:
         H, R = (int(x) for x in a.bsgs.split("x"))
         bkeys = [rnd(L, 2, K, n, limbs=K) for _ in range(R)]
@@ -89,7 +92,7 @@ def main():
         torch.cuda.synchronize()
         us = t0.elapsed_time(t1) * 1000 / a.reps
         print(json.dumps({"op": name if name != "bsgs" else "bsgs" + a.bsgs, "limbs": L, "us": round(us, 2),
-                          "hoist": os.environ.get("MHE_KS_HOIST", "1"), "lib": os.environ.get("MHE_LIB_PATH", "libmhe.so")}),
+                          "hoist": int(eng.hoist()[0]), "lib": os.environ.get("MHE_LIB_PATH", "libmhe.so")}),
               flush=True)
 
 
