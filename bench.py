@@ -292,8 +292,11 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
     if world > 1:
         dist.barrier()
     t2 = time.perf_counter()
+    runner.hoist_stats(reset=True)
     batch = runner.infer_batch(imgs, streams, fibers)
     batch_wall = time.perf_counter() - t2
+    hoisted, hoist_macs, _ = runner.hoist_stats(reset=True)
+    scratch = runner.scratch_bytes()
     # every image's decrypted logits against the plain network (exact ReLU), on every rank -- the
     # keys there may have arrived over RCCL; a miss fails the leg
     tol = 0.05 if layers <= 20 else 0.08
@@ -316,6 +319,13 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
         "batch_mode": (f"{streams} host threads x {fibers} images as one seal::FiberBatch each (merged key switches, "
                        "rescales and elementwise launches)" if fibers > 1 else f"{streams} host threads, one image each"),
         "setup_s": round(setup, 2),
+        # hoisted rotations (csrc/hoist.h, the engine default): rotations of one input in one batched
+        # call share one ModUp; counted over the batch
+        "hoisted_rotations_batch": hoisted,
+        "hoisted_mac_launches_batch": hoist_macs,
+        # device scratch the engine holds after the batch (per-stream workspaces, hoisting buffers,
+        # Galois mask tables), beyond keys and ciphertexts (mhe_scratch_bytes)
+        "scratch_GB": round(scratch / 1e9, 2),
         "galois_keys": info["galois_keys"],
         "galois_key_GB_resident": round(info["galois_key_gb"], 2),
         "key_format": ("prepared (mhe_key_prepare: 46-bit limbs streamed in 6 B)" if prepared else "SEAL layout")

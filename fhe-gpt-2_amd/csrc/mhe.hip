@@ -240,9 +240,10 @@ struct mhe_ctx
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
     int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
-    int ks_hoist = 0; // batched rotations of one input share their ModUp (hoist.h): MHE_KS_HOIST=1 or mhe_ctx_set_hoist
+    int ks_hoist = 1; // batched rotations of one input share their ModUp (hoist.h); mhe_ctx_set_hoist / MHE_KS_HOIST=0 turn it off
     int hoist_check = 0; // recompute every hoisted rotation by the classic path and compare (mhe_ctx_set_hoist)
     std::atomic<unsigned long long> hoist_rot{ 0 }, hoist_mac{ 0 }, hoist_bad{ 0 }; // mhe_hoist_stats
+    std::atomic<int> fail_alloc{ 0 }; // mhe_debug_fail_alloc: the n-th next allocation fails (0: off)
     TwF *cmodf = nullptr; // [K][K]: (q_j mod q_i, (q_j mod q_i) / q_i) as doubles, j major (hoist.h)
     std::mutex mask_mu;
     std::map<u32, u64 *> masks; // Galois element -> NTT of its negation mask, [K][n] (hoist.h)
@@ -295,6 +296,37 @@ static void timing_end(hipEvent_t *pair, hipStream_t st)
     if (pair) (void)hipEventRecord(pair[1], st);
 }
 
+// Scratch allocation that gives the stream-ordered pool's cached blocks back to the device when the
+// device reports out of memory: the pool keeps freed blocks (release threshold: never), which a plain
+// hipMalloc cannot reuse.  Trims what is free now, then once more after the device drained (frees
+// still queued on streams complete), retrying after each.
+static hipError_t dev_alloc(mhe_ctx *c, void **p, size_t bytes)
+{
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) return e;
+    (void)hipGetLastError();
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, c->device) != hipSuccess) return e;
+    for (int round = 0; round < 2; round++)
+    {
+        if (round == 1) (void)hipDeviceSynchronize();
+        (void)hipMemPoolTrimTo(pool, 0);
+        e = hipMalloc(p, bytes);
+        if (e == hipSuccess) return e;
+        (void)hipGetLastError();
+    }
+    return e;
+}
+
+// mhe_debug_fail_alloc's countdown: true for the allocation it designates
+static bool injected_alloc_failure(mhe_ctx *c)
+{
+    int v = c->fail_alloc.load();
+    while (v > 0)
+        if (c->fail_alloc.compare_exchange_weak(v, v - 1)) return v == 1;
+    return false;
+}
+
 // The scratch of stream st, for ciphertexts of up to `limbs` limbs and `entries` batch entries.
 // The context lock only guards the map; growing one stream's scratch (which drains that stream
 // first: its queued kernels may still use the old buffers) holds that workspace's own lock, so
@@ -324,8 +356,9 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int en
         const size_t per = Lc * n + (L + 1) * L * n + 2 * (L + 1) * n + 3 * L * n;
         size_t words = (size_t)E * per + L * n;
         HIP_TRY(hipSetDevice(c->device));
-        if (hipMalloc(&w.base, words * sizeof(u64)) != hipSuccess)
+        if (injected_alloc_failure(c) || dev_alloc(c, (void **)&w.base, words * sizeof(u64)) != hipSuccess)
         {
+            w.base = nullptr;
             w.max_limbs = 0;
             w.entries = 0;
             return fail(MHE_ERR_MEMORY, "workspace allocation failed");
@@ -2174,6 +2207,7 @@ MHE_EXPORT int mhe_malloc_async(mhe_ctx *c, void **dptr, size_t bytes, void *str
 {
     if (!valid_ctx(c) || !dptr) return fail(MHE_ERR_ARG, "invalid argument");
     const size_t kGuard = trace_on() ? ((size_t)16 << 20) : 0;
+    if (injected_alloc_failure(c)) return fail(MHE_ERR_MEMORY, "device allocation failed");
     if (mhe_internal_alloc(dptr, (bytes ? bytes : 1) + kGuard, S(stream)) != hipSuccess)
         return fail(MHE_ERR_MEMORY, "device allocation failed");
     if (trace_on())
@@ -2394,6 +2428,13 @@ MHE_EXPORT int mhe_ctx_set_timing(mhe_ctx *c, int on)
 }
 
 static bool hoist_ok(const mhe_ctx *c);
+
+MHE_EXPORT int mhe_debug_fail_alloc(mhe_ctx *c, int nth)
+{
+    if (!valid_ctx(c) || nth < 0) return fail(MHE_ERR_ARG, "invalid argument");
+    c->fail_alloc.store(nth);
+    return MHE_OK;
+}
 
 MHE_EXPORT int mhe_ctx_set_hoist(mhe_ctx *c, int on, int check)
 {
@@ -3030,7 +3071,11 @@ static int get_hoist(mhe_ctx *c, hipStream_t st, int entries, int ws_entries, in
         const size_t per = (size_t)(HL + 1) * HL * c->n, pacc = (size_t)2 * (HL + 1) * c->n;
         const int na = MHE_MAXB * MHE_HOIST_R;
         const size_t bytes = ((size_t)E * per + (size_t)na * pacc) * sizeof(u64);
-        if (hipMalloc(&w->hoist_base, bytes) != hipSuccess) return fail(MHE_ERR_MEMORY, "workspace allocation failed");
+        if (injected_alloc_failure(c) || dev_alloc(c, (void **)&w->hoist_base, bytes) != hipSuccess)
+        {
+            w->hoist_base = nullptr;
+            return fail(MHE_ERR_MEMORY, "workspace allocation failed");
+        }
         for (int i = 0; i < E; i++) w->hoist[i] = w->hoist_base + (size_t)i * per;
         for (int i = 0; i < na; i++) w->hacc[i] = w->hoist_base + (size_t)E * per + (size_t)i * pacc;
         w->hoist_entries = E;

@@ -203,6 +203,14 @@ struct BlockDims
 {
     int rows = 128, d_model = 768, heads = 12, d_ff = 3072;
 };
+// The weight of GELU's last piece (x for x >= 3): `reference` is b3 = 0.5 s2 as PolyApprox.cpp:484-485
+// and plain_approx/poly.py:33 write it (+-x/4 outside the middle pieces); `indicator` (the block's
+// default, a deliberate departure) is s2 + 1/2, the indicator of x >= 3 that GELU needs.
+enum class GeluLastPiece
+{
+    indicator,
+    reference
+};
 struct AttentionParams
 {
     double masked_score = -5.0; // masked scores pinned here before the row max
@@ -210,6 +218,7 @@ struct AttentionParams
     int inv_iters = 8;          // Goldschmidt steps
     int newton_iters = 3;       // layer-norm Newton steps
     double gelu_alpha = 0.1;    // GELU signs taken of alpha (x + shift)
+    GeluLastPiece gelu_last = GeluLastPiece::indicator; // the block's GELU x piece (reference: poly.py's 0.5 s2)
 };
 struct PlainBlockWeights
 {
@@ -291,14 +300,6 @@ void layer_norm_rows(Ciphertext &input, Ciphertext &output, const std::vector<do
                      const std::vector<double> &beta, int rows, int row_size, int newton_iters,
                      Bootstrapper &bootstrapper, CKKSEncoder &encoder, Encryptor &encryptor, Decryptor &decryptor,
                      Evaluator &evaluator, GaloisKeys &gal_keys, RelinKeys &relin_keys);
-// The weight of GELU's last piece (x for x >= 3): `reference` is b3 = 0.5 s2 as PolyApprox.cpp:484-485
-// and plain_approx/poly.py:33 write it (+-x/4 outside the middle pieces); `indicator` (the block's
-// default, a deliberate departure) is s2 + 1/2, the indicator of x >= 3 that GELU needs.
-enum class GeluLastPiece
-{
-    indicator,
-    reference
-};
 void compute_gelu_block(Ciphertext &inputs, Ciphertext &outputs, double alpha, CKKSEncoder &encoder,
                         Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
                         RelinKeys &relin_keys, GeluLastPiece last = GeluLastPiece::indicator);
@@ -315,7 +316,7 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, s
                       std::vector<Ciphertext> &W2, Ciphertext b2, std::vector<Ciphertext> &outputs, int rows, int cols,
                       int d_ff, double gelu_alpha, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
                       Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
-                      RelinKeys &relin_keys);
+                      RelinKeys &relin_keys, GeluLastPiece gelu_last = GeluLastPiece::indicator);
 void transformer_block(std::vector<Ciphertext> &x, BlockWeights &w, const std::vector<std::vector<double>> &keep,
                        std::vector<Ciphertext> &y, const BlockDims &dims, const AttentionParams &params,
                        Bootstrapper &bootstrapper, seal::KeyGenerator &keygen, CKKSEncoder &encoder,

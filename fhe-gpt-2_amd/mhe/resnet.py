@@ -43,6 +43,9 @@ def seal_lib():
             "mhe_resnet_key_traffic": (i32, [vp, dp, i32]),
             "mhe_resnet_op_counts": (i32, [vp, i32, u64p, i32]),
             "mhe_resnet_key_format": (i32, [vp, ip]),
+            "mhe_resnet_set_hoist": (i32, [vp, i32, i32]),
+            "mhe_resnet_hoist_stats": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
+            "mhe_resnet_scratch_bytes": (i32, [vp, ctypes.POINTER(ctypes.c_double)]),
             "mhe_resnet_plain_logits": (i32, [vp, dp, dp]),
         }
         for name, (res, args) in sig.items():
@@ -133,6 +136,20 @@ class Runner:
             _check(seal_lib().mhe_resnet_op_counts(self._h, k, c, 1 if reset else 0))
             out[name] = [int(x) for x in c]
         return out
+
+    def set_hoist(self, on, check=False):
+        _check(seal_lib().mhe_resnet_set_hoist(self._h, 1 if on else 0, 1 if check else 0))
+
+    def hoist_stats(self, reset=False):
+        """(hoisted rotations, hoisted key-MAC launches, words differing under check) since reset."""
+        v = (ctypes.c_uint64 * 3)()
+        _check(seal_lib().mhe_resnet_hoist_stats(self._h, v, 1 if reset else 0))
+        return tuple(int(x) for x in v)
+
+    def scratch_bytes(self):
+        b = ctypes.c_double()
+        _check(seal_lib().mhe_resnet_scratch_bytes(self._h, ctypes.byref(b)))
+        return b.value
 
     def keys_prepared(self):
         """True when the evaluation keys are in the engine's prepared format (mhe_key_prepare)."""

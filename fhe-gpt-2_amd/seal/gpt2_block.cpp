@@ -1019,7 +1019,7 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, s
                       std::vector<Ciphertext> &W2, Ciphertext b2, std::vector<Ciphertext> &outputs, int rows, int cols,
                       int d_ff, double gelu_alpha, Bootstrapper &bootstrapper, CKKSEncoder &encoder,
                       Encryptor &encryptor, Decryptor &decryptor, Evaluator &evaluator, GaloisKeys &gal_keys,
-                      RelinKeys &relin_keys)
+                      RelinKeys &relin_keys, GeluLastPiece gelu_last)
 {
     // layers.cpp:3-24 (layers.py:93-116): dense to d_ff, GELU, dense back, biases after each.  The
     // hidden state is held in `cols`-wide column chunks, each row-packed like the input: FC1 then
@@ -1046,7 +1046,7 @@ void FeedForwardLayer(std::vector<Ciphertext> &A, std::vector<Ciphertext> &W1, s
         Ciphertext &h = hidden[i];
         ensure_levels(h, 20, bootstrapper, evaluator);
         Ciphertext g;
-        compute_gelu_block(h, g, gelu_alpha, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+        compute_gelu_block(h, g, gelu_alpha, encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, gelu_last);
         h = g;
         ensure_levels(h, 3, bootstrapper, evaluator);
     });
@@ -1110,7 +1110,7 @@ void transformer_block(std::vector<Ciphertext> &x, BlockWeights &w, const std::v
     if (trace) trace->ln2 = ln2;
     std::vector<Ciphertext> ffn;
     FeedForwardLayer(ln2, w.fc_w, w.fc_b, w.pj_w, w.pj_b, ffn, T, d, dims.d_ff, params.gelu_alpha, bootstrapper,
-                     encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys);
+                     encoder, encryptor, decryptor, evaluator, gal_keys, relin_keys, params.gelu_last);
     stage("ffn");
     if (trace) trace->ffn = ffn;
     y.assign(x.size(), Ciphertext());

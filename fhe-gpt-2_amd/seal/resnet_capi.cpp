@@ -165,6 +165,28 @@ int mhe_resnet_key_format(mhe_resnet *r, int *prepared)
     });
 }
 
+int mhe_resnet_set_hoist(mhe_resnet *r, int on, int check)
+{
+    return guard([&] { r->runner->set_hoist(on != 0, check != 0); });
+}
+
+int mhe_resnet_hoist_stats(mhe_resnet *r, uint64_t *stats, int reset)
+{
+    return guard([&] {
+        if (!stats) throw std::invalid_argument("null argument");
+        const auto v = r->runner->hoist_stats(reset != 0);
+        std::copy(v.begin(), v.end(), stats);
+    });
+}
+
+int mhe_resnet_scratch_bytes(mhe_resnet *r, double *bytes)
+{
+    return guard([&] {
+        if (!bytes) throw std::invalid_argument("null argument");
+        *bytes = (double)r->runner->scratch_bytes();
+    });
+}
+
 int mhe_resnet_plain_logits(mhe_resnet *r, const double *image, double *logits)
 {
     return guard([&] {

@@ -133,8 +133,8 @@ int mhe_ctx_set_timing(mhe_ctx *ctx, int on);
 int mhe_kernel_time(mhe_ctx *ctx, int kernel, double *total_ms, int *launches);
 /* Hoisted rotations (no SEAL counterpart; csrc/hoist.h): the rotations of an input that appears
  * more than once in one mhe_apply_galois_batch share one ModUp of the unrotated c1 (bit-identical
- * to SEAL's one-at-a-time switch_key_inplace).  on = 1 turns it on for this context, 0 off (the
- * default, or MHE_KS_HOIST at context creation).  check = 1 also recomputes every hoisted
+ * to SEAL's one-at-a-time switch_key_inplace).  on = 1 turns it on for this context (the default;
+ * MHE_KS_HOIST=0 at context creation starts it off), 0 off.  check = 1 also recomputes every hoisted
  * rotation by the classic path on the same stream and compares the words (a debugging aid: one
  * host sync per hoisted pass; mismatches are counted and described on stderr).
  * mhe_hoist_stats: rotations that went through the hoisted path, launches of the hoisted key-MAC
@@ -146,6 +146,11 @@ int mhe_hoist_stats(mhe_ctx *ctx, uint64_t *rotations, uint64_t *mac_launches, u
  * 8 batch entries at the key level), hoisting buffers, Galois negation-mask tables, and the number
  * of streams with a workspace. */
 int mhe_scratch_bytes(mhe_ctx *ctx, uint64_t *workspace, uint64_t *hoisting, uint64_t *masks, int *streams);
+/* Fault injection for tests: the nth next device allocation of the context (mhe_malloc_async, or a
+ * workspace / hoisting scratch growth) fails with MHE_ERR_MEMORY as if the device were out of
+ * memory; 0 turns it off.  Used to check that a batched call that fails part way leaves its
+ * operands as they were (tests/cpp/seal_batch_test.cpp). */
+int mhe_debug_fail_alloc(mhe_ctx *ctx, int nth);
 int mhe_stream_create(mhe_ctx *ctx, void **stream);
 int mhe_stream_destroy(mhe_ctx *ctx, void *stream);
 

@@ -54,6 +54,14 @@ int mhe_resnet_op_counts(mhe_resnet *runner, int kind, uint64_t *counts, int res
 /* *prepared = 1 when the runner's evaluation keys are in the engine's prepared format
  * (mhe_key_prepare), 0 when they are in SEAL's layout (MHE_KEY_PREPARE=0). */
 int mhe_resnet_key_format(mhe_resnet *runner, int *prepared);
+/* Hoisted rotations of the runner's engine on / off (mhe_ctx_set_hoist; check: every hoisted rotation
+ * recomputed by the classic path and compared), and stats[3] = hoisted rotations, hoisted key-MAC
+ * launches, words that differed under check, since the last reset. */
+int mhe_resnet_set_hoist(mhe_resnet *runner, int on, int check);
+int mhe_resnet_hoist_stats(mhe_resnet *runner, uint64_t *stats, int reset);
+/* Device scratch the runner's engine holds (per-stream workspaces, hoisting buffers, Galois mask
+ * tables; mhe_scratch_bytes), beyond its keys and ciphertexts. */
+int mhe_resnet_scratch_bytes(mhe_resnet *runner, double *bytes);
 /* The same network in plain doubles with the exact ReLU (the check of a decrypted inference,
  * infer_seal.cpp:543-575 prints decrypted logits against the label): image 3 x 32 x 32 -> logits[10]. */
 int mhe_resnet_plain_logits(mhe_resnet *runner, const double *image, double *logits);

@@ -320,6 +320,8 @@ int main(int argc, char **argv)
             for (int j = 0; j <= r; j++) keep[r][j] = 1.0;
         AttentionParams ap;
         if (hdr.count("inv_iters")) ap.inv_iters = (int)hdr.at("inv_iters");
+        // a fixture made with make_fixture.py --gelu-ref: the block's GELU x piece as poly.py writes it
+        if (hdr.count("gelu_ref") && hdr.at("gelu_ref") != 0) ap.gelu_last = GeluLastPiece::reference;
         BlockDims dims;
         dims.rows = T;
         dims.d_model = d;
@@ -439,6 +441,11 @@ int main(int argc, char **argv)
             std::printf("   stages: ln1 %.3g  attn %.3g  x1 %.3g  ln2 %.3g  ffn %.3g  y %.3g; y %zu limbs; "
                         "vs exact GPT-2 block math %.3g\n",
                         e_ln1, e_attn, e_x1, e_ln2, e_ffn, e_y, y[0].coeff_modulus_size(), e_exact);
+            if (fx.count("y_polygelu"))
+                std::printf("   GELU x piece %s; y vs the block with plain_approx/poly.py's gelu as written (np.sign "
+                            "on x, no sign approximation): %.3g\n",
+                            ap.gelu_last == GeluLastPiece::reference ? "0.5 s2 (reference)" : "s2 + 1/2 (indicator)",
+                            err_rows(y, fx.at("y_polygelu")));
             std::printf("block_seconds %.3f\n", secs);
             report("GPT-2 block (T " + std::to_string(T) + ", d " + std::to_string(d) + ", " + std::to_string(H) +
                        " heads, d_ff " + std::to_string(F) + ") vs plain restatement",

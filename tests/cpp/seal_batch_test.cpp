@@ -4,6 +4,7 @@
 // levels, and unequal levels where the reduced-error adjustment runs).  N = 2^13 and 2^16.
 //   seal_batch_test <log N>
 #include "seal/seal.h"
+#include "../../include/mhe.h"
 
 #include <cmath>
 #include <cstdio>
@@ -254,6 +255,75 @@ int main(int argc, char **argv)
                 if (m != 2)
                     for (std::size_t i = 0; ok && i < alone[m].size(); i++) ok = same(alone[m][i], part[m][i]);
             check("FiberBatch: a fiber's exception comes back from run(), the other fibers' words unchanged", ok);
+        }
+
+        // An allocation that fails part way through a batched rescale (injected: the engine's nth
+        // next device allocation reports out of memory).  Alone, the call must throw with every entry
+        // unchanged; merged in a FiberBatch round, lockstep_execute re-runs each member's call on its
+        // own, so every member must end up rescaled exactly once -- a group committed before the
+        // failure and rescaled again by the retry is a silently wrong ciphertext (two levels down).
+        {
+            auto two_groups = [&](std::vector<Ciphertext> &v) {
+                v.clear();
+                for (int i = 0; i < 6; i++)
+                {
+                    Ciphertext a = fresh(i < 3 ? 1 : 0), b = fresh(i < 3 ? 1 : 0), m;
+                    ev.multiply(a, b, m);
+                    ev.relinearize_inplace(m, rlk);
+                    v.push_back(m);
+                }
+            };
+            std::vector<Ciphertext> base, want;
+            two_groups(base);
+            want = base;
+            for (auto &c : want) ev.rescale_to_next_inplace(c);
+            bool ok_alone = true, ok_fiber = true;
+            int threw_alone = 0, retried = 0;
+            for (int nth = 1; nth <= 10; nth++)
+            {
+                std::vector<Ciphertext> v = base;
+                std::vector<Ciphertext *> pv;
+                for (auto &c : v) pv.push_back(&c);
+                mhe_debug_fail_alloc(ctx.engine(), nth);
+                bool thrown = false;
+                try
+                {
+                    ev.rescale_to_next_inplace_many(pv);
+                }
+                catch (const std::runtime_error &)
+                {
+                    thrown = true;
+                }
+                mhe_debug_fail_alloc(ctx.engine(), 0);
+                threw_alone += thrown ? 1 : 0;
+                for (std::size_t i = 0; i < v.size(); i++) ok_alone = ok_alone && same(v[i], thrown ? base[i] : want[i]);
+                // two fibers rescaling one entry per round (rescale_to_next_inplace is a merge point):
+                // fiber 0 the lower-level f[0..2], fiber 1 the top-level f[3..5], so every merged call
+                // holds two (level, size) groups and a failure in the second finds the first done
+                std::vector<Ciphertext> f = base;
+                mhe_debug_fail_alloc(ctx.engine(), nth);
+                try
+                {
+                    FiberBatch::run(2, [&](std::size_t m) {
+                        for (int r = 0; r < 3; r++) ev.rescale_to_next_inplace(f[3 * m + r]);
+                    });
+                }
+                catch (const std::exception &e)
+                {
+                    std::printf("  nth %d: FiberBatch threw: %s\n", nth, e.what());
+                    ok_fiber = false;
+                }
+                const bool fired = nth <= 6; // 6 allocations: one per entry, two per merged round
+                mhe_debug_fail_alloc(ctx.engine(), 0);
+                retried += fired ? 1 : 0;
+                for (std::size_t i = 0; i < f.size(); i++) ok_fiber = ok_fiber && same(f[i], want[i]);
+            }
+            check("rescale_to_next_inplace_many: an allocation failure part way leaves every entry unchanged (" +
+                      std::to_string(threw_alone) + " of 10 injection points threw)",
+                  ok_alone && threw_alone > 0);
+            check("FiberBatch: a merged rescale that fails part way is re-run per member, each entry rescaled once (" +
+                      std::to_string(retried) + " failing merged calls)",
+                  ok_fiber && retried > 0);
         }
 
         bool threw = false;

@@ -81,13 +81,36 @@ def gelu_q(x):
             + (0.0001533078376 * x * x + 0.0002609111473 * x - 0.004401064777) * t4)
 
 
+GELU_REF = False  # --gelu-ref: the x piece weighted by poly.py's 0.5 s2 (GeluLastPiece::reference)
+
+
 def gelu_block(x):
     y = GELU_ALPHA * x
     s2 = 0.5 * sign_function(y + GELU_ALPHA * -3.0)
     s1 = 0.5 * sign_function(y + GELU_ALPHA * 1.95)
     s0 = 0.5 * sign_function(y + GELU_ALPHA * 4.0)
-    b1, b2, b3 = s0 - s1, s1 - s2, s2 + 0.5
+    b1, b2, b3 = s0 - s1, s1 - s2, (0.5 * s2 if GELU_REF else s2 + 0.5)
     return b1 * gelu_p(x) + b2 * gelu_q(x) + b3 * x
+
+
+# plain_approx/poly.py:15-28, the power-series gelu_p / gelu_q (coefficients highest power first)
+POLY_GELU_P = (-0.010674138350676401, -0.11491758706060971, -0.4134048031372351, -0.49783059647700406)
+POLY_GELU_Q = (0.0012264627004247512, 0.0020872891783959252, -0.036434980917200932, -0.0085812866991243648,
+               0.36217359096393054, 0.50622871052887408, 0.0072415619838619525)
+
+
+def _horner(x, coeffs):
+    u = np.zeros_like(x)
+    for c in coeffs:
+        u = u * x + c
+    return u
+
+
+def poly_gelu(x):
+    """plain_approx/poly.py:30-35 as written: np.sign of x - 3, x + 1.95, x + 4 (no approximation),
+    b1 = s0 - s1, b2 = s1 - s2, b3 = 0.5 s2 (b0 * 0 dropped)."""
+    s2, s1, s0 = 0.5 * np.sign(x - 3), 0.5 * np.sign(x + 1.95), 0.5 * np.sign(x + 4)
+    return (s0 - s1) * _horner(x, POLY_GELU_P) + (s1 - s2) * _horner(x, POLY_GELU_Q) + 0.5 * s2 * x
 
 
 def rot(v, k):
@@ -192,11 +215,12 @@ def block(x, w):
     g = gelu_block(hid)
     f = g @ w["pj_w"] + w["pj_b"]
     y = x1 + f
+    y_polygelu = x1 + poly_gelu(hid) @ w["pj_w"] + w["pj_b"]
     ranges.update(var1=(float(u1.min()), float(u1.max())), var2=(float(u2.min()), float(u2.max())),
                   scores=smax_in, hidden=(float(hid.min()), float(hid.max())), x1=float(np.abs(x1).max()),
                   gelu=float(np.abs(g).max()), qkv=float(max(np.abs(q).max(), np.abs(k).max(), np.abs(v).max())))
     return {"ln1": ln1, "q": q, "k": k, "v": v, "attn": attn, "x1": x1, "ln2": ln2, "hidden": hid, "gelu": g,
-            "ffn": f, "y": y}, ranges
+            "ffn": f, "y": y, "y_polygelu": y_polygelu}, ranges
 
 
 def exact_block(x, w):
@@ -255,7 +279,7 @@ def make_inputs(seed=SEED):
 
 ORDER_IN = ["x", "ln1_g", "ln1_b", "qw", "qb", "kw", "kb", "vw", "vb", "ow", "ob", "ln2_g", "ln2_b", "fc_w", "fc_b",
             "pj_w", "pj_b"]
-ORDER_OUT = ["ln1", "q", "k", "v", "attn", "x1", "ln2", "hidden", "gelu", "ffn", "y", "y_exact"]
+ORDER_OUT = ["ln1", "q", "k", "v", "attn", "x1", "ln2", "hidden", "gelu", "ffn", "y", "y_exact", "y_polygelu"]
 
 
 def arrays(seed=SEED):
@@ -268,7 +292,8 @@ def arrays(seed=SEED):
 
 def header():
     return (f"# gpt2 block fixture: T {T} d {D} heads {H} d_ff {F} seed {SEED} alpha {GELU_ALPHA} "
-            f"newton {NEWTON_ITERS} inv_iters {INV_ITERS}" + (f" qk_std {QK_STD}" if QK_STD != 1.0 else ""))
+            f"newton {NEWTON_ITERS} inv_iters {INV_ITERS}" + (f" qk_std {QK_STD}" if QK_STD != 1.0 else "")
+            + (" gelu_ref 1" if GELU_REF else ""))
 
 
 def write(dst=HERE, names=None):
@@ -290,12 +315,15 @@ def write(dst=HERE, names=None):
 
 
 if __name__ == "__main__":
+    if "--gelu-ref" in sys.argv:
+        sys.argv.remove("--gelu-ref")
+        GELU_REF = True
     if len(sys.argv) > 1 and sys.argv[1] in ("--full", "--full-expected"):
         set_dims(*[FULL[k] for k in ("T", "D", "H", "F", "INV_ITERS", "QK_STD")])
-        dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(HERE, "full")
+        dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(HERE, "full_ref" if GELU_REF else "full")
         os.makedirs(dst, exist_ok=True)
         if sys.argv[1] == "--full-expected":  # the committed pin: outputs only
-            r = write(dst, names={"y", "y_exact"})
+            r = write(dst, names={"y", "y_exact", "y_polygelu"} if GELU_REF else {"y", "y_exact"})
             os.replace(os.path.join(dst, "block.bin"), os.path.join(dst, "expected.bin"))
             os.replace(os.path.join(dst, "block.txt"), os.path.join(dst, "expected.txt"))
         else:

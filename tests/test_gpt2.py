@@ -173,6 +173,23 @@ def test_full_width_fixture_pinned(tmp_path):
     assert "heads 12" in open(os.path.join(str(tmp_path), "block.txt")).readline()
 
 
+def test_full_width_reference_gelu_fixture_pinned(tmp_path):
+    """The GPT-2-width fixture with the reference's GELU x piece (make_fixture.py --full --gelu-ref:
+    b3 = 0.5 s2 as plain_approx/poly.py:33 writes it) reproduces the committed full_ref/expected.bin,
+    including y_polygelu (the block with poly.py's gelu exactly as written, np.sign on x)."""
+    import numpy as np
+
+    subprocess.check_call([sys.executable, os.path.join(BLOCK_DIR, "make_fixture.py"), "--full", str(tmp_path),
+                           "--gelu-ref"], stdout=subprocess.DEVNULL)
+    got = _read_fixture(str(tmp_path), "block")
+    want = _read_fixture(os.path.join(BLOCK_DIR, "full_ref"), "expected")
+    for k in ("y", "y_exact", "y_polygelu"):
+        assert np.abs(got[k] - want[k]).max() < 1e-9, k
+    assert "gelu_ref 1" in open(os.path.join(str(tmp_path), "block.txt")).readline()
+    # the sign approximation is what separates the fixture from poly.py as written
+    assert np.abs(got["y"] - got["y_polygelu"]).max() < 0.05
+
+
 @pytest.mark.gpu
 def test_gpt2_block_full_width(tmp_path):
     """GPU, config C5 at GPT-2 width (T 128, d 768, 12 heads, d_ff 3072): the whole block against the
@@ -186,3 +203,20 @@ def test_gpt2_block_full_width(tmp_path):
     print(r.stdout)
     print(r.stderr)
     assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_gpt2_block_full_width_reference_gelu(tmp_path):
+    """GPU, config C5 at GPT-2 width with the block's GELU as the reference writes it
+    (GeluLastPiece::reference, poly.py's b3 = 0.5 s2): every stage within 1e-3 of the --gelu-ref
+    restatement; the error against the block with poly.py's gelu as written (np.sign) is printed.
+    Parity unpinned: the reference holds no outputs of its plain pipeline."""
+    _build()
+    subprocess.check_call([sys.executable, os.path.join(BLOCK_DIR, "make_fixture.py"), "--full", str(tmp_path),
+                           "--gelu-ref"], stdout=subprocess.DEVNULL)
+    r = subprocess.run([os.path.join(ROOT, "build", "gpt2_block_test"), str(tmp_path), "block"], capture_output=True,
+                       text=True, timeout=1500, cwd=ROOT)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0 and "ALL PASSED" in r.stdout, r.stdout + r.stderr
+    assert "0.5 s2 (reference)" in r.stdout, r.stdout

@@ -25,6 +25,11 @@ def _read(path, hwords):
 
 
 class Store:
+    """The trace's objects by id.  Small ones are cached; at N = 2^16 a ciphertext is tens of MB and
+    a parallel replay reads each one a few times, so the large ones are read from disk each time."""
+
+    CACHE_BYTES = 1 << 20
+
     def __init__(self, d):
         self.d = d
         self.cache = {}
@@ -48,7 +53,8 @@ class Store:
             v = a[:cnt] + 1j * a[cnt:2 * cnt] if cplx else a[:cnt].copy()
         else:
             raise ValueError(oid)
-        self.cache[oid] = v
+        if len(body) <= self.CACHE_BYTES:
+            self.cache[oid] = v
         return v
 
 
@@ -83,6 +89,7 @@ class Replayer:
         self.moduli = meta["moduli"]
         self.K = len(self.moduli)
         self.ctx = O.Context(meta["log_n"], self.moduli)
+        self.ctx._enc = O.lib().or_encoder_create(meta["log_n"])  # made once: a parallel replay shares it (read-only)
         keys = {}
         for f in os.listdir(d):
             if f.startswith("key_gal_"):
@@ -204,27 +211,44 @@ class Replayer:
             return a
         raise ValueError("unknown op " + op)
 
-    def replay(self):
-        """Returns (records checked, {op: count}); raises AssertionError at the first mismatch."""
+    def check(self, i, rec):
+        """Recompute record i and compare; returns None or the mismatch message."""
+        op = rec["op"]
+        want = self.expect(rec)
+        got = self.store.get(rec["out"])
+        if rec["out"][0] == "p":
+            gw, gs = got
+            ww, ws = want
+            if not np.array_equal(gw, ww):
+                return f"record {i} ({op}): plaintext words differ"
+            if gs != ws:
+                return f"record {i} ({op}): plaintext scale {gs!r} != {ws!r}"
+            return None
+        gc, _ = got
+        if gc.data.shape != want.data.shape:
+            return f"record {i} ({op}): shape {gc.data.shape} != {want.data.shape}"
+        bad = int((gc.data != want.data).sum())
+        if bad:
+            return f"record {i} ({op}): {bad} of {gc.data.size} words differ"
+        if gc.scale != want.scale:
+            return f"record {i} ({op}): scale {gc.scale!r} != {want.scale!r}"
+        return None
+
+    def replay(self, threads=1):
+        """Returns (records checked, {op: count}); raises AssertionError at the first mismatch (in
+        record order).  Records are independent given their recorded inputs, so threads > 1 checks
+        them concurrently (the oracle's C calls release the GIL)."""
         recs = [json.loads(l) for l in open(os.path.join(self.d, "trace.jsonl"))]
-        checked = 0
-        for i, rec in enumerate(recs):
-            op = rec["op"]
-            self.counts[op] = self.counts.get(op, 0) + 1
-            if op == "encrypt":
-                continue  # leaf
-            want = self.expect(rec)
-            got = self.store.get(rec["out"])
-            if rec["out"][0] == "p":
-                gw, gs = got
-                ww, ws = want
-                assert np.array_equal(gw, ww), f"record {i} ({op}): plaintext words differ"
-                assert gs == ws, f"record {i} ({op}): plaintext scale {gs!r} != {ws!r}"
-            else:
-                gc, _ = got
-                assert gc.data.shape == want.data.shape, f"record {i} ({op}): shape {gc.data.shape} != {want.data.shape}"
-                bad = int((gc.data != want.data).sum())
-                assert bad == 0, f"record {i} ({op}): {bad} of {gc.data.size} words differ"
-                assert gc.scale == want.scale, f"record {i} ({op}): scale {gc.scale!r} != {want.scale!r}"
-            checked += 1
-        return checked, dict(self.counts)
+        for rec in recs:
+            self.counts[rec["op"]] = self.counts.get(rec["op"], 0) + 1
+        todo = [(i, rec) for i, rec in enumerate(recs) if rec["op"] != "encrypt"]  # encryptions are leaves
+        if threads > 1:
+            from concurrent.futures import ThreadPoolExecutor
+
+            with ThreadPoolExecutor(max_workers=threads) as pool:
+                errs = list(pool.map(lambda ir: self.check(*ir), todo))
+        else:
+            errs = [self.check(i, rec) for i, rec in todo]
+        bad = [e for e in errs if e]
+        assert not bad, f"{len(bad)} of {len(todo)} records differ; first: {bad[0]}"
+        return len(todo), dict(self.counts)
