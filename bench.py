@@ -297,6 +297,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
     batch_wall = time.perf_counter() - t2
     hoisted, hoist_macs, _ = runner.hoist_stats(reset=True)
     scratch = runner.scratch_bytes()
+    free_b, total_b = torch.cuda.mem_get_info(device)  # device-wide (engine pool, keys, scratch, torch)
     # every image's decrypted logits against the plain network (exact ReLU), on every rank -- the
     # keys there may have arrived over RCCL; a miss fails the leg
     tol = 0.05 if layers <= 20 else 0.08
@@ -326,6 +327,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
         # device scratch the engine holds after the batch (per-stream workspaces, hoisting buffers,
         # Galois mask tables), beyond keys and ciphertexts (mhe_scratch_bytes)
         "scratch_GB": round(scratch / 1e9, 2),
+        "device_mem_used_GB_after_batch": round((total_b - free_b) / 1e9, 1),
         "galois_keys": info["galois_keys"],
         "galois_key_GB_resident": round(info["galois_key_gb"], 2),
         "key_format": ("prepared (mhe_key_prepare: 46-bit limbs streamed in 6 B)" if prepared else "SEAL layout")
@@ -527,13 +529,16 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host cores for the CPU baseline (16 = one GPU's share of the box's CPUs)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--resnet-images", type=int, default=8,
+    ap.add_argument("--resnet-images", type=int, default=24,
                     help="ResNet-20 CIFAR-10 images per GPU for the sec/image leg (0 = skip)")
     ap.add_argument("--resnet-layers", type=int, default=20, choices=(20, 110),
                     help="20: config C3 (ResNet-20); 110: config C4's network (ResNet-110, one image per GPU "
                          "with --resnet-images 1 --resnet-streams 1)")
-    ap.add_argument("--resnet-streams", type=int, default=2, help="host threads for the ResNet batch (one stream each)")
-    ap.add_argument("--resnet-fibers", type=int, default=4,
+    # 3 x 8 measured best on one MI355X (profiles/r05g_resnet_batch_shapes.txt: 1.43 images/s vs 1.30 at
+    # 2 x 4, 1.36 at 2 x 8, 1.18 at 4 x 8): 8 fibers fill a batched launch (MHE_MAXB), a third stream
+    # overlaps the small passes of the other two
+    ap.add_argument("--resnet-streams", type=int, default=3, help="host threads for the ResNet batch (one stream each)")
+    ap.add_argument("--resnet-fibers", type=int, default=8,
                     help="images per host thread at a time as one seal::FiberBatch (1 = one image per thread)")
     ap.add_argument("--c4", choices=("auto", "on", "off"), default="auto",
                     help="config C4 leg (ResNet-110, one image per GPU on the shared key set); auto = when N > 1")

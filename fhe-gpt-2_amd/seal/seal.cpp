@@ -193,7 +193,7 @@ parms_id_type EncryptionParameters::parms_id() const
 }
 
 // ------------------------------------------------------------------------------ SEALContext
-struct SEALContext::Impl
+struct SEALContext::Impl : std::enable_shared_from_this<SEALContext::Impl>
 {
     EncryptionParameters parms;
     std::vector<std::shared_ptr<ContextData>> levels; // by number of primes - 1
@@ -205,24 +205,60 @@ struct SEALContext::Impl
     bool insecure = false;
     std::mutex mu;
     std::unordered_map<std::thread::id, void *> streams;
+    // streams of threads that have exited: the next new thread takes one instead of creating a
+    // stream (and with it a scratch workspace) of its own.  A stream is never destroyed while the
+    // context lives -- objects written on it keep it as their writer -- so without the pool a
+    // process that starts threads per batch (the reference's OpenMP team, ResNetRunner::infer_batch)
+    // would grow one workspace per thread it ever ran.
+    std::vector<void *> idle;
+
+    // the calling thread's leases: on thread exit each still-living context gets the stream back
+    struct Leases
+    {
+        std::vector<std::weak_ptr<Impl>> ctx;
+        ~Leases()
+        {
+            const auto id = std::this_thread::get_id();
+            for (auto &w : ctx)
+                if (auto p = w.lock()) p->release(id);
+        }
+    };
+
+    void release(std::thread::id id)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = streams.find(id);
+        if (it == streams.end()) return;
+        idle.push_back(it->second);
+        streams.erase(it);
+    }
 
     void *stream()
     {
+        static thread_local Leases leases;
         std::lock_guard<std::mutex> g(mu);
         auto it = streams.find(std::this_thread::get_id());
         if (it != streams.end()) return it->second;
         void *s = nullptr;
-        chk(mhe_stream_create(eng, &s));
+        if (!idle.empty())
+        {
+            s = idle.back(); // ordered after its previous thread's work: same stream
+            idle.pop_back();
+        }
+        else
+            chk(mhe_stream_create(eng, &s));
         streams.emplace(std::this_thread::get_id(), s);
+        leases.ctx.push_back(weak_from_this());
         return s;
     }
 
     ~Impl()
     {
-        for (auto &kv : streams)
+        for (auto &kv : streams) idle.push_back(kv.second);
+        for (void *s : idle)
         {
-            (void)mhe_stream_sync(eng, kv.second);
-            (void)mhe_stream_destroy(eng, kv.second);
+            (void)mhe_stream_sync(eng, s);
+            (void)mhe_stream_destroy(eng, s);
         }
         if (eng) (void)mhe_ctx_destroy(eng);
     }

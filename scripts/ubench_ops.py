@@ -49,9 +49,9 @@ def main():
     keys = [rnd(L, 2, K, n, limbs=K) for _ in range(4)]
     for k in keys:
         eng.key_prepare(k)
-    cts = [rnd(2, L, n, limbs=L) for _ in range(4)]
+    cts = [rnd(2, L, n, limbs=L) for _ in range(8)]
     ct3 = [rnd(3, L, n, limbs=L) for _ in range(4)]
-    outs = [eng.empty(2, L - 1, n) for _ in range(4)]
+    outs = [eng.empty(2, L - 1, n) for _ in range(8)]
     rot_out = [eng.empty(2, L, n) for _ in range(4)]
     elts = [pow(5, s, 2 * n) for s in (1, 2, 4, 8)]
     # bsgs: the BSGS baby steps of several images (FiberBatch): each input rotated R ways, the R keys
@@ -69,11 +69,12 @@ def main():
 
     ops = {
         "rescale": lambda: eng.rescale_to_next(cts[0], outs[0]),
-        "rescale4": lambda: eng.rescale_batch(cts, outs),
+        "rescale4": lambda: eng.rescale_batch(cts[:4], outs[:4]),
+        "rescale8": lambda: eng.rescale_batch(cts, outs),
         "ks": lambda: eng.relinearize(ct3[0], keys[0]),
         "ks4": lambda: eng.switch_key_batch([c[:2] for c in ct3], [c[2] for c in ct3], keys),
         "ks4s": lambda: eng.switch_key_batch([c[:2] for c in ct3], [c[2] for c in ct3], [keys[0]] * 4),
-        "rot4": lambda: eng.apply_galois_batch(cts, elts, keys, rot_out),
+        "rot4": lambda: eng.apply_galois_batch(cts[:4], elts, keys, rot_out),
         "bsgs": lambda: eng.apply_galois_batch(b_in, b_el, b_k, b_out),
         "ntt": lambda: eng.ntt_forward(cts[1]),
         "hmult": lambda: eng.hmult(cts[2], cts[3], keys[0], outs[1]),

@@ -220,8 +220,8 @@ int main(int argc, char **argv)
             std::printf("  batch image %d: max |logit error| %.3g of max |logit| %.3g\n", id, err, mag);
             if (!(err < tol * std::max(1.0, mag))) fail++;
         }
-        std::printf("batch: %d images on %d streams in %.3f s = %.3f s/image (%.3f images/s)\n", images, threads, wall,
-                    wall / images, images / wall);
+        std::printf("batch: %d images on %d streams in %.3f s = %.3f s/image (%.3f images/s); engine scratch %.1f GB\n",
+                    images, threads, wall, wall / images, images / wall, runner.scratch_bytes() / 1e9);
     }
     std::printf("galois key memory %.1f GB; mean %.3f s/image\n", runner.galois_key_gb(),
                 total / std::max(1, sequential > 1 ? sequential - 1 : 1));
