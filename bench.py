@@ -263,6 +263,13 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
     params = os.path.join(ROOT, "tests", "golden", "resnet",
                           "resnet20_params.bin" if layers == 20 else f"resnet{layers}_params.d7")
     comp = os.path.join(ROOT, "tests", "golden", "comp")
+    mem = {}
+
+    def used(tag):  # device-wide bytes in use (engine pools, keys, scratch, torch), GB
+        free_b, total_b = torch.cuda.mem_get_info(device)
+        mem[tag] = round((total_b - free_b) / 1e9, 1)
+
+    used("before")
     t0 = time.perf_counter()
     runner = R.Runner(layers, params, comp, generate_keys=(rank == 0))
     shared = None
@@ -272,6 +279,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
         torch.cuda.synchronize(device)
         shared = {"buffers": nbuf, "GB": round(nbytes / 1e9, 2), "broadcast_s": round(time.perf_counter() - t1, 2)}
     setup = time.perf_counter() - t0
+    used("after_setup")
     info = runner.info()
     rng = np.random.default_rng(1000 + rank)
     imgs = rng.uniform(-2.5, 2.5, size=(images, 3072))
@@ -283,6 +291,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
     runner.key_traffic(reset=True)
     runner.op_counts(reset=True)
     one = runner.infer_batch(lat_imgs, 1)
+    used("after_latency_pass")
     key_bytes = runner.key_traffic(reset=True) / lat  # key-switching key bytes of one image
     # the engine operations of one image, by kind and level (mhe_op_counts): the op mix the CPU
     # estimate of the cpu_baseline leg prices
@@ -297,7 +306,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
     batch_wall = time.perf_counter() - t2
     hoisted, hoist_macs, _ = runner.hoist_stats(reset=True)
     scratch = runner.scratch_bytes()
-    free_b, total_b = torch.cuda.mem_get_info(device)  # device-wide (engine pool, keys, scratch, torch)
+    used("after_batch")
     # every image's decrypted logits against the plain network (exact ReLU), on every rank -- the
     # keys there may have arrived over RCCL; a miss fails the leg
     tol = 0.05 if layers <= 20 else 0.08
@@ -327,7 +336,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
         # device scratch the engine holds after the batch (per-stream workspaces, hoisting buffers,
         # Galois mask tables), beyond keys and ciphertexts (mhe_scratch_bytes)
         "scratch_GB": round(scratch / 1e9, 2),
-        "device_mem_used_GB_after_batch": round((total_b - free_b) / 1e9, 1),
+        "device_mem_used_GB": mem,
         "galois_keys": info["galois_keys"],
         "galois_key_GB_resident": round(info["galois_key_gb"], 2),
         "key_format": ("prepared (mhe_key_prepare: 46-bit limbs streamed in 6 B)" if prepared else "SEAL layout")
@@ -745,7 +754,11 @@ def main():
             "us_per_hmult": round(per_hmult_s * 1e6, 2),
         },
     }
-    del w  # the HMult leg's buffers (relin key, inputs) are not needed by the ResNet legs
+    # the HMult leg's engine (its per-stream workspaces: 8 entries at 44 limbs each) and buffers are
+    # not needed by the ResNet legs: destroyed here, not left to the garbage collector
+    torch.cuda.synchronize(dev)
+    w.eng.close()
+    del w
     torch.cuda.empty_cache()
     legs = []
     if args.resnet_images > 0:

@@ -296,25 +296,19 @@ static void timing_end(hipEvent_t *pair, hipStream_t st)
     if (pair) (void)hipEventRecord(pair[1], st);
 }
 
-// Scratch allocation that gives the stream-ordered pool's cached blocks back to the device when the
-// device reports out of memory: the pool keeps freed blocks (release threshold: never), which a plain
-// hipMalloc cannot reuse.  Trims what is free now, then once more after the device drained (frees
-// still queued on streams complete), retrying after each.
-static hipError_t dev_alloc(mhe_ctx *c, void **p, size_t bytes)
+// Scratch allocation (hipMalloc) that, when the device reports out of memory, first gives the
+// blocks the engine's caching allocator holds back to the device (mhe_internal_release_cached:
+// synchronises the device) and retries once.  Freed ciphertext / key buffers stay cached for reuse at
+// their own sizes; a plain hipMalloc cannot use them.
+static void release_cached_blocks();
+static hipError_t scratch_alloc(void **p, size_t bytes)
 {
     hipError_t e = hipMalloc(p, bytes);
     if (e == hipSuccess) return e;
     (void)hipGetLastError();
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, c->device) != hipSuccess) return e;
-    for (int round = 0; round < 2; round++)
-    {
-        if (round == 1) (void)hipDeviceSynchronize();
-        (void)hipMemPoolTrimTo(pool, 0);
-        e = hipMalloc(p, bytes);
-        if (e == hipSuccess) return e;
-        (void)hipGetLastError();
-    }
+    release_cached_blocks();
+    e = hipMalloc(p, bytes);
+    if (e != hipSuccess) (void)hipGetLastError();
     return e;
 }
 
@@ -356,7 +350,7 @@ static int get_ws(mhe_ctx *c, hipStream_t st, int limbs, Workspace **out, int en
         const size_t per = Lc * n + (L + 1) * L * n + 2 * (L + 1) * n + 3 * L * n;
         size_t words = (size_t)E * per + L * n;
         HIP_TRY(hipSetDevice(c->device));
-        if (injected_alloc_failure(c) || dev_alloc(c, (void **)&w.base, words * sizeof(u64)) != hipSuccess)
+        if (injected_alloc_failure(c) || scratch_alloc((void **)&w.base, words * sizeof(u64)) != hipSuccess)
         {
             w.base = nullptr;
             w.max_limbs = 0;
@@ -1352,6 +1346,13 @@ void release_cached(DevAlloc &a)
     a.cached = 0;
 }
 } // namespace
+
+static void release_cached_blocks()
+{
+    DevAlloc &a = dev_alloc();
+    std::lock_guard<std::mutex> g(a.mu);
+    release_cached(a);
+}
 
 // context lifetime on the current device (mhe_ctx_create / mhe_ctx_destroy): when the last context
 // of a device goes, its cached blocks go back to the device, so another process (or a later
@@ -2429,6 +2430,14 @@ MHE_EXPORT int mhe_ctx_set_timing(mhe_ctx *c, int on)
 
 static bool hoist_ok(const mhe_ctx *c);
 
+MHE_EXPORT int mhe_trim(mhe_ctx *c)
+{
+    if (!valid_ctx(c)) return fail(MHE_ERR_ARG, "context is not valid");
+    HIP_TRY(hipSetDevice(c->device));
+    release_cached_blocks();
+    return MHE_OK;
+}
+
 MHE_EXPORT int mhe_debug_fail_alloc(mhe_ctx *c, int nth)
 {
     if (!valid_ctx(c) || nth < 0) return fail(MHE_ERR_ARG, "invalid argument");
@@ -3071,7 +3080,7 @@ static int get_hoist(mhe_ctx *c, hipStream_t st, int entries, int ws_entries, in
         const size_t per = (size_t)(HL + 1) * HL * c->n, pacc = (size_t)2 * (HL + 1) * c->n;
         const int na = MHE_MAXB * MHE_HOIST_R;
         const size_t bytes = ((size_t)E * per + (size_t)na * pacc) * sizeof(u64);
-        if (injected_alloc_failure(c) || dev_alloc(c, (void **)&w->hoist_base, bytes) != hipSuccess)
+        if (injected_alloc_failure(c) || scratch_alloc((void **)&w->hoist_base, bytes) != hipSuccess)
         {
             w->hoist_base = nullptr;
             return fail(MHE_ERR_MEMORY, "workspace allocation failed");

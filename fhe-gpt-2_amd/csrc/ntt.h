@@ -904,16 +904,18 @@ static inline void launch_pass_a(const Job &job, int log_n, int jobs, long long 
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
     dim3 grid(subs / SH::S, jobs);
-    if (PASS == FWD_COL) hipLaunchKernelGGL((k_fwd_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
-    if (PASS == FWD_ROW)
+    // if constexpr: only the pass asked for is instantiated for this Job (four kernels per Job
+    // otherwise, most of them never launched)
+    if constexpr (PASS == FWD_COL) hipLaunchKernelGGL((k_fwd_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if constexpr (PASS == FWD_ROW)
     {
         if ((long)grid.x * grid.y <= row_pre_max_wg())
             hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP, true>), grid, dim3(256), 0, st, job, log_n, twd);
         else
             hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP, false>), grid, dim3(256), 0, st, job, log_n, twd);
     }
-    if (PASS == INV_ROW) hipLaunchKernelGGL((k_inv_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
-    if (PASS == INV_COL) hipLaunchKernelGGL((k_inv_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if constexpr (PASS == INV_ROW) hipLaunchKernelGGL((k_inv_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if constexpr (PASS == INV_COL) hipLaunchKernelGGL((k_inv_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
 }
 
 template <int PASS, int LOGR, class Job>

@@ -37,6 +37,7 @@ SIGNATURES = {
     "mhe_hoist_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_debug_fail_alloc": (ctypes.c_int, [vp, ctypes.c_int]),
+    "mhe_trim": (ctypes.c_int, [vp]),
     "mhe_scratch_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]),
     "mhe_malloc_async": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.c_size_t, vp]),

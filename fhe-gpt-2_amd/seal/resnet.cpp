@@ -385,6 +385,9 @@ void ResNetRunner::finish_setup(bool plan_galois_keys)
     }
     galois_keys_ = m.gal_keys.usage().size();
     prepare_keys();
+    // the planning inference's deferred keys and temporaries are freed by now; the allocator keeps
+    // them cached at their sizes, which the steady state (ciphertexts, scratch) never reuses
+    if (mhe_trim(m.context->engine()) != 0) throw std::runtime_error(mhe_last_error());
     setup_s_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count();
 }
 

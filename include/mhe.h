@@ -151,6 +151,11 @@ int mhe_scratch_bytes(mhe_ctx *ctx, uint64_t *workspace, uint64_t *hoisting, uin
  * memory; 0 turns it off.  Used to check that a batched call that fails part way leaves its
  * operands as they were (tests/cpp/seal_batch_test.cpp). */
 int mhe_debug_fail_alloc(mhe_ctx *ctx, int nth);
+/* Give the device memory the engine's caching allocator holds for reuse (freed ciphertext / key
+ * buffers, kept per size for the stream-ordered mhe_malloc_async) back to the device.  Synchronises
+ * the device.  For after a setup phase that freed much more than the steady state reuses (e.g. the
+ * ResNet runner's planning inference and its deferred keys). */
+int mhe_trim(mhe_ctx *ctx);
 int mhe_stream_create(mhe_ctx *ctx, void **stream);
 int mhe_stream_destroy(mhe_ctx *ctx, void *stream);
 
