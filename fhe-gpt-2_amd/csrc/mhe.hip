@@ -573,6 +573,8 @@ struct JobModDownCol
             if (reduce) t = barrett64(t, p);
             return t + fix;
         }
+        // the integer lift() stands for, from s canonical mod P: s - P when s > P/2, else s
+        __device__ double lift_c(u64 s) const { return fp_from_u52(s) - (s > half ? (double)P.q : 0.0); }
         __device__ u64 load(u32 x) const { return lift(src[x]); }
         __device__ void store(u32 x, u64 v) const { dst[x] = v; }
     };
@@ -683,6 +685,8 @@ struct JobRescaleCol
             if (reduce) v = barrett64(v, p);
             return v + neg_half;
         }
+        // the integer lift() stands for: s - q_last when s > q_last/2, else s
+        __device__ double lift_c(u64 s) const { return fp_from_u52(s) - (s > half ? (double)ql : 0.0); }
         __device__ u64 load(u32 x) const { return lift(src[x]); }
         __device__ void store(u32 x, u64 v) const { dst[x] = v; }
     };

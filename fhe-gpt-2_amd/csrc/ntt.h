@@ -532,21 +532,37 @@ struct ColSrc
     }
 };
 
+#ifndef MHE_ICOL_G
+#define MHE_ICOL_G 3 // at most this many output primes per k_icol_lift workgroup (icol_lift_a)
+#endif
 template <int LOGR, int LOGT, class Job, bool FP>
-__global__ __launch_bounds__(256) void k_icol_lift(ColSrc cs, Job job, int cnt, int log_n, long long dinv,
-                                                   long long dfwd)
+__global__ __launch_bounds__(256, 3) void k_icol_lift(ColSrc cs, Job job, int cnt, int log_n, long long dinv,
+                                                      long long dfwd)
 {
     using SH = Shape<LOGR, LOGT>;
     using A = NttArith<FP>;
     using T = typename A::T;
-    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
+    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD, R = SH::R;
     __shared__ T lds[S * LD];
+    // FP: the forward column twiddles of the group's primes (entries 1 .. R-1 of each table, the same
+    // for every column), staged once.  Read from global memory in the prime loop, each twiddle load's
+    // wait also waited for the previous prime's stores (one counter for loads and stores).
+    __shared__ TwF twc[FP ? MHE_ICOL_G * R : 1];
     const int tid = threadIdx.x, sl = tid % S, t = tid / S;
     const int logC = log_n - LOGR;
     const u32 c = blockIdx.x * S + sl;
     const int s = blockIdx.y;
     const int IG = gridDim.z, g = blockIdx.z;
-    const int i_lo = (cnt * g) / IG, i_hi = (cnt * (g + 1)) / IG;
+    const int i_lo = (cnt * g) / IG, i_hi = (cnt * (g + 1)) / IG; // i_hi - i_lo <= MHE_ICOL_G (host)
+    if constexpr (FP)
+    {
+        for (int i = i_lo; i < i_hi; i++)
+        {
+            const auto V = job.view(s * cnt + i);
+            const TwF *tf = reinterpret_cast<const TwF *>(reinterpret_cast<const char *>(V.tw) + dfwd);
+            for (int k = tid; k < R; k += 256) twc[(i - i_lo) * R + k] = tf[k];
+        }
+    }
     u64 x[E];
     {
         // the inverse column pass of k_inv_col, canonical output
@@ -573,37 +589,79 @@ __global__ __launch_bounds__(256) void k_icol_lift(ColSrc cs, Job job, int cnt, 
             for (int e = 0; e < gap; e++) ai.inv_last(v[e], v[e + gap], P);
         }
 #pragma unroll
-        for (int e = 0; e < E; e++)
-        {
-            if constexpr (FP)
-                x[e] = ai.out(v[e]);
-            else
-                x[e] = ai.canon(v[e]);
-        }
+        for (int e = 0; e < E; e++) x[e] = ai.canon(v[e]);
     }
     // x[e] is the coefficient at c + ((t + TPS e) << logC): the forward column pass's load order
-    for (int i = i_lo; i < i_hi; i++)
+    if constexpr (FP)
     {
-        const auto V = job.view(s * cnt + i);
-        const A ar(V.p, V.tw, dfwd);
-        T v[E];
+        // The lift as the centred integer c (|c| < 2^50, the same for every output prime) reduced
+        // mod q_i in FP64: congruent to the integer lift's [0, 2q_i) value, so the same residues,
+        // without its 64-bit Barrett reduction and u64 -> f64 conversion per prime.
+        double cd[E];
+        {
+            const auto V0 = job.view(s * cnt + i_lo);
 #pragma unroll
-        for (int e = 0; e < E; e++) v[e] = ar.in(V.lift(x[e]));
+            for (int e = 0; e < E; e++) cd[e] = V0.lift_c(x[e]);
+        }
+        // two sweeps over the group's primes, the q < 2^47 ones with the lazy forward butterflies
+        // first (the lift leaves |v| <= q/2 + 1, 8 stages grow it to <= 12.5q), so each loop body
+        // has one arithmetic variant (one body with both needed ~100 more VGPRs)
+        auto sweep = [&](auto lz) {
+            constexpr bool LZ = decltype(lz)::value;
+            for (int i = i_lo; i < i_hi; i++)
+            {
+                const auto V = job.view(s * cnt + i);
+                if ((V.p.q < (1ull << 47)) != LZ) continue; // uniform per workgroup
+                const NttArithF<LZ> ar(V.p, V.tw, dfwd);
+                const TwF *tl = &twc[(i - i_lo) * R];
+                T v[E];
 #pragma unroll
-        for (int st = 0; st < LOGE; st++)
-            ar.template fwd<E>(v, 1 << (LOGE - 1 - st), [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
-        lds_barrier(); // lds still holds the previous prime's (or the inverse pass's) transpose
+                for (int e = 0; e < E; e++) v[e] = fp_reduce(cd[e], ar.q, ar.qinv);
 #pragma unroll
-        for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
-        lds_barrier(); // LDS only: the previous prime's stores stay in flight
+                for (int st = 0; st < LOGE; st++)
+                    ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - st), tl, [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+                lds_barrier(); // lds still holds the previous prime's (or the inverse pass's) transpose
 #pragma unroll
-        for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+                for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+                lds_barrier(); // LDS only: the previous prime's stores stay in flight
 #pragma unroll
-        for (int st = LOGE; st < LOGR; st++)
-            ar.template fwd<E>(v, 1 << (LOGR - 1 - st),
-                               [&](int e) { return (1 << st) + ((E * t + e) >> (LOGR - st)); });
+                for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
-        for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
+                for (int st = LOGE; st < LOGR; st++)
+                    ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - st), tl,
+                                           [&](int e) { return (1 << st) + ((E * t + e) >> (LOGR - st)); });
+#pragma unroll
+                for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
+            }
+        };
+        sweep(std::true_type{});
+        sweep(std::false_type{});
+    }
+    else
+    {
+        for (int i = i_lo; i < i_hi; i++)
+        {
+            const auto V = job.view(s * cnt + i);
+            const A ar(V.p, V.tw, dfwd);
+            T v[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = ar.in(V.lift(x[e]));
+#pragma unroll
+            for (int st = 0; st < LOGE; st++)
+                ar.template fwd<E>(v, 1 << (LOGE - 1 - st), [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+            lds_barrier(); // lds still holds the previous prime's (or the inverse pass's) transpose
+#pragma unroll
+            for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+            lds_barrier(); // LDS only: the previous prime's stores stay in flight
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+#pragma unroll
+            for (int st = LOGE; st < LOGR; st++)
+                ar.template fwd<E>(v, 1 << (LOGR - 1 - st),
+                                   [&](int e) { return (1 << st) + ((E * t + e) >> (LOGR - st)); });
+#pragma unroll
+            for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
+        }
     }
 }
 
@@ -965,7 +1023,7 @@ static inline void icol_lift_a(const ColSrc &cs, const Job &job, int polys, int 
     // batched ones share the inverse stages over 2-3 primes (ubench at 31 / 20 limbs, profiles/r03v:
     // 4 rescales 207 -> 185 us)
     const int jobs = polys * cnt;
-    const int per = jobs >= 128 ? 3 : jobs >= 56 ? 2 : 1;
+    const int per = jobs >= 128 ? MHE_ICOL_G : jobs >= 56 ? 2 : 1;
     const int IG = (cnt + per - 1) / per;
     hipLaunchKernelGGL((k_icol_lift<LOGR, LOGT, Job, FP>), dim3(subs / SH::S, polys, IG), dim3(256), 0, st, cs, job,
                        cnt, log_n, dinv, dfwd);

@@ -5,7 +5,7 @@
 set -eu
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-D=$ROOT/build/var/$NAME
+D=$ROOT/build/${VARDIR:-var}/$NAME
 mkdir -p "$D"
 make -s -C "$ROOT/fhe-gpt-2_amd/csrc" OUT="$D/libmhe.so" BUILD="$D/obj" \
   HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -fvisibility=hidden -ffp-contract=off -Wall -Wno-unused-function $*"
