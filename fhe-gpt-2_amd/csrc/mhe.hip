@@ -808,6 +808,16 @@ struct JobMDRCol
             return csub(csub(u, p.two_q), p.q);
         }
         __device__ void store(u32 x, u64 v) const { dst[x] = v; }
+        // k_col_lift2 (FP): the two lifts' centred integers, the same for every output prime -- the
+        // special accumulator limb (in [0, 2P)) and the rescale's last limb (canonical mod q_last)
+        __device__ void src_c(u32 x, double &ct, double &cr) const
+        {
+            const u64 a = csub(accP[x], P.q), l = lastp[x];
+            ct = fp_from_u52(a) - (a > halfP ? (double)P.q : 0.0);
+            cr = fp_from_u52(l) - (l > halfL ? (double)ql : 0.0);
+        }
+        // t P^-1 + r mod p from them: |.| < 1.25p + 2^50, congruent to load()'s value
+        __device__ double lift_f(double ct, double cr) const { return fp_mulmod_gen(ct, pinvd, pd, pi) + cr; }
     };
     __device__ View view(int y) const
     {
@@ -1676,7 +1686,10 @@ static void run_moddown(mhe_ctx *c, const KsJob *jobs, int B, int L, Workspace *
             fwd_row(dr, log_n, 2 * B, c->nm, st);
             inv_row(li, log_n, 2 * B, c->nm, st);
             inv_col(j2, log_n, 2 * B, c->nm, st);
-            fwd_col(mc, log_n, 2 * (L - 1) * B, c->nm, st);
+            if (c->nm.fp == 1)
+                col_lift2(mc, 2 * B, L - 1, log_n, c->nm, st);
+            else
+                fwd_col(mc, log_n, 2 * (L - 1) * B, c->nm, st);
             fwd_row(mr, log_n, 2 * (L - 1) * B, c->nm, st);
         }
     }

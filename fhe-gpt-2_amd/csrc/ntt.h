@@ -200,6 +200,11 @@ struct NttArith<false>
     {
         inv_stage<E>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, q2);
     }
+    template <int E, class Ix>
+    __device__ void inv_tab(T (&v)[E], int gap, const TW *tab, Ix ix) const
+    {
+        inv_stage<E>(v, gap, [&](int e) { return &tab[ix(e)]; }, q, q2);
+    }
     __device__ void inv_last(T &x, T &y, const PrimeDev &p) const { inv_bfly_last(x, y, p); }
 };
 
@@ -232,6 +237,11 @@ struct NttArithF
     __device__ void inv(T (&v)[E], int gap, Ix ix) const
     {
         inv_stage_f<E>(v, gap, [&](int e) { return &tw[ix(e)]; }, q, qinv);
+    }
+    template <int E, class Ix>
+    __device__ void inv_tab(T (&v)[E], int gap, const TW *tab, Ix ix) const
+    {
+        inv_stage_f<E>(v, gap, [&](int e) { return &tab[ix(e)]; }, q, qinv);
     }
     __device__ void inv_last(T &x, T &y, const PrimeDev &p) const
     {
@@ -377,9 +387,16 @@ struct RowLds
     }
 };
 
+// Row passes load the twiddles of the first stage(s) after their transpose together with the data
+// (MHE_ROW_TWPF=0: where the stage uses them)
+#ifndef MHE_ROW_TWPF
+#define MHE_ROW_TWPF 1
+#endif
+
 // --------------------------------------------------------------------- forward, row pass
+// FP with the up-front prefetch: 3 waves/SIMD (<= 168 VGPRs)
 template <int LOGR, int LOGT, class Job, bool FP, bool PRE_ON = true>
-__global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long twd)
+__global__ __launch_bounds__(256, (FP && PRE_ON) ? 3 : 1) void k_fwd_row(Job job, int log_n, long long twd)
 {
     using SH = Shape<LOGR, LOGT>;
     using A = NttArith<FP>;
@@ -405,6 +422,20 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long t
 #pragma unroll
         for (int e = 0; e < E; e++) pr[e] = V.pre(base + t + TPS * e);
     }
+    // The twiddles of the first two stages after the transpose, loaded here with the data: the
+    // transpose's fence keeps the compiler from issuing them earlier, and each was a serialised L2
+    // round trip in the middle of the workgroup's life (3 workgroups per CU do not hide it).  Stage
+    // s >= LOGE uses entries (rb << s) + (E t >> (LOGR - s)) + (e >> (LOGR - s)).
+    using TWT = typename A::TW;
+    constexpr int C0 = E >> (LOGR - LOGE), C1 = E >> (LOGR - LOGE - 1);
+    [[maybe_unused]] TWT p0[C0], p1[C1];
+    if constexpr (MHE_ROW_TWPF)
+    {
+#pragma unroll
+        for (int j = 0; j < C0; j++) p0[j] = ar.tw[(rb << LOGE) + ((E * t) >> (LOGR - LOGE)) + j];
+#pragma unroll
+        for (int j = 0; j < C1; j++) p1[j] = ar.tw[(rb << (LOGE + 1)) + ((E * t) >> (LOGR - LOGE - 1)) + j];
+    }
 #pragma unroll
     for (int s = 0; s < LOGE; s++)
         ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (rb << s) + (e >> (LOGE - s)); });
@@ -415,11 +446,50 @@ __global__ __launch_bounds__(256) void k_fwd_row(Job job, int log_n, long long t
     for (int e = 0; e < E; e++) v[e] = lds[RL::at(sl, E * t + e)];
 #pragma unroll
     for (int s = LOGE; s < LOGR; s++)
-        ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
+    {
+        if (MHE_ROW_TWPF && s == LOGE)
+            ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - s), p0, [&](int e) { return e >> (LOGR - s); });
+        else if (MHE_ROW_TWPF && s == LOGE + 1)
+            ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - s), p1, [&](int e) { return e >> (LOGR - s); });
+        else
+            ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
+    }
     // transpose back so stores (and epilogue reads) are coalesced
 #pragma unroll
     for (int e = 0; e < E; e++) lds[RL::at(sl, E * t + e)] = v[e];
     wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
+    if constexpr (!PRE && PreOf<VW>::value)
+    {
+        // Large launches run without the up-front prefetch (4 instead of 3 waves/SIMD), and a plain
+        // store(x, o) would load its operands after the previous store: E serialised round trips.
+        // Groups of 4 instead, the next group's operands loaded before this group's stores.
+        constexpr int G = 4;
+        static_assert(E % G == 0, "epilogue groups");
+        using PT = typename PreOf<VW>::type;
+        PT cur[G], nxt[G];
+#pragma unroll
+        for (int k = 0; k < G; k++) cur[k] = V.pre(base + t + TPS * k);
+#pragma unroll
+        for (int e0 = 0; e0 < E; e0 += G)
+        {
+            if (e0 + G < E)
+            {
+#pragma unroll
+                for (int k = 0; k < G; k++) nxt[k] = V.pre(base + t + TPS * (e0 + G + k));
+            }
+#pragma unroll
+            for (int k = 0; k < G; k++)
+            {
+                const int e = e0 + k;
+                int src = t + TPS * e;
+                if constexpr (BrevOf<VW>::value && LOGR == 8) src = (int)brev8_ntt((u32)src);
+                V.store(base + t + TPS * e, ar.out(lds[RL::at(sl, src)]), cur[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < G; k++) cur[k] = nxt[k];
+        }
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < E; e++)
     {
@@ -451,6 +521,14 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long t
     if (V.skip) return; // uniform per workgroup, before any barrier
     const A ar(V.p, V.tw, twd);
     T v[E];
+    // the first stage's twiddles with the data (see k_fwd_row): entries (rb << s) + (E t >> 1) + j
+    using TWT = typename A::TW;
+    [[maybe_unused]] TWT p0[E / 2];
+    if constexpr (MHE_ROW_TWPF)
+    {
+#pragma unroll
+        for (int j = 0; j < E / 2; j++) p0[j] = ar.tw[(rb << (LOGR - 1)) + ((E * t) >> 1) + j];
+    }
 #pragma unroll
     for (int e = 0; e < E; e++) lds[RL::at(sl, t + TPS * e)] = ar.in(V.load(base + t + TPS * e));
     wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
@@ -458,7 +536,12 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long t
     for (int e = 0; e < E; e++) v[e] = lds[RL::at(sl, E * t + e)];
 #pragma unroll
     for (int s = LOGR - 1; s >= LOGE; s--)
-        ar.template inv<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
+    {
+        if (MHE_ROW_TWPF && s == LOGR - 1)
+            ar.template inv_tab<E>(v, 1 << (LOGR - 1 - s), p0, [&](int e) { return e >> 1; });
+        else
+            ar.template inv<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (rb << s) + ((E * t + e) >> (LOGR - s)); });
+    }
 #pragma unroll
     for (int e = 0; e < E; e++) lds[RL::at(sl, E * t + e)] = v[e];
     wave_lds_fence(); // a sub-transform is TPS <= 16 consecutive lanes of one wave
@@ -663,6 +746,72 @@ __global__ __launch_bounds__(256, 3) void k_icol_lift(ColSrc cs, Job job, int cn
             for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
         }
     }
+}
+
+// ------------------------------------------------------------- FP64 lift column pass, two sources
+// The fused HMult tail's column pass (JobMDRCol): every output prime's input is a function of two
+// prime-independent source words (the special accumulator limb and the rescale's last limb).  One
+// workgroup per (column block, source poly, group of <= MHE_ICOL_G output primes) reads them once,
+// as centred doubles (View::src_c), and per prime forms the lift (View::lift_f), reduces it and runs
+// the forward column stages with twiddles staged in LDS, the q < 2^47 primes with lazy butterflies
+// -- k_fwd_col instead re-read both sources and redid the integer lift per prime.  FP contexts only.
+template <int LOGR, int LOGT, class Job>
+__global__ __launch_bounds__(256, 3) void k_col_lift2(Job job, int cnt, int log_n, long long dfwd)
+{
+    using SH = Shape<LOGR, LOGT>;
+    using T = double;
+    constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD, R = SH::R;
+    __shared__ T lds[S * LD];
+    __shared__ TwF twc[MHE_ICOL_G * R];
+    const int tid = threadIdx.x, sl = tid % S, t = tid / S;
+    const int logC = log_n - LOGR;
+    const u32 c = blockIdx.x * S + sl;
+    const int s = blockIdx.y;
+    const int IG = gridDim.z, g = blockIdx.z;
+    const int i_lo = (cnt * g) / IG, i_hi = (cnt * (g + 1)) / IG; // i_hi - i_lo <= MHE_ICOL_G (host)
+    for (int i = i_lo; i < i_hi; i++)
+    {
+        const auto V = job.view(s * cnt + i);
+        const TwF *tf = reinterpret_cast<const TwF *>(reinterpret_cast<const char *>(V.tw) + dfwd);
+        for (int k = tid; k < R; k += 256) twc[(i - i_lo) * R + k] = tf[k];
+    }
+    double ca[E], cb[E];
+    {
+        const auto V0 = job.view(s * cnt + i_lo);
+#pragma unroll
+        for (int e = 0; e < E; e++) V0.src_c(c + ((u32)(t + TPS * e) << logC), ca[e], cb[e]);
+    }
+    lds_barrier(); // twiddles visible
+    auto sweep = [&](auto lz) {
+        constexpr bool LZ = decltype(lz)::value;
+        for (int i = i_lo; i < i_hi; i++)
+        {
+            const auto V = job.view(s * cnt + i);
+            if ((V.p.q < (1ull << 47)) != LZ) continue; // uniform per workgroup
+            const NttArithF<LZ> ar(V.p, V.tw, dfwd);
+            const TwF *tl = &twc[(i - i_lo) * R];
+            T v[E];
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = fp_reduce(V.lift_f(ca[e], cb[e]), ar.q, ar.qinv);
+#pragma unroll
+            for (int st = 0; st < LOGE; st++)
+                ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - st), tl, [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+            lds_barrier(); // lds still holds the previous prime's transpose
+#pragma unroll
+            for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
+            lds_barrier(); // LDS only: the previous prime's stores stay in flight
+#pragma unroll
+            for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
+#pragma unroll
+            for (int st = LOGE; st < LOGR; st++)
+                ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - st), tl,
+                                       [&](int e) { return (1 << st) + ((E * t + e) >> (LOGR - st)); });
+#pragma unroll
+            for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
+        }
+    };
+    sweep(std::true_type{});
+    sweep(std::false_type{});
 }
 
 // ------------------------------------------------- key-switch ModUp, digit-major column pass
@@ -1047,6 +1196,30 @@ static inline void icol_lift(const ColSrc &cs, const Job &job, int polys, int cn
         if (m.fp) icol_lift_a<8, Job, true>(cs, job, polys, cnt, log_n, m.dinv, m.dfwd, st);
         else icol_lift_a<8, Job, false>(cs, job, polys, cnt, log_n, 0, 0, st);
         break;
+    }
+}
+// k_col_lift2 over `polys` source polys and `cnt` output primes each (job s * cnt + i), FP contexts
+template <int LOGR, class Job>
+static inline void col_lift2_a(const Job &job, int polys, int cnt, int log_n, long long dfwd, hipStream_t st)
+{
+    constexpr int LOGT = LOGR <= 7 ? 3 : 4;
+    using SH = Shape<LOGR, LOGT>;
+    const int subs = 1 << (log_n - LOGR);
+    const int jobs = polys * cnt;
+    const int per = jobs >= 128 ? MHE_ICOL_G : jobs >= 56 ? 2 : 1; // as icol_lift_a
+    const int IG = (cnt + per - 1) / per;
+    hipLaunchKernelGGL((k_col_lift2<LOGR, LOGT, Job>), dim3(subs / SH::S, polys, IG), dim3(256), 0, st, job, cnt, log_n,
+                       dfwd);
+}
+template <class Job>
+static inline void col_lift2(const Job &job, int polys, int cnt, int log_n, const NttMode &m, hipStream_t st)
+{
+    if (cnt <= 0 || polys <= 0 || m.fp != 1) return;
+    switch ((log_n + 1) / 2)
+    {
+    case 6: col_lift2_a<6>(job, polys, cnt, log_n, m.dfwd, st); break;
+    case 7: col_lift2_a<7>(job, polys, cnt, log_n, m.dfwd, st); break;
+    case 8: col_lift2_a<8>(job, polys, cnt, log_n, m.dfwd, st); break;
     }
 }
 template <class Job> static inline void fwd_col(const Job &j, int log_n, int jobs, const NttMode &m, hipStream_t st) { launch_col<FWD_COL>(j, log_n, jobs, m, st); }
