@@ -1099,6 +1099,8 @@ enum PassKind
 // the operands in registers the kernel runs at 3 instead of 4 waves/SIMD, which pays for latency-bound
 // launches of a few rounds (ResNet's rescales and ModDowns) but not for the HMult tail's ~11k
 // workgroups.
+// (r05t: with the grouped epilogue loads of the large launches applied everywhere instead, the
+// ResNet-20 batch ran at 1.398 instead of 1.450 images/s; the ops at 25-31 limbs measured equal)
 static inline long row_pre_max_wg()
 {
     return 8192L;
