@@ -387,10 +387,27 @@ struct RowLds
     }
 };
 
+// Bijective LDS index swizzle: conflict-free ds_write_b64 / ds_read_b64 for all three
+// transpose layouts (bank model of MI355X_MICROARCH.md §LDS; checked in scripts).
+__device__ __forceinline__ u32 swz(u32 r)
+{
+    return r ^ ((r >> 3) & 3) ^ (((r >> 5) & 7) << 2);
+}
+
+// Residue index held in slot e by lane t for a layout whose 3 in-lane bits start at b_lo.
+__device__ __forceinline__ u32 lay(u32 t, int e, int b_lo)
+{
+    return ((t >> b_lo) << (b_lo + 3)) | ((u32)e << b_lo) | (t & ((1u << b_lo) - 1));
+}
+
 // Row passes load the twiddles of the first stage(s) after their transpose together with the data
 // (MHE_ROW_TWPF=0: where the stage uses them)
 #ifndef MHE_ROW_TWPF
 #define MHE_ROW_TWPF 1
+#endif
+// row passes at n = 2^16 in FP64 run k_fwd_row3 / k_inv_row3 (8 residues per lane, three phases)
+#ifndef MHE_ROW3
+#define MHE_ROW3 1
 #endif
 
 // --------------------------------------------------------------------- forward, row pass
@@ -503,6 +520,69 @@ __global__ __launch_bounds__(256, (FP && PRE_ON) ? 3 : 1) void k_fwd_row(Job job
     }
 }
 
+// ------------------------------------------- forward row pass, 2^8-point rows, three phases
+// k_fwd_row holds 16 residues per lane (two register phases, one transpose): with an epilogue
+// prefetch that is ~150 VGPRs, 3 waves/SIMD, and each workgroup does one load-compute-store round,
+// so the latency of the small launches shows.  Here 8 residues per lane in three register phases
+// of 3, 3 and 2 stages (k_ks_row_mac's layouts: positions lay(t, e, 5), lay(t, e, 2) and 8t + e,
+// wave-local swizzled transposes), 8 rows of 32 lanes per workgroup: about 100 VGPRs and 16 KB of
+// LDS.  A third transpose returns to the first layout, in which loads, epilogue operands and
+// stores are coalesced across lanes.  n = 2^16, FP64.
+template <class Job>
+__global__ __launch_bounds__(256) void k_fwd_row3(Job job, int log_n, long long twd)
+{
+    constexpr int LOGR = 8, R = 256, TPS = 32, S = 8, B_A = 5, B_B = 2;
+    using A = NttArith<true>;
+    using T = double;
+    __shared__ T lds[S * R];
+    const int tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
+    const u32 b = blockIdx.x * S + sl;
+    const u32 base = b << LOGR;
+    const u32 rb = (1u << (log_n - LOGR)) + b;
+    const auto V = job.view(blockIdx.y);
+    if (V.skip) return; // uniform per workgroup
+    using VW = std::remove_cv_t<decltype(V)>;
+    constexpr bool PRE = PreOf<VW>::value;
+    const A ar(V.p, V.tw, twd);
+    T *x = &lds[sl * R];
+    T v[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) v[e] = ar.in(V.load(base + lay(t, e, B_A)));
+    [[maybe_unused]] typename PreOf<VW>::type pr[8];
+    if constexpr (PRE)
+    {
+#pragma unroll
+        for (int e = 0; e < 8; e++) pr[e] = V.pre(base + lay(t, e, B_A));
+    }
+    auto stages = [&](int b_lo, int s0, int s1) {
+#pragma unroll
+        for (int s = s0; s < s1; s++)
+            ar.template fwd<8>(v, 1 << (LOGR - 1 - s - b_lo), [&](int e) { return (rb << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
+    };
+    auto transpose = [&](int from, int to) {
+        wave_lds_fence(); // the previous transpose's reads come first
+#pragma unroll
+        for (int e = 0; e < 8; e++) x[swz(lay(t, e, from))] = v[e];
+        wave_lds_fence(); // a row is 32 lanes of one wave
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = x[swz(lay(t, e, to))];
+    };
+    stages(B_A, 0, 3);
+    transpose(B_A, B_B);
+    stages(B_B, 3, 6);
+    transpose(B_B, 0);
+    stages(0, 6, 8);
+    transpose(0, B_A); // back to the coalesced layout for the epilogue
+#pragma unroll
+    for (int e = 0; e < 8; e++)
+    {
+        if constexpr (PRE)
+            V.store(base + lay(t, e, B_A), ar.out(v[e]), pr[e]);
+        else
+            V.store(base + lay(t, e, B_A), ar.out(v[e]));
+    }
+}
+
 // --------------------------------------------------------------------- inverse, row pass
 template <int LOGR, int LOGT, class Job, bool FP>
 __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long twd)
@@ -552,6 +632,50 @@ __global__ __launch_bounds__(256) void k_inv_row(Job job, int log_n, long long t
         ar.template inv<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (rb << s) + (e >> (LOGE - s)); });
 #pragma unroll
     for (int e = 0; e < E; e++) V.store(base + t + TPS * e, ar.out(v[e]));
+}
+
+// ------------------------------------------- inverse row pass, 2^8-point rows, three phases
+// The mirror of k_fwd_row3: coalesced loads, a transpose to the 8t + e layout, stages 7-6, 5-3,
+// 2-0 with two more wave-local transposes, coalesced stores.
+template <class Job>
+__global__ __launch_bounds__(256) void k_inv_row3(Job job, int log_n, long long twd)
+{
+    constexpr int LOGR = 8, R = 256, TPS = 32, S = 8, B_A = 5, B_B = 2;
+    using A = NttArith<true>;
+    using T = double;
+    __shared__ T lds[S * R];
+    const int tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
+    const u32 b = blockIdx.x * S + sl;
+    const u32 base = b << LOGR;
+    const u32 rb = (1u << (log_n - LOGR)) + b;
+    const auto V = job.view(blockIdx.y);
+    if (V.skip) return; // uniform per workgroup
+    const A ar(V.p, V.tw, twd);
+    T *x = &lds[sl * R];
+    T v[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) v[e] = ar.in(V.load(base + lay(t, e, B_A)));
+    auto stages = [&](int b_lo, int s_hi, int s_lo) {
+#pragma unroll
+        for (int s = s_hi; s >= s_lo; s--)
+            ar.template inv<8>(v, 1 << (LOGR - 1 - s - b_lo), [&](int e) { return (rb << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
+    };
+    auto transpose = [&](int from, int to) {
+        wave_lds_fence(); // the previous transpose's reads come first
+#pragma unroll
+        for (int e = 0; e < 8; e++) x[swz(lay(t, e, from))] = v[e];
+        wave_lds_fence(); // a row is 32 lanes of one wave
+#pragma unroll
+        for (int e = 0; e < 8; e++) v[e] = x[swz(lay(t, e, to))];
+    };
+    transpose(B_A, 0); // loaded coalesced
+    stages(0, 7, 6);
+    transpose(0, B_B);
+    stages(B_B, 5, 3);
+    transpose(B_B, B_A);
+    stages(B_A, 2, 0);
+#pragma unroll
+    for (int e = 0; e < 8; e++) V.store(base + lay(t, e, B_A), ar.out(v[e]));
 }
 
 // ------------------------------------------------------------------ inverse, column pass
@@ -1118,12 +1242,31 @@ static inline void launch_pass_a(const Job &job, int log_n, int jobs, long long 
     if constexpr (PASS == FWD_COL) hipLaunchKernelGGL((k_fwd_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
     if constexpr (PASS == FWD_ROW)
     {
+        if constexpr (MHE_ROW3 && FP && LOGR == 8 && !BrevOf<std::remove_cv_t<decltype(job.view(0))>>::value)
+        {
+            if (log_n == 16)
+            {
+                hipLaunchKernelGGL((k_fwd_row3<Job>), dim3(subs / 8, jobs), dim3(256), 0, st, job, log_n, twd);
+                return;
+            }
+        }
         if ((long)grid.x * grid.y <= row_pre_max_wg())
             hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP, true>), grid, dim3(256), 0, st, job, log_n, twd);
         else
             hipLaunchKernelGGL((k_fwd_row<LOGR, LOGT, Job, FP, false>), grid, dim3(256), 0, st, job, log_n, twd);
     }
-    if constexpr (PASS == INV_ROW) hipLaunchKernelGGL((k_inv_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    if constexpr (PASS == INV_ROW)
+    {
+        if constexpr (MHE_ROW3 && FP && LOGR == 8)
+        {
+            if (log_n == 16)
+            {
+                hipLaunchKernelGGL((k_inv_row3<Job>), dim3(subs / 8, jobs), dim3(256), 0, st, job, log_n, twd);
+                return;
+            }
+        }
+        hipLaunchKernelGGL((k_inv_row<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
+    }
     if constexpr (PASS == INV_COL) hipLaunchKernelGGL((k_inv_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
 }
 
@@ -1255,19 +1398,6 @@ struct RowMacShape
     static_assert(TPS <= 64, "a block's transposes must stay inside one wave");
     static constexpr int S = 256 / TPS;   // blocks per workgroup
 };
-
-// Bijective LDS index swizzle: conflict-free ds_write_b64 / ds_read_b64 for all three
-// transpose layouts (bank model of MI355X_MICROARCH.md §LDS; checked in scripts).
-__device__ __forceinline__ u32 swz(u32 r)
-{
-    return r ^ ((r >> 3) & 3) ^ (((r >> 5) & 7) << 2);
-}
-
-// Residue index held in slot e by lane t for a layout whose 3 in-lane bits start at b_lo.
-__device__ __forceinline__ u32 lay(u32 t, int e, int b_lo)
-{
-    return ((t >> b_lo) << (b_lo + 3)) | ((u32)e << b_lo) | (t & ((1u << b_lo) - 1));
-}
 
 
 
