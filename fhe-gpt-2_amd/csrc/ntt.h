@@ -520,6 +520,22 @@ __global__ __launch_bounds__(256, (FP && PRE_ON) ? 3 : 1) void k_fwd_row(Job job
     }
 }
 
+// The twiddles of stage s of a 2^8-point row in layout lay(t, e, b_lo) (b_lo + s <= 8): entry
+// (rb << s) + (hi >> (8 - s)) + (e >> (8 - s - b_lo)), hi the lane's bits above the layout's e
+// bits -- 2^(b_lo + s - 5) distinct values (at least 1), loaded ahead of the stage's turn.
+#ifndef MHE_ROW3_PF
+#define MHE_ROW3_PF 1
+#endif
+template <int S_, int BLO, class AR>
+__device__ __forceinline__ void row3_tw(const AR &ar, u32 rb, u32 t, typename AR::TW (&w)[4])
+{
+    constexpr int C = 1 << ((BLO + S_ - 5) > 0 ? (BLO + S_ - 5) : 0);
+    const u32 hi = (t >> BLO) << (BLO + 3);
+    const u32 b0 = (rb << S_) + (hi >> (8 - S_));
+#pragma unroll
+    for (int j = 0; j < C; j++) w[j] = ar.tw[b0 + j];
+}
+
 // ------------------------------------------- forward row pass, 2^8-point rows, three phases
 // k_fwd_row holds 16 residues per lane (two register phases, one transpose): with an epilogue
 // prefetch that is ~150 VGPRs, 3 waves/SIMD, and each workgroup does one load-compute-store round,
@@ -567,11 +583,30 @@ __global__ __launch_bounds__(256) void k_fwd_row3(Job job, int log_n, long long 
 #pragma unroll
         for (int e = 0; e < 8; e++) v[e] = x[swz(lay(t, e, to))];
     };
-    stages(B_A, 0, 3);
-    transpose(B_A, B_B);
-    stages(B_B, 3, 6);
-    transpose(B_B, 0);
-    stages(0, 6, 8);
+    if constexpr (MHE_ROW3_PF)
+    {
+        // the first stage of each later phase takes twiddles loaded a phase ahead: the transposes'
+        // fences would otherwise hold their loads back to the stage itself
+        using TWT = typename A::TW;
+        TWT w3[4], w6[4];
+        row3_tw<3, B_B>(ar, rb, t, w3);
+        stages(B_A, 0, 3);
+        row3_tw<6, 0>(ar, rb, t, w6);
+        transpose(B_A, B_B);
+        ar.template fwd_tab<8>(v, 1 << (LOGR - 1 - 3 - B_B), w3, [&](int e) { return e >> (8 - 3 - B_B); });
+        stages(B_B, 4, 6);
+        transpose(B_B, 0);
+        ar.template fwd_tab<8>(v, 1 << (LOGR - 1 - 6), w6, [&](int e) { return e >> (8 - 6); });
+        stages(0, 7, 8);
+    }
+    else
+    {
+        stages(B_A, 0, 3);
+        transpose(B_A, B_B);
+        stages(B_B, 3, 6);
+        transpose(B_B, 0);
+        stages(0, 6, 8);
+    }
     transpose(0, B_A); // back to the coalesced layout for the epilogue
 #pragma unroll
     for (int e = 0; e < 8; e++)
@@ -668,12 +703,33 @@ __global__ __launch_bounds__(256) void k_inv_row3(Job job, int log_n, long long 
 #pragma unroll
         for (int e = 0; e < 8; e++) v[e] = x[swz(lay(t, e, to))];
     };
-    transpose(B_A, 0); // loaded coalesced
-    stages(0, 7, 6);
-    transpose(0, B_B);
-    stages(B_B, 5, 3);
-    transpose(B_B, B_A);
-    stages(B_A, 2, 0);
+    if constexpr (MHE_ROW3_PF)
+    {
+        using TWT = typename A::TW;
+        TWT w7[4], w6[4], w5[4], w2[4];
+        row3_tw<7, 0>(ar, rb, t, w7);
+        row3_tw<6, 0>(ar, rb, t, w6);
+        transpose(B_A, 0); // loaded coalesced
+        row3_tw<5, B_B>(ar, rb, t, w5);
+        ar.template inv_tab<8>(v, 1 << (LOGR - 1 - 7), w7, [&](int e) { return e >> (8 - 7); });
+        ar.template inv_tab<8>(v, 1 << (LOGR - 1 - 6), w6, [&](int e) { return e >> (8 - 6); });
+        transpose(0, B_B);
+        row3_tw<2, B_A>(ar, rb, t, w2);
+        ar.template inv_tab<8>(v, 1 << (LOGR - 1 - 5 - B_B), w5, [&](int e) { return e >> (8 - 5 - B_B); });
+        stages(B_B, 4, 3);
+        transpose(B_B, B_A);
+        ar.template inv_tab<8>(v, 1 << (LOGR - 1 - 2 - B_A), w2, [&](int e) { return e >> (8 - 2 - B_A); });
+        stages(B_A, 1, 0);
+    }
+    else
+    {
+        transpose(B_A, 0); // loaded coalesced
+        stages(0, 7, 6);
+        transpose(0, B_B);
+        stages(B_B, 5, 3);
+        transpose(B_B, B_A);
+        stages(B_A, 2, 0);
+    }
 #pragma unroll
     for (int e = 0; e < 8; e++) V.store(base + lay(t, e, B_A), ar.out(v[e]));
 }
