@@ -177,6 +177,10 @@ def cpu_baseline(moduli, L_main, threads):
 
 
 RESNET_BITS = [51] + [46] * 16 + [51] * 14 + [51]  # cnn/infer_seal.cpp:288-316: 31 data limbs + special
+# The ResNet runner's PRNG seed (keys and encryption randomness): with fresh random keys the logit
+# error against the plain network moved run to run (0.41-0.56 on the same images, profiles/r05v),
+# close to the 5 % check; a fixed seed makes the leg repeat exactly.
+RESNET_KEY_SEED = 0x5EED2026
 
 
 def resnet_cpu_estimate(ops, threads):
@@ -271,7 +275,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
 
     used("before")
     t0 = time.perf_counter()
-    runner = R.Runner(layers, params, comp, generate_keys=(rank == 0))
+    runner = R.Runner(layers, params, comp, generate_keys=(rank == 0), seed=RESNET_KEY_SEED + rank)
     shared = None
     if world > 1:
         t1 = time.perf_counter()
@@ -345,6 +349,7 @@ def resnet_leg(device, images, streams, layers=20, fibers=1):
         # image and stays resident in HBM (no eviction tier at 65 GB of 288), and the evaluation keys
         # hold no secret key
         "key_residency": "design: all planned keys resident, none streamed from the host per image",
+        "key_seed": RESNET_KEY_SEED,
         "logit_check": {"vs": "plain network, exact ReLU (resnet_plain_logits)", "tol_rel": tol,
                         "max_abs_err_per_image": errs},
         # ResNet roofline: the key-switching key bytes one image streams (the algorithmic bytes of its

@@ -30,6 +30,8 @@ def seal_lib():
         dp, ip, u64p = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32), ctypes.POINTER(u64)
         sig = {
             "mhe_resnet_create": (i32, [ctypes.POINTER(vp), i32, ctypes.c_char_p, ctypes.c_char_p, i32]),
+            "mhe_resnet_create_seeded": (i32, [ctypes.POINTER(vp), i32, ctypes.c_char_p, ctypes.c_char_p, i32,
+                                               ctypes.c_uint64]),
             "mhe_resnet_destroy": (i32, [vp]),
             "mhe_resnet_last_error": (ctypes.c_char_p, []),
             "mhe_resnet_key_count": (i32, [vp, ip]),
@@ -63,10 +65,11 @@ def _check(rc):
 class Runner:
     """One ResNet runner on the calling process's GPU (MHE_DEVICE selects it)."""
 
-    def __init__(self, layers, params_bin, comp_dir, generate_keys=True):
+    def __init__(self, layers, params_bin, comp_dir, generate_keys=True, seed=0):
+        """seed != 0: the runner's PRNG (keys, encryption) is seeded, so runs repeat (0: random)."""
         h = ctypes.c_void_p()
-        _check(seal_lib().mhe_resnet_create(ctypes.byref(h), layers, params_bin.encode(), comp_dir.encode(),
-                                            1 if generate_keys else 0))
+        _check(seal_lib().mhe_resnet_create_seeded(ctypes.byref(h), layers, params_bin.encode(), comp_dir.encode(),
+                                                   1 if generate_keys else 0, int(seed)))
         self._h = h
 
     def close(self):

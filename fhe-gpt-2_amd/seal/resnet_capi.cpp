@@ -56,7 +56,8 @@ const char *mhe_resnet_last_error(void)
     return g_err.c_str();
 }
 
-int mhe_resnet_create(mhe_resnet **out, int layers, const char *params_bin, const char *comp_dir, int generate_keys)
+int mhe_resnet_create_seeded(mhe_resnet **out, int layers, const char *params_bin, const char *comp_dir,
+                             int generate_keys, uint64_t seed)
 {
     return guard([&] {
         if (!out || !params_bin || !comp_dir) throw std::invalid_argument("null argument");
@@ -64,10 +65,16 @@ int mhe_resnet_create(mhe_resnet **out, int layers, const char *params_bin, cons
         r->runner = std::make_unique<ResNetRunner>((std::size_t)layers, load_params(params_bin, (std::size_t)layers),
                                                    comp_dir,
                                                    generate_keys ? ResNetRunner::KeySource::generate
-                                                                 : ResNetRunner::KeySource::import);
+                                                                 : ResNetRunner::KeySource::import,
+                                                   seed);
         if (generate_keys) r->keys = r->runner->export_keys();
         *out = r.release();
     });
+}
+
+int mhe_resnet_create(mhe_resnet **out, int layers, const char *params_bin, const char *comp_dir, int generate_keys)
+{
+    return mhe_resnet_create_seeded(out, layers, params_bin, comp_dir, generate_keys, 0);
 }
 
 int mhe_resnet_destroy(mhe_resnet *r)

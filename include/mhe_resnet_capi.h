@@ -21,6 +21,11 @@ typedef struct mhe_resnet mhe_resnet;
  * format); comp_dir: holds d13.txt; generate_keys 1 = make the key set here (client + server),
  * 0 = keys follow through mhe_resnet_key_import + mhe_resnet_finish_import. */
 int mhe_resnet_create(mhe_resnet **runner, int layers, const char *params_bin, const char *comp_dir, int generate_keys);
+/* The same with the runner's PRNG seeded (keys, encryption randomness): seed != 0 makes every run
+ * draw the same keys, so decrypted logits repeat run to run; 0 = a fresh random seed, as
+ * mhe_resnet_create. */
+int mhe_resnet_create_seeded(mhe_resnet **runner, int layers, const char *params_bin, const char *comp_dir,
+                             int generate_keys, uint64_t seed);
 int mhe_resnet_destroy(mhe_resnet *runner);
 const char *mhe_resnet_last_error(void);
 

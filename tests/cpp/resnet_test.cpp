@@ -155,7 +155,8 @@ int main(int argc, char **argv)
         std::printf("params: %zu values, sum %.17g\n", count, sum);
         return 0;
     }
-    ResNetRunner runner(layers, prm, argv[2]);
+    // seeded like bench.py (RESNET_KEY_SEED): the same keys every run, so the logit check repeats
+    ResNetRunner runner(layers, prm, argv[2], ResNetRunner::KeySource::generate, 0x5EED2026ull);
     std::printf("setup: %.2f s (planning inference %.2f s, %zu truncated Galois keys made in %.2f s, %.1f GB resident)\n",
                 runner.setup_seconds(), runner.plan_seconds(), runner.galois_keys(), runner.keygen_seconds(),
                 runner.galois_key_gb());
