@@ -607,7 +607,19 @@ __global__ __launch_bounds__(256) void k_fwd_row3(Job job, int log_n, long long 
         transpose(B_B, 0);
         stages(0, 6, 8);
     }
-    transpose(0, B_A); // back to the coalesced layout for the epilogue
+    // back to the coalesced layout for the epilogue; a brev View (hoist.h) stores at position p the
+    // value of position brev8(p)
+    wave_lds_fence();
+#pragma unroll
+    for (int e = 0; e < 8; e++) x[swz(lay(t, e, 0))] = v[e];
+    wave_lds_fence();
+#pragma unroll
+    for (int e = 0; e < 8; e++)
+    {
+        u32 src = lay(t, e, B_A);
+        if constexpr (BrevOf<VW>::value) src = brev8_ntt(src);
+        v[e] = x[swz(src)];
+    }
 #pragma unroll
     for (int e = 0; e < 8; e++)
     {
@@ -1298,7 +1310,7 @@ static inline void launch_pass_a(const Job &job, int log_n, int jobs, long long 
     if constexpr (PASS == FWD_COL) hipLaunchKernelGGL((k_fwd_col<LOGR, LOGT, Job, FP>), grid, dim3(256), 0, st, job, log_n, twd);
     if constexpr (PASS == FWD_ROW)
     {
-        if constexpr (MHE_ROW3 && FP && LOGR == 8 && !BrevOf<std::remove_cv_t<decltype(job.view(0))>>::value)
+        if constexpr (MHE_ROW3 && FP && LOGR == 8)
         {
             if (log_n == 16)
             {

@@ -78,6 +78,9 @@ def main():
         "bsgs": lambda: eng.apply_galois_batch(b_in, b_el, b_k, b_out),
         "ntt": lambda: eng.ntt_forward(cts[1]),
         "hmult": lambda: eng.hmult(cts[2], cts[3], keys[0], outs[1]),
+        # elementwise, one ciphertext (2 x L limbs): HBM-bound, so us -> GB/s directly
+        "add": lambda: eng.add(cts[0], cts[1], rot_out[0]),
+        "mulplain": lambda: eng.multiply_plain(cts[0], cts[2][0], rot_out[0]),
     }
     st = torch.cuda.current_stream(eng.torch_device)
     for name in a.ops.split(","):
