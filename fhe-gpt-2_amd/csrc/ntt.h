@@ -312,6 +312,15 @@ __global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n, long long t
     T v[E];
 #pragma unroll
     for (int e = 0; e < E; e++) v[e] = ar.in(V.load(c + ((u32)(t + TPS * e) << logC)));
+    // the per-lane twiddles of the first two stages after the barrier, loaded with the data (the
+    // barrier would otherwise hold their loads back; cf. k_fwd_row): entries (1 << s) + (E t >> (LOGR - s)) + j
+    using TWT = typename A::TW;
+    constexpr int C0 = E >> (LOGR - LOGE), C1 = E >> (LOGR - LOGE - 1);
+    TWT p0[C0], p1[C1];
+#pragma unroll
+    for (int j = 0; j < C0; j++) p0[j] = ar.tw[(1 << LOGE) + ((E * t) >> (LOGR - LOGE)) + j];
+#pragma unroll
+    for (int j = 0; j < C1; j++) p1[j] = ar.tw[(1 << (LOGE + 1)) + ((E * t) >> (LOGR - LOGE - 1)) + j];
 #pragma unroll
     for (int s = 0; s < LOGE; s++)
         ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
@@ -322,7 +331,14 @@ __global__ __launch_bounds__(256) void k_fwd_col(Job job, int log_n, long long t
     for (int e = 0; e < E; e++) v[e] = lds[sl * LD + E * t + e];
 #pragma unroll
     for (int s = LOGE; s < LOGR; s++)
-        ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
+    {
+        if (s == LOGE)
+            ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - s), p0, [&](int e) { return e >> (LOGR - s); });
+        else if (s == LOGE + 1)
+            ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - s), p1, [&](int e) { return e >> (LOGR - s); });
+        else
+            ar.template fwd<E>(v, 1 << (LOGR - 1 - s), [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
+    }
 #pragma unroll
     for (int e = 0; e < E; e++) V.store(c + ((u32)(E * t + e) << logC), ar.out(v[e]));
 }
