@@ -1,4 +1,4 @@
-# r05z: GPU busy fraction of the ResNet-20 3 x 8 batch: kernel trace of a 24-image run, reduced on
+# r05z(b): GPU busy fraction and idle gaps of the ResNet-20 3 x 8 batch: kernel trace of a 24-image run, reduced on
 # the box to the union of kernel intervals over the batch window (scripts/busy.py)
 set -u
 cd "$GRAFT_REPO_ROOT"
