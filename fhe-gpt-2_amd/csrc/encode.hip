@@ -51,7 +51,12 @@ struct mhe_encoder
     std::vector<cd> root_powers;
 
     // device state (lazily created on the first encode of each device)
-    static constexpr int kRing = 8;
+    // Pinned upload slots, reused round robin.  Reusing a slot waits (under `mu`, so for every
+    // thread) until its last upload has run, and that upload sits behind whatever its stream had
+    // queued -- with 8 slots, 3 host threads x 8 fibers wrapped the ring within one merged step and
+    // every thread stalled behind another stream's key switches.  64 slots (32 MB at n = 2^16) are
+    // reused only after ~0.1 s of encodes, when no stream is that far behind.
+    static constexpr int kRing = 64;
     struct DevRoots
     {
         int dev;
