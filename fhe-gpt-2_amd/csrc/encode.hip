@@ -204,6 +204,37 @@ __global__ __launch_bounds__(256) void k_enc_fft_block(double2 *cv, const double
     for (size_t t = threadIdx.x; t < B; t += 256) cv[base + t] = sh[t];
 }
 
+// stages lb .. log_n-1 (gap 2^lb .. 2^(log_n-1)) in one launch: they only pair elements with the same
+// low lb bits, so a lane holds the 2^(log_n-lb) <= 16 elements of one such column in registers and
+// runs the stages in order -- the same butterflies on the same values as one k_enc_fft_stage launch
+// per stage, so the same doubles, in one launch instead of log_n - lb
+template <int LR> // log_n - lb
+__global__ __launch_bounds__(256) void k_enc_fft_tail(double2 *cv, const double2 *roots, int log_n, int lb,
+                                                      double scalar)
+{
+    constexpr int R = 1 << LR;
+    const size_t n = (size_t)1 << log_n, c = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= ((size_t)1 << lb)) return;
+    double2 v[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) v[j] = cv[c + ((size_t)j << lb)];
+#pragma unroll
+    for (int s = 0; s < LR; s++)
+    {
+        const int st = lb + s;
+        const size_t m = n >> (st + 1);
+#pragma unroll
+        for (int j = 0; j < R; j++)
+            if (!(j & (1 << s)))
+            {
+                const double2 r = roots[n - 2 * m + 1 + (size_t)(j >> (s + 1))];
+                enc_bfly(v[j], v[j + (1 << s)], r, m == 1, scalar);
+            }
+    }
+#pragma unroll
+    for (int j = 0; j < R; j++) cv[c + ((size_t)j << lb)] = v[j];
+}
+
 // one later stage (gap 2^st) over the whole vector
 __global__ void k_enc_fft_stage(double2 *cv, const double2 *roots, int log_n, int st, double scalar)
 {
@@ -389,9 +420,19 @@ extern "C" __attribute__((visibility("default"))) int mhe_ckks_encode_at(mhe_ctx
     {
         const int lb = std::min(log_n, kEncLogBlock);
         hipLaunchKernelGGL(k_enc_fft_block, dim3((unsigned)(n >> lb)), dim3(256), 0, st, cv, roots, log_n, lb, fix);
-        for (int s2 = lb; s2 < log_n; s2++)
-            hipLaunchKernelGGL(k_enc_fft_stage, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, st, cv, roots,
-                               log_n, s2, fix);
+        const dim3 tg((unsigned)(((1u << lb) + 255) / 256));
+        if (log_n - lb == 4)
+            hipLaunchKernelGGL(k_enc_fft_tail<4>, tg, dim3(256), 0, st, cv, roots, log_n, lb, fix);
+        else if (log_n - lb == 3)
+            hipLaunchKernelGGL(k_enc_fft_tail<3>, tg, dim3(256), 0, st, cv, roots, log_n, lb, fix);
+        else if (log_n - lb == 2)
+            hipLaunchKernelGGL(k_enc_fft_tail<2>, tg, dim3(256), 0, st, cv, roots, log_n, lb, fix);
+        else if (log_n - lb == 1)
+            hipLaunchKernelGGL(k_enc_fft_tail<1>, tg, dim3(256), 0, st, cv, roots, log_n, lb, fix);
+        else
+            for (int s2 = lb; s2 < log_n; s2++)
+                hipLaunchKernelGGL(k_enc_fft_stage, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, st, cv, roots,
+                                   log_n, s2, fix);
         err = hipGetLastError();
     }
     if (err == hipSuccess && exact_check)
