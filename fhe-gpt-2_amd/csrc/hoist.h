@@ -81,17 +81,21 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
         const int kl = P.key_limbs[bz][r];
         return P.key[bz][r] + (size_t)((I == L) ? kl - 1 : I) * n;
     };
-    u32 kpm = 0; // bit r: rotation r's key is prepared (48-bit planes for this prime)
+    // bit r: rotation r's key slot for this prime holds doubles (kdm) / 48-bit planes (k48)
+    u32 kdm = 0, k48 = 0;
 #pragma unroll
     for (int r = 0; r < R; r++)
     {
-        if (p.q < (1ull << 48) && kslot(r)[n - 1] == KEY_PACK_TAG) kpm |= 1u << r;
+        const int f = key_slot_format(kslot(r)[n - 1]);
+        kdm |= (f == 1 ? 1u : 0u) << r;
+        k48 |= (f == 2 ? 1u : 0u) << r;
         k[r] = galois_src(m, P.einv[bz][r], log_n);
         mk[r] = fp_from_u52(P.mask[bz][r][(size_t)pi * n + k[r]]);
         a0[r] = a1[r] = 0.0;
     }
-    // the same load instructions every digit (KP: every key prepared / none / per key), so the
-    // compiler counts the waits of the one-digit-ahead prefetch instead of draining it
+    // the same load instructions every digit (KP: every key's slot SEAL's layout 0 / doubles 1 /
+    // 48-bit planes 2, or -1 per key), so the compiler counts the waits of the one-digit-ahead
+    // prefetch instead of draining it
     auto load = [&](int J, u64 &dv, u64 (&w0)[R], u64 (&w1)[R], auto kp_tag) {
         constexpr int KP = decltype(kp_tag)::value;
         dv = (J == I) ? c1[(size_t)J * n + m] : D[(size_t)J * n + bx * 256u + u];
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
             const size_t ks = (size_t)P.key_limbs[bz][r] * n;
             const u64 *k0 = kslot(r) + (size_t)(2 * J) * ks;
             const u64 *k1 = k0 + ks;
-            if (KP == 1 || (KP == -1 && ((kpm >> r) & 1)))
+            if (KP == 2 || (KP == -1 && ((k48 >> r) & 1)))
             {
                 const u32 *l0 = reinterpret_cast<const u32 *>(k0), *l1 = reinterpret_cast<const u32 *>(k1);
                 w0[r] = (u64)l0[k[r]] | ((u64)reinterpret_cast<const unsigned short *>(l0 + n)[k[r]] << 32);
@@ -113,6 +117,12 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
                 w1[r] = k1[k[r]];
             }
         }
+    };
+    // a key word as a double
+    auto kw = [&](u64 w, int r, auto kp_tag) {
+        constexpr int KP = decltype(kp_tag)::value;
+        if (KP == 1 || (KP == -1 && ((kdm >> r) & 1))) return key_word_f(w);
+        return fp_from_u52(w);
     };
     // lazy sums while L products (|.| < 1.25p each) add up exactly, else a reduction every second digit
     const bool lz = p.q < (1ull << 47) && (double)L * 1.25 * q < 9007199254740992.0;
@@ -130,8 +140,8 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
         {
             // canonical D (< p) + c M (|.| < 1.5p): |.| < 2.5p < 2^53, centred by one reduction
             const double d = fp_reduce(dd + fp_mulmod(mk[r], c.x, c.y, q), q, qinv);
-            a0[r] += fp_mulmod_gen(d, fp_from_u52(w0[r]), q, qinv);
-            a1[r] += fp_mulmod_gen(d, fp_from_u52(w1[r]), q, qinv);
+            a0[r] += fp_mulmod_gen(d, kw(w0[r], r, kp_tag), q, qinv);
+            a1[r] += fp_mulmod_gen(d, kw(w1[r], r, kp_tag), q, qinv);
             if (!lz && (J & 1))
             {
                 a0[r] = fp_reduce(a0[r], q, qinv);
@@ -147,9 +157,12 @@ __global__ __launch_bounds__(256, (R <= 4) ? 4 : 2) void k_ks_hoist_mac(HoistPtr
         }
     }
     };
-    if (kpm == (1u << R) - 1)
+    const u32 all = (1u << R) - 1;
+    if (kdm == all)
         run(std::integral_constant<int, 1>{});
-    else if (kpm == 0)
+    else if (k48 == all)
+        run(std::integral_constant<int, 2>{});
+    else if ((kdm | k48) == 0)
         run(std::integral_constant<int, 0>{});
     else
         run(std::integral_constant<int, -1>{});
@@ -220,14 +233,16 @@ __global__ __launch_bounds__(1024) void k_ks_hoist_mac_sh(HoistShared P, const P
 #pragma unroll
     for (int r = 0; r < R; r++) kcol[r / 4] |= brev8(galois_src(m, P.einv[r], log_n) & 255u) << (8 * (r % 4));
     double a0[IPL][R], a1[IPL][R];
-    u32 kpm = 0; // bit r: rotation r's key is prepared (48-bit planes for this prime), read once
+    u32 kdm = 0, k48 = 0; // bit r: rotation r's key slot holds doubles / 48-bit planes, read once
 #pragma unroll
     for (int r = 0; r < R; r++)
     {
 #pragma unroll
         for (int it = 0; it < IPL; it++) a0[it][r] = a1[it][r] = 0.0;
         const int kl = P.key_limbs[r];
-        if (p.q < (1ull << 48) && P.key[r][(size_t)((I == L) ? kl - 1 : I) * n + n - 1] == KEY_PACK_TAG) kpm |= 1u << r;
+        const int f = key_slot_format(P.key[r][(size_t)((I == L) ? kl - 1 : I) * n + n - 1]);
+        kdm |= (f == 1 ? 1u : 0u) << r;
+        k48 |= (f == 2 ? 1u : 0u) << r;
     }
     // staging: word v = tid + 1024 s is bit-reversed column v & 255 of key row (kk, r) =
     // (v / (256 R), (v / 256) % R), read from the key at its natural column and written to kb at v.
@@ -235,7 +250,7 @@ __global__ __launch_bounds__(1024) void k_ks_hoist_mac_sh(HoistShared P, const P
     // words, discarded), so the loads in flight have fixed counts and the compiler waits for the
     // oldest ones only (vmcnt(N)) instead of draining all of them at each digit.
     auto stage_load = [&](int J, u64 (&sv)[S], auto kp_tag) {
-        constexpr int KP = decltype(kp_tag)::value; // 1 prepared (48-bit planes), 0 SEAL layout, -1 per key
+        constexpr int KP = decltype(kp_tag)::value; // as in k_ks_hoist_mac
 #pragma unroll
         for (int s = 0; s < S; s++)
         {
@@ -245,7 +260,7 @@ __global__ __launch_bounds__(1024) void k_ks_hoist_mac_sh(HoistShared P, const P
             const int kl = P.key_limbs[r];
             const u64 *slot = P.key[r] + ((size_t)(2 * J + kk) * kl + (size_t)((I == L) ? kl - 1 : I)) * n;
             const u32 x = (galois_src(blockIdx.x * 256u, P.einv[r], log_n) & ~255u) + brev8((u32)c); // block rho_r^-1
-            if (KP == 1 || (KP == -1 && ((kpm >> r) & 1)))
+            if (KP == 2 || (KP == -1 && ((k48 >> r) & 1)))
             {
                 const u32 *lo = reinterpret_cast<const u32 *>(slot);
                 sv[s] = (u64)lo[x] | ((u64)reinterpret_cast<const unsigned short *>(lo + n)[x] << 32);
@@ -289,7 +304,11 @@ __global__ __launch_bounds__(1024) void k_ks_hoist_mac_sh(HoistShared P, const P
                 for (int s = 0; s < S; s++)
                 {
                     const int v = tid + 1024 * s;
-                    const double w = fp_from_u52(sv[u][s]);
+                    // the staged word as a double
+                    constexpr int KP = decltype(kp_tag)::value;
+                    const int kr = __builtin_amdgcn_readfirstlane((min(v, NV - 1) >> 8) % R);
+                    const double w = (KP == 1 || (KP == -1 && ((kdm >> kr) & 1))) ? key_word_f(sv[u][s])
+                                                                                  : fp_from_u52(sv[u][s]);
                     if (v < NV) kb[buf][v] = w;
                     kc[s] += fp_mulmod(w, c.x, c.y, q); // |term| < 1.5p; reduced every second digit
                     if (J & 1) kc[s] = fp_reduce(kc[s], q, qinv);
@@ -328,9 +347,11 @@ __global__ __launch_bounds__(1024) void k_ks_hoist_mac_sh(HoistShared P, const P
         }
     };
     const u32 all = (1u << R) - 1;
-    if (kpm == all)
+    if (kdm == all)
         run(std::integral_constant<int, 1>{});
-    else if (kpm == 0)
+    else if (k48 == all)
+        run(std::integral_constant<int, 2>{});
+    else if ((kdm | k48) == 0)
         run(std::integral_constant<int, 0>{});
     else
         run(std::integral_constant<int, -1>{});

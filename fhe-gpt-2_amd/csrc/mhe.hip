@@ -195,7 +195,8 @@ struct Workspace
     // key-switch kernels on this stream, read back by mhe_kernel_time
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[2];
     size_t ev_used[2] = { 0, 0 };
-    size_t bytes = 0, hoist_bytes = 0; // device bytes of base / hoist_base (mhe_scratch_bytes)
+    // device bytes of base / hoist_base: written under mu, read by mhe_scratch_bytes without it
+    std::atomic<size_t> bytes{ 0 }, hoist_bytes{ 0 };
     int hoist_limbs = 0;                // the hoisting buffers' level (per-input ModUp of up to this many limbs)
     std::mutex mu;                      // growth of this stream's buffers
 };
@@ -240,8 +241,10 @@ struct mhe_ctx
     int ks_pack = 1; // n = 2^16: ModUp intermediate of primes < 2^48 stored in 48 bits (MHE_KS_PACK=0: 64 bits)
     int icol_fused = 1; // ModDown / rescale: inverse column pass fused into the lift column pass (MHE_ICOL_FUSED=0: separate)
     int galois_fused = 1; // apply_galois: one permutation launch, c1 written by the ModDown (MHE_GALOIS_FUSED=0: SEAL's order with a zero fill)
-    int ks_hoist = 1; // batched rotations of one input share their ModUp (hoist.h); mhe_ctx_set_hoist / MHE_KS_HOIST=0 turn it off
-    int hoist_check = 0; // recompute every hoisted rotation by the classic path and compare (mhe_ctx_set_hoist)
+    // read by every thread's rotations, written by mhe_ctx_set_hoist at any time: atomic
+    std::atomic<int> ks_hoist{ 1 }; // batched rotations of one input share their ModUp (hoist.h); mhe_ctx_set_hoist / MHE_KS_HOIST=0 turn it off
+    std::atomic<int> hoist_check{ 0 }; // recompute every hoisted rotation by the classic path and compare (mhe_ctx_set_hoist)
+    std::atomic<int> fail_switch{ 0 }; // mhe_debug_fail_switch: the n-th next batched key switch fails (0: off)
     std::atomic<unsigned long long> hoist_rot{ 0 }, hoist_mac{ 0 }, hoist_bad{ 0 }; // mhe_hoist_stats
     std::atomic<int> fail_alloc{ 0 }; // mhe_debug_fail_alloc: the n-th next allocation fails (0: off)
     TwF *cmodf = nullptr; // [K][K]: (q_j mod q_i, (q_j mod q_i) / q_i) as doubles, j major (hoist.h)
@@ -251,27 +254,35 @@ struct mhe_ctx
     std::map<hipStream_t, Workspace> ws;
 };
 
-// Key limbs of a prepared key that the fused MAC reads packed: primes below 2^48 (ntt.h load_key).
-static bool key_limb_packed(const mhe_ctx *c, int limb, int key_limbs)
+// Key limbs a prepared key converts: format 1 (doubles) every prime below 2^51, the FP64 path's;
+// format 2 (48-bit planes) every prime below 2^48 (ntt.h KEY_PREP_MIN, KEY_PACK_TAG).
+static bool key_limb_packed(const mhe_ctx *c, int limb, int key_limbs, int fmt)
 {
     const int pi = (limb == key_limbs - 1) ? c->K - 1 : limb;
-    return c->q[pi] < (1ull << 48);
+    return c->q[pi] < (fmt == 2 ? (1ull << 48) : (1ull << 51));
 }
 
-// Is `key` in the prepared format?  Reads the tag word of its first packed slot (host sync:
-// only prepare / unprepare and the separate-MAC debugging path ask).
+// The prepared format of `key` (0: SEAL's layout, 1 doubles, 2 48-bit planes), from the last word of
+// its first slot that either format converts (host sync: only prepare / unprepare and the
+// separate-MAC debugging path ask).
 static int key_tagged(mhe_ctx *c, const u64 *key, int key_limbs, hipStream_t st, int *tagged)
 {
     *tagged = 0;
-    for (int l = 0; l < key_limbs; l++)
-        if (key_limb_packed(c, l, key_limbs))
-        {
-            u64 w = 0;
-            HIP_TRY(hipMemcpyAsync(&w, key + (size_t)l * c->n + c->n - 1, 8, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            *tagged = (w == KEY_PACK_TAG) ? 1 : 0;
-            return MHE_OK;
-        }
+    for (int fmt = 2; fmt >= 1; fmt--)
+        for (int l = 0; l < key_limbs; l++)
+            if (key_limb_packed(c, l, key_limbs, fmt))
+            {
+                u64 w = 0;
+                HIP_TRY(hipMemcpyAsync(&w, key + (size_t)l * c->n + c->n - 1, 8, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                const int f = key_slot_format(w);
+                if (f == fmt)
+                {
+                    *tagged = f;
+                    return MHE_OK;
+                }
+                break; // this format's first slot is not in it
+            }
     return MHE_OK;
 }
 
@@ -301,6 +312,9 @@ static void timing_end(hipEvent_t *pair, hipStream_t st)
 // synchronises the device) and retries once.  Freed ciphertext / key buffers stay cached for reuse at
 // their own sizes; a plain hipMalloc cannot use them.
 static void release_cached_blocks();
+// process-wide counts for mhe_alloc_stats: allocations that succeeded only after the cache was
+// released, and allocations that failed (including injected ones)
+static std::atomic<unsigned long long> g_alloc_retries{ 0 }, g_alloc_failures{ 0 };
 static hipError_t scratch_alloc(void **p, size_t bytes)
 {
     hipError_t e = hipMalloc(p, bytes);
@@ -308,7 +322,13 @@ static hipError_t scratch_alloc(void **p, size_t bytes)
     (void)hipGetLastError();
     release_cached_blocks();
     e = hipMalloc(p, bytes);
-    if (e != hipSuccess) (void)hipGetLastError();
+    if (e != hipSuccess)
+    {
+        (void)hipGetLastError();
+        g_alloc_failures.fetch_add(1);
+    }
+    else
+        g_alloc_retries.fetch_add(1);
     return e;
 }
 
@@ -317,7 +337,11 @@ static bool injected_alloc_failure(mhe_ctx *c)
 {
     int v = c->fail_alloc.load();
     while (v > 0)
-        if (c->fail_alloc.compare_exchange_weak(v, v - 1)) return v == 1;
+        if (c->fail_alloc.compare_exchange_weak(v, v - 1))
+        {
+            if (v == 1) g_alloc_failures.fetch_add(1);
+            return v == 1;
+        }
     return false;
 }
 
@@ -1418,7 +1442,12 @@ extern "C" __attribute__((visibility("hidden"))) hipError_t mhe_internal_alloc(v
         (void)hipGetLastError();
         release_cached(a);
         e = hipMalloc(p, sz);
-        if (e != hipSuccess) return e;
+        if (e != hipSuccess)
+        {
+            g_alloc_failures.fetch_add(1);
+            return e;
+        }
+        g_alloc_retries.fetch_add(1);
     }
     a.live[*p] = sz;
     a.in_use += sz;
@@ -1584,8 +1613,8 @@ struct KsJob
 static int ks_check_key(mhe_ctx *c, const KsJob &j, int L, hipStream_t st, int *kpack)
 {
     if (j.key_limbs < L + 1 || j.key_limbs > c->K) return fail(MHE_ERR_ARG, "kswitch_keys is not valid for encryption parameters");
-    // a prepared key (mhe_key_prepare) is recognised by the fused MAC itself (KEY_PACK_TAG in
-    // each packed slot); the separate-MAC debugging path reads SEAL's layout only
+    // a prepared key (mhe_key_prepare) is recognised by the fused MAC itself (key_word_prepared
+    // on a word of each slot); the separate-MAC debugging path reads SEAL's layout only
     *kpack = 1;
     if (!c->ks_fused)
     {
@@ -1597,9 +1626,9 @@ static int ks_check_key(mhe_ctx *c, const KsJob &j, int L, hipStream_t st, int *
     }
     // the key slice one switch streams: L digits x 2 polys x (L + 1) primes
     c->key_bytes += 2ull * (unsigned long long)L * (unsigned long long)(L + 1) * c->n * 8ull;
-    unsigned long long per = 0; // bytes per residue over the slice's L + 1 limbs, prepared format
-    for (int l = 0; l <= L; l++) per += key_limb_packed(c, l == L ? j.key_limbs - 1 : l, j.key_limbs) ? 6 : 8;
-    c->key_bytes_prep += 2ull * (unsigned long long)L * c->n * per;
+    // prepared: doubles stream the same 8 B per residue, the 48-bit planes 6 B for primes below 2^48
+    // (the format of a prepared key is not known here without a host sync: counted as doubles)
+    c->key_bytes_prep += 2ull * (unsigned long long)L * (unsigned long long)(L + 1) * c->n * 8ull;
     return MHE_OK;
 }
 
@@ -1705,6 +1734,13 @@ static void run_moddown(mhe_ctx *c, const KsJob *jobs, int B, int L, Workspace *
 static int run_switch_key_batch(mhe_ctx *c, const KsJob *jobs, int B, int L, hipStream_t st, int c1_write = 0)
 {
     if (B < 1 || B > MHE_MAXB) return fail(MHE_ERR_ARG, "key switch: batch size out of range");
+    // mhe_debug_fail_switch's countdown (tests): this launch sequence fails before its first launch
+    for (int v = c->fail_switch.load(); v > 0;)
+        if (c->fail_switch.compare_exchange_weak(v, v - 1))
+        {
+            if (v == 1) return fail(MHE_ERR_MEMORY, "device allocation failed (injected)");
+            break;
+        }
     const bool hm = jobs[0].rescale_out != nullptr;
     for (int e = 0; e < B; e++)
         if ((jobs[e].rescale_out != nullptr) != hm) return fail(MHE_ERR_ARG, "key switch: mixed fused-rescale batch");
@@ -2455,6 +2491,21 @@ MHE_EXPORT int mhe_trim(mhe_ctx *c)
     return MHE_OK;
 }
 
+MHE_EXPORT int mhe_debug_fail_switch(mhe_ctx *c, int nth)
+{
+    if (!valid_ctx(c) || nth < 0) return fail(MHE_ERR_ARG, "invalid argument");
+    c->fail_switch.store(nth);
+    return MHE_OK;
+}
+
+MHE_EXPORT int mhe_alloc_stats(uint64_t *retries, uint64_t *failures, int reset)
+{
+    if (!retries || !failures) return fail(MHE_ERR_ARG, "invalid argument");
+    *retries = reset ? g_alloc_retries.exchange(0) : g_alloc_retries.load();
+    *failures = reset ? g_alloc_failures.exchange(0) : g_alloc_failures.load();
+    return MHE_OK;
+}
+
 MHE_EXPORT int mhe_debug_fail_alloc(mhe_ctx *c, int nth)
 {
     if (!valid_ctx(c) || nth < 0) return fail(MHE_ERR_ARG, "invalid argument");
@@ -2474,7 +2525,7 @@ MHE_EXPORT int mhe_ctx_get_hoist(mhe_ctx *c, int *on, int *check)
 {
     if (!valid_ctx(c) || !on || !check) return fail(MHE_ERR_ARG, "invalid argument");
     *on = hoist_ok(c) ? 1 : 0;
-    *check = c->hoist_check;
+    *check = c->hoist_check.load();
     return MHE_OK;
 }
 
@@ -2590,11 +2641,27 @@ MHE_EXPORT int mhe_key_traffic(mhe_ctx *c, uint64_t *bytes, int reset)
     return MHE_OK;
 }
 
-// Pack (dir 1) or unpack (dir 0) the limb slots of one digit of a key: src is a copy of the
-// digit's 2 x key_limbs slots, dst the key's.  Packed slot of a prime below 2^48: a 32-bit plane
-// [n] then a 16-bit plane [n] (natural order); other slots are copied unchanged.
-__global__ void k_key_pack(const u64 *__restrict__ src, u64 *__restrict__ dst, const unsigned char *__restrict__ packed,
-                           int key_limbs, int log_n, int dir)
+// Format 1 (doubles): prepare (dir 1) or unprepare (dir 0) the limb slots of a key in place: a slot
+// of a prime below 2^51 holds its residues as doubles (-0.0 for zero, so every word is >=
+// KEY_PREP_MIN); other slots keep SEAL's layout.  blockIdx.y: digit * 2 * key_limbs + poly *
+// key_limbs + limb.
+__global__ void k_key_pack(u64 *__restrict__ key, const unsigned char *__restrict__ packed, int key_limbs, int log_n,
+                           int dir)
+{
+    const size_t n = (size_t)1 << log_n;
+    const int slot = blockIdx.y;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || !packed[slot % key_limbs]) return;
+    u64 *d = key + (size_t)slot * n;
+    const u64 v = d[i];
+    d[i] = dir ? (v ? (u64)__double_as_longlong((double)v) : 0x8000000000000000ull) : key_word_u(v);
+}
+
+// Format 2 (48-bit planes): pack (dir 1) or unpack (dir 0) the slots of one digit: src is a copy of
+// the digit's 2 x key_limbs slots, dst the key's.  A slot of a prime below 2^48: a 32-bit plane [n]
+// then a 16-bit plane [n] (natural order) and KEY_PACK_TAG in the last word; other slots copied.
+__global__ void k_key_pack48(const u64 *__restrict__ src, u64 *__restrict__ dst, const unsigned char *__restrict__ packed,
+                             int key_limbs, int log_n, int dir)
 {
     const size_t n = (size_t)1 << log_n;
     const int slot = blockIdx.y; // poly * key_limbs + limb
@@ -2622,29 +2689,47 @@ __global__ void k_key_pack(const u64 *__restrict__ src, u64 *__restrict__ dst, c
     }
 }
 
-static int key_pack_run(mhe_ctx *c, u64 *key, int digits, int key_limbs, int dir, hipStream_t st)
+static int key_pack_run(mhe_ctx *c, u64 *key, int digits, int key_limbs, int dir, int fmt, hipStream_t st)
 {
-    const size_t n = c->n, slots = 2 * (size_t)key_limbs;
+    const size_t n = c->n, slots1 = 2 * (size_t)key_limbs;
     std::vector<unsigned char> pk(key_limbs);
-    for (int l = 0; l < key_limbs; l++) pk[l] = key_limb_packed(c, l, key_limbs) ? 1 : 0;
+    for (int l = 0; l < key_limbs; l++) pk[l] = key_limb_packed(c, l, key_limbs, fmt) ? 1 : 0;
     HIP_TRY(hipSetDevice(c->device));
-    u64 *tmp = nullptr;
-    unsigned char *pkd = nullptr;
-    if (hipMalloc(&tmp, slots * n * sizeof(u64) + 256) != hipSuccess) return fail(MHE_ERR_MEMORY, "key prepare: scratch allocation failed");
-    pkd = reinterpret_cast<unsigned char *>(tmp + slots * n);
+    u64 *tmp = nullptr; // format 2: one digit's copy, then the limb table
+    const size_t tmp_words = fmt == 2 ? slots1 * n : 0;
+    if (hipMalloc(&tmp, tmp_words * sizeof(u64) + 256 + (size_t)key_limbs) != hipSuccess)
+        return fail(MHE_ERR_MEMORY, "key prepare: scratch allocation failed");
+    unsigned char *pkd = reinterpret_cast<unsigned char *>(tmp + tmp_words);
     int rc = MHE_OK;
     if (hipMemcpyAsync(pkd, pk.data(), key_limbs, hipMemcpyHostToDevice, st) != hipSuccess) rc = fail(MHE_ERR_DEVICE, "key prepare: copy");
-    for (int J = 0; J < digits && rc == MHE_OK; J++)
+    if (fmt == 2)
     {
-        u64 *dg = key + (size_t)J * slots * n;
-        if (hipMemcpyAsync(tmp, dg, slots * n * sizeof(u64), hipMemcpyDeviceToDevice, st) != hipSuccess)
+        for (int J = 0; J < digits && rc == MHE_OK; J++)
         {
-            rc = fail(MHE_ERR_DEVICE, "key prepare: copy");
-            break;
+            u64 *dg = key + (size_t)J * slots1 * n;
+            if (hipMemcpyAsync(tmp, dg, slots1 * n * sizeof(u64), hipMemcpyDeviceToDevice, st) != hipSuccess)
+            {
+                rc = fail(MHE_ERR_DEVICE, "key prepare: copy");
+                break;
+            }
+            hipLaunchKernelGGL(k_key_pack48, dim3((unsigned)((n + 255) / 256), (unsigned)slots1), dim3(256), 0, st, tmp,
+                               dg, pkd, key_limbs, c->log_n, dir);
+            if (hipGetLastError() != hipSuccess) rc = fail(MHE_ERR_DEVICE, "key prepare: launch");
         }
-        hipLaunchKernelGGL(k_key_pack, dim3((unsigned)((n + 255) / 256), (unsigned)slots), dim3(256), 0, st, tmp, dg,
-                           pkd, key_limbs, c->log_n, dir);
-        if (hipGetLastError() != hipSuccess) rc = fail(MHE_ERR_DEVICE, "key prepare: launch");
+    }
+    else
+    {
+        // grid.y is at most 65535 slots per launch: whole groups of key_limbs slots each, so the
+        // kernel's slot % key_limbs stays the limb
+        const size_t slots = slots1 * (size_t)digits, per = (65535 / (size_t)key_limbs) * (size_t)key_limbs;
+        for (size_t s0 = 0; s0 < slots && rc == MHE_OK;)
+        {
+            const size_t cnt = std::min(per, slots - s0);
+            hipLaunchKernelGGL(k_key_pack, dim3((unsigned)((n + 255) / 256), (unsigned)cnt), dim3(256), 0, st,
+                               key + s0 * n, pkd, key_limbs, c->log_n, dir);
+            if (hipGetLastError() != hipSuccess) rc = fail(MHE_ERR_DEVICE, "key prepare: launch");
+            s0 += cnt;
+        }
     }
     // the scratch is freed only after the stream has used it
     if (hipStreamSynchronize(st) != hipSuccess && rc == MHE_OK) rc = fail(MHE_ERR_DEVICE, "key prepare: sync");
@@ -2652,15 +2737,31 @@ static int key_pack_run(mhe_ctx *c, u64 *key, int digits, int key_limbs, int dir
     return rc;
 }
 
-MHE_EXPORT int mhe_key_prepare(mhe_ctx *c, uint64_t *key, int digits, int key_limbs, void *s)
+// the format mhe_key_prepare makes: MHE_KEY_FMT=2 chooses the 48-bit planes, default doubles
+static int default_key_format()
 {
-    if (!valid_ctx(c) || !key || digits < 1 || key_limbs < 2 || key_limbs > c->K || digits > key_limbs - 1)
+    static const int f = [] {
+        const char *e = getenv("MHE_KEY_FMT");
+        return (e && atoi(e) == 2) ? 2 : 1;
+    }();
+    return f;
+}
+
+MHE_EXPORT int mhe_key_prepare_as(mhe_ctx *c, uint64_t *key, int digits, int key_limbs, int format, void *s)
+{
+    if (!valid_ctx(c) || !key || digits < 1 || key_limbs < 2 || key_limbs > c->K || digits > key_limbs - 1 ||
+        (format != MHE_KEY_FMT_DOUBLE && format != MHE_KEY_FMT_PACK48))
         return fail(MHE_ERR_ARG, "invalid argument");
     int tagged = 0;
     int r = key_tagged(c, key, key_limbs, S(s), &tagged);
     if (r) return r;
     if (tagged) return fail(MHE_ERR_ARG, "key prepare: key is already prepared");
-    return key_pack_run(c, key, digits, key_limbs, 1, S(s));
+    return key_pack_run(c, key, digits, key_limbs, 1, format, S(s));
+}
+
+MHE_EXPORT int mhe_key_prepare(mhe_ctx *c, uint64_t *key, int digits, int key_limbs, void *s)
+{
+    return mhe_key_prepare_as(c, key, digits, key_limbs, default_key_format(), s);
 }
 
 MHE_EXPORT int mhe_key_unprepare(mhe_ctx *c, uint64_t *key, int digits, int key_limbs, void *s)
@@ -2671,7 +2772,7 @@ MHE_EXPORT int mhe_key_unprepare(mhe_ctx *c, uint64_t *key, int digits, int key_
     int r = key_tagged(c, key, key_limbs, S(s), &tagged);
     if (r) return r;
     if (!tagged) return fail(MHE_ERR_ARG, "key unprepare: key is not prepared");
-    return key_pack_run(c, key, digits, key_limbs, 0, S(s));
+    return key_pack_run(c, key, digits, key_limbs, 0, tagged, S(s));
 }
 
 MHE_EXPORT int mhe_key_traffic_prepared(mhe_ctx *c, uint64_t *bytes, int reset)

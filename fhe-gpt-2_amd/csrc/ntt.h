@@ -66,10 +66,34 @@ __device__ __forceinline__ u32 tile16(u32 idx)
     const u32 r = idx >> 8, c = idx & 255;
     return ((((r >> 4) << 4) | (c >> 4)) << 8) | ((r & 15) << 4) | (c & 15);
 }
-// Prepared key (mhe_key_prepare): every limb slot of a prime below 2^48 holds a 32-bit plane [n],
-// a 16-bit plane [n] and, in its last word, this tag -- never a residue of a SEAL key (>= 2^63),
-// so the key MAC tells a prepared key from SEAL's layout by itself.
+// Prepared key (mhe_key_prepare): every limb slot of a prime below 2^51 (the FP64 path's primes)
+// holds its residues as IEEE doubles -- the FP64 key MAC's operand, loaded with no unpacking (-0.0
+// for a zero residue).  Every such word is >= 2^61, which no residue of a SEAL key reaches (primes
+// of at most 60 bits), so the key MAC tells a prepared slot from SEAL's layout by any one word.
+#define KEY_PREP_MIN (1ull << 61)
+__host__ __device__ __forceinline__ bool key_word_prepared(u64 w)
+{
+    return w >= KEY_PREP_MIN;
+}
+// The second prepared format, for keys streamed by one ciphertext at a time (where the MAC's key
+// bytes matter more than its unpacking): a slot of a prime below 2^48 holds a 32-bit plane [n], a
+// 16-bit plane [n] and, in its unused last quarter, this tag (6 B per residue).
 #define KEY_PACK_TAG 0xF0E1D2C3B4A59687ull
+// a slot's format from its last word: 0 SEAL's layout, 1 doubles, 2 48-bit planes
+__host__ __device__ __forceinline__ int key_slot_format(u64 last_word)
+{
+    return last_word == KEY_PACK_TAG ? 2 : key_word_prepared(last_word) ? 1 : 0;
+}
+// a prepared word as the residue's double / as the u64 residue (integer kernels): 2^52 + x holds x
+// in its mantissa field (-0.0 + 2^52 = 2^52)
+__device__ __forceinline__ double key_word_f(u64 w)
+{
+    return __longlong_as_double((long long)w);
+}
+__device__ __forceinline__ u64 key_word_u(u64 w)
+{
+    return (u64)__double_as_longlong(__longlong_as_double((long long)w) + 4503599627370496.0) & 0x000FFFFFFFFFFFFFull;
+}
 // The 16-bit plane pairs rows instead: in a tile, u32 word (r/2, c) holds the high halves of rows
 // r and r+1 of column c (u16 index returned), so a column-pass lane, which holds both rows, writes
 // one u32 per row pair and 16 lanes fill a whole 64-byte segment (2-byte stores left 32-byte
@@ -1508,12 +1532,15 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
 
 template <int LOGR, bool FP, bool MIX = false>
 #ifndef MHE_KS_OCC
-#define MHE_KS_OCC 2 // waves per SIMD the fused MAC is compiled for
+#define MHE_KS_OCC 3 // waves per SIMD the FP64 fused MAC at n = 2^16 is compiled for (the others: 2)
 #endif
-#ifndef MHE_KS_XCH
-#define MHE_KS_XCH 2 // LDS transpose buffers of the fused MAC (1 or 2)
+#ifndef MHE_KS_PP
+#define MHE_KS_PP 0 // digit loop unrolled twice, prefetched digit in alternating registers
 #endif
-__global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
+#ifndef MHE_KS_KPF
+#define MHE_KS_KPF 0 // key limbs loaded one digit ahead too (32 VGPRs more)
+#endif
+__global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int log_n,
                                                        long long twd, int I0, int pack, int kpack, int share,
                                                        const Tw *__restrict__ itw_all, long long tinv, int inv_special)
@@ -1550,8 +1577,9 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
     constexpr int B_A = LOGR - 3, B_B = LOGR - 6;
     // one transpose buffer is enough (every transpose stays inside one wave and a wave's LDS
     // operations complete in order; the fences only stop the compiler from reordering them):
-    // 49 KB per workgroup fits 3 workgroups per CU, two buffers (65.6 KB) only 2
-    __shared__ T xch[MHE_KS_XCH][S * R];
+    // 48 KB per workgroup fits 3 workgroups per CU, two buffers (64 KB) only 2
+    constexpr int XCH = (FP && !MIX && LOGR == 8 && MHE_KS_OCC >= 3) ? 1 : 2;
+    __shared__ T xch[XCH][S * R];
     __shared__ TW twl[S * R];
     const int j0 = 0, j1 = L;
     const u32 tid = threadIdx.x, t = tid % TPS, sl = tid / TPS;
@@ -1586,7 +1614,7 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
             }
         }
         const TW *mytw = &twl_a[sl * R];
-        T *x0 = reinterpret_cast<T *>(&xch[0][sl * R]), *x1 = reinterpret_cast<T *>(&xch[MHE_KS_XCH - 1][sl * R]);
+        T *x0 = reinterpret_cast<T *>(&xch[0][sl * R]), *x1 = reinterpret_cast<T *>(&xch[XCH - 1][sl * R]);
         // FP: the key inner products run in FP64 as well (fp_mulmod_gen); with q < 2^47 and
         // 1.25 (j1 - j0) q < 2^53 (LZ, chosen below) the digits stay unreduced and the products
         // (|.| < 1.25q each) sum exactly, otherwise digits are reduced and the sums every second
@@ -1604,48 +1632,73 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
                 a0[e] = a1[e] = Acc128{ 0, 0 };
         }
 
-        // digit J of this output prime: the input limb itself (J == I, already NTT form) or the
-        // column-pass output, packed (tile16) when the column pass packed it.  The digit loop is
-        // instantiated per (packed intermediate, prepared key) pair -- uniform per workgroup -- and
-        // issues the same load instructions every digit (the input limb of J == I read with the
-        // packed shape when the intermediate is packed: its residues are below 2^48 too; the last
-        // digit's prefetch repeated past the end): with a data-dependent load count the compiler
-        // drained every load in flight (vmcnt(0)) at the top of each digit.
+        // Digit J of this output prime is the input limb itself (J == I, already NTT form) or the
+        // column-pass output, packed (tile16) when the column pass packed it.  The input limb is
+        // taken first, on its own; the loop then runs over the other digits in order (I skipped),
+        // so every iteration issues the same load instructions from the same per-lane offsets
+        // (only the uniform base moves) -- with the input limb inside the loop, the compiler
+        // selected between two offset sets and rebuilt 16 64-bit addresses per digit.  The loop is
+        // unrolled twice with the prefetched digit in alternating registers (no copies), and
+        // instantiated per (packed intermediate, prepared key) pair, uniform per workgroup.  The
+        // last digit's prefetch is repeated past the end: with a data-dependent load count the
+        // compiler drained every load in flight (vmcnt(0)) at the top of each digit.
         const bool pk = inter_packed(pack, p.q); // uniform per workgroup
-        // key limbs of a digit: issued at the top of the digit, consumed after the digit's NTT (a
-        // one-digit-ahead key prefetch measured equal and costs 32 VGPRs)
-        // a prepared key (mhe_key_prepare) holds the limbs of primes below 2^48 as a 32-bit plane
-        // [n] and a 16-bit plane [n] in natural order (6 of the slot's 8 bytes per residue)
-        const bool kpk = kpack && p.q < (1ull << 48) && key[(size_t)ki * n + n - 1] == KEY_PACK_TAG; // uniform
-        auto loop = [&](auto pk_c, auto kpk_c) {
-            constexpr bool PK = decltype(pk_c)::value, KPK = decltype(kpk_c)::value;
-            auto load_digit = [&](int J, u64 (&v)[8]) {
-                const bool self = J == I; // uniform
-                if constexpr (PK)
+        // a prepared slot (mhe_key_prepare): the residues as doubles (no unpacking) or as 48-bit planes
+        const int kfmt = kpack ? key_slot_format(key[(size_t)ki * n + n - 1]) : 0; // uniform
+        const bool has_self = I < L;                                                 // uniform
+        const int nd = has_self ? L - 1 : L; // digits other than I
+        auto loop = [&](auto pk_c, auto kf_c) {
+            constexpr bool PK = decltype(pk_c)::value;
+            constexpr int KF = decltype(kf_c)::value; // key slot format (key_slot_format)
+            auto digit_of = [&](int u) { return u + ((has_self && u >= I) ? 1 : 0); };
+            // packed digit slots at n = 2^16: byte offsets of this lane's residue 0 in the 32-bit
+            // plane and in the 16-bit plane (which starts at 4n)
+            const u32 off_lo = 4u * tile16(base + lay(t, 0, B_A));
+            const u32 off_hi = 4u * (u32)n + 2u * tile16h(base + lay(t, 0, B_A));
+            auto load_inter = [&](int J, u64 (&v)[8]) {
+                if constexpr (PK && LOGR == 8)
                 {
-                    const u32 *lo = self ? reinterpret_cast<const u32 *>(target + (size_t)J * n)
-                                         : reinterpret_cast<const u32 *>(inter + ((size_t)(I - I0) * L + J) * n);
-                    const unsigned short *hi = self ? reinterpret_cast<const unsigned short *>(target + (size_t)J * n)
-                                                    : reinterpret_cast<const unsigned short *>(lo + n);
+                    // buffer loads: the digit's slot as a descriptor built from uniform values and
+                    // loop-invariant 32-bit lane offsets (global loads rebuilt a 64-bit address per
+                    // load and digit).  At n = 2^16 a lane's residues e = 0..7 are one column block
+                    // apart in both planes: tile16 / tile16h of base + lay(t, e, 5) grow by 512 e.
+                    const u64 *slot = inter + ((size_t)(I - I0) * L + J) * n;
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc(const_cast<u64 *>(slot), 0, (int)(8 * n), 0x00020000);
+                    constexpr int AUX = ((MHE_NT >> 2) & 1) ? 2 : 0; // nt
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        // the per-residue step as the scalar offset: two lane offsets in VGPRs
+                        const u32 l = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off_lo, 2048 * e, AUX);
+                        const u32 h = __builtin_amdgcn_raw_buffer_load_b16(rs, (int)off_hi, 1024 * e, AUX);
+                        v[e] = (u64)l | ((u64)h << 32);
+                    }
+                }
+                else if constexpr (PK)
+                {
+                    const u32 *lo = reinterpret_cast<const u32 *>(inter + ((size_t)(I - I0) * L + J) * n);
+                    const unsigned short *hi = reinterpret_cast<const unsigned short *>(lo + n);
 #pragma unroll
                     for (int e = 0; e < 8; e++)
                     {
                         const u32 idx = base + lay(t, e, B_A);
-                        const u32 il = self ? 2 * idx : tile16(idx), ih = self ? 4 * idx + 2 : tile16h(idx);
-                        v[e] = (u64)ld_nt<2>(&lo[il]) | ((u64)ld_nt<2>(&hi[ih]) << 32);
+                        v[e] = (u64)ld_nt<2>(&lo[tile16(idx)]) | ((u64)ld_nt<2>(&hi[tile16h(idx)]) << 32);
                     }
                 }
                 else
                 {
-                    const u64 *src = (self ? target + (size_t)J * n : inter + ((size_t)(I - I0) * L + J) * n) + base;
+                    const u64 *src = inter + ((size_t)(I - I0) * L + J) * n + base;
 #pragma unroll
                     for (int e = 0; e < 8; e++) v[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
                 }
             };
+            // key limbs of a digit: issued at the top of the digit, consumed after the digit's NTT
+            // (a one-digit-ahead key prefetch measured equal and costs 32 VGPRs)
             auto load_key = [&](int J, u64 (&ka)[8], u64 (&kb)[8]) {
                 const u64 *k0 = key + (size_t)(2 * J) * kstride + (size_t)ki * n;
                 const u64 *k1 = k0 + kstride;
-                if constexpr (KPK)
+                if constexpr (KF == 2)
                 {
                     const u32 *l0 = reinterpret_cast<const u32 *>(k0) + base;
                     const u32 *l1 = reinterpret_cast<const u32 *>(k1) + base;
@@ -1669,80 +1722,21 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
                     }
                 }
             };
-            u64 vin[8];
-            load_digit(j0, vin);
-            lds_barrier(); // twiddles visible
-            u64 kk0[8], kk1[8];
-            for (int J = j0; J < j1; J++)
-            {
-                u64 vnext[8];
-                load_key(J, kk0, kk1);
-                load_digit(J + 1 < j1 ? J + 1 : J, vnext); // one digit ahead (the last one again at the end)
-                T d[8]; // the digit in the coalesced layout, NTT form
-                if (J != I)
-                {
-                    T w[8];
-#pragma unroll
-                    for (int e = 0; e < 8; e++)
-                    {
-                        // the column-pass output: FP and packed, a centred 48-bit residue (fp_to_s48);
-                        // otherwise canonical
-                        if constexpr (FPA)
-                            w[e] = PK ? fp_from_s48(vin[e]) : ar.in52(vin[e]);
-                        else
-                            w[e] = ar.in52(vin[e]);
-                    }
-                    row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
-                    wave_lds_fence(); // the previous digit's reads of x0 come first
-#pragma unroll
-                    for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
-                    wave_lds_fence();
-#pragma unroll
-                    for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
-                    row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
-                    T *xl = x1;
-                    int bl = B_B;
-                    if (LOGR > 6)
-                    {
-                        wave_lds_fence();
-#pragma unroll
-                        for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
-                        wave_lds_fence();
-#pragma unroll
-                        for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
-                        row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
-                        xl = x0;
-                        bl = 0;
-                    }
-                    // back to the coalesced layout of the key stream (integer: canonical digits
-                    // keep the 128-bit sums exact for any digit count below 2^8)
-                    wave_lds_fence();
-#pragma unroll
-                    for (int e = 0; e < 8; e++)
-                    {
-                        if constexpr (FPA)
-                            xl[swz(lay(t, e, bl))] = w[e];
-                        else
-                            xl[swz(lay(t, e, bl))] = ar.canon(w[e]);
-                    }
-                    wave_lds_fence();
-#pragma unroll
-                    for (int e = 0; e < 8; e++) d[e] = xl[swz(lay(t, e, B_A))];
-                }
-                else
-                {
-#pragma unroll
-                    for (int e = 0; e < 8; e++) d[e] = ar.in52(vin[e]); // the target: a canonical ciphertext limb
-                }
+            // d (the digit in the coalesced layout, NTT form) times both key limbs; `odd` is the
+            // parity of the digits taken so far (the non-lazy FP sums are reduced every second one)
+            auto mac = [&](const T (&d)[8], const u64 (&ka)[8], const u64 (&kb)[8], bool odd) {
                 if constexpr (FPA)
                 {
 #pragma unroll
                     for (int e = 0; e < 8; e++)
                     {
                         const double dv = LZ ? d[e] : fp_reduce(d[e], ar.q, ar.qinv);
-                        a0[e] += fp_mulmod_gen(dv, fp_from_u52(kk0[e]), ar.q, ar.qinv); // canonical key residues
-                        a1[e] += fp_mulmod_gen(dv, fp_from_u52(kk1[e]), ar.q, ar.qinv);
-                        if (!LZ && ((J - j0) & 1))
+                        // canonical key residues
+                        const double k0v = KF == 1 ? key_word_f(ka[e]) : fp_from_u52(ka[e]);
+                        const double k1v = KF == 1 ? key_word_f(kb[e]) : fp_from_u52(kb[e]);
+                        a0[e] += fp_mulmod_gen(dv, k0v, ar.q, ar.qinv);
+                        a1[e] += fp_mulmod_gen(dv, k1v, ar.q, ar.qinv);
+                        if (!LZ && odd)
                         {
                             a0[e] = fp_reduce(a0[e], ar.q, ar.qinv);
                             a1[e] = fp_reduce(a1[e], ar.q, ar.qinv);
@@ -1754,22 +1748,136 @@ __global__ __launch_bounds__(256, MHE_KS_OCC) void k_ks_row_mac(KsPtrs P, const 
 #pragma unroll
                     for (int e = 0; e < 8; e++)
                     {
-                        mac128(a0[e], d[e], kk0[e]);
-                        mac128(a1[e], d[e], kk1[e]);
+                        mac128(a0[e], d[e], KF == 1 ? key_word_u(ka[e]) : ka[e]);
+                        mac128(a1[e], d[e], KF == 1 ? key_word_u(kb[e]) : kb[e]);
                     }
                 }
+            };
+            // the row stages of a column-pass output (J != I)
+            auto ntt_digit = [&](const u64 (&vin)[8], T (&d)[8]) {
+                T w[8];
 #pragma unroll
-                for (int e = 0; e < 8; e++) vin[e] = vnext[e];
+                for (int e = 0; e < 8; e++)
+                {
+                    // the column-pass output: FP and packed, a centred 48-bit residue (fp_to_s48);
+                    // otherwise canonical
+                    if constexpr (FPA)
+                        w[e] = PK ? fp_from_s48(vin[e]) : ar.in52(vin[e]);
+                    else
+                        w[e] = ar.in52(vin[e]);
+                }
+                row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
+                wave_lds_fence(); // the previous digit's reads of x0 come first
+#pragma unroll
+                for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
+                wave_lds_fence();
+#pragma unroll
+                for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
+                row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
+                T *xl = x1;
+                int bl = B_B;
+                if (LOGR > 6)
+                {
+                    wave_lds_fence();
+#pragma unroll
+                    for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
+                    wave_lds_fence();
+#pragma unroll
+                    for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
+                    row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
+                    xl = x0;
+                    bl = 0;
+                }
+                // back to the coalesced layout of the key stream (integer: canonical digits keep
+                // the 128-bit sums exact for any digit count below 2^8)
+                wave_lds_fence();
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    if constexpr (FPA)
+                        xl[swz(lay(t, e, bl))] = w[e];
+                    else
+                        xl[swz(lay(t, e, bl))] = ar.canon(w[e]);
+                }
+                wave_lds_fence();
+#pragma unroll
+                for (int e = 0; e < 8; e++) d[e] = xl[swz(lay(t, e, B_A))];
+            };
+            u64 ka[8], kb[8], va[8], vb[8];
+            if (nd > 0) load_inter(digit_of(0), va); // nd == 0: one data limb, output prime 0
+            lds_barrier();                             // twiddles visible
+            if (has_self)
+            {
+                // the input limb of digit I: a canonical ciphertext limb, already NTT form
+                const u64 *src = target + (size_t)I * n + base;
+#pragma unroll
+                for (int e = 0; e < 8; e++) vb[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
+                load_key(I, ka, kb);
+                T d[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) d[e] = ar.in52(vb[e]);
+                mac(d, ka, kb, false);
             }
+            const int c0 = has_self ? 1 : 0; // digits taken before the loop
+#if MHE_KS_KPF
+            // keys one digit ahead as well: digit u's key limbs are in ka / kb when its step starts
+            if (nd > 0) load_key(digit_of(0), ka, kb);
+            auto step = [&](int u, const u64 (&cur)[8], u64 (&nxt)[8]) {
+                const int un = u + 1 < nd ? u + 1 : u;
+                u64 na[8], nb[8];
+                load_key(digit_of(un), na, nb);
+                load_inter(digit_of(un), nxt); // one digit ahead
+                T d[8];
+                ntt_digit(cur, d);
+                mac(d, ka, kb, ((u + c0) & 1) != 0);
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                {
+                    ka[e] = na[e];
+                    kb[e] = nb[e];
+                }
+            };
+#else
+            auto step = [&](int u, const u64 (&cur)[8], u64 (&nxt)[8]) {
+                load_key(digit_of(u), ka, kb);
+                load_inter(digit_of(u + 1 < nd ? u + 1 : u), nxt); // one digit ahead
+                T d[8];
+                ntt_digit(cur, d);
+                mac(d, ka, kb, ((u + c0) & 1) != 0);
+            };
+#endif
+#if MHE_KS_PP
+            int u = 0;
+            for (; u + 1 < nd; u += 2)
+            {
+                step(u, va, vb);
+                step(u + 1, vb, va);
+            }
+            if (u < nd) step(u, va, vb);
+#else
+            for (int u = 0; u < nd; u++)
+            {
+                step(u, va, vb);
+#pragma unroll
+                for (int e = 0; e < 8; e++) va[e] = vb[e];
+            }
+#endif
         };
-        if (pk && kpk)
-            loop(std::true_type{}, std::true_type{});
-        else if (pk)
-            loop(std::true_type{}, std::false_type{});
-        else if (kpk)
-            loop(std::false_type{}, std::true_type{});
+        using F0 = std::integral_constant<int, 0>;
+        using F1 = std::integral_constant<int, 1>;
+        using F2 = std::integral_constant<int, 2>;
+        if (pk)
+        {
+            if (kfmt == 1) loop(std::true_type{}, F1{});
+            else if (kfmt == 2) loop(std::true_type{}, F2{});
+            else loop(std::true_type{}, F0{});
+        }
         else
-            loop(std::false_type{}, std::false_type{});
+        {
+            if (kfmt == 1) loop(std::false_type{}, F1{});
+            else if (kfmt == 2) loop(std::false_type{}, F2{});
+            else loop(std::false_type{}, F0{});
+        }
         u64 *o0 = acc + (size_t)I * n + base;
         u64 *o1 = o0 + (size_t)(L + 1) * n;
         if (inv_special && I == L) // uniform per workgroup

@@ -67,3 +67,19 @@ void minimax_ReLU_seal(long comp_no, std::vector<int> deg, long alpha, std::vect
                        seal::Decryptor &decryptor, seal::CKKSEncoder &encoder, seal::PublicKey &public_key,
                        seal::SecretKey &secret_key, seal::RelinKeys &relin_keys, seal::Ciphertext &cipher_in,
                        seal::Ciphertext &cipher_res);
+
+// minimax_ReLU_seal restated on plain doubles (same coefficients, scalings and evaluation trees), for
+// checking a decrypted network against its plain twin: u -> u (1 + sgn~(u)) / 2.
+class MinimaxReluPlain
+{
+public:
+    MinimaxReluPlain(long comp_no, std::vector<int> deg, long alpha, std::vector<Tree> tree, double scaled_val);
+    double operator()(double u) const;
+
+private:
+    double eval_component(long c, double x) const;
+    long comp_no_;
+    std::vector<int> deg_;
+    std::vector<Tree> tree_;
+    std::vector<std::vector<double>> coeff_;
+};

@@ -16,6 +16,7 @@
 #include <complex>
 #include <cstdint>
 #include <iosfwd>
+#include <functional>
 #include <vector>
 
 #include "mhe_boot.h"
@@ -41,6 +42,10 @@ ResNetParams load_resnet_params_bin(const std::string &path, std::size_t layer_n
 // the reference prints decrypted logits next to the label, infer_seal.cpp:543-575): image is
 // 3 x 32 x 32 values before the /B of infer_seal.cpp:444; returns the 10 logits.
 std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector<double> &image, std::size_t layer_num);
+// The same with `relu` applied in place at every ReLU (e.g. the minimax composite of the encrypted
+// network, ResNetRunner::plain_logits_approx).
+std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector<double> &image, std::size_t layer_num,
+                                        const std::function<void(std::vector<double> &)> &relu);
 
 struct ResNetResult
 {
@@ -69,9 +74,10 @@ public:
         import
     };
     // comp_dir: directory holding d<alpha>.txt of the approximate ReLU (mhe_comp.h)
-    // rng_seed != 0: the context's PRNG factory uses that fixed seed for every generator it makes
-    // (SEAL's Blake2xbPRNGFactory(default_seed), a debugging mode: keys and every encryption become
-    // deterministic, so two runs of one image give the same words; never for real use)
+    // rng_seed != 0: a debugging mode (seal.h Blake2xbSeedSequence): every generator of the setup --
+    // secret, public, relinearization and Galois keys -- gets its own seed derived from rng_seed, and
+    // after the setup every encryption uses rng_seed itself, so two runs of one image give the same
+    // words whatever the thread or fiber order; never for real use
     ResNetRunner(std::size_t layer_num, const ResNetParams &params, const std::string &comp_dir,
                  KeySource keys = KeySource::generate, std::uint64_t rng_seed = 0);
     ~ResNetRunner();
@@ -109,6 +115,10 @@ public:
     bool keys_prepared() const { return keys_prepared_; }
     // resnet_plain_logits with this runner's parameters
     std::vector<double> plain_logits(const std::vector<double> &image) const;
+    // the same with the encrypted network's own ReLU: the minimax composite polynomial of
+    // minimax_ReLU_seal on x / B, restated in plain doubles (MinimaxReluPlain), so a decrypted result
+    // differs from it by the encryption's error alone (noise, rescaling, bootstrapping)
+    std::vector<double> plain_logits_approx(const std::vector<double> &image) const;
 
     // key buffers as device memory, for sharing one key set across GPUs: kind 0 secret key [K][n],
     // 1 public key [2][K][n], 2 relinearization key [K-1][2][K][n], 3 Galois key `index` with

@@ -21,6 +21,7 @@
 //  * serialization (save/load) is not provided yet.
 #pragma once
 
+#include <atomic>
 #include <algorithm>
 #include <array>
 #include <complex>
@@ -198,7 +199,7 @@ public:
     const prng_seed_type &default_seed() const noexcept { return default_seed_; }
     static std::shared_ptr<UniformRandomGeneratorFactory> DefaultFactory();
     // (not SEAL API) the seed create() gives its generator: 512 fresh bits, or the default seed
-    prng_seed_type next_seed() const;
+    virtual prng_seed_type next_seed() const;
 
 private:
     prng_seed_type default_seed_{};
@@ -210,6 +211,30 @@ class Blake2xbPRNGFactory : public UniformRandomGeneratorFactory
 public:
     Blake2xbPRNGFactory() = default;
     explicit Blake2xbPRNGFactory(prng_seed_type default_seed) : UniformRandomGeneratorFactory(default_seed) {}
+};
+
+// (not SEAL API) A reproducible factory for debugging runs.  Blake2xbPRNGFactory(default_seed)
+// hands every generator the same seed, so every key would share its uniform polynomial and error.
+// While counting, generator i gets `base` with its last word XOR-ed by i + 1: keys drawn one after
+// the other are independent and the same sequence repeats from run to run.  Once frozen, create()
+// gives `base` itself, SEAL's debugging behaviour, so encryptions issued by concurrent threads or
+// fibers stay reproducible whatever their order.  Never for real use.
+class Blake2xbSeedSequence : public UniformRandomGeneratorFactory
+{
+public:
+    explicit Blake2xbSeedSequence(prng_seed_type base) : UniformRandomGeneratorFactory(base) {}
+    prng_seed_type next_seed() const override
+    {
+        prng_seed_type s = default_seed();
+        if (!frozen_.load()) s[prng_seed_uint64_count - 1] ^= count_.fetch_add(1) + 1;
+        return s;
+    }
+    void freeze() { frozen_.store(true); }
+    std::uint64_t generators() const { return count_.load(); }
+
+private:
+    mutable std::atomic<std::uint64_t> count_{ 0 };
+    std::atomic<bool> frozen_{ false };
 };
 
 // randomtostd.h: a UniformRandomGenerator as a 32-bit standard URBG
@@ -716,6 +741,11 @@ private:
 // entry runs as its own call (the words are the same either way: tests compare the two).
 void set_batched_launches(bool on);
 bool batched_launches();
+
+// (not SEAL API) How many merged Lockstep / FiberBatch calls failed and were re-run member by
+// member (Evaluator::lockstep_execute), process-wide; reset: return the count and start from 0.
+// A healthy run reports 0: the engine's allocation retries and failures are in mhe_alloc_stats.
+std::uint64_t merged_call_fallbacks(bool reset = false);
 
 // (not SEAL API) Lockstep: threads that evaluate the same operation sequence on different data (the
 // images of a batch) join one group.  While joined, every top-level rotation (rotate_vector[s],

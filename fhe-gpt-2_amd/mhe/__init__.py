@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("MHE_LIB_PATH") or os.path.join(_PKG, "libmhe.so")  # override: build experiments
+_DEFAULT_LIB = os.path.join(_PKG, "libmhe.so")
+LIB_PATH = os.environ.get("MHE_LIB_PATH") or _DEFAULT_LIB  # override: build experiments
 _lib = None
 
 u64p = ctypes.POINTER(ctypes.c_uint64)
@@ -37,6 +38,8 @@ SIGNATURES = {
     "mhe_hoist_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_debug_fail_alloc": (ctypes.c_int, [vp, ctypes.c_int]),
+    "mhe_debug_fail_switch": (ctypes.c_int, [vp, ctypes.c_int]),
+    "mhe_alloc_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "mhe_trim": (ctypes.c_int, [vp]),
     "mhe_scratch_bytes": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]),
@@ -56,6 +59,7 @@ SIGNATURES = {
     "mhe_set_launch_hook": (ctypes.c_int, [vp, vp]),
     "mhe_launch_run": (ctypes.c_int, [vp, vp, ctypes.c_int]),
     "mhe_key_prepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
+    "mhe_key_prepare_as": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_unprepare": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.c_int, vp]),
     "mhe_key_is_prepared": (ctypes.c_int, [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), vp]),
     "mhe_key_traffic_prepared": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
@@ -123,6 +127,10 @@ def lib():
 
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            # an A/B build from an older tree (MHE_LIB_PATH) may lack the newest entry points; the
+            # in-tree library must export all of them (tests/test_capi.py)
+            if LIB_PATH != _DEFAULT_LIB and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -225,6 +233,13 @@ class Engine:
         r, m, b = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib().mhe_hoist_stats(self._h, ctypes.byref(r), ctypes.byref(m), ctypes.byref(b), 1 if reset else 0))
         return r.value, m.value, b.value
+
+    @staticmethod
+    def alloc_stats(reset=False):
+        """mhe_alloc_stats: (allocations that needed the cache released and a retry, failed ones), process-wide."""
+        r, f = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().mhe_alloc_stats(ctypes.byref(r), ctypes.byref(f), 1 if reset else 0))
+        return r.value, f.value
 
     def scratch_bytes(self):
         """mhe_scratch_bytes: (workspace, hoisting, Galois masks) device bytes and the stream count."""
@@ -343,10 +358,15 @@ class Engine:
     def _key_limbs(key):
         return key.shape[2]  # [digits][2][key_limbs][n]
 
-    def key_prepare(self, key):
-        """mhe_key_prepare: convert `key` [digits][2][key_limbs][n] in place to the engine's packed
-        key format (48-bit planes for primes below 2^48); switches given it stay bit-identical."""
-        _check(lib().mhe_key_prepare(self._h, _ptr(key), key.shape[0], self._key_limbs(key), self.stream()))
+    def key_prepare(self, key, fmt=None):
+        """mhe_key_prepare(_as): convert `key` [digits][2][key_limbs][n] in place to one of the engine's
+        key formats (fmt 1: residues of primes below 2^51 as doubles, 2: 48-bit planes for primes below
+        2^48; None: mhe_key_prepare's default); switches given it stay bit-identical."""
+        if fmt is None:
+            _check(lib().mhe_key_prepare(self._h, _ptr(key), key.shape[0], self._key_limbs(key), self.stream()))
+        else:
+            _check(lib().mhe_key_prepare_as(self._h, _ptr(key), key.shape[0], self._key_limbs(key), int(fmt),
+                                            self.stream()))
         return key
 
     def key_unprepare(self, key):
@@ -355,9 +375,13 @@ class Engine:
         return key
 
     def key_is_prepared(self, key):
+        return self.key_format(key) != 0
+
+    def key_format(self, key):
+        """0: SEAL's layout; 1: doubles; 2: 48-bit planes (mhe_key_is_prepared)."""
         v = ctypes.c_int()
         _check(lib().mhe_key_is_prepared(self._h, _ptr(key), self._key_limbs(key), ctypes.byref(v), self.stream()))
-        return bool(v.value)
+        return v.value
 
     def switch_key(self, ct, target, key):
         _check(lib().mhe_switch_key(self._h, _ptr(ct), _ptr(target), _ptr(key), self._key_limbs(key), ct.shape[1],

@@ -49,6 +49,8 @@ def seal_lib():
             "mhe_resnet_hoist_stats": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
             "mhe_resnet_scratch_bytes": (i32, [vp, ctypes.POINTER(ctypes.c_double)]),
             "mhe_resnet_plain_logits": (i32, [vp, dp, dp]),
+            "mhe_resnet_plain_logits_approx": (i32, [vp, dp, dp]),
+            "mhe_resnet_fallback_stats": (i32, [ctypes.POINTER(ctypes.c_uint64), i32]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -167,6 +169,22 @@ class Runner:
         dp = ctypes.POINTER(ctypes.c_double)
         _check(seal_lib().mhe_resnet_plain_logits(self._h, img.ctypes.data_as(dp), out.ctypes.data_as(dp)))
         return out
+
+    def plain_logits_approx(self, image):
+        """The network in plain doubles with the encrypted network's minimax-composite ReLU."""
+        img = np.ascontiguousarray(image, dtype=np.float64).reshape(3072)
+        out = np.zeros(10)
+        dp = ctypes.POINTER(ctypes.c_double)
+        _check(seal_lib().mhe_resnet_plain_logits_approx(self._h, img.ctypes.data_as(dp), out.ctypes.data_as(dp)))
+        return out
+
+    @staticmethod
+    def fallback_stats(reset=False):
+        """(merged calls re-run member by member, allocations retried after a cache release, failed
+        allocations), process-wide since the last reset: all 0 in a healthy run."""
+        v = (ctypes.c_uint64 * 3)()
+        _check(seal_lib().mhe_resnet_fallback_stats(v, 1 if reset else 0))
+        return tuple(int(x) for x in v)
 
     def check_logits(self, images, logits, tol=0.05):
         """Decrypted logits vs the plain network: max |error| per image must stay below

@@ -485,3 +485,100 @@ void minimax_ReLU_seal(long comp_no, std::vector<int> deg, long alpha, std::vect
     evaluator.multiply_reduced_error(cipher_temp, cipher_in, relin_keys, cipher_res);
     evaluator.rescale_to_next_inplace(cipher_res);
 }
+
+// ------------------------------------------------------------------------ plain restatement
+// minimax_ReLU_seal on plain doubles, for checking decrypted results: the same d<alpha>.txt
+// coefficients, the same scalings between the components and the same odd baby-step giant-step
+// trees, evaluated as eval_polynomial_integrate's oddbaby branch does (SEALfunc.cpp:60-313) -- the
+// leaves in T_1, T_3, ..., the right spines, T_{2^i} = 2 T_{2^(i-1)}^2 - T_0 and the odd baby steps
+// T_j = 2 T_{2^(i-1)} T_{j-2^(i-1)} - T_{2^i-j} -- on one value.  So a decrypted network and its
+// plain twin differ by the encryption's error (noise, rescaling, bootstrapping) only, not by the
+// polynomial's distance from the exact ReLU.
+MinimaxReluPlain::MinimaxReluPlain(long comp_no, std::vector<int> deg, long alpha, std::vector<Tree> tree,
+                                   double scaled_val)
+    : comp_no_(comp_no), deg_(std::move(deg)), tree_(std::move(tree))
+{
+    const char *dir = std::getenv("MHE_COMP_DIR");
+    const std::string path = std::string(dir ? dir : "../result") + "/d" + std::to_string(alpha) + ".txt";
+    std::ifstream in(path);
+    if (!in) throw std::runtime_error("cannot open " + path);
+    coeff_.assign(comp_no, {});
+    for (long i = 0; i < comp_no; i++)
+    {
+        if (tree_[i].type != evaltype::oddbaby) throw std::invalid_argument("MinimaxReluPlain: oddbaby trees only");
+        for (long j = 0; j < minicomp::coeff_number(deg_[i], tree_[i]); j++)
+        {
+            double c;
+            if (!(in >> c)) throw std::runtime_error("too few coefficients in " + path);
+            coeff_[i].push_back(c);
+        }
+    }
+    // the scalings of minimax_ReLU_seal
+    std::vector<double> scale_val(comp_no, 2.0);
+    scale_val[0] = 1.0;
+    scale_val[comp_no - 1] = scaled_val;
+    for (long i = 0; i + 1 < comp_no; i++)
+        for (double &c : coeff_[i]) c /= scale_val[i + 1];
+    for (double &c : coeff_[comp_no - 1]) c *= 0.5;
+}
+
+double MinimaxReluPlain::eval_component(long c, double x) const
+{
+    const Tree &tree = tree_[c];
+    const long deg = deg_[c];
+    const std::vector<double> &dc = coeff_[c];
+    const long total_depth = ceil_to_int(std::log(static_cast<double>(deg + 1)) / std::log(2.0));
+    const long nodes = pow2(tree.depth + 1);
+    const std::vector<long> ddeg = minicomp::node_degrees(deg, tree);
+    std::vector<long> start_index(static_cast<size_t>(nodes), -1);
+    long temp_index = 1;
+    for (long i = 1; i < nodes; i++)
+        if (tree.tree[i] == 0)
+        {
+            start_index[i] = temp_index;
+            temp_index += ddeg[i] + 1;
+        }
+    std::vector<double> T(1024, std::nan("")), pt(static_cast<size_t>(nodes), std::nan(""));
+    T[0] = 1.0;
+    T[1] = x;
+    for (long i = 1; i <= total_depth; i++)
+    {
+        for (long j = 1; j < nodes; j++)
+        {
+            if (tree.tree[j] != 0 || total_depth + 1 - minicomp::num_one(j) != i) continue;
+            long idx = start_index[j];
+            double v = T[1] * dc[idx];
+            idx += 2;
+            for (long k = 3; k <= ddeg[j]; k += 2, idx += 2) v += T[k] * dc[idx];
+            pt[j] = v;
+        }
+        std::vector<std::pair<long, double>> next_T;
+        for (long j = 1; j < nodes; j++)
+        {
+            if (tree.tree[j] <= 0 || total_depth + 1 - minicomp::num_one(j) != i || j % 2 != 1) continue;
+            long k = j;
+            double v = T[tree.tree[k]] * pt[2 * k + 1];
+            k *= 2;
+            while (tree.tree[k] != 0)
+            {
+                v += T[tree.tree[k]] * pt[2 * k + 1];
+                k *= 2;
+            }
+            pt[j] = v + pt[k];
+        }
+        if (i <= tree.m - 1) next_T.push_back({ pow2(i), 2.0 * T[pow2(i - 1)] * T[pow2(i - 1)] - T[0] });
+        if (i <= tree.l)
+            for (long j = pow2(i - 1) + 1; j <= pow2(i) - 1; j += 2)
+                next_T.push_back({ j, 2.0 * T[pow2(i - 1)] * T[j - pow2(i - 1)] - T[pow2(i) - j] });
+        for (auto &g : next_T) T[g.first] = g.second;
+    }
+    if (std::isnan(pt[1])) throw std::runtime_error("MinimaxReluPlain: tree left the root unset");
+    return pt[1];
+}
+
+double MinimaxReluPlain::operator()(double u) const
+{
+    double x = u;
+    for (long i = 0; i < comp_no_; i++) x = eval_component(i, x);
+    return (x + 0.5) * u; // x is sgn(u)/2
+}

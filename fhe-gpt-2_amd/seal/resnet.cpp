@@ -214,7 +214,8 @@ void plain_relu(std::vector<double> &v)
 }
 } // namespace
 
-std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector<double> &img, std::size_t layer_num)
+std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector<double> &img, std::size_t layer_num,
+                                        const std::function<void(std::vector<double> &)> &relu)
 {
     // the block structure of infer_seal.cpp:445-540 (conv, BN, ReLU; option-A shortcut with a
     // stride-2 subsample for the first block of stages 2 and 3), then average pooling and FC
@@ -222,7 +223,7 @@ std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector
     std::vector<double> x = plain_conv(img, p.conv_weight[0], 32, 3, 16, 1);
     int h = 32, c = 16;
     plain_bn(x, p, 0, c, h * h);
-    plain_relu(x);
+    relu(x);
     for (int j = 0; j < 3; j++)
         for (int k = 0; k <= end_num; k++)
         {
@@ -232,7 +233,7 @@ std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector
             std::vector<double> y = plain_conv(x, p.conv_weight[s1], h, c, co, st);
             const int ho = h / st;
             plain_bn(y, p, s1, co, ho * ho);
-            plain_relu(y);
+            relu(y);
             y = plain_conv(y, p.conv_weight[s2], ho, co, co, 1);
             plain_bn(y, p, s2, co, ho * ho);
             if (st == 2)
@@ -246,7 +247,7 @@ std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector
                 temp = ds;
             }
             for (std::size_t i = 0; i < y.size(); i++) y[i] += temp[i];
-            plain_relu(y);
+            relu(y);
             x = y;
             h = ho;
             c = co;
@@ -319,11 +320,14 @@ ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, co
     m.parms.set_poly_modulus_degree(poly_modulus_degree);
     m.parms.set_coeff_modulus(CoeffModulus::Create(poly_modulus_degree, coeff_bit_vec));
     m.parms.set_secret_key_hamming_weight(192);
+    std::shared_ptr<Blake2xbSeedSequence> seeds;
     if (rng_seed)
     {
+        // reproducible keys, each from its own seed; frozen after setup (seal.h Blake2xbSeedSequence)
         prng_seed_type seed{};
         seed[0] = rng_seed;
-        m.parms.set_random_generator(std::make_shared<Blake2xbPRNGFactory>(seed));
+        seeds = std::make_shared<Blake2xbSeedSequence>(seed);
+        m.parms.set_random_generator(seeds);
     }
     m.context = std::make_unique<SEALContext>(m.parms);
     m.encoder = std::make_unique<CKKSEncoder>(*m.context);
@@ -336,6 +340,7 @@ ResNetRunner::ResNetRunner(std::size_t layer_num, const ResNetParams &params, co
         m.keygen->create_relin_keys(m.relin_keys);
         finish_setup(true);
     }
+    if (seeds) seeds->freeze();
 }
 
 void ResNetRunner::finish_setup(bool plan_galois_keys)
@@ -553,9 +558,24 @@ std::vector<std::uint64_t> ResNetRunner::op_counts(int kind, bool reset)
     return c;
 }
 
+std::vector<double> resnet_plain_logits(const ResNetParams &p, const std::vector<double> &img, std::size_t layer_num)
+{
+    return resnet_plain_logits(p, img, layer_num, plain_relu);
+}
+
 std::vector<double> ResNetRunner::plain_logits(const std::vector<double> &image) const
 {
-    return resnet_plain_logits(impl_->prm, image, impl_->layer_num);
+    return resnet_plain_logits(impl_->prm, image, impl_->layer_num, plain_relu);
+}
+
+std::vector<double> ResNetRunner::plain_logits_approx(const std::vector<double> &image) const
+{
+    const Impl &m = *impl_;
+    const MinimaxReluPlain r(m.comp_no, m.deg, m.alpha, m.tree, m.scaled_val);
+    const double B = m.B; // the encrypted network runs on x / B (infer_seal.cpp:444)
+    return resnet_plain_logits(m.prm, image, m.layer_num, [&](std::vector<double> &v) {
+        for (double &x : v) x = B * r(x / B);
+    });
 }
 
 ResNetResult ResNetRunner::infer(const std::vector<double> &img)

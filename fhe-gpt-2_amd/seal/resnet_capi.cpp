@@ -203,6 +203,24 @@ int mhe_resnet_plain_logits(mhe_resnet *r, const double *image, double *logits)
     });
 }
 
+int mhe_resnet_plain_logits_approx(mhe_resnet *r, const double *image, double *logits)
+{
+    return guard([&] {
+        if (!image || !logits) throw std::invalid_argument("null argument");
+        const std::vector<double> out = r->runner->plain_logits_approx(std::vector<double>(image, image + 3072));
+        for (int k = 0; k < 10; k++) logits[k] = out[k];
+    });
+}
+
+int mhe_resnet_fallback_stats(uint64_t *stats, int reset)
+{
+    return guard([&] {
+        if (!stats) throw std::invalid_argument("null argument");
+        stats[0] = seal::merged_call_fallbacks(reset != 0);
+        if (mhe_alloc_stats(&stats[1], &stats[2], reset) != 0) throw std::runtime_error(mhe_last_error());
+    });
+}
+
 int mhe_resnet_info(mhe_resnet *r, double *setup_s, double *gb, int *nkeys)
 {
     return guard([&] {

@@ -28,7 +28,9 @@
 #include <thread>
 #include <unordered_map>
 
+#include <sys/mman.h>
 #include <ucontext.h>
+#include <unistd.h>
 
 namespace seal
 {
@@ -2296,10 +2298,40 @@ struct Lockstep::Impl
 // ------------------------------------------------------------------------------ FiberBatch
 struct FiberBatch::Impl
 {
+    // A fiber's stack: mmap'ed, with a PROT_NONE guard page below it (stacks grow down), so an
+    // overflow faults at a known address instead of silently corrupting a neighbouring heap block.
+    struct Stack
+    {
+        void *base = nullptr; // guard page + usable bytes
+        std::size_t bytes = 0;
+        Stack() = default;
+        Stack(const Stack &) = delete;
+        Stack &operator=(const Stack &) = delete;
+        Stack(Stack &&o) noexcept : base(o.base), bytes(o.bytes) { o.base = nullptr; }
+        ~Stack()
+        {
+            if (base) munmap(base, bytes);
+        }
+        void alloc(std::size_t usable)
+        {
+            const std::size_t page = (std::size_t)sysconf(_SC_PAGESIZE);
+            usable = (usable + page - 1) / page * page;
+            bytes = usable + page;
+            base = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_STACK, -1, 0);
+            if (base == MAP_FAILED)
+            {
+                base = nullptr;
+                throw std::runtime_error("FiberBatch: stack allocation failed");
+            }
+            if (mprotect(base, page, PROT_NONE) != 0) throw std::runtime_error("FiberBatch: guard page failed");
+        }
+        char *sp() const { return static_cast<char *>(base) + (bytes - usable()); }
+        std::size_t usable() const { return bytes - (std::size_t)sysconf(_SC_PAGESIZE); }
+    };
     struct Fiber
     {
         ucontext_t ctx{};
-        std::unique_ptr<char[]> stack;
+        Stack stack;
         std::size_t idx = 0;
         bool done = false, blocked = false;
         std::exception_ptr err;
@@ -2334,10 +2366,10 @@ struct FiberBatch::Impl
     {
         Fiber &f = fibers[i];
         f.idx = i;
-        f.stack.reset(new char[stack_bytes]);
+        f.stack.alloc(stack_bytes);
         if (getcontext(&f.ctx) != 0) throw std::runtime_error("FiberBatch: getcontext failed");
-        f.ctx.uc_stack.ss_sp = f.stack.get();
-        f.ctx.uc_stack.ss_size = stack_bytes;
+        f.ctx.uc_stack.ss_sp = f.stack.sp();
+        f.ctx.uc_stack.ss_size = f.stack.usable();
         f.ctx.uc_link = &sched;
         const std::uintptr_t self = reinterpret_cast<std::uintptr_t>(this);
         makecontext(&f.ctx, reinterpret_cast<void (*)()>(&Impl::entry), 2, (unsigned)(self & 0xFFFFFFFFu),
@@ -2510,6 +2542,13 @@ bool Evaluator::lockstep_submit(LsOp &op) const
     return true;
 }
 
+static std::atomic<std::uint64_t> g_merged_fallbacks{ 0 };
+
+std::uint64_t merged_call_fallbacks(bool reset)
+{
+    return reset ? g_merged_fallbacks.exchange(0) : g_merged_fallbacks.load();
+}
+
 void Evaluator::lockstep_execute(std::vector<LsOp *> &ops) const
 {
     // one member's call as it would have run alone
@@ -2594,7 +2633,9 @@ void Evaluator::lockstep_execute(std::vector<LsOp *> &ops) const
         // The merged call validates every entry before its first launch (rescale / relinearize), or
         // wrote only outputs that are not inputs (rotations, products through temporaries), so the
         // members' operands are unchanged here: each member's call runs again on its own and gets
-        // its own result or its own error, as without the group.
+        // its own result or its own error, as without the group.  Counted (merged_call_fallbacks):
+        // a fallback means a merged launch failed, which a healthy run never sees.
+        g_merged_fallbacks.fetch_add(1);
         for (LsOp *o : ops) run_one(*o);
     }
 }
@@ -2745,9 +2786,18 @@ void Evaluator::relinearize_inplace_many(const std::vector<Ciphertext *> &encryp
             ct.push_back(d);
             target.push_back(d + 2 * L * c->poly_modulus_degree());
         }
-        chk(mhe_switch_key_batch(context_.engine(), (int)v.size(), ct.data(), target.data(), keys.data(), kls.data(),
-                                 (int)L, s));
-        for (Ciphertext *c : v) c->resize(2);
+        // one engine launch sequence (at most 8 entries, MHE_MAXB) per chunk, and each chunk's entries
+        // marked relinearized (size 2) as soon as it is done: the switches work in place, so if a later
+        // chunk fails, a member re-run by lockstep_execute finds the finished entries at size 2 and
+        // skips them instead of switching them a second time
+        constexpr std::size_t kChunk = 8;
+        for (std::size_t i0 = 0; i0 < v.size(); i0 += kChunk)
+        {
+            const int B = (int)std::min(kChunk, v.size() - i0);
+            chk(mhe_switch_key_batch(context_.engine(), B, ct.data() + i0, target.data() + i0, keys.data() + i0,
+                                     kls.data() + i0, (int)L, s));
+            for (int e = 0; e < B; e++) v[i0 + e]->resize(2);
+        }
     }
     for (Ciphertext *c : encrypted)
         if (c->size() > 2) relinearize_inplace(*c, relin_keys);

@@ -75,8 +75,8 @@ int mhe_stream_wait(mhe_ctx *ctx, void *waiter, void *waitee);
 /* Key-switching key bytes streamed by the key switches run on the context since the last reset
  * (L digits x 2 x (L+1) primes x n x 8 per switch): the algorithmic key traffic of a workload. */
 int mhe_key_traffic(mhe_ctx *ctx, uint64_t *bytes, int reset);
-/* The same key slices counted in the prepared key format (mhe_key_prepare): 6 B per residue for
- * primes below 2^48, 8 B otherwise -- the bytes a switch streams when its key is prepared. */
+/* The same key slices counted as a prepared key streams them (8 B per residue for the doubles
+ * format, as in SEAL's layout). */
 int mhe_key_traffic_prepared(mhe_ctx *ctx, uint64_t *bytes, int reset);
 /* Operations run on the context since the last reset, by kind and level (limbs): counts[l] for
  * l < levels (reset != 0 zeroes every level of the kind).  Units: one key switch per entry
@@ -151,6 +151,16 @@ int mhe_scratch_bytes(mhe_ctx *ctx, uint64_t *workspace, uint64_t *hoisting, uin
  * memory; 0 turns it off.  Used to check that a batched call that fails part way leaves its
  * operands as they were (tests/cpp/seal_batch_test.cpp). */
 int mhe_debug_fail_alloc(mhe_ctx *ctx, int nth);
+/* Fault injection for tests: the nth next batched key-switch launch sequence of the context (one
+ * chunk of at most 8 entries of mhe_switch_key_batch, mhe_hmult_batch, ...) fails with MHE_ERR_MEMORY
+ * before its first launch; 0 turns it off.  Used to fail the second chunk of a merged relinearization
+ * (tests/cpp/seal_batch_test.cpp). */
+int mhe_debug_fail_switch(mhe_ctx *ctx, int nth);
+/* Process-wide allocation health, since the last reset: device allocations (ciphertext buffers and
+ * scratch) that succeeded only after the caching allocator gave its cached blocks back to the device
+ * and retried, and allocations that failed (injected failures included).  A healthy run reports 0
+ * and 0; the SEAL surface's re-run merged calls are counted by seal::merged_call_fallbacks. */
+int mhe_alloc_stats(uint64_t *retries, uint64_t *failures, int reset);
 /* Give the device memory the engine's caching allocator holds for reuse (freed ciphertext / key
  * buffers, kept per size for the stream-ordered mhe_malloc_async) back to the device.  Synchronises
  * the device.  For after a setup phase that freed much more than the steady state reuses (e.g. the
@@ -212,16 +222,25 @@ int mhe_ct_square(mhe_ctx *ctx, const uint64_t *a, uint64_t *out3, int limbs, vo
  * limb i is limb i.  A full SEAL key has key_limbs = chain count and digits = count-1; a
  * level-truncated slice for L-limb ciphertexts may keep only L digits and L+1 limbs. */
 
-/* Engine key format (optional, no SEAL counterpart; the role of SEAL's KSwitchKeys
+/* Engine key formats (optional, no SEAL counterpart; the role of SEAL's KSwitchKeys
  * storage, keygenerator.cpp:384-414).  Converts a key of `digits` digits and `key_limbs` limbs
- * in place: each limb slot of a prime below 2^48 then holds a 32-bit plane [n], a 16-bit plane
- * [n] and a tag word (>= 2^63, never a residue) in its unused last quarter, so the key MAC
- * streams 6 instead of 8 bytes per residue and recognises the format by itself; every key
- * switch stays bit-identical.  The buffer is not a SEAL key again until mhe_key_unprepare.
- * Preparing a prepared key (or unpreparing a SEAL key) fails with MHE_ERR_ARG. */
+ * in place, and every key switch given it stays bit-identical:
+ *   MHE_KEY_FMT_DOUBLE: each limb slot of a prime below 2^51 holds its residues as IEEE doubles
+ *     (-0.0 for zero; every word >= 2^61, never a residue), the FP64 key MAC's operand with no
+ *     unpacking -- for keys streamed by batched launches (the relinearization key of 8 HMults);
+ *   MHE_KEY_FMT_PACK48: each limb slot of a prime below 2^48 holds a 32-bit plane [n], a 16-bit
+ *     plane [n] and a tag word (>= 2^63) in its unused last quarter -- 6 instead of 8 bytes per
+ *     residue, for keys streamed by one ciphertext at a time.
+ * The key MAC recognises either format from the buffer itself.  The buffer is not a SEAL key again
+ * until mhe_key_unprepare.  Preparing a prepared key (or unpreparing a SEAL key) fails with
+ * MHE_ERR_ARG.  mhe_key_prepare makes MHE_KEY_FMT_DOUBLE (MHE_KEY_FMT=2 in the environment: PACK48). */
+#define MHE_KEY_FMT_DOUBLE 1
+#define MHE_KEY_FMT_PACK48 2
 int mhe_key_prepare(mhe_ctx *ctx, uint64_t *key, int digits, int key_limbs, void *stream);
+int mhe_key_prepare_as(mhe_ctx *ctx, uint64_t *key, int digits, int key_limbs, int format, void *stream);
 int mhe_key_unprepare(mhe_ctx *ctx, uint64_t *key, int digits, int key_limbs, void *stream);
-/* *prepared = 1 when `key` is in the prepared format (reads one tag word; host sync). */
+/* *prepared = the format of `key`: 0 SEAL's layout, MHE_KEY_FMT_DOUBLE or MHE_KEY_FMT_PACK48
+ * (reads one or two words; host sync). */
 int mhe_key_is_prepared(mhe_ctx *ctx, const uint64_t *key, int key_limbs, int *prepared, void *stream);
 
 /* Evaluator::switch_key_inplace (evaluator.cpp:2281-2525): ct[2][L][n] += KS(target[L][n]). */

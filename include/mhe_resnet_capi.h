@@ -70,6 +70,15 @@ int mhe_resnet_scratch_bytes(mhe_resnet *runner, double *bytes);
 /* The same network in plain doubles with the exact ReLU (the check of a decrypted inference,
  * infer_seal.cpp:543-575 prints decrypted logits against the label): image 3 x 32 x 32 -> logits[10]. */
 int mhe_resnet_plain_logits(mhe_resnet *runner, const double *image, double *logits);
+/* The same network in plain doubles with the encrypted network's own ReLU, the minimax composite
+ * polynomial on x / B restated on doubles (mhe_comp.h MinimaxReluPlain): a decrypted result differs
+ * from it by the encryption's error alone (noise, rescaling, bootstrapping). */
+int mhe_resnet_plain_logits_approx(mhe_resnet *runner, const double *image, double *logits);
+/* stats[3]: merged FiberBatch / Lockstep calls that failed and were re-run member by member
+ * (seal::merged_call_fallbacks), device allocations that succeeded only after the engine released
+ * its cached blocks and retried, and allocations that failed (mhe_alloc_stats); process-wide, since
+ * the last reset.  A healthy run reports 0, 0, 0. */
+int mhe_resnet_fallback_stats(uint64_t *stats, int reset);
 
 #ifdef __cplusplus
 }

@@ -279,6 +279,10 @@ int main(int argc, char **argv)
             for (auto &c : want) ev.rescale_to_next_inplace(c);
             bool ok_alone = true, ok_fiber = true;
             int threw_alone = 0, retried = 0;
+            // the fallbacks and failed allocations must be counted, not silent
+            const std::uint64_t fb0 = merged_call_fallbacks();
+            std::uint64_t ar0 = 0, af0 = 0;
+            mhe_alloc_stats(&ar0, &af0, 0);
             for (int nth = 1; nth <= 10; nth++)
             {
                 std::vector<Ciphertext> v = base;
@@ -324,6 +328,47 @@ int main(int argc, char **argv)
             check("FiberBatch: a merged rescale that fails part way is re-run per member, each entry rescaled once (" +
                       std::to_string(retried) + " failing merged calls)",
                   ok_fiber && retried > 0);
+            std::uint64_t ar1 = 0, af1 = 0;
+            mhe_alloc_stats(&ar1, &af1, 0);
+            const std::uint64_t fb = merged_call_fallbacks() - fb0, af = af1 - af0;
+            check("the merged-call fallbacks (" + std::to_string(fb) + ") and failed allocations (" + std::to_string(af) +
+                      ") are counted: at least one per failing merged call / injected failure",
+                  fb >= (std::uint64_t)retried && af >= (std::uint64_t)(retried + threw_alone));
+        }
+
+        // A merged relinearization of more than 8 entries (10 fibers, one relinearize_inplace each)
+        // runs as two engine chunks of in-place key switches.  When the second chunk fails
+        // (injected), lockstep_execute re-runs each member alone: the first chunk's entries are
+        // already relinearized (size 2) and must not be switched a second time.
+        {
+            const int F = 10;
+            std::vector<Ciphertext> base(F), want(F);
+            for (int i = 0; i < F; i++)
+            {
+                Ciphertext a = fresh(1), b = fresh(1);
+                ev.multiply(a, b, base[i]);
+                want[i] = base[i];
+                ev.relinearize_inplace(want[i], rlk);
+            }
+            const std::uint64_t fb0 = merged_call_fallbacks();
+            std::vector<Ciphertext> f = base;
+            mhe_debug_fail_switch(ctx.engine(), 2);
+            bool ok = true;
+            try
+            {
+                FiberBatch::run(F, [&](std::size_t m) { ev.relinearize_inplace(f[m], rlk); });
+            }
+            catch (const std::exception &e)
+            {
+                std::printf("  FiberBatch threw: %s\n", e.what());
+                ok = false;
+            }
+            mhe_debug_fail_switch(ctx.engine(), 0);
+            for (int i = 0; i < F; i++) ok = ok && same(f[i], want[i]);
+            const std::uint64_t fb = merged_call_fallbacks() - fb0;
+            check("FiberBatch: a 10-entry merged relinearization whose second chunk fails is re-run per member, "
+                  "each entry switched once (" + std::to_string(fb) + " fallback)",
+                  ok && fb == 1);
         }
 
         bool threw = false;

@@ -3,7 +3,7 @@
 bench.HMultWorkload is the bench's own workload object (not a copy of it): N=2^16, the C2 chain
 (44 data limbs + the special prime), L = 44, 32 independent HMults per step issued as 4
 mhe_hmult_batch calls of 8 entries (the relin key stream shared through the XCD-grouped entries of
-k_ks_row_mac), the prepared 48-bit key format, the calls dealt round robin over 4 HIP streams.
+k_ks_row_mac), the prepared key format (residues as doubles), the calls dealt round robin over 4 HIP streams.
 One step runs as the bench runs it; every one of the 32 outputs must equal the oracle's HMult
 (SEAL/evaluator.cpp:673-814 multiply, :2281-2525 relinearize, util/rns.cpp:737-808 rescale) on the
 same inputs and the SEAL-layout key."""

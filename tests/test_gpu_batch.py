@@ -25,15 +25,17 @@ def resnet():
 
 
 class hoisting:
-    """Hoisted rotations on for the block (mhe_ctx_set_hoist; the context default is off), with
+    """Hoisted rotations on for the block (mhe_ctx_set_hoist; on is also the context default) with
     the engine's own check (every hoisted rotation recomputed by the classic path and compared).
     On exit: the hoisted key-MAC kernels must have run (mhe_hoist_stats) and the check must have
-    found no differing word; hoisting goes off again."""
+    found no differing word; the context's previous setting is restored, so the tests after this
+    one see the same default whatever the order."""
 
     def __init__(self, eng, min_rotations=1):
         self.eng, self.min_rotations = eng, min_rotations
 
     def __enter__(self):
+        self.saved = self.eng.hoist()
         self.eng.set_hoist(True, check=True)
         assert self.eng.hoist() == (True, True)
         self.eng.hoist_stats(reset=True)
@@ -42,7 +44,7 @@ class hoisting:
     def __exit__(self, *exc):
         self.eng.synchronize()
         rot, mac, bad = self.eng.hoist_stats(reset=True)
-        self.eng.set_hoist(False)
+        self.eng.set_hoist(*self.saved)
         if exc[0] is None:
             assert rot >= self.min_rotations and mac >= 1, (rot, mac)
             assert bad == 0, f"{bad} words of hoisted rotations differ from the classic path"
@@ -86,7 +88,7 @@ def test_rotate_batch_many_inputs(small, count):
 
 
 def test_rotate_batch_prepared_keys_n16(resnet):
-    """N = 2^16 on the ResNet chain with prepared (48-bit) keys: the packed ModUp intermediate and
+    """N = 2^16 on the ResNet chain with prepared keys (residues as doubles): the packed ModUp intermediate and
     key planes per entry, at a bootstrap-like level."""
     ch = resnet
     L = 6
@@ -94,7 +96,8 @@ def test_rotate_batch_prepared_keys_n16(resnet):
     steps = [1, 2, 4, 8]
     elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
     keys = [truncated(ch.rand_key(digits=L), L) for _ in steps]
-    dkeys = [ch.eng.key_prepare(ch.up(k)) for k in keys]
+    # both prepared formats in one call (doubles, 48-bit planes, alternating)
+    dkeys = [ch.eng.key_prepare(ch.up(k), 1 + i % 2) for i, k in enumerate(keys)]
     outs = ch.eng.apply_galois_batch([ch.up(ct)] * len(steps), elts, dkeys)
     full = [np.zeros((L, 2, ch.K, ch.n), np.uint64) for _ in keys]
     for f, k in zip(full, keys):  # the truncated slice inside a full-shape key for the oracle
@@ -194,7 +197,7 @@ def test_rotate_batch_hoisted_n16(resnet):
     cts = [ch.rand(2, L, ch.n), with_zero_coeffs(ch, L, 2), ch.rand(2, L, ch.n)]
     steps = [1, 2, 3]
     keys = [truncated(ch.rand_key(digits=L), L) for _ in steps]
-    dkeys = [ch.eng.key_prepare(ch.up(k)) for k in keys]
+    dkeys = [ch.eng.key_prepare(ch.up(k), 1 + i % 2) for i, k in enumerate(keys)]  # mixed formats
     full = [np.zeros((L, 2, ch.K, ch.n), np.uint64) for _ in keys]
     for f, k in zip(full, keys):
         f[:, :, :L] = k[:, :, :L]
@@ -221,14 +224,21 @@ def test_rotate_batch_hoisted_fiber_bsgs_shape(resnet, zero_input):
     L = 24
     steps = [1, 2, 3, 4, 5, 6, 7]
     keys = [truncated(ch.rand_key(digits=L), L) for _ in steps]
-    dkeys = [ch.eng.key_prepare(ch.up(k)) for k in keys]
+    # the zero-input case with mixed key formats (the shared kernel's per-row format), the other
+    # with the default
+    dkeys = [ch.eng.key_prepare(ch.up(k), (1 + i % 2) if zero_input is not None else None) for i, k in enumerate(keys)]
     cts = [with_zero_coeffs(ch, L, 2) if i == zero_input else ch.rand(2, L, ch.n) for i in range(8)]
     srcs = [ch.up(c) for c in cts]
     elts = [mhe.galois_elt_from_step(ch.log_n, s) for s in steps]
     ins = [s for s in srcs for _ in steps]
     with hoisting(ch.eng, len(ins)):
         outs = ch.eng.apply_galois_batch(ins, elts * 8, dkeys * 8)
-    classic = ch.eng.apply_galois_batch(ins, elts * 8, dkeys * 8)  # hoisting off again
+    saved = ch.eng.hoist()
+    ch.eng.set_hoist(False)  # the classic path, explicitly
+    try:
+        classic = ch.eng.apply_galois_batch(ins, elts * 8, dkeys * 8)
+    finally:
+        ch.eng.set_hoist(*saved)
     for j in range(len(ins)):
         assert np.array_equal(ch.down(outs[j]), ch.down(classic[j])), f"input {j // 7} step {steps[j % 7]}"
     full = [np.zeros((L, 2, ch.K, ch.n), np.uint64) for _ in keys]
@@ -281,15 +291,15 @@ def test_hmult_batch(small, count):
         assert np.array_equal(ch.down(outs[i]), want), i
 
 
-@pytest.mark.parametrize("prepared", [False, True])
+@pytest.mark.parametrize("prepared", [0, 1, 2], ids=["seal", "doubles", "pack48"])
 def test_hmult_batch_resnet_size(resnet, prepared):
     """N = 2^16 (the grid where every tile count is a multiple of 8): 9 HMults in one call (8 + 1)
-    equal one-by-one mhe_hmult, with SEAL's key layout and the prepared 48-bit key."""
+    equal one-by-one mhe_hmult, with SEAL's key layout and both prepared key formats."""
     ch = resnet
     L = 6
     key = ch.up(truncated(ch.rand_key(), L))
     if prepared:
-        key = ch.eng.key_prepare(key)
+        key = ch.eng.key_prepare(key, prepared)
     a = [ch.up(ch.rand(2, L, ch.n)) for _ in range(9)]
     b = [ch.up(ch.rand(2, L, ch.n)) for _ in range(9)]
     outs = ch.eng.hmult_batch(a, b, key)

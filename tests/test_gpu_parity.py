@@ -303,22 +303,31 @@ def test_hmult_small(small):
     assert np.array_equal(got, ch.oc.hmult(a, b, key))
 
 
-def test_prepared_key_bit_exact(small):
-    """mhe_key_prepare (engine key format: 48-bit planes for primes below 2^48) leaves every key
-    switch bit-identical -- full and level-truncated keys, switch / relinearize / rotate / HMult --
+@pytest.mark.parametrize("fmt", [1, 2], ids=["doubles", "pack48"])
+def test_prepared_key_bit_exact(small, fmt):
+    """mhe_key_prepare_as, both engine key formats -- 1: the residues of primes below 2^51 as doubles
+    (-0.0 for a zero); 2: 48-bit planes and a tag word for primes below 2^48 -- leaves every key
+    switch bit-identical (full and level-truncated keys, switch / relinearize / rotate / HMult),
     and mhe_key_unprepare restores SEAL's layout word for word."""
     ch = small
     key = ch.rand_key()
+    key[0, 0, 1, 5] = 0  # a zero residue: -0.0 as a double
     dkey = ch.up(key)
-    ch.eng.key_prepare(dkey)
-    assert ch.eng.key_is_prepared(dkey)
+    ch.eng.key_prepare(dkey, fmt)
+    assert ch.eng.key_format(dkey) == fmt
     packed = ch.down(dkey)
-    assert not np.array_equal(packed, key)  # the 46-bit limbs are repacked and tagged
-    assert np.array_equal(packed[:, :, 0], key[:, :, 0]) and np.array_equal(packed[:, :, -1], key[:, :, -1])  # 51-bit
-    lo = packed[:, :, 1].view(np.uint32)[..., : ch.n]
-    hi = packed[:, :, 1].view(np.uint16)[..., 2 * ch.n: 3 * ch.n]
-    assert np.array_equal(lo.astype(np.uint64) | (hi.astype(np.uint64) << 32), key[:, :, 1])
-    assert (packed[:, :, 1, -1] == 0xF0E1D2C3B4A59687).all()
+    if fmt == 1:
+        assert all(q < (1 << 51) for q in ch.moduli)  # every limb of this chain is converted
+        want = key.astype(np.float64).view(np.uint64).copy()
+        want[key == 0] = 0x8000000000000000
+        assert np.array_equal(packed, want)
+        assert (packed >= (1 << 61)).all()  # no residue of a SEAL key reaches 2^61
+    else:
+        assert np.array_equal(packed[:, :, 0], key[:, :, 0]) and np.array_equal(packed[:, :, -1], key[:, :, -1])  # 51-bit
+        lo = packed[:, :, 1].view(np.uint32)[..., : ch.n]
+        hi = packed[:, :, 1].view(np.uint16)[..., 2 * ch.n: 3 * ch.n]
+        assert np.array_equal(lo.astype(np.uint64) | (hi.astype(np.uint64) << 32), key[:, :, 1])
+        assert (packed[:, :, 1, -1] == 0xF0E1D2C3B4A59687).all()
     for L in (1, 5, ch.K - 1):
         ct, target = ch.rand(2, L, ch.n), ch.rand(L, ch.n)
         got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), dkey))
@@ -336,7 +345,7 @@ def test_prepared_key_bit_exact(small):
     # a level-truncated slice, prepared on its own
     Lt = 4
     trunc = np.concatenate([key[:Lt, :, :Lt], key[:Lt, :, -1:]], axis=2).copy()
-    dt = ch.eng.key_prepare(ch.up(trunc))
+    dt = ch.eng.key_prepare(ch.up(trunc), fmt)
     ct, target = ch.rand(2, Lt, ch.n), ch.rand(Lt, ch.n)
     got = ch.down(ch.eng.switch_key(ch.up(ct), ch.up(target), dt))
     assert np.array_equal(got, ch.oc.switch_key(ct, target, key))
@@ -346,8 +355,9 @@ def test_prepared_key_bit_exact(small):
 
 def test_prepared_key_errors_and_noop():
     """Unpreparing a SEAL-layout key fails with SEAL-style argument errors; on a chain with no
-    prime below 2^48 preparation leaves the key as it is (nothing to pack) and switches still match."""
-    ch = Chain(12, [51] * 5, seed=11)
+    prime below 2^51 (integer kernels) preparation leaves the key as it is (nothing to convert) and
+    switches still match."""
+    ch = Chain(12, [60] * 5, seed=11)
     key = ch.rand_key()
     dkey = ch.up(key)
     assert not ch.eng.key_is_prepared(dkey)

@@ -59,24 +59,27 @@ def test_sparse_bootstrap_matches_oracle(tmp_path, log_n, logn):
         assert counts.get(op, 0) > 0, f"{op} not exercised: {counts}"
 
 
-def test_sparse_bootstrap_resnet_shape_matches_oracle(tmp_path):
-    """The bootstrap ResNet runs, at its own shape: bootstrap_real_3 at N = 2^16 on
-    the 31 + 1 prime chain (cnn/infer_seal.cpp:288-316) with logn 12 sparse slots, the third
-    bootstrapper of ResNet-20 (Bootstrapper.cpp:3166-3236, called from infer_seal.cpp:486-533),
-    replayed op by op through the oracle on 16 host threads; every word and scale must be equal."""
+@pytest.mark.parametrize("logn", [12, 14])
+def test_sparse_bootstrap_resnet_shape_matches_oracle(tmp_path, logn):
+    """The bootstraps ResNet runs, at their own shape: bootstrap_real_3
+    at N = 2^16 on the 31 + 1 prime chain (cnn/infer_seal.cpp:288-316) with logn 12 sparse slots, the
+    third bootstrapper of ResNet-20, and logn 14, the first and largest one (76 rotations, its own
+    giant-step split, COMMON/func.cpp:203) (Bootstrapper.cpp:3166-3236, called from
+    infer_seal.cpp:340-342,486-533), replayed op by op through the oracle on 16 host threads; every
+    word and scale must be equal."""
     import shutil
 
-    d = tmp_path / "boot16_12"
+    d = tmp_path / f"boot16_{logn}"
     d.mkdir()
     exe = os.path.join(ROOT, "build", "trace_caller_test")
-    r = subprocess.run([exe, "16", str(d), os.path.join(ROOT, "tests", "golden", "comp"), "boot", "12"],
+    r = subprocess.run([exe, "16", str(d), os.path.join(ROOT, "tests", "golden", "comp"), "boot", str(logn)],
                        capture_output=True, text=True, timeout=600)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     size = sum(f.stat().st_size for f in d.iterdir())
     rp = Replayer(str(d))
     checked, counts = rp.replay(threads=16)
-    print(f"N=2^16, logn 12: {checked} bootstrap operations ({size / 1e9:.1f} GB of trace) match the oracle: {counts}")
+    print(f"N=2^16, logn {logn}: {checked} bootstrap operations ({size / 1e9:.1f} GB of trace) match the oracle: {counts}")
     for op in ("modraise", "rotate", "galois", "multiply_plain", "rescale", "mul_re", "add_re"):
         assert counts.get(op, 0) > 0, f"{op} not exercised: {counts}"
     shutil.rmtree(d, ignore_errors=True)
