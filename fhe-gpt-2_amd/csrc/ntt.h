@@ -1532,13 +1532,17 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
 
 template <int LOGR, bool FP, bool MIX = false>
 #ifndef MHE_KS_OCC
-#define MHE_KS_OCC 3 // waves per SIMD the FP64 fused MAC at n = 2^16 is compiled for (the others: 2)
+#define MHE_KS_OCC 2 // waves per SIMD the FP64 fused MAC at n = 2^16 is compiled for (3: 168 VGPRs, one
+                     // LDS transpose buffer; equal on the C2 bench, 2 % slower on single key switches, r06c)
 #endif
 #ifndef MHE_KS_PP
 #define MHE_KS_PP 0 // digit loop unrolled twice, prefetched digit in alternating registers
 #endif
 #ifndef MHE_KS_KPF
 #define MHE_KS_KPF 0 // key limbs loaded one digit ahead too (32 VGPRs more)
+#endif
+#ifndef MHE_KS_FL
+#define MHE_KS_FL 1 // keys and accumulators in the row transform's last layout (no transpose back per digit)
 #endif
 __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) void k_ks_row_mac(KsPtrs P, const PrimeDev *__restrict__ primes,
                                                        const Tw *__restrict__ tw_all, int L, int K, int log_n,
@@ -1575,6 +1579,11 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
     using TW = typename A::TW;
     constexpr int R = SH::R, TPS = SH::TPS, S = SH::S;
     constexpr int B_A = LOGR - 3, B_B = LOGR - 6;
+    static_assert(LOGR >= 6, "the row transform ends in layout lay(t, e, 0)");
+    // layout of the key limbs, the input limb and the accumulators: the row transform's last
+    // (lay(t, e, 0): 8 consecutive residues per lane) with MHE_KS_FL, so a digit needs no transpose
+    // back to the coalesced layout lay(t, e, B_A) -- the accumulators take it once, at the end
+    constexpr int BK = MHE_KS_FL ? 0 : B_A;
     // one transpose buffer is enough (every transpose stays inside one wave and a wave's LDS
     // operations complete in order; the fences only stop the compiler from reordering them):
     // 48 KB per workgroup fits 3 workgroups per CU, two buffers (64 KB) only 2
@@ -1707,7 +1716,7 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
 #pragma unroll
                     for (int e = 0; e < 8; e++)
                     {
-                        const u32 r = lay(t, e, B_A);
+                        const u32 r = lay(t, e, BK);
                         ka[e] = (u64)ld_nt<1>(&l0[r]) | ((u64)ld_nt<1>(&h0[r]) << 32);
                         kb[e] = (u64)ld_nt<1>(&l1[r]) | ((u64)ld_nt<1>(&h1[r]) << 32);
                     }
@@ -1717,8 +1726,8 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
 #pragma unroll
                     for (int e = 0; e < 8; e++)
                     {
-                        ka[e] = ld_nt<1>(&k0[base + lay(t, e, B_A)]);
-                        kb[e] = ld_nt<1>(&k1[base + lay(t, e, B_A)]);
+                        ka[e] = ld_nt<1>(&k0[base + lay(t, e, BK)]);
+                        kb[e] = ld_nt<1>(&k1[base + lay(t, e, BK)]);
                     }
                 }
             };
@@ -1766,13 +1775,21 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
                     else
                         w[e] = ar.in52(vin[e]);
                 }
+                // LDS slots of the transposes: swz is linear over GF(2) and lay(t, e, b) is the
+                // disjoint OR of a lane part and e << b, so slot = swz(lane part) ^ swz(e << b).  The
+                // non-lazy sweep (more live values) recomputes the XORs from three per-lane bases
+                // each digit (asm barrier: not hoisted) instead of keeping 24 slots in VGPRs, which
+                // at 3 waves/SIMD were spilled and reloaded behind vmcnt(0) every digit.
+                u32 sa = swz(lay(t, 0, B_A)), sb = swz(lay(t, 0, B_B)), s0 = swz(lay(t, 0, 0));
+                if constexpr (!LZ) asm volatile("" : "+v"(sa), "+v"(sb), "+v"(s0));
+                auto slot = [&](u32 lane_part, int e, int b) { return lane_part ^ swz((u32)e << b); };
                 row_stages<LOGR>(w, t, B_A, 0, 3, mytw, ar);
                 wave_lds_fence(); // the previous digit's reads of x0 come first
 #pragma unroll
-                for (int e = 0; e < 8; e++) x0[swz(lay(t, e, B_A))] = w[e];
+                for (int e = 0; e < 8; e++) x0[slot(sa, e, B_A)] = w[e];
                 wave_lds_fence();
 #pragma unroll
-                for (int e = 0; e < 8; e++) w[e] = x0[swz(lay(t, e, B_B))];
+                for (int e = 0; e < 8; e++) w[e] = x0[slot(sb, e, B_B)];
                 row_stages<LOGR>(w, t, B_B, 3, 6, mytw, ar);
                 T *xl = x1;
                 int bl = B_B;
@@ -1780,13 +1797,27 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
                 {
                     wave_lds_fence();
 #pragma unroll
-                    for (int e = 0; e < 8; e++) x1[swz(lay(t, e, B_B))] = w[e];
+                    for (int e = 0; e < 8; e++) x1[slot(sb, e, B_B)] = w[e];
                     wave_lds_fence();
 #pragma unroll
-                    for (int e = 0; e < 8; e++) w[e] = x1[swz(lay(t, e, 0))];
+                    for (int e = 0; e < 8; e++) w[e] = x1[slot(s0, e, 0)];
                     row_stages<LOGR>(w, t, 0, 6, LOGR, mytw, ar);
                     xl = x0;
                     bl = 0;
+                }
+                if constexpr (MHE_KS_FL)
+                {
+                    // already the keys' layout (integer: canonical digits keep the 128-bit sums
+                    // exact for any digit count below 2^8)
+#pragma unroll
+                    for (int e = 0; e < 8; e++)
+                    {
+                        if constexpr (FPA)
+                            d[e] = w[e];
+                        else
+                            d[e] = ar.canon(w[e]);
+                    }
+                    return;
                 }
                 // back to the coalesced layout of the key stream (integer: canonical digits keep
                 // the 128-bit sums exact for any digit count below 2^8)
@@ -1811,7 +1842,7 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
                 // the input limb of digit I: a canonical ciphertext limb, already NTT form
                 const u64 *src = target + (size_t)I * n + base;
 #pragma unroll
-                for (int e = 0; e < 8; e++) vb[e] = ld_nt<2>(&src[lay(t, e, B_A)]);
+                for (int e = 0; e < 8; e++) vb[e] = ld_nt<2>(&src[lay(t, e, BK)]);
                 load_key(I, ka, kb);
                 T d[8];
 #pragma unroll
@@ -1905,7 +1936,7 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
                                        [&](int e) { return (rbi << s) + (lay(t, e, b_lo) >> (LOGR - s)); });
             };
             auto inv_rows = [&](T (&w)[8]) {
-                tr(w, B_A, 0);
+                if constexpr (BK != 0) tr(w, BK, 0);
                 stages(w, 0, LOGR - 1, LOGR - 3);
                 tr(w, 0, 3);
                 stages(w, 3, LOGR - 4, LOGR > 6 ? LOGR - 6 : 0);
@@ -1941,20 +1972,42 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
             }
             return;
         }
+        u64 c0v[8], c1v[8]; // canonical key products, layout BK
+#pragma unroll
+        for (int e = 0; e < 8; e++)
+        {
+            if constexpr (FPA)
+            {
+                c0v[e] = fp_canon(a0[e], ar.q, ar.qinv);
+                c1v[e] = fp_canon(a1[e], ar.q, ar.qinv);
+            }
+            else
+            {
+                c0v[e] = barrett128(a0[e].lo, a0[e].hi, p);
+                c1v[e] = barrett128(a1[e].lo, a1[e].hi, p);
+            }
+        }
+        if constexpr (BK != B_A)
+        {
+            // one transpose per workgroup to the coalesced layout for the stores
+            u64 *xu = reinterpret_cast<u64 *>(x0);
+            auto back = [&](u64 (&v)[8]) {
+                wave_lds_fence();
+#pragma unroll
+                for (int e = 0; e < 8; e++) xu[swz(lay(t, e, BK))] = v[e];
+                wave_lds_fence();
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = xu[swz(lay(t, e, B_A))];
+            };
+            back(c0v);
+            back(c1v);
+        }
 #pragma unroll
         for (int e = 0; e < 8; e++)
         {
             const u32 r = lay(t, e, B_A);
-            if constexpr (FPA)
-            {
-                o0[r] = fp_canon(a0[e], ar.q, ar.qinv);
-                o1[r] = fp_canon(a1[e], ar.q, ar.qinv);
-            }
-            else
-            {
-                o0[r] = barrett128(a0[e].lo, a0[e].hi, p);
-                o1[r] = barrett128(a1[e].lo, a1[e].hi, p);
-            }
+            o0[r] = c0v[e];
+            o1[r] = c1v[e];
         }
     };
     if constexpr (FP)

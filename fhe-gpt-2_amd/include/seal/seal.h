@@ -747,6 +747,11 @@ bool batched_launches();
 // A healthy run reports 0: the engine's allocation retries and failures are in mhe_alloc_stats.
 std::uint64_t merged_call_fallbacks(bool reset = false);
 
+// (not SEAL API) True when `addr` lies in the guard page below a live seal::FiberBatch fiber stack
+// (a stack overflow).  Reads a lock-free list, so a SIGSEGV handler may call it; FiberBatch::run
+// gives its thread an alternate signal stack for handlers installed with SA_ONSTACK.
+bool fiber_stack_guard(const void *addr);
+
 // (not SEAL API) Lockstep: threads that evaluate the same operation sequence on different data (the
 // images of a batch) join one group.  While joined, every top-level rotation (rotate_vector[s],
 // rotate_vector_inplace), relinearization (relinearize_inplace, and the one inside

@@ -28,6 +28,7 @@
 #include <thread>
 #include <unordered_map>
 
+#include <csignal>
 #include <sys/mman.h>
 #include <ucontext.h>
 #include <unistd.h>
@@ -2296,10 +2297,35 @@ struct Lockstep::Impl
 };
 
 // ------------------------------------------------------------------------------ FiberBatch
+// Guard pages of the live fiber stacks, lock-free so a signal handler may read them.
+static constexpr int kGuardSlots = 4096;
+static std::atomic<std::uintptr_t> g_guards[kGuardSlots];
+static void guard_list(void *page, bool add)
+{
+    const std::uintptr_t a = reinterpret_cast<std::uintptr_t>(page);
+    for (auto &slot : g_guards)
+    {
+        std::uintptr_t want = add ? 0 : a;
+        if (slot.compare_exchange_strong(want, add ? a : 0)) return;
+    }
+}
+
+bool fiber_stack_guard(const void *addr)
+{
+    const std::uintptr_t x = reinterpret_cast<std::uintptr_t>(addr), page = (std::uintptr_t)sysconf(_SC_PAGESIZE);
+    for (const auto &slot : g_guards)
+    {
+        const std::uintptr_t g = slot.load(std::memory_order_relaxed);
+        if (g && x >= g && x < g + page) return true;
+    }
+    return false;
+}
+
 struct FiberBatch::Impl
 {
     // A fiber's stack: mmap'ed, with a PROT_NONE guard page below it (stacks grow down), so an
     // overflow faults at a known address instead of silently corrupting a neighbouring heap block.
+    // Live guard pages are listed in g_guards for fiber_stack_guard (a fault handler's question).
     struct Stack
     {
         void *base = nullptr; // guard page + usable bytes
@@ -2310,7 +2336,9 @@ struct FiberBatch::Impl
         Stack(Stack &&o) noexcept : base(o.base), bytes(o.bytes) { o.base = nullptr; }
         ~Stack()
         {
-            if (base) munmap(base, bytes);
+            if (!base) return;
+            guard_list(base, false);
+            munmap(base, bytes);
         }
         void alloc(std::size_t usable)
         {
@@ -2324,6 +2352,7 @@ struct FiberBatch::Impl
                 throw std::runtime_error("FiberBatch: stack allocation failed");
             }
             if (mprotect(base, page, PROT_NONE) != 0) throw std::runtime_error("FiberBatch: guard page failed");
+            guard_list(base, true);
         }
         char *sp() const { return static_cast<char *>(base) + (bytes - usable()); }
         std::size_t usable() const { return bytes - (std::size_t)sysconf(_SC_PAGESIZE); }
@@ -2432,6 +2461,32 @@ void FiberBatch::run(std::size_t count, const std::function<void(std::size_t)> &
     g.work = &work;
     g.fibers.resize(count);
     for (std::size_t i = 0; i < count; i++) g.init(i, stack_bytes);
+    // an alternate signal stack for this thread (if it has none), so a handler installed with
+    // SA_ONSTACK can still run -- and report -- when a fiber overflows into its guard page
+    struct AltStack
+    {
+        std::vector<char> mem;
+        bool set = false;
+        AltStack()
+        {
+            stack_t cur{};
+            if (sigaltstack(nullptr, &cur) == 0 && (cur.ss_flags & SS_DISABLE))
+            {
+                mem.resize(64 * 1024);
+                stack_t st{};
+                st.ss_sp = mem.data();
+                st.ss_size = mem.size();
+                set = sigaltstack(&st, nullptr) == 0;
+            }
+        }
+        ~AltStack()
+        {
+            if (!set) return;
+            stack_t st{};
+            st.ss_flags = SS_DISABLE;
+            (void)sigaltstack(&st, nullptr);
+        }
+    } alt;
     tl_fb = &g;
     mhe_set_launch_hook(&Impl::launch_hook, &g);
     struct Reset

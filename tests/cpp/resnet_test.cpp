@@ -17,13 +17,18 @@
 #include <random>
 #include <string>
 
-static void on_fault(int sig)
+static void on_fault(int sig, siginfo_t *si, void *)
 {
-    // a host fault (seen only under rocprofv3 so far): print the call stack before dying
+    // a host fault (seen only under rocprofv3 so far): the faulting address, whether it is a fiber
+    // stack's guard page (an overflow), and the call stack, before dying.  Runs on the alternate
+    // signal stack FiberBatch sets up (SA_ONSTACK), so an overflowed fiber stack can still report.
+    char buf[160];
+    const bool guard = seal::fiber_stack_guard(si->si_addr);
+    const int len = std::snprintf(buf, sizeof(buf), "resnet_test: fatal signal %d at address %p (%s), backtrace:\n", sig,
+                                  si->si_addr, guard ? "a fiber stack's guard page: stack overflow" : "not a fiber guard page");
+    (void)!write(2, buf, len > 0 ? (std::size_t)len : 0);
     void *frames[64];
     const int n = backtrace(frames, 64);
-    const char msg[] = "resnet_test: fatal signal, backtrace:\n";
-    (void)!write(2, msg, sizeof(msg) - 1);
     backtrace_symbols_fd(frames, n, 2);
     std::signal(sig, SIG_DFL);
     std::raise(sig);
@@ -128,8 +133,14 @@ static int fibercheck(const ResNetParams &prm, const char *comp_dir, int images,
 
 int main(int argc, char **argv)
 {
-    std::signal(SIGSEGV, on_fault);
-    std::signal(SIGBUS, on_fault);
+    {
+        struct sigaction sa{};
+        sa.sa_sigaction = on_fault;
+        sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+        sigemptyset(&sa.sa_mask);
+        sigaction(SIGSEGV, &sa, nullptr);
+        sigaction(SIGBUS, &sa, nullptr);
+    }
     if (argc < 3)
     {
         std::fprintf(stderr, "usage: resnet_test <params.bin|.d7> <comp_dir> [images (-1: load only)] [layers] [threads]\n");
