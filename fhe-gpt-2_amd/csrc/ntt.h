@@ -1068,6 +1068,10 @@ struct KsPtrs
 #ifndef MHE_MODUP_OCC
 #define MHE_MODUP_OCC 3 // waves per SIMD the ModUp column pass is compiled for (168 VGPRs)
 #endif
+#ifndef MHE_MODUP_WAVE
+#define MHE_MODUP_WAVE 0 // n = 2^16: a column's lanes in one wave, wave-local transposes (k_modup_col);
+                         // with non-temporal stores 8x slower (16-byte store segments, profiles/r06f)
+#endif
 #ifndef MHE_MODUP_TWG
 #define MHE_MODUP_TWG 5 // output primes per group whose twiddles the ModUp column pass stages in LDS
 #endif
@@ -1090,13 +1094,21 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
     using T = typename A::T;
     constexpr int E = SH::E, TPS = SH::TPS, LOGE = SH::LOGE, S = SH::S, LD = SH::LD;
     constexpr int R = SH::R;
-    __shared__ T lds[S * LD];
+    // MHE_MODUP_WAVE (n = 2^16, 16 lanes per column): a column's 16 lanes are consecutive lanes of
+    // one wave (4 columns per wave) instead of one lane in each of 16 waves' worth of rows, so the
+    // transpose between the two register phases stays inside the wave: no workgroup barrier per
+    // output prime (round 5: two, a third of the kernel's wave time waiting).  The column's LDS image
+    // is unpadded and XOR-skewed (wslot): conflict-free for the transpose's ds_write_b64 (one column's
+    // 16 lanes) and ds_read_b64 (two columns' 32 lanes) under MI355X_MICROARCH.md §LDS's bank rules.
+    constexpr bool WV = MHE_MODUP_WAVE && LOGR == 8 && TPS == 16;
+    __shared__ T lds[WV ? S * R : S * LD];
+    auto wslot = [](int col, int r) { return col * R + ((r ^ ((r >> 4) & 15)) ^ ((col & 1) << 4)); };
     // The column-pass twiddles of the group's output primes (entries 1 .. R-1 of each prime's table,
     // the same for every column), staged once per workgroup.  Read from global memory stage by stage
     // instead, each twiddle load's s_waitcnt also waited for the previous prime's stores (one
     // counter for loads and stores), so compute and stores of consecutive primes never overlapped.
     __shared__ Tw twc[MHE_MODUP_TWG > 0 ? MHE_MODUP_TWG * R : 1];
-    const int tid = threadIdx.x, sl = tid % S, t = tid / S;
+    const int tid = threadIdx.x, sl = WV ? tid / TPS : tid % S, t = WV ? tid % TPS : tid / S;
     const int logC = log_n - LOGR;
     // 1-D grid of X column blocks x L digits x IG output-prime groups.  xcd: the IG groups of one
     // (column block, digit) get ids i, i + 8, ..., i + 8 (IG - 1) -- workgroups are dealt to the 8
@@ -1197,11 +1209,28 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
                 for (int s = 0; s < LOGE; s++)
                     ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
             }
+            if constexpr (WV)
+            {
+                // wslot is XOR-linear in e: row t + 16e sits at wslot(sl, t) ^ 17e, row 16t + e at
+                // wslot(sl, 16t) ^ e; the two bases go through an empty asm each output prime so the
+                // 32 slots are recomputed (one v_xor each) rather than hoisted into 32 VGPRs
+                u32 wb = (u32)wslot(sl, t), rb = (u32)wslot(sl, 16 * t);
+                asm volatile("" : "+v"(wb), "+v"(rb));
+                wave_lds_fence(); // the previous output prime's reads of this column come first
 #pragma unroll
-            for (int e = 0; e < E; e++) lds_v[sl * LD + t + TPS * e] = v[e];
-            lds_barrier(); // LDS only: the previous output prime's stores stay in flight
+                for (int e = 0; e < E; e++) lds_v[wb ^ (17u * e)] = v[e];
+                wave_lds_fence();
 #pragma unroll
-            for (int e = 0; e < E; e++) v[e] = lds_v[sl * LD + E * t + e];
+                for (int e = 0; e < E; e++) v[e] = lds_v[rb ^ (u32)e];
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < E; e++) lds_v[sl * LD + t + TPS * e] = v[e];
+                lds_barrier(); // LDS only: the previous output prime's stores stay in flight
+#pragma unroll
+                for (int e = 0; e < E; e++) v[e] = lds_v[sl * LD + E * t + e];
+            }
             if (twl_on)
             {
 #pragma unroll
@@ -1260,7 +1289,7 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
 #pragma unroll
                 for (int e = 0; e < E; e++) st_nt<0>(d0 + (size_t)e * stride, ar.out(v[e]));
             }
-            lds_barrier(); // lds is rewritten by the next output prime (its stores need not land)
+            if constexpr (!WV) lds_barrier(); // lds is rewritten by the next output prime (its stores need not land)
         }
     };
     if constexpr (FP)
