@@ -29,6 +29,7 @@ struct PrimeDev
     u64 ninv_q;   // Shoup quotient of ninv
     u64 last_w;   // psi^-1 (itw[1]) * n^-1 mod q: last INTT stage twiddle (dwthandler.h:273-314)
     u64 last_wq;
+    double qd, qi; // q and fl(1/q) as doubles: the elementwise kernels' FP64 products (q < 2^51)
 };
 
 // 64-bit products built only from v_mad_u64_u32 (32x32+64 -> 64), which gfx950 issues at

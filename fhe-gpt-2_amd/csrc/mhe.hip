@@ -1006,6 +1006,24 @@ struct JobStrided
 // Elementwise kernels process 2 residues per lane (16-B loads); n is a multiple of 512.
 #define ELEM_GRID(total2) dim3((unsigned)(((total2) + 255) / 256))
 
+// Elementwise products in FP64 (csrc/fparith.h) for primes below 2^51, where the integer path's
+// 64 x 64 -> 128-bit product and Barrett reduction cost several half- and quarter-rate instructions:
+// canonical residues are exact doubles, fp_mulmod_gen leaves a*b mod q in (-1.25q, 1.25q) and
+// fp_canon returns the canonical residue, so the words are the integer path's.  fp: the context's
+// FP64 mode (MHE_FP=0 keeps every product on the integer path).
+__device__ __forceinline__ bool elem_fp(int fp, const PrimeDev &p)
+{
+    return fp && p.q < (1ull << 51);
+}
+__device__ __forceinline__ double mulmod_fd(u64 a, u64 b, const PrimeDev &p) // (-1.25q, 1.25q)
+{
+    return fp_mulmod_gen(fp_from_u52(a), fp_from_u52(b), p.qd, p.qi);
+}
+__device__ __forceinline__ u64 mulmod_e(u64 a, u64 b, const PrimeDev &p, bool f)
+{
+    return f ? fp_canon(mulmod_fd(a, b, p), p.qd, p.qi) : mulmod(a, b, p);
+}
+
 __device__ __forceinline__ void addsub_at(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs,
                                           int log_n, size_t i2, int op)
 {
@@ -1043,30 +1061,31 @@ __global__ void k_addsub(const u64 *a, const u64 *b, u64 *out, const PrimeDev *p
 
 // dyadic product with b broadcast over polys (multiply_plain_ntt)
 __device__ __forceinline__ void mulplain_at(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs,
-                                            int log_n, size_t i2)
+                                            int log_n, size_t i2, int fp)
 {
     const size_t i = i2 * 2;
     const size_t limb_words = (size_t)limbs << log_n;
     const int l = (int)((i >> log_n) % limbs);
     const PrimeDev p = primes[l];
+    const bool f = elem_fp(fp, p); // uniform: a wave's residues are of one limb
     ulonglong2 x = *(const ulonglong2 *)(a + i);
     ulonglong2 y = *(const ulonglong2 *)(b + i % limb_words);
     ulonglong2 r;
-    r.x = mulmod(x.x, y.x, p);
-    r.y = mulmod(x.y, y.y, p);
+    r.x = mulmod_e(x.x, y.x, p, f);
+    r.y = mulmod_e(x.y, y.y, p, f);
     *(ulonglong2 *)(out + i) = r;
 }
 
 __global__ void k_mulplain(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
-                           size_t total2)
+                           size_t total2, int fp)
 {
     size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 < total2) mulplain_at(a, b, out, primes, limbs, log_n, i2);
+    if (i2 < total2) mulplain_at(a, b, out, primes, limbs, log_n, i2, fp);
 }
 
 // acc += a * b, b broadcast over polys (multiply_plain_ntt then add_inplace, one pass)
 __device__ __forceinline__ void mulplain_add_at(const u64 *a, const u64 *b, u64 *acc, const PrimeDev *primes,
-                                                int limbs, int log_n, size_t i2)
+                                                int limbs, int log_n, size_t i2, int fp)
 {
     const size_t i = i2 * 2;
     const size_t limb_words = (size_t)limbs << log_n;
@@ -1076,16 +1095,25 @@ __device__ __forceinline__ void mulplain_add_at(const u64 *a, const u64 *b, u64 
     ulonglong2 y = *(const ulonglong2 *)(b + i % limb_words);
     ulonglong2 z = *(const ulonglong2 *)(acc + i);
     ulonglong2 r;
-    r.x = addmod(z.x, mulmod(x.x, y.x, p), p.q);
-    r.y = addmod(z.y, mulmod(x.y, y.y, p), p.q);
+    if (elem_fp(fp, p))
+    {
+        // canonical acc (< q) + a product in (-1.25q, 1.25q): |.| < 2.25q, exact
+        r.x = fp_canon(fp_from_u52(z.x) + mulmod_fd(x.x, y.x, p), p.qd, p.qi);
+        r.y = fp_canon(fp_from_u52(z.y) + mulmod_fd(x.y, y.y, p), p.qd, p.qi);
+    }
+    else
+    {
+        r.x = addmod(z.x, mulmod(x.x, y.x, p), p.q);
+        r.y = addmod(z.y, mulmod(x.y, y.y, p), p.q);
+    }
     *(ulonglong2 *)(acc + i) = r;
 }
 
 __global__ void k_mulplain_add(const u64 *a, const u64 *b, u64 *acc, const PrimeDev *primes, int limbs, int log_n,
-                               size_t total2)
+                               size_t total2, int fp)
 {
     size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 < total2) mulplain_add_at(a, b, acc, primes, limbs, log_n, i2);
+    if (i2 < total2) mulplain_add_at(a, b, acc, primes, limbs, log_n, i2, fp);
 }
 
 // acc = (accumulate ? acc : 0) + sum_k a_k * b_k, up to 16 terms per launch (pointers in the kernel
@@ -1097,7 +1125,7 @@ struct SumPtrs
     const u64 *b[MHE_SUM_TERMS];
 };
 __global__ void k_mulplain_sum(SumPtrs P, int cnt, u64 *acc, int accumulate, const PrimeDev *primes, int limbs,
-                               int log_n, size_t total2)
+                               int log_n, size_t total2, int fp)
 {
     size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i2 >= total2) return;
@@ -1106,12 +1134,35 @@ __global__ void k_mulplain_sum(SumPtrs P, int cnt, u64 *acc, int accumulate, con
     const int l = (int)((i >> log_n) % limbs);
     const PrimeDev p = primes[l];
     ulonglong2 z = accumulate ? *(const ulonglong2 *)(acc + i) : ulonglong2{ 0, 0 };
-    for (int k = 0; k < cnt; k++)
+    if (elem_fp(fp, p))
     {
-        const ulonglong2 x = *(const ulonglong2 *)(P.a[k] + i);
-        const ulonglong2 y = *(const ulonglong2 *)(P.b[k] + i % limb_words);
-        z.x = addmod(z.x, mulmod(x.x, y.x, p), p.q);
-        z.y = addmod(z.y, mulmod(x.y, y.y, p), p.q);
+        // FP64 sums: products in (-1.25q, 1.25q), centred by fp_reduce after every second one, so
+        // |sum| < q/2 + 1 + 2.5q < 2^53 throughout; one fp_canon at the end
+        double sx = fp_from_u52(z.x), sy = fp_from_u52(z.y);
+        for (int k = 0; k < cnt; k++)
+        {
+            const ulonglong2 x = *(const ulonglong2 *)(P.a[k] + i);
+            const ulonglong2 y = *(const ulonglong2 *)(P.b[k] + i % limb_words);
+            sx += mulmod_fd(x.x, y.x, p);
+            sy += mulmod_fd(x.y, y.y, p);
+            if (k & 1)
+            {
+                sx = fp_reduce(sx, p.qd, p.qi);
+                sy = fp_reduce(sy, p.qd, p.qi);
+            }
+        }
+        z.x = fp_canon(sx, p.qd, p.qi);
+        z.y = fp_canon(sy, p.qd, p.qi);
+    }
+    else
+    {
+        for (int k = 0; k < cnt; k++)
+        {
+            const ulonglong2 x = *(const ulonglong2 *)(P.a[k] + i);
+            const ulonglong2 y = *(const ulonglong2 *)(P.b[k] + i % limb_words);
+            z.x = addmod(z.x, mulmod(x.x, y.x, p), p.q);
+            z.y = addmod(z.y, mulmod(x.y, y.y, p), p.q);
+        }
     }
     *(ulonglong2 *)(acc + i) = z;
 }
@@ -1158,7 +1209,7 @@ __global__ void k_scalar(const u64 *a, u64 *out, const PrimeDev *primes, ScalarT
 
 // ckks_multiply tile loop (evaluator.cpp:714-773) / ckks_square (:1000-1059), fused.
 __device__ __forceinline__ void tensor_at(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs,
-                                          int log_n, size_t i2, int square)
+                                          int log_n, size_t i2, int square, int fp)
 {
     const size_t i = i2 * 2;
     const size_t ps = (size_t)limbs << log_n;
@@ -1166,7 +1217,19 @@ __device__ __forceinline__ void tensor_at(const u64 *a, const u64 *b, u64 *out, 
     const PrimeDev p = primes[l];
     ulonglong2 x0 = *(const ulonglong2 *)(a + i), x1 = *(const ulonglong2 *)(a + ps + i);
     ulonglong2 r0, r1, r2;
-    if (square)
+    if (elem_fp(fp, p))
+    {
+        // FP64: each product in (-1.25q, 1.25q), the cross term's two in (-2.5q, 2.5q), exact
+        const ulonglong2 y0 = square ? x0 : *(const ulonglong2 *)(b + i), y1 = square ? x1 : *(const ulonglong2 *)(b + ps + i);
+        const double qd = p.qd, qi = p.qi;
+        r0.x = fp_canon(mulmod_fd(x0.x, y0.x, p), qd, qi);
+        r0.y = fp_canon(mulmod_fd(x0.y, y0.y, p), qd, qi);
+        r1.x = fp_canon(mulmod_fd(x0.x, y1.x, p) + mulmod_fd(x1.x, y0.x, p), qd, qi);
+        r1.y = fp_canon(mulmod_fd(x0.y, y1.y, p) + mulmod_fd(x1.y, y0.y, p), qd, qi);
+        r2.x = fp_canon(mulmod_fd(x1.x, y1.x, p), qd, qi);
+        r2.y = fp_canon(mulmod_fd(x1.y, y1.y, p), qd, qi);
+    }
+    else if (square)
     {
         r0.x = mulmod(x0.x, x0.x, p);
         r0.y = mulmod(x0.y, x0.y, p);
@@ -1192,10 +1255,10 @@ __device__ __forceinline__ void tensor_at(const u64 *a, const u64 *b, u64 *out, 
 }
 
 __global__ void k_tensor(const u64 *a, const u64 *b, u64 *out, const PrimeDev *primes, int limbs, int log_n,
-                         size_t total2, int square)
+                         size_t total2, int square, int fp)
 {
     size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (i2 < total2) tensor_at(a, b, out, primes, limbs, log_n, i2, square);
+    if (i2 < total2) tensor_at(a, b, out, primes, limbs, log_n, i2, square, fp);
 }
 
 // The same elementwise kernels over up to MHE_MAXB entries of one shape (entry = blockIdx.y): the
@@ -1209,7 +1272,7 @@ struct ElemPtrs
 };
 
 __global__ void k_elem_b(ElemPtrs P, const PrimeDev *primes, ScalarTab st, int limbs, int log_n, size_t total2,
-                         int kind, int op)
+                         int kind, int op, int fp)
 {
     const size_t i2 = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i2 >= total2) return;
@@ -1217,10 +1280,10 @@ __global__ void k_elem_b(ElemPtrs P, const PrimeDev *primes, ScalarTab st, int l
     switch (kind)
     {
     case MHE_LK_ADDSUB: addsub_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2, op); break;
-    case MHE_LK_MULPLAIN: mulplain_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2); break;
-    case MHE_LK_MULPLAIN_ADD: mulplain_add_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2); break;
+    case MHE_LK_MULPLAIN: mulplain_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2, fp); break;
+    case MHE_LK_MULPLAIN_ADD: mulplain_add_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2, fp); break;
     case MHE_LK_SCALAR: scalar_at(P.a[e], P.out[e], primes, st, limbs, log_n, i2, op); break;
-    case MHE_LK_TENSOR: tensor_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2, op); break;
+    case MHE_LK_TENSOR: tensor_at(P.a[e], P.b[e], P.out[e], primes, limbs, log_n, i2, op, fp); break;
     }
 }
 
@@ -2029,6 +2092,8 @@ MHE_EXPORT int mhe_ctx_create(mhe_ctx **out, int log_n, const uint64_t *moduli, 
         p.q = q;
         p.two_q = 2 * q;
         p.four_q = 4 * q;
+        p.qd = (double)q;
+        p.qi = 1.0 / (double)q;
         u128 ratio = (~(u128)0) / q;
         p.r0 = (u64)ratio;
         p.r1 = (u64)(ratio >> 64);
@@ -2464,7 +2529,7 @@ MHE_EXPORT int mhe_launch_run(mhe_ctx *c, mhe_launch *const *ls, int count)
             count_op(c, opk, l0.limbs, (unsigned long long)B * (l0.kind == MHE_LK_TENSOR ? 1 : l0.polys));
             if (l0.kind == MHE_LK_MULPLAIN_ADD) count_op(c, MHE_OPK_ADDSUB, l0.limbs, (unsigned long long)B * l0.polys);
             hipLaunchKernelGGL(k_elem_b, dim3(ELEM_GRID(total2).x, (unsigned)B), dim3(256), 0, st, P, c->primes, t,
-                               l0.limbs, c->log_n, total2, l0.kind, l0.op);
+                               l0.limbs, c->log_n, total2, l0.kind, l0.op, c->nm.fp ? 1 : 0);
         }
         const hipError_t e = hipGetLastError();
         const int rc = e == hipSuccess ? MHE_OK : fail(MHE_ERR_DEVICE, hipGetErrorString(e));
@@ -2912,7 +2977,7 @@ MHE_EXPORT int mhe_multiply_plain(mhe_ctx *c, const uint64_t *a, const uint64_t 
     count_op(c, MHE_OPK_MULPLAIN, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_mulplain, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, out, c->primes, limbs, c->log_n,
-                       total2);
+                       total2, c->nm.fp ? 1 : 0);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }
@@ -2938,7 +3003,7 @@ MHE_EXPORT int mhe_multiply_plain_add(mhe_ctx *c, const uint64_t *a, const uint6
     count_op(c, MHE_OPK_ADDSUB, limbs, (unsigned long long)polys);
     size_t total2 = ((size_t)polys * limbs << c->log_n) / 2;
     hipLaunchKernelGGL(k_mulplain_add, ELEM_GRID(total2), dim3(256), 0, S(s), a, b, acc, c->primes, limbs, c->log_n,
-                       total2);
+                       total2, c->nm.fp ? 1 : 0);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }
@@ -2966,7 +3031,7 @@ MHE_EXPORT int mhe_multiply_plain_sum(mhe_ctx *c, int count, const uint64_t *con
             P.b[k] = b[k0 + k];
         }
         hipLaunchKernelGGL(k_mulplain_sum, ELEM_GRID(total2), dim3(256), 0, S(s), P, cnt, out,
-                           (accumulate || k0 > 0) ? 1 : 0, c->primes, limbs, c->log_n, total2);
+                           (accumulate || k0 > 0) ? 1 : 0, c->primes, limbs, c->log_n, total2, c->nm.fp ? 1 : 0);
         HIP_LAUNCH_CHECK();
     }
     return MHE_OK;
@@ -3031,7 +3096,7 @@ static int launch_tensor(mhe_ctx *c, const u64 *a, const u64 *b, u64 *out3, int 
     count_op(c, MHE_OPK_TENSOR, L, 1);
     size_t total2 = ((size_t)L << c->log_n) / 2;
     hipLaunchKernelGGL(k_tensor, ELEM_GRID(total2), dim3(256), 0, st, a, b, out3, c->primes, L, c->log_n, total2,
-                       square);
+                       square, c->nm.fp ? 1 : 0);
     HIP_LAUNCH_CHECK();
     return MHE_OK;
 }

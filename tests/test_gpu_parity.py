@@ -155,6 +155,36 @@ def test_multiply_plain_sum(small, terms):
     assert np.array_equal(got2, ch.oc.add(acc, want))
 
 
+@pytest.mark.parametrize("env", [{}, {"MHE_FP": "0"}], ids=["fp64", "integer"])
+def test_elementwise_products_both_paths(env):
+    """The elementwise products -- multiply_plain, the multi-term product sum (past 16 terms,
+    accumulating), ckks_multiply / ckks_square -- in the FP64 path (primes below 2^51, round 6) and
+    the integer path (MHE_FP=0), on residues that include 0 and q - 1 in every limb: bit-identical to
+    the oracle both ways."""
+    ch = _variant_chain(env, 91)
+    L = ch.K - 1
+    qs = np.array(ch.moduli[:L], np.uint64)
+
+    a, b = ch.rand(2, L, ch.n), ch.rand(2, L, ch.n)
+    for x in (a, b):
+        x[:, :, 0] = 0
+        x[:, :, 1] = (qs - np.uint64(1))[None, :]
+    pt = ch.rand(L, ch.n)
+    pt[:, 1] = qs - np.uint64(1)
+    assert np.array_equal(ch.down(ch.eng.multiply_plain(ch.up(a), ch.up(pt))), ch.oc.multiply_plain(a, pt))
+    assert np.array_equal(ch.down(ch.eng.multiply(ch.up(a), ch.up(b))), ch.oc.multiply(a, b))
+    assert np.array_equal(ch.down(ch.eng.square(ch.up(a))), ch.oc.square(a))
+    cts = [a if k % 2 else b for k in range(18)]
+    pts = [pt] * 18
+    want = ch.oc.multiply_plain(cts[0], pts[0])
+    for c, p in zip(cts[1:], pts[1:]):
+        want = ch.oc.add(want, ch.oc.multiply_plain(c, p))
+    acc = b.copy()
+    got = ch.down(ch.eng.multiply_plain_sum([ch.up(c) for c in cts], [ch.up(p) for p in pts], out=ch.up(acc),
+                                            accumulate=True))
+    assert np.array_equal(got, ch.oc.add(acc, want))
+
+
 def test_multiply_add_scalar(small):
     ch = small
     L = ch.K - 1
