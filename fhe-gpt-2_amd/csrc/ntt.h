@@ -1072,6 +1072,9 @@ struct KsPtrs
 #define MHE_MODUP_WAVE 0 // n = 2^16: a column's lanes in one wave, wave-local transposes (k_modup_col);
                          // with non-temporal stores 8x slower (16-byte store segments, profiles/r06f)
 #endif
+#ifndef MHE_MODUP_PING
+#define MHE_MODUP_PING 1 // n = 2^16: alternate two LDS images per output prime, one barrier per prime (k_modup_col)
+#endif
 #ifndef MHE_MODUP_TWG
 #define MHE_MODUP_TWG 5 // output primes per group whose twiddles the ModUp column pass stages in LDS
 #endif
@@ -1101,7 +1104,25 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
     // is unpadded and XOR-skewed (wslot): conflict-free for the transpose's ds_write_b64 (one column's
     // 16 lanes) and ds_read_b64 (two columns' 32 lanes) under MI355X_MICROARCH.md §LDS's bank rules.
     constexpr bool WV = MHE_MODUP_WAVE && LOGR == 8 && TPS == 16;
-    __shared__ T lds[WV ? S * R : S * LD];
+    // MHE_MODUP_PING (n = 2^16): the transpose's LDS image alternates between two placements from
+    // one output prime to the next.  Prime k writes row t + 16e of its column at the slot the same
+    // lane read row 16t + e from in prime k - 1, and reads row 16t + e from the slot it wrote row
+    // t + 16e to in prime k - 1: every slot a lane overwrites was last read by that lane itself, so
+    // the barrier after each prime's reads (round 5: two barriers per prime) is not needed.  The
+    // placements are the padded image (column sl at sl * LD) with the two roles of t and e swapped, so
+    // both address patterns stay a lane base plus immediates and the LDS size (occupancy: 3 workgroups
+    // per CU, one more element per column already drops it to 2, profiles/r06k) is unchanged.  Banks
+    // (MI355X_MICROARCH.md §LDS): the writes are conflict-free either way (16 lanes, sl = 0..15); the
+    // reads of rows 16t + e from the swapped placement (element sl * 257 + t + 16e) are 2-way
+    // conflicted, on every second output prime.
+    constexpr bool PG = !WV && MHE_MODUP_PING && LOGR == 8 && TPS == 16;
+#ifndef MHE_MODUP_LDS_EXTRA
+#define MHE_MODUP_LDS_EXTRA 0 // A/B only: extra elements in the LDS image (occupancy probe)
+#endif
+#ifndef MHE_MODUP_PING_BAR
+#define MHE_MODUP_PING_BAR 0 // A/B only: keep the end-of-prime barrier with the ping-pong image
+#endif
+    __shared__ T lds[(WV ? S * R : S * LD) + MHE_MODUP_LDS_EXTRA];
     auto wslot = [](int col, int r) { return col * R + ((r ^ ((r >> 4) & 15)) ^ ((col & 1) << 4)); };
     // The column-pass twiddles of the group's output primes (entries 1 .. R-1 of each prime's table,
     // the same for every column), staged once per workgroup.  Read from global memory stage by stage
@@ -1163,6 +1184,9 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
 #pragma unroll
         for (int e = 0; e < E; e++) xd[e] = fp_from_u52(x[e]); // canonical INTT output
     }
+    // PG: the two lane bases, pa + 16e and pb + e
+    const u32 pa = (u32)(sl * LD + t), pb = (u32)(sl * LD + 16 * t);
+    int ph = 0; // PG: placement of the next output prime (uniform), carried across the sweeps
     // two sweeps over the group's output primes when FP: first the q < 2^47 ones with the lazy
     // forward butterflies, then the rest, so each loop body has one arithmetic variant
     auto sweep = [&](auto mode) {
@@ -1222,6 +1246,30 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
                 wave_lds_fence();
 #pragma unroll
                 for (int e = 0; e < E; e++) v[e] = lds_v[rb ^ (u32)e];
+            }
+            else if constexpr (PG)
+            {
+                // the asm markers keep the two read sequences apart: merged, they took their offsets
+                // from SGPRs, one v_add per read
+                if (!ph)
+                {
+#pragma unroll
+                    for (int e = 0; e < E; e++) lds_v[pa + 16 * e] = v[e];
+                    lds_barrier(); // LDS only: the previous output prime's stores stay in flight
+#pragma unroll
+                    for (int e = 0; e < E; e++) v[e] = lds_v[pb + e];
+                    asm volatile("; modup placement 0");
+                }
+                else
+                {
+#pragma unroll
+                    for (int e = 0; e < E; e++) lds_v[pb + e] = v[e];
+                    lds_barrier();
+#pragma unroll
+                    for (int e = 0; e < E; e++) v[e] = lds_v[pa + 16 * e];
+                    asm volatile("; modup placement 1");
+                }
+                ph ^= 1;
             }
             else
             {
@@ -1289,7 +1337,7 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
 #pragma unroll
                 for (int e = 0; e < E; e++) st_nt<0>(d0 + (size_t)e * stride, ar.out(v[e]));
             }
-            if constexpr (!WV) lds_barrier(); // lds is rewritten by the next output prime (its stores need not land)
+            if constexpr (!WV && (!PG || MHE_MODUP_PING_BAR)) lds_barrier(); // lds is rewritten by the next output prime (its stores need not land)
         }
     };
     if constexpr (FP)
@@ -1561,14 +1609,19 @@ __device__ __forceinline__ void row_stages(typename A::T (&v)[8], u32 t, int b_l
 
 template <int LOGR, bool FP, bool MIX = false>
 #ifndef MHE_KS_OCC
-#define MHE_KS_OCC 2 // waves per SIMD the FP64 fused MAC at n = 2^16 is compiled for (3: 168 VGPRs, one
-                     // LDS transpose buffer; equal on the C2 bench, 2 % slower on single key switches, r06c)
+#define MHE_KS_OCC 3 // waves per SIMD the FP64 fused MAC at n = 2^16 is compiled for: 168 VGPRs, one LDS
+                     // transpose buffer (48 KB).  With the loads at the top of each digit (MHE_KS_SB)
+                     // C2's k_ks_row_mac 2743 -> 2698 us, ResNet-level ops equal (profiles/r06n); without
+                     // them 3 waves were equal on C2 and 2 % slower on single key switches (r06c)
 #endif
 #ifndef MHE_KS_PP
 #define MHE_KS_PP 0 // digit loop unrolled twice, prefetched digit in alternating registers
 #endif
 #ifndef MHE_KS_KPF
 #define MHE_KS_KPF 0 // key limbs loaded one digit ahead too (32 VGPRs more)
+#endif
+#ifndef MHE_KS_SB
+#define MHE_KS_SB 1 // digit loop: key and next-digit loads issued at the top of the step (sched_barrier)
 #endif
 #ifndef MHE_KS_FL
 #define MHE_KS_FL 1 // keys and accumulators in the row transform's last layout (no transpose back per digit)
@@ -1901,6 +1954,11 @@ __global__ __launch_bounds__(256, (FP && !MIX && LOGR == 8) ? MHE_KS_OCC : 2) vo
             auto step = [&](int u, const u64 (&cur)[8], u64 (&nxt)[8]) {
                 load_key(digit_of(u), ka, kb);
                 load_inter(digit_of(u + 1 < nd ? u + 1 : u), nxt); // one digit ahead
+                // issue both streams before the digit's transform: left to the scheduler, they went
+                // out a quarter into it and the copy of the prefetched digit at the end of the step
+                // waited for them (vmcnt(0)).  FP64 without MIX only: the integer and MIX variants
+                // spill already and spilled more
+                if constexpr (MHE_KS_SB && FP && !MIX) __builtin_amdgcn_sched_barrier(0);
                 T d[8];
                 ntt_digit(cur, d);
                 mac(d, ka, kb, ((u + c0) & 1) != 0);
