@@ -32,6 +32,32 @@ struct PrimeDev
     double qd, qi; // q and fl(1/q) as doubles: the elementwise kernels' FP64 products (q < 2^51)
 };
 
+// Table reads through the constant address space: with a uniform index they become scalar loads.  A
+// kernel that also stores makes the compiler read a table behind a plain pointer with vector loads,
+// and their s_waitcnt vmcnt also waits for every store in flight (one counter for both): in a column
+// pass's output-prime loop, each prime's setup waited for the previous prime's stores.  The tables
+// (primes, inverse factors) are never written while a kernel runs.
+typedef const __attribute__((address_space(4))) u64 *const_u64_p;
+static_assert(sizeof(PrimeDev) % 8 == 0, "PrimeDev is read as 64-bit words");
+__device__ __forceinline__ PrimeDev prime_at(const PrimeDev *t, int i)
+{
+    constexpr int W = (int)(sizeof(PrimeDev) / 8);
+    const const_u64_p w = (const_u64_p)t + (size_t)i * W;
+    PrimeDev r;
+    u64 *d = reinterpret_cast<u64 *>(&r);
+#pragma unroll
+    for (int k = 0; k < W; k++) d[k] = w[k];
+    return r;
+}
+__device__ __forceinline__ Tw tw_at(const Tw *t, size_t i)
+{
+    const const_u64_p w = (const_u64_p)t + 2 * i;
+    Tw r;
+    r.x = w[0];
+    r.y = w[1];
+    return r;
+}
+
 // 64-bit products built only from v_mad_u64_u32 (32x32+64 -> 64), which gfx950 issues at
 // half rate.  The default lowering of u64 '*' and __umul64hi uses v_mul_lo_u32 / v_mul_hi_u32,
 // which are quarter rate (measured: scripts/ubench_valu.hip, DESIGN.md "Arithmetic"), and

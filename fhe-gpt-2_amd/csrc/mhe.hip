@@ -503,9 +503,9 @@ struct JobModUpCol
         View v;
         v.src = coeff + ((size_t)J << log_n);
         v.dst = modup + ((size_t)y << log_n);
-        v.p = primes[pi];
+        v.p = prime_at(primes, pi);
         v.tw = tw + ((size_t)pi << log_n);
-        v.reduce = primes[J].q > v.p.q; // key_modulus[J] <= key_modulus[key_index] -> copy
+        v.reduce = prime_at(primes, J).q > v.p.q; // key_modulus[J] <= key_modulus[key_index] -> copy
         v.skip = (I == J);
         return v;
     }
@@ -531,7 +531,7 @@ struct JobModUpRow
     {
         const int I = I0 + y / L, J = y % L;
         const int pi = (I == L) ? K - 1 : I;
-        return View{ modup + ((size_t)y << log_n), primes[pi], tw + ((size_t)pi << log_n), I == J };
+        return View{ modup + ((size_t)y << log_n), prime_at(primes, pi), tw + ((size_t)pi << log_n), I == J };
     }
 };
 
@@ -566,7 +566,7 @@ struct JobModUpRowH
         const int I = y / L, J = y % L;
         const int pi = (I == L) ? K - 1 : I;
         const size_t off = (size_t)y << log_n;
-        return View{ src + off, dst + off, primes[pi], tw + ((size_t)pi << log_n), I == J };
+        return View{ src + off, dst + off, prime_at(primes, pi), tw + ((size_t)pi << log_n), I == J };
     }
 };
 
@@ -608,8 +608,8 @@ struct JobModDownCol
         View v;
         v.src = acc + ((size_t)(k * (L + 1) + L) << log_n);
         v.dst = scratch + ((size_t)y << log_n);
-        v.p = primes[i];
-        v.P = primes[K - 1];
+        v.p = prime_at(primes, i);
+        v.P = prime_at(primes, K - 1);
         v.tw = tw + ((size_t)i << log_n);
         v.half = v.P.q >> 1;
         v.fix = v.p.q - barrett64(v.half, v.p);
@@ -671,9 +671,9 @@ struct JobModDownRow
         v.buf = scratch + ((size_t)y << log_n);
         v.accp = acc + ((size_t)(k * (L + 1) + i) << log_n);
         v.ctp = ct + ((size_t)(k * L + i) << log_n);
-        v.p = primes[i];
+        v.p = prime_at(primes, i);
         v.tw = tw + ((size_t)i << log_n);
-        v.inv = invq[(size_t)(K - 1) * K + i];
+        v.inv = tw_at(invq, (size_t)(K - 1) * K + i);
         v.skip = false;
         v.replace = c1_write && k == 1;
         v.fp = fp != 0;
@@ -720,8 +720,8 @@ struct JobRescaleCol
         View v;
         v.src = last + ((size_t)s << log_n);
         v.dst = scratch + ((size_t)y << log_n);
-        v.p = primes[i];
-        v.ql = primes[L - 1].q;
+        v.p = prime_at(primes, i);
+        v.ql = prime_at(primes, L - 1).q;
         v.half = v.ql >> 1;
         v.neg_half = v.p.q - barrett64(v.half, v.p);
         v.tw = tw + ((size_t)i << log_n);
@@ -770,9 +770,9 @@ struct JobRescaleRow
         v.buf = scratch + ((size_t)y << log_n);
         v.inp = in + ((size_t)(s * L + i) << log_n);
         v.outp = out + ((size_t)(s * (L - 1) + i) << log_n);
-        v.p = primes[i];
+        v.p = prime_at(primes, i);
         v.tw = tw + ((size_t)i << log_n);
-        v.inv = invq[(size_t)(L - 1) * K + i];
+        v.inv = tw_at(invq, (size_t)(L - 1) * K + i);
         v.skip = false;
         v.fp = fp != 0;
         v.pd = (double)v.p.q;
@@ -850,14 +850,14 @@ struct JobMDRCol
         v.accP = acc + ((size_t)(k * (L + 1) + L) << log_n);
         v.lastp = last + ((size_t)k << log_n);
         v.dst = scratch + ((size_t)y << log_n);
-        v.p = primes[i];
-        v.P = primes[K - 1];
+        v.p = prime_at(primes, i);
+        v.P = prime_at(primes, K - 1);
         v.tw = tw + ((size_t)i << log_n);
-        v.pinv = invq[(size_t)(K - 1) * K + i];
+        v.pinv = tw_at(invq, (size_t)(K - 1) * K + i);
         v.halfP = v.P.q >> 1;
         v.fixP = v.p.q - barrett64(v.halfP, v.p);
         v.redP = v.P.q > v.p.q;
-        v.ql = primes[L - 1].q;
+        v.ql = prime_at(primes, L - 1).q;
         v.halfL = v.ql >> 1;
         v.neg_halfL = v.p.q - barrett64(v.halfL, v.p);
         v.redL = v.p.q < v.ql;
@@ -922,10 +922,10 @@ struct JobMDRRow
         v.accp = acc + ((size_t)(k * (L + 1) + i) << log_n);
         v.ctp = ct + ((size_t)(k * L + i) << log_n);
         v.outp = out + ((size_t)(k * (L - 1) + i) << log_n);
-        v.p = primes[i];
+        v.p = prime_at(primes, i);
         v.tw = tw + ((size_t)i << log_n);
-        v.pinv = invq[(size_t)(K - 1) * K + i];
-        v.qlinv = invq[(size_t)(L - 1) * K + i];
+        v.pinv = tw_at(invq, (size_t)(K - 1) * K + i);
+        v.qlinv = tw_at(invq, (size_t)(L - 1) * K + i);
         v.skip = false;
         v.fp = fp != 0;
         v.pd = (double)v.p.q;
@@ -961,7 +961,7 @@ struct JobLastInv
         View v;
         v.src = in + ((size_t)(y * L + (L - 1)) << log_n);
         v.dst = last + ((size_t)y << log_n);
-        v.p = primes[L - 1];
+        v.p = prime_at(primes, L - 1);
         v.tw = itw + ((size_t)(L - 1) << log_n);
         v.lazy = lazy;
         v.skip = false;

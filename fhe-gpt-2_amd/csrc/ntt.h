@@ -832,6 +832,16 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long t
 // finishes the INTT of its columns once (canonical), then for each output prime lifts (the job's
 // View::lift) and runs the forward column stages: the separate inverse-column launch and its HBM
 // round trip disappear, and the outputs are the same words.
+// q < 2^47 (the lazy forward butterflies) as a scalar compare of the high word: the compiler folds any
+// 64-bit form into v_cmp_lt_u64 against a 2^47 it keeps in a VGPR pair, which the column passes spilled
+// and reloaded in every output prime's skip test (with a vmcnt(0) that also drained the stores)
+__device__ __forceinline__ bool lazy_prime(u64 q)
+{
+    u32 hi = (u32)(q >> 32);
+    asm volatile("" : "+s"(hi));
+    return hi < (1u << 15);
+}
+
 struct ColSrc
 {
     const u64 *src[MHE_MAXB]; // poly s of batch entry e at src[e] + s * stride, after the inverse row pass
@@ -926,7 +936,7 @@ __global__ __launch_bounds__(256, 3) void k_icol_lift(ColSrc cs, Job job, int cn
             for (int i = i_lo; i < i_hi; i++)
             {
                 const auto V = job.view(s * cnt + i);
-                if ((V.p.q < (1ull << 47)) != LZ) continue; // uniform per workgroup
+                if (lazy_prime(V.p.q) != LZ) continue; // uniform per workgroup
                 const NttArithF<LZ> ar(V.p, V.tw, dfwd);
                 const TwF *tl = &twc[(i - i_lo) * R];
                 T v[E];
@@ -1019,7 +1029,7 @@ __global__ __launch_bounds__(256, 3) void k_col_lift2(Job job, int cnt, int log_
         for (int i = i_lo; i < i_hi; i++)
         {
             const auto V = job.view(s * cnt + i);
-            if ((V.p.q < (1ull << 47)) != LZ) continue; // uniform per workgroup
+            if (lazy_prime(V.p.q) != LZ) continue; // uniform per workgroup
             const NttArithF<LZ> ar(V.p, V.tw, dfwd);
             const TwF *tl = &twc[(i - i_lo) * R];
             T v[E];
