@@ -1085,6 +1085,9 @@ struct KsPtrs
 #ifndef MHE_MODUP_PING
 #define MHE_MODUP_PING 1 // n = 2^16: alternate two LDS images per output prime, one barrier per prime (k_modup_col)
 #endif
+#ifndef MHE_MODUP_STW
+#define MHE_MODUP_STW 1 // k_modup_col (FP): first-phase twiddles as scalar loads instead of LDS reads
+#endif
 #ifndef MHE_MODUP_TWG
 #define MHE_MODUP_TWG 5 // output primes per group whose twiddles the ModUp column pass stages in LDS
 #endif
@@ -1231,7 +1234,24 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
                     v[e] = red ? barrett64(xe, p) : xe;
                 }
             }
-            if (twl_on)
+            if constexpr (MHE_MODUP_STW && M != 0)
+            {
+                // the first phase's twiddles (entries 1 .. E-1, the same for every lane) as scalar loads
+                // of the prime's FP table, all issued with the prime's setup: read from the LDS copy,
+                // each stage's ds_read was waited for a few instructions after it was issued
+                const const_u64_p g = (const_u64_p)(reinterpret_cast<const char *>(tw_all + ((size_t)pi << log_n)) + twd);
+                TWA w1[E];
+#pragma unroll
+                for (int k = 1; k < E; k++)
+                {
+                    w1[k].x = __longlong_as_double((long long)g[2 * k]);
+                    w1[k].y = __longlong_as_double((long long)g[2 * k + 1]);
+                }
+#pragma unroll
+                for (int s = 0; s < LOGE; s++)
+                    ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - s), w1, [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+            }
+            else if (twl_on)
             {
 #pragma unroll
                 for (int s = 0; s < LOGE; s++)
