@@ -832,6 +832,29 @@ __global__ __launch_bounds__(256) void k_inv_col(Job job, int log_n, long long t
 // finishes the INTT of its columns once (canonical), then for each output prime lifts (the job's
 // View::lift) and runs the forward column stages: the separate inverse-column launch and its HBM
 // round trip disappear, and the outputs are the same words.
+// The first register phase of a forward column pass (stages 0 .. LOGE-1) uses twiddle entries
+// 1 .. E-1, the same for every lane: read them as scalar loads of the prime's FP table (ftab), issued
+// together, instead of per-stage LDS reads each waited for a few instructions later.
+#ifndef MHE_COL_STW
+#define MHE_COL_STW 0 // k_icol_lift / k_col_lift2 (FP): scalar first-phase twiddles (k_modup_col: MHE_MODUP_STW);
+                      // measured equal (profiles/r06s), so off
+#endif
+template <int E, int LOGE, class AR>
+__device__ __forceinline__ void fwd_first_phase_s(const AR &ar, typename AR::T (&v)[E], const void *ftab)
+{
+    const const_u64_p g = (const_u64_p)ftab;
+    typename AR::TW w1[E];
+#pragma unroll
+    for (int k = 1; k < E; k++)
+    {
+        w1[k].x = __longlong_as_double((long long)g[2 * k]);
+        w1[k].y = __longlong_as_double((long long)g[2 * k + 1]);
+    }
+#pragma unroll
+    for (int s = 0; s < LOGE; s++)
+        ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - s), w1, [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+}
+
 // q < 2^47 (the lazy forward butterflies) as a scalar compare of the high word: the compiler folds any
 // 64-bit form into v_cmp_lt_u64 against a 2^47 it keeps in a VGPR pair, which the column passes spilled
 // and reloaded in every output prime's skip test (with a vmcnt(0) that also drained the stores)
@@ -942,9 +965,14 @@ __global__ __launch_bounds__(256, 3) void k_icol_lift(ColSrc cs, Job job, int cn
                 T v[E];
 #pragma unroll
                 for (int e = 0; e < E; e++) v[e] = fp_reduce(cd[e], ar.q, ar.qinv);
+                if constexpr (MHE_COL_STW)
+                    fwd_first_phase_s<E, LOGE>(ar, v, reinterpret_cast<const char *>(V.tw) + dfwd);
+                else
+                {
 #pragma unroll
-                for (int st = 0; st < LOGE; st++)
-                    ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - st), tl, [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+                    for (int st = 0; st < LOGE; st++)
+                        ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - st), tl, [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+                }
                 lds_barrier(); // lds still holds the previous prime's (or the inverse pass's) transpose
 #pragma unroll
                 for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
@@ -1035,9 +1063,14 @@ __global__ __launch_bounds__(256, 3) void k_col_lift2(Job job, int cnt, int log_
             T v[E];
 #pragma unroll
             for (int e = 0; e < E; e++) v[e] = fp_reduce(V.lift_f(ca[e], cb[e]), ar.q, ar.qinv);
+            if constexpr (MHE_COL_STW)
+                fwd_first_phase_s<E, LOGE>(ar, v, reinterpret_cast<const char *>(V.tw) + dfwd);
+            else
+            {
 #pragma unroll
-            for (int st = 0; st < LOGE; st++)
-                ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - st), tl, [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+                for (int st = 0; st < LOGE; st++)
+                    ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - st), tl, [&](int e) { return (1 << st) + (e >> (LOGE - st)); });
+            }
             lds_barrier(); // lds still holds the previous prime's transpose
 #pragma unroll
             for (int e = 0; e < E; e++) lds[sl * LD + t + TPS * e] = v[e];
@@ -1087,6 +1120,10 @@ struct KsPtrs
 #endif
 #ifndef MHE_MODUP_STW
 #define MHE_MODUP_STW 1 // k_modup_col (FP): first-phase twiddles as scalar loads instead of LDS reads
+#endif
+#ifndef MHE_MODUP_TPF
+#define MHE_MODUP_TPF 0 // k_modup_col: stage-4 (2: and stage-5) twiddles read before the transpose; at 168 VGPRs
+                        // both spill (6 / 14 bytes per lane), so off
 #endif
 #ifndef MHE_MODUP_TWG
 #define MHE_MODUP_TWG 5 // output primes per group whose twiddles the ModUp column pass stages in LDS
@@ -1236,20 +1273,9 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
             }
             if constexpr (MHE_MODUP_STW && M != 0)
             {
-                // the first phase's twiddles (entries 1 .. E-1, the same for every lane) as scalar loads
-                // of the prime's FP table, all issued with the prime's setup: read from the LDS copy,
-                // each stage's ds_read was waited for a few instructions after it was issued
-                const const_u64_p g = (const_u64_p)(reinterpret_cast<const char *>(tw_all + ((size_t)pi << log_n)) + twd);
-                TWA w1[E];
-#pragma unroll
-                for (int k = 1; k < E; k++)
-                {
-                    w1[k].x = __longlong_as_double((long long)g[2 * k]);
-                    w1[k].y = __longlong_as_double((long long)g[2 * k + 1]);
-                }
-#pragma unroll
-                for (int s = 0; s < LOGE; s++)
-                    ar.template fwd_tab<E>(v, 1 << (LOGE - 1 - s), w1, [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+                // the first phase's twiddles as scalar loads (fwd_first_phase_s), issued with the prime's
+                // setup
+                fwd_first_phase_s<E, LOGE>(ar, v, reinterpret_cast<const char *>(tw_all + ((size_t)pi << log_n)) + twd);
             }
             else if (twl_on)
             {
@@ -1262,6 +1288,21 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
 #pragma unroll
                 for (int s = 0; s < LOGE; s++)
                     ar.template fwd<E>(v, 1 << (LOGE - 1 - s), [&](int e) { return (1 << s) + (e >> (LOGE - s)); });
+            }
+            // MHE_MODUP_TPF: the twiddles of the first two stages after the transpose (1 and 2 per lane)
+            // read before it, so their LDS round trip overlaps the transpose's
+            [[maybe_unused]] TWA q4[1], q5[2];
+            if constexpr (MHE_MODUP_TPF && LOGE == 4 && LOGR == 8)
+            {
+                if (twl_on)
+                {
+                    q4[0] = tl[16 + t];
+                    if constexpr (MHE_MODUP_TPF > 1)
+                    {
+                        q5[0] = tl[32 + 2 * t];
+                        q5[1] = tl[32 + 2 * t + 1];
+                    }
+                }
             }
             if constexpr (WV)
             {
@@ -1311,8 +1352,12 @@ __global__ __launch_bounds__(256, (FP && !MIX) ? MHE_MODUP_OCC : MHE_MODUP_OCC_I
             }
             if (twl_on)
             {
+                constexpr int S0 = (MHE_MODUP_TPF && LOGE == 4 && LOGR == 8) ? LOGE + (MHE_MODUP_TPF > 1 ? 2 : 1) : LOGE;
+                // stage 4: entry 16 + t; stage 5: 32 + 2t + (e >> 3)
+                if constexpr (S0 > LOGE) ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - LOGE), q4, [&](int) { return 0; });
+                if constexpr (S0 > LOGE + 1) ar.template fwd_tab<E>(v, 1 << (LOGR - 2 - LOGE), q5, [&](int e) { return e >> 3; });
 #pragma unroll
-                for (int s = LOGE; s < LOGR; s++)
+                for (int s = S0; s < LOGR; s++)
                     ar.template fwd_tab<E>(v, 1 << (LOGR - 1 - s), tl,
                                            [&](int e) { return (1 << s) + ((E * t + e) >> (LOGR - s)); });
             }
