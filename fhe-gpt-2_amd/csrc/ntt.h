@@ -1562,6 +1562,16 @@ static inline void launch_row(const Job &job, int log_n, int jobs, const NttMode
     }
 }
 
+// MHE_ICOL_PER=1..MHE_ICOL_G (A/B runs): output primes per lift workgroup, instead of the size rule
+static inline int icol_per_override()
+{
+    static const int v = [] {
+        const char *e = getenv("MHE_ICOL_PER");
+        const int x = e ? atoi(e) : 0;
+        return x >= 1 && x <= MHE_ICOL_G ? x : 0;
+    }();
+    return v;
+}
 // k_icol_lift over `polys` source polys (all batch entries: cs.per polys each) and `cnt` output
 // primes each (job index s * cnt + i), the column-pass shape of launch_col; IG groups of output
 // primes per (column block, poly)
@@ -1577,7 +1587,8 @@ static inline void icol_lift_a(const ColSrc &cs, const Job &job, int polys, int 
     // batched ones share the inverse stages over 2-3 primes (ubench at 31 / 20 limbs, profiles/r03v:
     // 4 rescales 207 -> 185 us)
     const int jobs = polys * cnt;
-    const int per = jobs >= 128 ? MHE_ICOL_G : jobs >= 56 ? 2 : 1;
+    int per = jobs >= 128 ? MHE_ICOL_G : jobs >= 56 ? 2 : 1;
+    if (const int po = icol_per_override()) per = po;
     const int IG = (cnt + per - 1) / per;
     hipLaunchKernelGGL((k_icol_lift<LOGR, LOGT, Job, FP>), dim3(subs / SH::S, polys, IG), dim3(256), 0, st, cs, job,
                        cnt, log_n, dinv, dfwd);
@@ -1611,7 +1622,8 @@ static inline void col_lift2_a(const Job &job, int polys, int cnt, int log_n, lo
     using SH = Shape<LOGR, LOGT>;
     const int subs = 1 << (log_n - LOGR);
     const int jobs = polys * cnt;
-    const int per = jobs >= 128 ? MHE_ICOL_G : jobs >= 56 ? 2 : 1; // as icol_lift_a
+    int per = jobs >= 128 ? MHE_ICOL_G : jobs >= 56 ? 2 : 1; // as icol_lift_a
+    if (const int po = icol_per_override()) per = po;
     const int IG = (cnt + per - 1) / per;
     hipLaunchKernelGGL((k_col_lift2<LOGR, LOGT, Job>), dim3(subs / SH::S, polys, IG), dim3(256), 0, st, job, cnt, log_n,
                        dfwd);
