@@ -881,7 +881,8 @@ struct ColSrc
 };
 
 #ifndef MHE_ICOL_G
-#define MHE_ICOL_G 3 // at most this many output primes per k_icol_lift workgroup (icol_lift_a)
+#define MHE_ICOL_G 5 // at most this many output primes per lift-pass workgroup (icol_lift_a); 5 fills the LDS
+                     // of 3 workgroups per CU: 8 rescales at 25 limbs -5 % against 3 (profiles/r06w)
 #endif
 template <int LOGR, int LOGT, class Job, bool FP>
 __global__ __launch_bounds__(256, 3) void k_icol_lift(ColSrc cs, Job job, int cnt, int log_n, long long dinv,
@@ -1584,7 +1585,7 @@ static inline void icol_lift_a(const ColSrc &cs, const Job &job, int polys, int 
     const int subs = 1 << (log_n - LOGR);
     // output primes per workgroup: each workgroup redoes the inverse column stages of its columns
     // (from L2) once per group, so small launches keep one prime per workgroup (the widest grid) and
-    // batched ones share the inverse stages over 2-3 primes (ubench at 31 / 20 limbs, profiles/r03v:
+    // batched ones share the inverse stages over 2 to MHE_ICOL_G primes (ubench at 31 / 20 limbs, profiles/r03v:
     // 4 rescales 207 -> 185 us)
     const int jobs = polys * cnt;
     int per = jobs >= 128 ? MHE_ICOL_G : jobs >= 56 ? 2 : 1;
